@@ -1,0 +1,261 @@
+"""fractencode_amd — MI355X-native range×domain search for fractal block-matching.
+
+Python binding of the C ABI in include/fracenc.h (libfracenc.so, built in-tree by
+``__graft_entry__.build()``).  The product path is the HIP library; there is no
+CPU fallback: constructing an :class:`Engine` without the library or without a
+GPU raises.
+
+The names mirror the reference's engine API for this path
+(sebsgit/fractencode encode/EncodingEngine2.hpp, encode/TransformEstimator2.hpp):
+  * :func:`create_uniform_grid`  — Frac2::createUniformGrid (image/partition2.hpp:109-135)
+  * :func:`preclassify`          — BrightnessBlocksClassifier2::preclassify (Classifier2.cpp:64-68)
+  * :class:`Engine`              — an AbstractEncodingEngine2 that encodes a whole batch
+                                   of range items per call on one GPU
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libfracenc.so")
+
+GRID_ITEM = np.dtype([("x", "<u4"), ("y", "<u4"), ("w", "<u4"), ("h", "<u4"), ("category", "<i4")])
+ENCODE_ITEM = np.dtype([("x", "<u4"), ("y", "<u4"), ("w", "<u4"), ("h", "<u4"),
+                        ("distance", "<f8"), ("contrast", "<f8"), ("brightness", "<f8"),
+                        ("transform", "<i4"), ("_pad", "<i4"),
+                        ("dx", "<u4"), ("dy", "<u4"), ("sw", "<u4"), ("sh", "<u4")])
+assert GRID_ITEM.itemsize == 20 and ENCODE_ITEM.itemsize == 64
+
+ENGINE_AUTO, ENGINE_VALU, ENGINE_MFMA = 0, 1, 2
+FLAG_TIMING = 1
+
+# Frac::TransformType (image/transform.h:16-25)
+TRANSFORM_NAMES = ("Id", "Rotate_90", "Rotate_180", "Rotate_270", "Flip", "Flip_Rotate_90", "Flip_Rotate_180",
+                   "Flip_Rotate_270")
+
+
+class FracParams(C.Structure):
+    _fields_ = [("transforms", C.c_uint32), ("use_classifier", C.c_int32), ("rms_threshold", C.c_double),
+                ("s_max", C.c_double), ("engine", C.c_uint32), ("flags", C.c_uint32)]
+
+
+class FracStats(C.Structure):
+    _fields_ = [("rejected_mappings", C.c_uint64), ("total_mappings", C.c_uint64), ("hit_ranges", C.c_uint32),
+                ("fallback_ranges", C.c_uint32), ("empty_ranges", C.c_uint32), ("engine", C.c_uint32),
+                ("ms_device", C.c_double), ("ms_search", C.c_double), ("ms_prep", C.c_double),
+                ("ms_finish", C.c_double)]
+
+    def as_dict(self) -> dict:
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+class FracError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    """The HIP engine library; raises FracError when it has not been built."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise FracError(f"{LIB_PATH} not built: run __graft_entry__.build() (no CPU fallback exists)")
+        L = C.CDLL(LIB_PATH)
+        vp, u32, i32, sz = C.c_void_p, C.c_uint32, C.c_int, C.c_size_t
+        sig = {
+            "frac_abi_version": (i32, []),
+            "frac_create": (vp, [i32, C.POINTER(FracParams)]),
+            "frac_destroy": (None, [vp]),
+            "frac_last_error": (C.c_char_p, [vp]),
+            "frac_set_params": (i32, [vp, C.POINTER(FracParams)]),
+            "frac_set_frame": (i32, [vp, vp, u32, u32, u32]),
+            "frac_set_planes": (i32, [vp, vp, u32, u32, u32, vp, u32, u32, u32]),
+            "frac_set_frame_device": (i32, [vp, vp, u32, u32, u32]),
+            "frac_set_domains": (i32, [vp, vp, sz]),
+            "frac_set_ranges": (i32, [vp, vp, sz]),
+            "frac_run": (i32, [vp]),
+            "frac_fetch": (i32, [vp, vp, C.POINTER(FracStats)]),
+            "frac_sync": (i32, [vp]),
+            "frac_search": (i32, [vp, vp, sz, vp, C.POINTER(FracStats)]),
+            "frac_set_stream": (i32, [vp, vp]),
+            "frac_get_stream": (vp, [vp]),
+            "frac_device_results": (vp, [vp]),
+            "frac_copy_results_device": (i32, [vp, vp]),
+            "frac_uniform_grid": (sz, [u32, u32, u32, u32, vp, sz]),
+            "frac_classify": (i32, [vp, u32, u32, u32, vp, sz]),
+            "frac_transform_index": (i32, [u32, u32, u32]),
+            "frac_hit_limit": (C.c_int64, [C.c_double, u32]),
+        }
+        for name, (res, args) in sig.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def last_error(ctx=None) -> str:
+    msg = lib().frac_last_error(ctx)
+    return msg.decode() if msg else ""
+
+
+# ---- host helpers ----------------------------------------------------------------
+
+def create_uniform_grid(width: int, height: int, item_size: int, item_offset: int) -> np.ndarray:
+    """Frac2::createUniformGrid: row-major items, x fastest (categories -1)."""
+    n = lib().frac_uniform_grid(width, height, item_size, item_offset, None, 0)
+    out = np.zeros(n, dtype=GRID_ITEM)
+    if n:
+        lib().frac_uniform_grid(width, height, item_size, item_offset, out.ctypes.data, n)
+    return out
+
+
+def preclassify(plane: np.ndarray, items: np.ndarray) -> np.ndarray:
+    """Categories of BrightnessBlocksClassifier2 computed on `plane` (returns a copy)."""
+    plane = np.ascontiguousarray(plane, dtype=np.uint8)
+    items = np.ascontiguousarray(items, dtype=GRID_ITEM).copy()
+    rc = lib().frac_classify(plane.ctypes.data, plane.shape[1], plane.shape[0], plane.shape[1], items.ctypes.data,
+                             len(items))
+    if rc != 0:
+        raise FracError(last_error())
+    return items
+
+
+def transform_index(n: int, t: int, pix: int) -> int:
+    return lib().frac_transform_index(n, t, pix)
+
+
+def hit_limit(rms_threshold: float, n: int) -> int:
+    return lib().frac_hit_limit(rms_threshold, n)
+
+
+# ---- engine ---------------------------------------------------------------------
+
+class Engine:
+    """One search context on one GPU (an AbstractEncodingEngine2 that takes batches).
+
+    Parameters mirror encode_parameters_t / TransformMatcher: ``transforms`` 4 (the
+    reference's TransformMatcher::match) or 8, ``use_classifier``, ``rms_threshold``,
+    ``s_max``.
+    """
+
+    def __init__(self, device: int = 0, transforms: int = 4, use_classifier: bool = False,
+                 rms_threshold: float = 0.0, s_max: float = -1.0, engine: int = ENGINE_AUTO, timing: bool = False):
+        self._p = FracParams(transforms, int(use_classifier), rms_threshold, s_max, engine,
+                             FLAG_TIMING if timing else 0)
+        self._ctx = lib().frac_create(device, C.byref(self._p))
+        if not self._ctx:
+            raise FracError("frac_create failed: " + last_error())
+        self._nr = 0
+        self._keep = []
+
+    def close(self) -> None:
+        if getattr(self, "_ctx", None):
+            lib().frac_destroy(self._ctx)
+            self._ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def _check(self, rc: int) -> None:
+        if rc != 0:
+            raise FracError(f"rc={rc}: {last_error(self._ctx)}")
+
+    def set_params(self, transforms=None, use_classifier=None, rms_threshold=None, s_max=None, engine=None):
+        if transforms is not None:
+            self._p.transforms = transforms
+        if use_classifier is not None:
+            self._p.use_classifier = int(use_classifier)
+        if rms_threshold is not None:
+            self._p.rms_threshold = rms_threshold
+        if s_max is not None:
+            self._p.s_max = s_max
+        if engine is not None:
+            self._p.engine = engine
+        self._check(lib().frac_set_params(self._ctx, C.byref(self._p)))
+
+    def set_frame(self, plane) -> None:
+        """Source == target plane (Encoder2).  numpy uint8 [H, W] or a CUDA torch tensor."""
+        if hasattr(plane, "is_cuda") and plane.is_cuda:
+            assert plane.dtype.itemsize == 1 and plane.dim() == 2
+            self._check(lib().frac_set_frame_device(self._ctx, C.c_void_p(plane.data_ptr()), plane.shape[1],
+                                                    plane.shape[0], plane.stride(0)))
+            return
+        plane = np.ascontiguousarray(plane, dtype=np.uint8)
+        self._check(lib().frac_set_frame(self._ctx, plane.ctypes.data, plane.shape[1], plane.shape[0],
+                                         plane.shape[1]))
+
+    def set_planes(self, source: np.ndarray, target: np.ndarray) -> None:
+        s = np.ascontiguousarray(source, dtype=np.uint8)
+        t = np.ascontiguousarray(target, dtype=np.uint8)
+        self._check(lib().frac_set_planes(self._ctx, s.ctypes.data, s.shape[1], s.shape[0], s.shape[1], t.ctypes.data,
+                                          t.shape[1], t.shape[0], t.shape[1]))
+
+    def set_domains(self, items: np.ndarray) -> None:
+        items = np.ascontiguousarray(items, dtype=GRID_ITEM)
+        self._check(lib().frac_set_domains(self._ctx, items.ctypes.data if len(items) else None, len(items)))
+
+    def set_ranges(self, items: np.ndarray) -> None:
+        items = np.ascontiguousarray(items, dtype=GRID_ITEM)
+        self._check(lib().frac_set_ranges(self._ctx, items.ctypes.data if len(items) else None, len(items)))
+        self._nr = len(items)
+
+    def run(self) -> None:
+        self._check(lib().frac_run(self._ctx))
+
+    def sync(self) -> None:
+        self._check(lib().frac_sync(self._ctx))
+
+    def fetch(self):
+        out = np.zeros(self._nr, dtype=ENCODE_ITEM)
+        st = FracStats()
+        self._check(lib().frac_fetch(self._ctx, out.ctypes.data if self._nr else None, C.byref(st)))
+        return out, st.as_dict()
+
+    def search(self, ranges: np.ndarray):
+        """set_ranges + run + fetch → (encode items in range order, stats dict)."""
+        self.set_ranges(ranges)
+        self.run()
+        return self.fetch()
+
+    def set_stream(self, stream_handle: int | None) -> None:
+        self._check(lib().frac_set_stream(self._ctx, C.c_void_p(stream_handle) if stream_handle else None))
+
+    def copy_results_device(self, dst_ptr: int) -> None:
+        """Async D2D copy of the last run's results (64 B each) to a device buffer."""
+        self._check(lib().frac_copy_results_device(self._ctx, C.c_void_p(dst_ptr)))
+
+    def device_results_ptr(self) -> int:
+        return lib().frac_device_results(self._ctx) or 0
+
+
+def encode(plane: np.ndarray, range_size: int = 8, domain_size: int | None = None, transforms: int = 4,
+           use_classifier: bool = False, rms_threshold: float = 0.0, s_max: float = -1.0, device: int = 0,
+           engine: int = ENGINE_AUTO):
+    """Encoder2's search half for one plane, with grids built like main.cpp:142-162."""
+    plane = np.ascontiguousarray(plane, dtype=np.uint8)
+    H, W = plane.shape
+    dsz = domain_size or 2 * range_size
+    doms = create_uniform_grid(W, H, dsz, dsz // 2)
+    rngs = create_uniform_grid(W, H, range_size, range_size)
+    if use_classifier:
+        doms = preclassify(plane, doms)
+        rngs = preclassify(plane, rngs)
+    with Engine(device, transforms, use_classifier, rms_threshold, s_max, engine) as e:
+        e.set_frame(plane)
+        e.set_domains(doms)
+        return e.search(rngs)

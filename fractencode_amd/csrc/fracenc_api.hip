@@ -1,0 +1,804 @@
+// fracenc_api.hip — C ABI (include/fracenc.h): contexts, host-side bucketing of the
+// domain pool by classifier category, work lists, kernel launches and statistics.
+//
+// Host logic mirrored from the reference:
+//   classifier gating      encode/Classifier2.cpp:8-81   (categories computed on the host,
+//                          a stored −1 re-computed on the item's own plane like compare())
+//   rejected-mapping count encode/TransformEstimator2.hpp:43-45,59 (derived from the winner)
+//   search order / ties    encode/TransformEstimator2.hpp:29-48
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "fracenc_common.h"
+#include "fracenc_kernels.hip"
+
+using namespace fracenc;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+template <class T>
+struct DBuf {
+    T* ptr = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t n)
+    {
+        if (n <= cap && ptr)
+            return hipSuccess;
+        if (ptr)
+            (void)hipFree(ptr);
+        ptr = nullptr;
+        cap = 0;
+        const size_t want = std::max<size_t>(n, 1);
+        hipError_t e = hipMalloc(reinterpret_cast<void**>(&ptr), want * sizeof(T));
+        if (e == hipSuccess)
+            cap = want;
+        return e;
+    }
+    void release()
+    {
+        if (ptr)
+            (void)hipFree(ptr);
+        ptr = nullptr;
+        cap = 0;
+    }
+};
+
+struct HostPlane {
+    std::vector<uint8_t> data; // tightly packed, stride == w
+    uint32_t w = 0, h = 0;
+};
+
+// --- classifier (host) -------------------------------------------------------
+// ImageStatistics2::sum (image/ImageStatistics.hpp:12-17): u16 up to 16 wide.
+double block_sum(const HostPlane& p, uint32_t x, uint32_t y, uint32_t w, uint32_t h)
+{
+    uint32_t s = 0;
+    for (uint32_t j = 0; j < h; ++j) {
+        const uint8_t* row = p.data.data() + (size_t)(y + j) * p.w + x;
+        for (uint32_t i = 0; i < w; ++i)
+            s += row[i];
+    }
+    return w <= 16 ? (double)(uint16_t)s : (double)s;
+}
+
+// BrightnessBlocksClassifier2::getCategory(a1..a4) — encode/Classifier2.cpp:8-62
+int category4(double a1, double a2, double a3, double a4)
+{
+    // rule (i, j, k): a_i > a_j && a_j > a_k && a_k > a_l, listed as quadruples (i j k l)
+    static const unsigned char rules[24][4] = {
+        {1, 2, 3, 4}, {3, 1, 4, 2}, {4, 3, 2, 1}, {2, 4, 1, 3}, // 0
+        {1, 3, 2, 4}, {2, 1, 4, 3}, {4, 2, 3, 1}, {3, 4, 1, 2}, // 1
+        {1, 4, 3, 2}, {4, 1, 2, 3}, {3, 2, 4, 1}, {2, 3, 1, 4}, // 2
+        {1, 2, 4, 3}, {3, 1, 2, 4}, {4, 3, 1, 2}, {2, 4, 3, 1}, // 3
+        {2, 1, 3, 4}, {1, 3, 4, 2}, {3, 4, 2, 1}, {4, 2, 1, 3}, // 4
+        {1, 4, 2, 3}, {4, 1, 3, 4}, {2, 3, 4, 1}, {3, 2, 1, 4}, // 5
+    };
+    const double a[5] = {0.0, a1, a2, a3, a4};
+    for (int r = 0; r < 24; ++r) {
+        const unsigned char* q = rules[r];
+        if (a[q[0]] > a[q[1]] && a[q[1]] > a[q[2]] && a[q[2]] > a[q[3]])
+            return r / 4;
+    }
+    return -1;
+}
+
+int category(const HostPlane& p, const frac_grid_item& it)
+{
+    const uint32_t hw = it.w / 2, hh = it.h / 2;
+    return category4(block_sum(p, it.x, it.y, hw, hh), block_sum(p, it.x + hw, it.y, hw, hh),
+                     block_sum(p, it.x, it.y + hh, hw, hh), block_sum(p, it.x + hw, it.y + hh, hw, hh));
+}
+
+// Largest S16 whose reference distance fl64((S16/16)/area) is <= thr
+// (TransformMatcher::checkDistance, encode/transformmatcher.h:32-34); −1 if none.
+int64_t compute_hit_limit(double thr, uint32_t area)
+{
+    auto pred = [&](int64_t s) { return ((double)s * 0.0625) / (double)area <= thr; };
+    if (!pred(0))
+        return -1;
+    int64_t lo = 0, hi = 1ll << 40;
+    if (pred(hi))
+        return hi;
+    while (hi - lo > 1) {
+        const int64_t mid = lo + (hi - lo) / 2;
+        if (pred(mid))
+            lo = mid;
+        else
+            hi = mid;
+    }
+    return lo;
+}
+
+} // namespace
+
+struct frac_ctx {
+    int device = 0;
+    frac_params p{};
+    hipStream_t own_stream = nullptr;
+    hipStream_t stream = nullptr;
+    std::string err;
+
+    HostPlane src, tgt;
+    bool same_plane = true;
+    bool planes_set = false;
+    DBuf<uint8_t> d_src, d_tgt;
+    uint32_t d_sstride = 0, d_tstride = 0;
+
+    std::vector<frac_grid_item> doms, ranges;
+    bool doms_set = false, ranges_set = false;
+    bool dirty = true;
+
+    // prepared state
+    int n = 0;
+    uint32_t G = 4, NG = 1;
+    std::vector<uint32_t> porig;            // pool position → domain index
+    std::vector<uint32_t> bucket_begin, bucket_end; // per bucket (category + 1)
+    std::vector<int32_t> range_bucket;      // per range
+    std::vector<uint2> rbucket;             // per range pool slice
+    std::vector<int32_t> slot_range;
+    std::vector<uint4> work;
+    int64_t hitH = -1;
+    bool all_fallback = false;
+    std::vector<uint32_t> fb_iota;
+
+    DBuf<frac_grid_item> d_doms, d_ranges;
+    DBuf<uint32_t> d_porig, d_pool, d_fb_list, d_fb_count;
+    DBuf<int32_t> d_negsd2, d_slot_range;
+    DBuf<uint4> d_work;
+    DBuf<uint2> d_rbucket;
+    DBuf<unsigned long long> d_best_key;
+    DBuf<frac_encode_item> d_out;
+    DBuf<RangeAux> d_aux;
+
+    std::vector<RangeAux> h_aux;
+    hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+    bool ran = false;
+    uint32_t engine_ran = FRAC_ENGINE_VALU;
+
+    int fail(int code, const std::string& msg)
+    {
+        err = msg;
+        g_last_error = msg;
+        return code;
+    }
+    int hip(hipError_t e, const char* what)
+    {
+        if (e == hipSuccess)
+            return FRAC_OK;
+        return fail(FRAC_E_DEVICE, std::string(what) + ": " + hipGetErrorString(e));
+    }
+};
+
+#define FRAC_TRY(expr)                                                                                                 \
+    do {                                                                                                               \
+        int _rc = (expr);                                                                                              \
+        if (_rc != FRAC_OK)                                                                                            \
+            return _rc;                                                                                                \
+    } while (0)
+#define FRAC_HIP(ctx, expr) FRAC_TRY((ctx)->hip((expr), #expr))
+
+namespace {
+
+int check_params(const frac_params* p, std::string& msg)
+{
+    if (!p) {
+        msg = "params is NULL";
+        return FRAC_E_INVALID;
+    }
+    if (p->transforms != 4 && p->transforms != 8) {
+        msg = "transforms must be 4 or 8";
+        return FRAC_E_INVALID;
+    }
+    if (p->engine > FRAC_ENGINE_MFMA) {
+        msg = "unknown engine";
+        return FRAC_E_INVALID;
+    }
+    return FRAC_OK;
+}
+
+int upload_plane(frac_ctx* c, const HostPlane& hp, DBuf<uint8_t>& d, uint32_t& dstride)
+{
+    dstride = (hp.w + 63u) & ~63u;
+    // one extra row + column of slack: kernels never read it, but keeps every 2×2 read in-bounds
+    FRAC_HIP(c, d.ensure((size_t)dstride * (hp.h + 1)));
+    FRAC_HIP(c, hipMemcpy2DAsync(d.ptr, dstride, hp.data.data(), hp.w, hp.w, hp.h, hipMemcpyHostToDevice, c->stream));
+    return FRAC_OK;
+}
+
+int prepare(frac_ctx* c)
+{
+    if (!c->planes_set || !c->doms_set || !c->ranges_set)
+        return c->fail(FRAC_E_STATE, "planes, domains and ranges must be set before frac_run");
+    const uint32_t T = c->p.transforms;
+    // geometry: the engine implements the ratio-2 path of TransformMatcher (n×n ranges,
+    // 2n×2n domains), n ∈ {2, 4, 8, 16}
+    int n = c->ranges.empty() ? 8 : (int)c->ranges[0].w;
+    for (const auto& r : c->ranges) {
+        if ((int)r.w != n || (int)r.h != n)
+            return c->fail(FRAC_E_INVALID, "all ranges must be square and of one size");
+        if ((uint64_t)r.x + r.w > c->tgt.w || (uint64_t)r.y + r.h > c->tgt.h)
+            return c->fail(FRAC_E_INVALID, "range outside the target plane");
+    }
+    if (n != 2 && n != 4 && n != 8 && n != 16)
+        return c->fail(FRAC_E_INVALID, "range size must be 2, 4, 8 or 16");
+    for (const auto& d : c->doms) {
+        if ((int)d.w != 2 * n || (int)d.h != 2 * n)
+            return c->fail(FRAC_E_INVALID, "domains must be square with twice the range size");
+        if ((uint64_t)d.x + d.w > c->src.w || (uint64_t)d.y + d.h > c->src.h)
+            return c->fail(FRAC_E_INVALID, "domain outside the source plane");
+    }
+    if (c->doms.size() >= (1u << 24))
+        return c->fail(FRAC_E_INVALID, "at most 2^24 - 1 domains");
+    c->n = n;
+    c->G = n == 16 ? 1u : (n <= 4 ? T : 4u);
+    c->NG = T / c->G;
+
+    // buckets: category + 1 (0 = category −1) with the classifier, a single bucket without
+    const int nb = c->p.use_classifier ? 7 : 1;
+    std::vector<int32_t> dbk(c->doms.size(), 0);
+    c->range_bucket.assign(c->ranges.size(), 0);
+    if (c->p.use_classifier) {
+        for (size_t i = 0; i < c->doms.size(); ++i) {
+            int cat = c->doms[i].category;
+            if (cat == -1)
+                cat = category(c->src, c->doms[i]);
+            dbk[i] = cat + 1;
+        }
+        for (size_t i = 0; i < c->ranges.size(); ++i) {
+            int cat = c->ranges[i].category;
+            if (cat == -1)
+                cat = category(c->tgt, c->ranges[i]);
+            c->range_bucket[i] = cat + 1;
+        }
+        for (size_t i = 0; i < c->doms.size(); ++i)
+            if (dbk[i] < 0 || dbk[i] >= nb)
+                return c->fail(FRAC_E_INVALID, "domain category outside -1..5");
+        for (size_t i = 0; i < c->ranges.size(); ++i)
+            if (c->range_bucket[i] < 0 || c->range_bucket[i] >= nb)
+                return c->fail(FRAC_E_INVALID, "range category outside -1..5");
+    }
+    c->bucket_begin.assign(nb, 0);
+    c->bucket_end.assign(nb, 0);
+    c->porig.clear();
+    c->porig.reserve(c->doms.size());
+    for (int b = 0; b < nb; ++b) {
+        c->bucket_begin[b] = (uint32_t)c->porig.size();
+        for (size_t i = 0; i < c->doms.size(); ++i)
+            if (dbk[i] == b)
+                c->porig.push_back((uint32_t)i);
+        c->bucket_end[b] = (uint32_t)c->porig.size();
+    }
+    c->rbucket.resize(c->ranges.size());
+    for (size_t i = 0; i < c->ranges.size(); ++i) {
+        const int b = c->range_bucket[i];
+        c->rbucket[i] = make_uint2(c->bucket_begin[b], c->bucket_end[b]);
+    }
+    // range slots: per bucket, padded to whole waves of 64
+    c->slot_range.clear();
+    c->work.clear();
+    std::vector<std::pair<uint32_t, int>> blocks; // (slot base, bucket)
+    for (int b = 0; b < nb; ++b) {
+        const uint32_t base = (uint32_t)c->slot_range.size();
+        for (size_t i = 0; i < c->ranges.size(); ++i)
+            if (c->range_bucket[i] == b)
+                c->slot_range.push_back((int32_t)i);
+        const uint32_t cnt = (uint32_t)c->slot_range.size() - base;
+        if (cnt == 0)
+            continue;
+        while (c->slot_range.size() % 64)
+            c->slot_range.push_back(-1);
+        for (uint32_t s = base; s < c->slot_range.size(); s += 64)
+            blocks.emplace_back(s, b);
+    }
+    size_t total_blocks = 0;
+    for (auto& bl : blocks)
+        if (c->bucket_end[bl.second] > c->bucket_begin[bl.second])
+            total_blocks += c->NG;
+    // domain splits: enough waves to fill 256 CUs several times over, ≥ 32 domains per wave
+    const size_t target_waves = 8192;
+    for (auto& bl : blocks) {
+        const uint32_t b0 = c->bucket_begin[bl.second], b1 = c->bucket_end[bl.second];
+        const uint32_t D = b1 - b0;
+        if (D == 0)
+            continue;
+        size_t splits = total_blocks ? (target_waves + total_blocks - 1) / total_blocks : 1;
+        splits = std::min<size_t>(splits, std::max<uint32_t>(1u, D / 32u));
+        splits = std::max<size_t>(splits, 1);
+        for (uint32_t g = 0; g < c->NG; ++g)
+            for (size_t s = 0; s < splits; ++s) {
+                const uint32_t pb = b0 + (uint32_t)((uint64_t)D * s / splits);
+                const uint32_t pe = b0 + (uint32_t)((uint64_t)D * (s + 1) / splits);
+                if (pe > pb)
+                    c->work.push_back(make_uint4(bl.first, pb, pe, g));
+            }
+    }
+    c->hitH = compute_hit_limit(c->p.rms_threshold, (uint32_t)(4 * n * n));
+    c->all_fallback = c->hitH >= kExactLimit;
+
+    const size_t nr = c->ranges.size(), P = c->porig.size();
+    FRAC_HIP(c, c->d_doms.ensure(c->doms.size()));
+    FRAC_HIP(c, c->d_ranges.ensure(nr));
+    FRAC_HIP(c, c->d_porig.ensure(P));
+    FRAC_HIP(c, c->d_pool.ensure(P * (size_t)(n * n / 2)));
+    FRAC_HIP(c, c->d_negsd2.ensure(P));
+    FRAC_HIP(c, c->d_slot_range.ensure(c->slot_range.size()));
+    FRAC_HIP(c, c->d_work.ensure(c->work.size()));
+    FRAC_HIP(c, c->d_rbucket.ensure(nr));
+    FRAC_HIP(c, c->d_best_key.ensure(nr));
+    FRAC_HIP(c, c->d_out.ensure(nr));
+    FRAC_HIP(c, c->d_aux.ensure(nr));
+    FRAC_HIP(c, c->d_fb_list.ensure(nr));
+    FRAC_HIP(c, c->d_fb_count.ensure(1));
+    auto up = [&](void* dst, const void* srcp, size_t bytes) {
+        return bytes ? c->hip(hipMemcpyAsync(dst, srcp, bytes, hipMemcpyHostToDevice, c->stream), "upload") : 0;
+    };
+    FRAC_TRY(up(c->d_doms.ptr, c->doms.data(), c->doms.size() * sizeof(frac_grid_item)));
+    FRAC_TRY(up(c->d_ranges.ptr, c->ranges.data(), nr * sizeof(frac_grid_item)));
+    FRAC_TRY(up(c->d_porig.ptr, c->porig.data(), P * sizeof(uint32_t)));
+    FRAC_TRY(up(c->d_slot_range.ptr, c->slot_range.data(), c->slot_range.size() * sizeof(int32_t)));
+    FRAC_TRY(up(c->d_work.ptr, c->work.data(), c->work.size() * sizeof(uint4)));
+    FRAC_TRY(up(c->d_rbucket.ptr, c->rbucket.data(), nr * sizeof(uint2)));
+    if (c->all_fallback) {
+        c->fb_iota.resize(nr);
+        for (size_t i = 0; i < nr; ++i)
+            c->fb_iota[i] = (uint32_t)i;
+        FRAC_TRY(up(c->d_fb_list.ptr, c->fb_iota.data(), nr * sizeof(uint32_t)));
+    }
+    c->h_aux.resize(nr);
+    c->dirty = false;
+    return FRAC_OK;
+}
+
+template <int N>
+int launch_all(frac_ctx* c)
+{
+    const uint32_t nr = (uint32_t)c->ranges.size(), P = (uint32_t)c->porig.size();
+    const bool timing = (c->p.flags & FRAC_FLAG_TIMING) != 0;
+    const uint8_t* dsrc = c->d_src.ptr;
+    const uint8_t* dtgt = c->same_plane ? c->d_src.ptr : c->d_tgt.ptr;
+    const uint32_t tstride = c->same_plane ? c->d_sstride : c->d_tstride;
+    if (timing)
+        FRAC_HIP(c, hipEventRecord(c->ev[0], c->stream));
+    if (nr)
+        FRAC_HIP(c, hipMemsetAsync(c->d_best_key.ptr, 0xff, nr * sizeof(unsigned long long), c->stream));
+    const uint32_t fbc = c->all_fallback ? nr : 0u;
+    FRAC_HIP(c, hipMemcpyAsync(c->d_fb_count.ptr, &fbc, sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
+    if (P)
+        pool_build<N><<<(P + 3) / 4, 256, 0, c->stream>>>(dsrc, c->d_sstride, c->d_doms.ptr, c->d_porig.ptr, P,
+                                                          c->d_pool.ptr, c->d_negsd2.ptr);
+    if (timing)
+        FRAC_HIP(c, hipEventRecord(c->ev[1], c->stream));
+    if (!c->all_fallback && !c->work.empty()) {
+        SearchArgs a;
+        a.tgt = dtgt;
+        a.tstride = tstride;
+        a.ranges = c->d_ranges.ptr;
+        a.slot_range = c->d_slot_range.ptr;
+        a.pool = c->d_pool.ptr;
+        a.negsd2 = c->d_negsd2.ptr;
+        a.work = c->d_work.ptr;
+        a.nwork = (uint32_t)c->work.size();
+        a.hitH = (int32_t)std::max<int64_t>(c->hitH, 0);
+        a.best_key = c->d_best_key.ptr;
+        const dim3 grid((a.nwork + 3) / 4), block(256);
+        const bool hits = c->hitH >= 0;
+        if constexpr (N == 16) {
+            if (hits)
+                search_valu<N, 1, true><<<grid, block, 0, c->stream>>>(a);
+            else
+                search_valu<N, 1, false><<<grid, block, 0, c->stream>>>(a);
+        } else if constexpr (N <= 4) {
+            if (c->G == 8) {
+                if (hits)
+                    search_valu<N, 8, true><<<grid, block, 0, c->stream>>>(a);
+                else
+                    search_valu<N, 8, false><<<grid, block, 0, c->stream>>>(a);
+            } else {
+                if (hits)
+                    search_valu<N, 4, true><<<grid, block, 0, c->stream>>>(a);
+                else
+                    search_valu<N, 4, false><<<grid, block, 0, c->stream>>>(a);
+            }
+        } else {
+            if (hits)
+                search_valu<N, 4, true><<<grid, block, 0, c->stream>>>(a);
+            else
+                search_valu<N, 4, false><<<grid, block, 0, c->stream>>>(a);
+        }
+    }
+    if (timing)
+        FRAC_HIP(c, hipEventRecord(c->ev[2], c->stream));
+    if (!c->all_fallback && nr) {
+        FitArgs f;
+        f.tgt = dtgt;
+        f.tstride = tstride;
+        f.ranges = c->d_ranges.ptr;
+        f.doms = c->d_doms.ptr;
+        f.porig = c->d_porig.ptr;
+        f.pool = c->d_pool.ptr;
+        f.best_key = c->d_best_key.ptr;
+        f.nr = nr;
+        f.T = c->p.transforms;
+        f.hitH = c->hitH;
+        f.smax = c->p.s_max;
+        f.all_fallback = 0;
+        f.out = c->d_out.ptr;
+        f.aux = c->d_aux.ptr;
+        f.fb_count = c->d_fb_count.ptr;
+        f.fb_list = c->d_fb_list.ptr;
+        fit_winner<N><<<(nr + 3) / 4, 256, 0, c->stream>>>(f);
+    }
+    if (nr) {
+        FallbackArgs b;
+        b.tgt = dtgt;
+        b.tstride = tstride;
+        b.ranges = c->d_ranges.ptr;
+        b.doms = c->d_doms.ptr;
+        b.porig = c->d_porig.ptr;
+        b.pool = c->d_pool.ptr;
+        b.rbucket = c->d_rbucket.ptr;
+        b.fb_count = c->d_fb_count.ptr;
+        b.fb_list = c->d_fb_list.ptr;
+        b.T = c->p.transforms;
+        b.thr = c->p.rms_threshold;
+        b.smax = c->p.s_max;
+        b.out = c->d_out.ptr;
+        b.aux = c->d_aux.ptr;
+        fallback_fp32<N><<<512, 256, 0, c->stream>>>(b);
+    }
+    if (timing)
+        FRAC_HIP(c, hipEventRecord(c->ev[3], c->stream));
+    FRAC_HIP(c, hipGetLastError());
+    c->engine_ran = FRAC_ENGINE_VALU;
+    return FRAC_OK;
+}
+
+} // namespace
+
+extern "C" {
+
+int frac_abi_version(void) { return FRAC_ABI_VERSION; }
+
+const char* frac_last_error(const frac_ctx* ctx) { return ctx ? ctx->err.c_str() : g_last_error.c_str(); }
+
+frac_ctx* frac_create(int device, const frac_params* params)
+{
+    std::string msg;
+    if (check_params(params, msg) != FRAC_OK) {
+        g_last_error = msg;
+        return nullptr;
+    }
+    int count = 0;
+    hipError_t e = hipGetDeviceCount(&count);
+    if (e != hipSuccess || count == 0) {
+        g_last_error = std::string("no HIP device: ") + hipGetErrorString(e);
+        return nullptr;
+    }
+    if (device < 0 || device >= count) {
+        g_last_error = "device index out of range";
+        return nullptr;
+    }
+    e = hipSetDevice(device);
+    if (e != hipSuccess) {
+        g_last_error = std::string("hipSetDevice: ") + hipGetErrorString(e);
+        return nullptr;
+    }
+    auto* c = new frac_ctx();
+    c->device = device;
+    c->p = *params;
+    if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) {
+        g_last_error = "hipStreamCreate failed";
+        delete c;
+        return nullptr;
+    }
+    c->stream = c->own_stream;
+    for (auto& ev : c->ev)
+        if (hipEventCreate(&ev) != hipSuccess) {
+            g_last_error = "hipEventCreate failed";
+            frac_destroy(c);
+            return nullptr;
+        }
+    return c;
+}
+
+void frac_destroy(frac_ctx* c)
+{
+    if (!c)
+        return;
+    (void)hipSetDevice(c->device);
+    if (c->stream)
+        (void)hipStreamSynchronize(c->stream);
+    c->d_src.release();
+    c->d_tgt.release();
+    c->d_doms.release();
+    c->d_ranges.release();
+    c->d_porig.release();
+    c->d_pool.release();
+    c->d_fb_list.release();
+    c->d_fb_count.release();
+    c->d_negsd2.release();
+    c->d_slot_range.release();
+    c->d_work.release();
+    c->d_rbucket.release();
+    c->d_best_key.release();
+    c->d_out.release();
+    c->d_aux.release();
+    for (auto& ev : c->ev)
+        if (ev)
+            (void)hipEventDestroy(ev);
+    if (c->own_stream)
+        (void)hipStreamDestroy(c->own_stream);
+    delete c;
+}
+
+int frac_set_params(frac_ctx* c, const frac_params* params)
+{
+    if (!c)
+        return FRAC_E_INVALID;
+    std::string msg;
+    if (check_params(params, msg) != FRAC_OK)
+        return c->fail(FRAC_E_INVALID, msg);
+    c->p = *params;
+    c->dirty = true;
+    return FRAC_OK;
+}
+
+static int copy_host_plane(HostPlane& hp, const uint8_t* p, uint32_t w, uint32_t h, uint32_t stride)
+{
+    if (!p || w == 0 || h == 0 || stride < w)
+        return FRAC_E_INVALID;
+    hp.w = w;
+    hp.h = h;
+    hp.data.resize((size_t)w * h);
+    for (uint32_t y = 0; y < h; ++y)
+        std::memcpy(hp.data.data() + (size_t)y * w, p + (size_t)y * stride, w);
+    return FRAC_OK;
+}
+
+int frac_set_planes(frac_ctx* c, const uint8_t* src, uint32_t sw, uint32_t sh, uint32_t sstride, const uint8_t* tgt,
+                    uint32_t tw, uint32_t th, uint32_t tstride)
+{
+    if (!c)
+        return FRAC_E_INVALID;
+    FRAC_HIP(c, hipSetDevice(c->device));
+    if (copy_host_plane(c->src, src, sw, sh, sstride) != FRAC_OK)
+        return c->fail(FRAC_E_INVALID, "invalid source plane");
+    c->same_plane = tgt == nullptr || tgt == src;
+    if (!c->same_plane) {
+        if (copy_host_plane(c->tgt, tgt, tw, th, tstride) != FRAC_OK)
+            return c->fail(FRAC_E_INVALID, "invalid target plane");
+    } else {
+        c->tgt = c->src;
+    }
+    FRAC_TRY(upload_plane(c, c->src, c->d_src, c->d_sstride));
+    if (!c->same_plane)
+        FRAC_TRY(upload_plane(c, c->tgt, c->d_tgt, c->d_tstride));
+    c->planes_set = true;
+    c->dirty = true;
+    return FRAC_OK;
+}
+
+int frac_set_frame(frac_ctx* c, const uint8_t* plane, uint32_t w, uint32_t h, uint32_t stride)
+{
+    return frac_set_planes(c, plane, w, h, stride, nullptr, 0, 0, 0);
+}
+
+int frac_set_frame_device(frac_ctx* c, const void* d_plane, uint32_t w, uint32_t h, uint32_t stride)
+{
+    if (!c)
+        return FRAC_E_INVALID;
+    if (!d_plane || w == 0 || h == 0 || stride < w)
+        return c->fail(FRAC_E_INVALID, "invalid device plane");
+    FRAC_HIP(c, hipSetDevice(c->device));
+    // host copy for the classifier's category pre-pass (host-side, as in the reference)
+    c->src.w = w;
+    c->src.h = h;
+    c->src.data.resize((size_t)w * h);
+    FRAC_HIP(c, hipMemcpy2DAsync(c->src.data.data(), w, d_plane, stride, w, h, hipMemcpyDeviceToHost, c->stream));
+    c->d_sstride = (w + 63u) & ~63u;
+    FRAC_HIP(c, c->d_src.ensure((size_t)c->d_sstride * (h + 1)));
+    FRAC_HIP(c, hipMemcpy2DAsync(c->d_src.ptr, c->d_sstride, d_plane, stride, w, h, hipMemcpyDeviceToDevice, c->stream));
+    FRAC_HIP(c, hipStreamSynchronize(c->stream));
+    c->same_plane = true;
+    c->tgt = c->src;
+    c->planes_set = true;
+    c->dirty = true;
+    return FRAC_OK;
+}
+
+int frac_set_domains(frac_ctx* c, const frac_grid_item* d, size_t nd)
+{
+    if (!c)
+        return FRAC_E_INVALID;
+    if (nd && !d)
+        return c->fail(FRAC_E_INVALID, "domains is NULL");
+    c->doms.assign(d, d + nd);
+    c->doms_set = true;
+    c->dirty = true;
+    return FRAC_OK;
+}
+
+int frac_set_ranges(frac_ctx* c, const frac_grid_item* r, size_t nr)
+{
+    if (!c)
+        return FRAC_E_INVALID;
+    if (nr && !r)
+        return c->fail(FRAC_E_INVALID, "ranges is NULL");
+    c->ranges.assign(r, r + nr);
+    c->ranges_set = true;
+    c->dirty = true;
+    c->ran = false;
+    return FRAC_OK;
+}
+
+int frac_run(frac_ctx* c)
+{
+    if (!c)
+        return FRAC_E_INVALID;
+    FRAC_HIP(c, hipSetDevice(c->device));
+    if (c->dirty)
+        FRAC_TRY(prepare(c));
+    int rc;
+    switch (c->n) {
+    case 2: rc = launch_all<2>(c); break;
+    case 4: rc = launch_all<4>(c); break;
+    case 16: rc = launch_all<16>(c); break;
+    default: rc = launch_all<8>(c); break;
+    }
+    if (rc == FRAC_OK)
+        c->ran = true;
+    return rc;
+}
+
+int frac_sync(frac_ctx* c)
+{
+    if (!c)
+        return FRAC_E_INVALID;
+    FRAC_HIP(c, hipStreamSynchronize(c->stream));
+    return FRAC_OK;
+}
+
+int frac_fetch(frac_ctx* c, frac_encode_item* out, frac_stats* stats)
+{
+    if (!c)
+        return FRAC_E_INVALID;
+    if (!c->ran)
+        return c->fail(FRAC_E_STATE, "frac_fetch before frac_run");
+    const size_t nr = c->ranges.size();
+    if (nr && out)
+        FRAC_HIP(c, hipMemcpyAsync(out, c->d_out.ptr, nr * sizeof(frac_encode_item), hipMemcpyDeviceToHost, c->stream));
+    if (nr)
+        FRAC_HIP(c, hipMemcpyAsync(c->h_aux.data(), c->d_aux.ptr, nr * sizeof(RangeAux), hipMemcpyDeviceToHost,
+                                   c->stream));
+    FRAC_HIP(c, hipStreamSynchronize(c->stream));
+    if (stats) {
+        std::memset(stats, 0, sizeof(*stats));
+        stats->total_mappings = (uint64_t)c->doms.size() * nr;
+        stats->engine = c->engine_ran;
+        const uint64_t nd = c->doms.size();
+        for (size_t r = 0; r < nr; ++r) {
+            const RangeAux& ax = c->h_aux[r];
+            const int b = c->range_bucket[r];
+            const uint64_t bsize = c->bucket_end[b] - c->bucket_begin[b];
+            if (ax.flags & kAuxEmpty) {
+                ++stats->empty_ranges;
+                if (c->p.use_classifier)
+                    stats->rejected_mappings += nd;
+                continue;
+            }
+            if (ax.flags & kAuxFallback)
+                ++stats->fallback_ranges;
+            if (ax.flags & kAuxHit) {
+                ++stats->hit_ranges;
+                if (c->p.use_classifier)
+                    stats->rejected_mappings += (uint64_t)c->porig[ax.pos] - (ax.pos - c->bucket_begin[b]);
+            } else if (c->p.use_classifier) {
+                stats->rejected_mappings += nd - bsize;
+            }
+        }
+        if (c->p.flags & FRAC_FLAG_TIMING) {
+            float ms = 0.f;
+            if (hipEventElapsedTime(&ms, c->ev[0], c->ev[3]) == hipSuccess)
+                stats->ms_device = ms;
+            if (hipEventElapsedTime(&ms, c->ev[0], c->ev[1]) == hipSuccess)
+                stats->ms_prep = ms;
+            if (hipEventElapsedTime(&ms, c->ev[1], c->ev[2]) == hipSuccess)
+                stats->ms_search = ms;
+            if (hipEventElapsedTime(&ms, c->ev[2], c->ev[3]) == hipSuccess)
+                stats->ms_finish = ms;
+        }
+    }
+    return FRAC_OK;
+}
+
+int frac_search(frac_ctx* c, const frac_grid_item* ranges, size_t nr, frac_encode_item* out, frac_stats* stats)
+{
+    FRAC_TRY(frac_set_ranges(c, ranges, nr));
+    FRAC_TRY(frac_run(c));
+    return frac_fetch(c, out, stats);
+}
+
+int frac_set_stream(frac_ctx* c, void* s)
+{
+    if (!c)
+        return FRAC_E_INVALID;
+    c->stream = s ? reinterpret_cast<hipStream_t>(s) : c->own_stream;
+    return FRAC_OK;
+}
+
+void* frac_get_stream(frac_ctx* c) { return c ? reinterpret_cast<void*>(c->stream) : nullptr; }
+
+const frac_encode_item* frac_device_results(frac_ctx* c) { return c ? c->d_out.ptr : nullptr; }
+
+int frac_copy_results_device(frac_ctx* c, void* d_dst)
+{
+    if (!c)
+        return FRAC_E_INVALID;
+    if (!c->ran)
+        return c->fail(FRAC_E_STATE, "no results: frac_run has not been called");
+    const size_t nr = c->ranges.size();
+    if (nr)
+        FRAC_HIP(c, hipMemcpyAsync(d_dst, c->d_out.ptr, nr * sizeof(frac_encode_item), hipMemcpyDeviceToDevice,
+                                   c->stream));
+    return FRAC_OK;
+}
+
+size_t frac_uniform_grid(uint32_t W, uint32_t H, uint32_t size, uint32_t offset, frac_grid_item* out, size_t cap)
+{
+    if (size == 0 || offset == 0 || W < size || H < size)
+        return 0;
+    size_t n = 0;
+    uint32_t x = 0, y = 0;
+    for (;;) {
+        if (out && n < cap)
+            out[n] = frac_grid_item{x, y, size, size, -1};
+        ++n;
+        x += offset;
+        if (x + size > W) {
+            x = 0;
+            y += offset;
+            if (y + size > H)
+                break;
+        }
+    }
+    return n;
+}
+
+int frac_classify(const uint8_t* plane, uint32_t w, uint32_t h, uint32_t stride, frac_grid_item* items, size_t n)
+{
+    HostPlane hp;
+    if (copy_host_plane(hp, plane, w, h, stride) != FRAC_OK || (n && !items)) {
+        g_last_error = "frac_classify: invalid arguments";
+        return FRAC_E_INVALID;
+    }
+    for (size_t i = 0; i < n; ++i) {
+        if ((uint64_t)items[i].x + items[i].w > w || (uint64_t)items[i].y + items[i].h > h) {
+            g_last_error = "frac_classify: item outside the plane";
+            return FRAC_E_INVALID;
+        }
+        items[i].category = category(hp, items[i]);
+    }
+    return FRAC_OK;
+}
+
+int frac_transform_index(uint32_t n, uint32_t t, uint32_t pix)
+{
+    if (t > 7 || pix >= n * n)
+        return -1;
+    switch (n) {
+    case 2: return fwd_index<2>((int)t, (int)pix);
+    case 4: return fwd_index<4>((int)t, (int)pix);
+    case 8: return fwd_index<8>((int)t, (int)pix);
+    case 16: return fwd_index<16>((int)t, (int)pix);
+    default: return -1;
+    }
+}
+
+int64_t frac_hit_limit(double rms_threshold, uint32_t n) { return compute_hit_limit(rms_threshold, 4u * n * n); }
+
+} // extern "C"

@@ -1,0 +1,95 @@
+// fracenc_common.h — shared device/host definitions of the MI355X search engine.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/fracenc.h"
+
+namespace fracenc {
+
+typedef unsigned short ushort2_t __attribute__((ext_vector_type(2)));
+
+// Dihedral transforms as the reference's 2×4 affine LUT (image/transform.h:32-41):
+//   x' = a0·x + a1·y + a2·(sx−1) + a3·(sy−1),  y' = a4·x + a5·y + a6·(sx−1) + a7·(sy−1)
+struct Aff {
+    int a0, a1, a2, a3, a4, a5, a6, a7;
+};
+
+__host__ __device__ constexpr Aff lut(int t)
+{
+    switch (t) {
+    case 0: return {1, 0, 0, 0, 0, 1, 0, 0};    // Id
+    case 1: return {0, 1, 0, 0, -1, 0, 1, 0};   // Rotate_90
+    case 2: return {-1, 0, 1, 0, 0, -1, 0, 1};  // Rotate_180
+    case 3: return {0, -1, 0, 1, 1, 0, 0, 0};   // Rotate_270
+    case 4: return {1, 0, 0, 0, 0, -1, 0, 1};   // Flip
+    case 5: return {0, 1, 0, 0, 1, 0, 0, 0};    // Flip_Rotate_90
+    case 6: return {-1, 0, 1, 0, 0, 1, 0, 0};   // Flip_Rotate_180
+    default: return {0, -1, 0, 1, -1, 0, 1, 0}; // Flip_Rotate_270
+    }
+}
+
+// Ratio-2 decimate-then-permute (verified there for n = 4, 8, 16):
+// SamplerBilinear::sample (image/sampler.h:21-38) of range pixel (x, y) under t reads the
+// 2×2 block of the domain whose decimated index is D4[by][bx] with
+//   bx = a0·x + a1·y + (a2 + a3)·(n−1),  by = a4·x + a5·y + (a6 + a7)·(n−1).
+// fwd(t, pix) = by·n + bx  for pix = y·n + x.
+template <int N>
+__host__ __device__ constexpr int fwd_index(int t, int pix)
+{
+    const Aff a = lut(t);
+    const int x = pix % N, y = pix / N;
+    const int bx = a.a0 * x + a.a1 * y + (a.a2 + a.a3) * (N - 1);
+    const int by = a.a4 * x + a.a5 * y + (a.a6 + a.a7) * (N - 1);
+    return by * N + bx;
+}
+
+// Inverse permutation: the range pixel that meets decimated domain cell q under t.
+// The linear part is a signed permutation matrix M, so M^-1 = M^T.
+template <int N>
+__host__ __device__ constexpr int inv_index(int t, int q)
+{
+    const Aff a = lut(t);
+    const int qx = q % N, qy = q / N;
+    const int dx = qx - (a.a2 + a.a3) * (N - 1);
+    const int dy = qy - (a.a6 + a.a7) * (N - 1);
+    const int px = a.a0 * dx + a.a4 * dy;
+    const int py = a.a1 * dx + a.a5 * dy;
+    return py * N + px;
+}
+
+// Selection key of one (range, domain) candidate, reduced by a u64 atomicMin:
+//   hit  (S16 <= H):  (0 << 63) | pool_position
+//   miss:             (1 << 63) | (S16 << 32) | pool_position
+// Pool positions preserve the reference's domain order inside a classifier bucket,
+// so min(key) = "first hit, else least error, ties to the earliest domain"
+// (encode/TransformEstimator2.hpp:34-41).  The transform is re-derived for the winner.
+constexpr unsigned long long kKeyNone = ~0ull;
+constexpr unsigned long long kKeyMiss = 1ull << 63;
+
+// S16 = Σ(4r − D4)² is the reference's fp32 error ×16 (image/metrics.h:37-50);
+// the fp32 sum is exact iff S16 < 2^24.
+constexpr int64_t kExactLimit = 1ll << 24;
+
+enum AuxFlags : uint32_t { kAuxHit = 1u, kAuxFallback = 2u, kAuxEmpty = 4u };
+
+struct RangeAux {
+    uint32_t pos;   // winning pool position
+    uint32_t flags; // AuxFlags
+};
+
+struct SearchArgs {
+    const uint8_t* tgt;
+    uint32_t tstride;
+    const frac_grid_item* ranges;
+    const int32_t* slot_range; // range index per range slot (−1 = padding)
+    const uint32_t* pool;      // [P][n²/2] packed u16 pairs of D4
+    const int32_t* negsd2;     // [P] −ΣD4²
+    const uint4* work;         // per wave: {slot_base, p_begin, p_end, group}
+    uint32_t nwork;
+    int32_t hitH;              // S16 threshold of a hit (≥ 0), see host compute_hit_limit
+    unsigned long long* best_key; // [nr]
+};
+
+} // namespace fracenc

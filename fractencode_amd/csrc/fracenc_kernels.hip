@@ -1,0 +1,493 @@
+// fracenc_kernels.hip — HIP/CDNA4 (gfx950) kernels of the range×domain search.
+//
+// Pipeline per frame:
+//   pool_build      domain → decimated 2×2-sum vector D4 (n² u16, packed pairs) + −ΣD4²
+//   search_valu     per (range, transform group, domain slice): exact integer error of every
+//                   candidate with v_dot2_u32_u16 (range copies in VGPRs, domain vector
+//                   broadcast from SGPRs), u64 atomicMin of the selection key per range
+//   fit_winner      per range: re-derive the transform of the winning domain, the reference's
+//                   least-squares contrast/brightness (FP64) and its fp32 error
+//   fallback_fp32   ranges whose best error leaves the exact fp32 regime: sequential fp32
+//                   emulation of image/metrics.h over all candidates
+#include "fracenc_common.h"
+
+namespace fracenc {
+
+__device__ inline int wave_sum_i(int v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1)
+        v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+__device__ inline long long wave_sum_ll(long long v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1)
+        v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// ---------------------------------------------------------------------------
+// pool_build: one wave per domain pool position p (bucket order).  D4[i][j] is the
+// 2×2 sum at domain pixel (2j, 2i): SamplerBilinear::sample's integer sum
+// (image/sampler.h:21-38) for the identity transform at range pixel (j, i).
+// ---------------------------------------------------------------------------
+template <int N>
+__global__ void __launch_bounds__(256) pool_build(const uint8_t* __restrict__ src, uint32_t sstride,
+                                                  const frac_grid_item* __restrict__ doms,
+                                                  const uint32_t* __restrict__ porig, uint32_t P,
+                                                  uint32_t* __restrict__ pool, int32_t* __restrict__ negsd2)
+{
+    constexpr int NN = N * N, K2 = NN / 2;
+    const uint32_t p = blockIdx.x * 4u + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (p >= P)
+        return;
+    const frac_grid_item d = doms[porig[p]];
+    int sq = 0;
+    for (int q0 = 0; q0 < NN; q0 += 128) {
+        const int q = q0 + 2 * lane;
+        uint32_t packed = 0;
+        if (q < NN) {
+            int v[2];
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                const int qi = q + e;
+                const uint32_t x = d.x + 2u * (qi % N), y = d.y + 2u * (qi / N);
+                const uint8_t* r0 = src + (size_t)y * sstride + x;
+                v[e] = (int)r0[0] + (int)r0[1] + (int)r0[sstride] + (int)r0[sstride + 1];
+                sq += v[e] * v[e];
+            }
+            packed = (uint32_t)v[0] | ((uint32_t)v[1] << 16);
+            pool[(size_t)p * K2 + (q >> 1)] = packed;
+        }
+    }
+    sq = wave_sum_i(sq);
+    if (lane == 0)
+        negsd2[p] = -sq;
+}
+
+// ---------------------------------------------------------------------------
+// search_valu<N, G, HITS>
+//
+// One wave = 64 ranges (one per lane, same classifier bucket) × one transform group
+// (G transforms) × one slice [p_begin, p_end) of the bucket's domain pool.
+// Lane state: G inverse-permuted copies of its range as packed u16 pairs (G·n²/2
+// VGPRs), so that X_t = Σ_q copy_t[q]·D4[q] is one dot product against the
+// UNPERMUTED domain vector, which is wave-uniform and therefore lives in SGPRs
+// (s_load_dwordx16) and feeds v_dot2_u32_u16's scalar operand.
+// Per candidate: w = 8·X − ΣD4² = C_r − S16 with C_r = 16Σr² (exact int32);
+// the max over the group's transforms is kept per lane with strict '>' across
+// domains (earliest domain wins ties), hits (S16 <= H) saturate to INT_MAX.
+// ---------------------------------------------------------------------------
+// Packs range pixels i0, i1 (bytes of the packed pixel dwords) as the u16 pair
+// (i0 | i1 << 16) with one v_perm_b32: selectors 4..7 pick bytes of src0,
+// 0..3 bytes of src1, 0x0c yields zero.
+template <int N>
+__device__ inline uint32_t pix_pair(const uint32_t (&pk)[(N * N + 3) / 4], int i0, int i1)
+{
+    const uint32_t sel = (uint32_t)(4 + (i0 & 3)) | (0x0cu << 8) | ((uint32_t)(i1 & 3) << 16) | (0x0cu << 24);
+    return __builtin_amdgcn_perm(pk[i0 >> 2], pk[i1 >> 2], sel);
+}
+
+// Loads an N×N u8 block, four pixels per dword in row-major order.  Rows are read
+// as aligned dwords and realigned with v_alignbyte_b32 (any x), which keeps only a
+// few loads in flight per row; the device plane has a slack row, so reading up to
+// 4 bytes past a row end stays in bounds.
+template <int N>
+__device__ inline void load_range_packed(const uint8_t* __restrict__ plane, uint32_t stride, uint32_t x, uint32_t y,
+                                         uint32_t (&pk)[(N * N + 3) / 4])
+{
+    if constexpr (N < 4) {
+        uint32_t w = 0;
+#pragma unroll
+        for (int q = 0; q < N * N; ++q)
+            w |= (uint32_t)plane[(size_t)(y + q / N) * stride + x + (q % N)] << (8 * q);
+        pk[0] = w;
+    } else {
+        constexpr int W = N / 4; // dwords per row
+#pragma unroll
+        for (int r = 0; r < N; ++r) {
+            const uintptr_t addr = (uintptr_t)(plane + (size_t)(y + r) * stride + x);
+            const uint32_t* base = (const uint32_t*)(addr & ~(uintptr_t)3);
+            const uint32_t sh = (uint32_t)(addr & 3);
+            uint32_t w[W + 1];
+#pragma unroll
+            for (int i = 0; i <= W; ++i)
+                w[i] = base[i];
+#pragma unroll
+            for (int i = 0; i < W; ++i)
+                pk[r * W + i] = __builtin_amdgcn_alignbyte(w[i + 1], w[i], sh * 8u);
+        }
+    }
+}
+
+template <int N, int G, int GROUP>
+__device__ inline void build_copies(const uint32_t (&pk)[(N * N + 3) / 4], uint32_t (&cp)[G][N * N / 2])
+{
+#pragma unroll
+    for (int j = 0; j < G; ++j) {
+#pragma unroll
+        for (int k = 0; k < N * N / 2; ++k) {
+            const int t = GROUP * G + j;
+            cp[j][k] = pix_pair<N>(pk, inv_index<N>(t, 2 * k), inv_index<N>(t, 2 * k + 1));
+        }
+    }
+}
+
+template <int N, int G, bool HITS>
+__global__ void __launch_bounds__(256) search_valu(SearchArgs a)
+{
+    constexpr int NN = N * N, K2 = NN / 2;
+    constexpr int KC = K2 < 32 ? K2 : 32; // dwords of the domain vector held in SGPRs at once
+    const uint32_t wid = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
+    if (wid >= a.nwork)
+        return;
+    const uint4 wk = a.work[wid];
+    const uint32_t lane = threadIdx.x & 63u;
+    const int ri = a.slot_range[wk.x + lane];
+    const bool live = ri >= 0;
+    const frac_grid_item rg = a.ranges[live ? ri : a.slot_range[wk.x]];
+
+    // range pixels, four per dword (keeps the copy-building phase inside the
+    // register budget of the main loop)
+    uint32_t pix[(NN + 3) / 4];
+    load_range_packed<N>(a.tgt, a.tstride, rg.x, rg.y, pix);
+    int sum2 = 0;
+#pragma unroll
+    for (int q = 0; q < NN; ++q) {
+        const int v = (int)((pix[q >> 2] >> (8 * (q & 3))) & 0xffu);
+        sum2 += v * v;
+    }
+    const int Cr = 16 * sum2; // 16Σr² ≤ 2^28 for n ≤ 16
+    const int hitlevel = Cr - a.hitH;
+
+    uint32_t cp[G][K2];
+    switch (wk.w) {
+    case 0: build_copies<N, G, 0>(pix, cp); break;
+    case 1: build_copies<N, G, 1>(pix, cp); break;
+    case 2: if constexpr (G <= 2) build_copies<N, G, 2>(pix, cp); break;
+    case 3: if constexpr (G <= 2) build_copies<N, G, 3>(pix, cp); break;
+    case 4: if constexpr (G == 1) build_copies<N, G, 4>(pix, cp); break;
+    case 5: if constexpr (G == 1) build_copies<N, G, 5>(pix, cp); break;
+    case 6: if constexpr (G == 1) build_copies<N, G, 6>(pix, cp); break;
+    default: if constexpr (G == 1) build_copies<N, G, 7>(pix, cp); break;
+    }
+
+    int best = INT_MIN;
+    uint32_t bestp = 0;
+    const uint32_t pe = wk.z;
+    for (uint32_t p = wk.y; p < pe; ++p) {
+        const uint32_t* __restrict__ dp = a.pool + (size_t)p * K2;
+        uint32_t acc[G];
+#pragma unroll
+        for (int j = 0; j < G; ++j)
+            acc[j] = 0;
+#pragma unroll
+        for (int kc = 0; kc < K2; kc += KC) {
+            uint32_t dv[KC];
+#pragma unroll
+            for (int k = 0; k < KC; ++k)
+                dv[k] = dp[kc + k];
+#pragma unroll
+            for (int j = 0; j < G; ++j)
+#pragma unroll
+                for (int k = 0; k < KC; ++k)
+                    acc[j] = __builtin_amdgcn_udot2(__builtin_bit_cast(ushort2_t, dv[k]),
+                                                    __builtin_bit_cast(ushort2_t, cp[j][kc + k]), acc[j], false);
+        }
+        const int ns = a.negsd2[p];
+        int m = INT_MIN;
+#pragma unroll
+        for (int j = 0; j < G; ++j)
+            m = max(m, (int)((acc[j] << 3) + (uint32_t)ns));
+        if constexpr (HITS)
+            m = m >= hitlevel ? INT_MAX : m;
+        if (m > best) {
+            best = m;
+            bestp = p;
+        }
+        if constexpr (HITS) {
+            if (__all(best == INT_MAX))
+                break;
+        }
+    }
+    if (live && best != INT_MIN) {
+        unsigned long long key;
+        if (HITS && best == INT_MAX)
+            key = (unsigned long long)bestp;
+        else
+            key = kKeyMiss | ((unsigned long long)(uint32_t)(Cr - best) << 32) | (unsigned long long)bestp;
+        atomicMin(&a.best_key[ri], key);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// fit_winner<N>: one wave per range.  Re-derives the winner's transform from the
+// integer errors of its domain, then TransformMatcher::match_generic's fit
+// (encode/transformmatcher.h:89-108).  All of ΣA, ΣA², ΣB = ΣD4/4, ΣAB = X/4
+// are exact in FP64, so s is bit-exact in any summation order; o uses the
+// reference's FMA-contracted form.  Distance = (S16/16)/(domain area), the
+// reference's fp32 sum (exact here) divided in FP64 (image/metrics.h:49).
+// ---------------------------------------------------------------------------
+struct FitArgs {
+    const uint8_t* tgt;
+    uint32_t tstride;
+    const frac_grid_item* ranges;
+    const frac_grid_item* doms;
+    const uint32_t* porig;
+    const uint32_t* pool;
+    const unsigned long long* best_key;
+    uint32_t nr;
+    uint32_t T;
+    int64_t hitH;
+    double smax;
+    int all_fallback;
+    frac_encode_item* out;
+    RangeAux* aux;
+    uint32_t* fb_count;
+    uint32_t* fb_list;
+};
+
+__device__ inline void write_fit(frac_encode_item& o, const frac_grid_item& rg, const frac_grid_item& d, int t,
+                                 double sumA, double sumA2, double sumB, double sumAB, double N, double smax,
+                                 double dist)
+{
+    const double tmp = (N * sumA2 - (sumA - 1) * sumA);
+    double s = fabs(tmp) < 0.00001 ? 0.0 : (N * sumAB - sumA * sumB) / tmp;
+    if (smax > 0.0)
+        s = s > smax ? smax : (s < -smax ? -smax : s);
+    const double br = __fma_rn(-s, sumA, sumB) / N;
+    o.x = rg.x;
+    o.y = rg.y;
+    o.w = rg.w;
+    o.h = rg.h;
+    o.match.score.distance = dist;
+    o.match.score.contrast = s;
+    o.match.score.brightness = br;
+    o.match.score.transform = t;
+    o.match.score._pad = 0;
+    o.match.x = d.x;
+    o.match.y = d.y;
+    o.match.sw = d.w;
+    o.match.sh = d.h;
+}
+
+__device__ inline void write_default(frac_encode_item& o, const frac_grid_item& rg)
+{
+    // item_match_t{} defaults (encode/datatypes.h:8-19): distance 1e5, s = o = 0, Id, (0,0), size (0,0)
+    o.x = rg.x;
+    o.y = rg.y;
+    o.w = rg.w;
+    o.h = rg.h;
+    o.match.score.distance = 100000.0;
+    o.match.score.contrast = 0.0;
+    o.match.score.brightness = 0.0;
+    o.match.score.transform = 0;
+    o.match.score._pad = 0;
+    o.match.x = 0;
+    o.match.y = 0;
+    o.match.sw = 0;
+    o.match.sh = 0;
+}
+
+template <int N>
+__global__ void __launch_bounds__(256) fit_winner(FitArgs a)
+{
+    constexpr int NN = N * N;
+    const uint32_t r = blockIdx.x * 4u + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (r >= a.nr)
+        return;
+    const frac_grid_item rg = a.ranges[r];
+    const unsigned long long key = a.best_key[r];
+    if (key == kKeyNone) {
+        if (lane == 0) {
+            write_default(a.out[r], rg);
+            a.aux[r] = RangeAux{0u, (uint32_t)kAuxEmpty};
+        }
+        return;
+    }
+    const uint32_t p = (uint32_t)(key & 0xffffffffull);
+    const bool hit = (key >> 63) == 0;
+    const frac_grid_item d = a.doms[a.porig[p]];
+    const uint32_t* dp = a.pool + (size_t)p * (NN / 2);
+
+    long long sA = 0, sA2 = 0, sD = 0, sD2 = 0;
+    long long X[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int q = lane; q < NN; q += 64) {
+        const int rv = a.tgt[(size_t)(rg.y + q / N) * a.tstride + rg.x + (q % N)];
+        const uint32_t dw = dp[q >> 1];
+        const int dv = (q & 1) ? (int)(dw >> 16) : (int)(dw & 0xffffu);
+        sA += rv;
+        sA2 += rv * rv;
+        sD += dv;
+        sD2 += dv * dv;
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            if (t < (int)a.T) {
+                // range pixel q meets D4[fwd(t, q)]
+                const int f = fwd_index<N>(t, q);
+                const uint32_t fw = dp[f >> 1];
+                const int fv = (f & 1) ? (int)(fw >> 16) : (int)(fw & 0xffffu);
+                X[t] += (long long)rv * fv;
+            }
+        }
+    }
+    sA = wave_sum_ll(sA);
+    sA2 = wave_sum_ll(sA2);
+    sD = wave_sum_ll(sD);
+    sD2 = wave_sum_ll(sD2);
+#pragma unroll
+    for (int t = 0; t < 8; ++t)
+        X[t] = wave_sum_ll(X[t]);
+    if (lane != 0)
+        return;
+    long long S16[8];
+    long long minS = LLONG_MAX;
+    int tsel = -1;
+    for (int t = 0; t < (int)a.T; ++t) {
+        S16[t] = 16 * sA2 - 8 * X[t] + sD2;
+        if (S16[t] < minS)
+            minS = S16[t];
+    }
+    if (hit) {
+        for (int t = 0; t < (int)a.T; ++t)
+            if (S16[t] <= a.hitH) {
+                tsel = t;
+                break;
+            }
+    } else {
+        for (int t = 0; t < (int)a.T; ++t)
+            if (S16[t] == minS)
+                tsel = t; // later transform wins ties (transformmatcher.h:57,67 use <=)
+    }
+    uint32_t flags = hit ? (uint32_t)kAuxHit : 0u;
+    if (a.all_fallback || (!hit && minS >= kExactLimit)) {
+        flags |= kAuxFallback;
+        const uint32_t idx = atomicAdd(a.fb_count, 1u);
+        a.fb_list[idx] = r;
+    }
+    const double Nd = (double)NN;
+    const double area = (double)(d.w * d.h);
+    const double dist = ((double)S16[tsel] * 0.0625) / area;
+    write_fit(a.out[r], rg, d, tsel, (double)sA, (double)sA2, (double)sD * 0.25, (double)X[tsel] * 0.25, Nd, a.smax,
+              dist);
+    a.aux[r] = RangeAux{p, flags};
+}
+
+// ---------------------------------------------------------------------------
+// fallback_fp32<N>: one block per flagged range (grid-stride over the list).
+// Evaluates every candidate of the range's bucket with the reference's exact
+// arithmetic: fp32 sum over range pixels in row-major order of
+// (float(r) − float(2×2 sum)/4)² (image/metrics.h:37-50).  Selection key:
+//   hit  (dist <= thr): (pos_local << 3) | t
+//   miss:               (1 << 63) | (F_bits << 27) | (pos_local << 3) | (T−1−t)
+// ---------------------------------------------------------------------------
+struct FallbackArgs {
+    const uint8_t* tgt;
+    uint32_t tstride;
+    const frac_grid_item* ranges;
+    const frac_grid_item* doms;
+    const uint32_t* porig;
+    const uint32_t* pool;
+    const uint2* rbucket; // per range: pool slice [x, y)
+    const uint32_t* fb_count;
+    const uint32_t* fb_list;
+    uint32_t T;
+    double thr;
+    double smax;
+    frac_encode_item* out;
+    RangeAux* aux;
+};
+
+template <int N>
+__global__ void __launch_bounds__(256) fallback_fp32(FallbackArgs a)
+{
+    constexpr int NN = N * N;
+    __shared__ float rpix[NN];
+    __shared__ unsigned long long red[256];
+    const uint32_t count = *a.fb_count;
+    for (uint32_t e = blockIdx.x; e < count; e += gridDim.x) {
+        const uint32_t r = a.fb_list[e];
+        const frac_grid_item rg = a.ranges[r];
+        const uint2 bk = a.rbucket[r];
+        __syncthreads();
+        for (int q = threadIdx.x; q < NN; q += blockDim.x)
+            rpix[q] = (float)(int16_t)a.tgt[(size_t)(rg.y + q / N) * a.tstride + rg.x + (q % N)];
+        __syncthreads();
+        unsigned long long best = kKeyNone;
+        const uint32_t ncand = (bk.y - bk.x) * a.T;
+        for (uint32_t c = threadIdx.x; c < ncand; c += blockDim.x) {
+            const uint32_t pl = c / a.T;
+            const int t = (int)(c % a.T);
+            const uint32_t* dp = a.pool + (size_t)(bk.x + pl) * (NN / 2);
+            float F = 0.0f;
+            for (int q = 0; q < NN; ++q) {
+                const int f = fwd_index<N>(t, q);
+                const uint32_t fw = dp[f >> 1];
+                const float smp = (float)((f & 1) ? (fw >> 16) : (fw & 0xffffu)) / 4.0f;
+                const float val = __fsub_rn(rpix[q], smp);
+                F = __fadd_rn(F, __fmul_rn(val, val));
+            }
+            const double dist = (double)F / (double)(4 * NN);
+            unsigned long long key;
+            if (dist <= a.thr)
+                key = ((unsigned long long)pl << 3) | (unsigned long long)t;
+            else
+                key = kKeyMiss | ((unsigned long long)__float_as_uint(F) << 27) | ((unsigned long long)pl << 3) |
+                      (unsigned long long)(a.T - 1 - t);
+            best = key < best ? key : best;
+        }
+        red[threadIdx.x] = best;
+        __syncthreads();
+        for (int s = blockDim.x / 2; s > 0; s >>= 1) {
+            if ((int)threadIdx.x < s) {
+                const unsigned long long o = red[threadIdx.x + s];
+                if (o < red[threadIdx.x])
+                    red[threadIdx.x] = o;
+            }
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) {
+            const unsigned long long k = red[0];
+            if (k != kKeyNone) {
+                const bool hit = (k >> 63) == 0;
+                const uint32_t pl = (uint32_t)((k >> 3) & 0xffffffu);
+                const int t = hit ? (int)(k & 7u) : (int)(a.T - 1 - (uint32_t)(k & 7u));
+                const float F = hit ? 0.0f : __uint_as_float((uint32_t)((k >> 27) & 0xffffffffull));
+                const uint32_t p = bk.x + pl;
+                const frac_grid_item d = a.doms[a.porig[p]];
+                const uint32_t* dp = a.pool + (size_t)p * (NN / 2);
+                long long sA = 0, sA2 = 0, sD = 0, X = 0;
+                float Fh = 0.0f;
+                for (int q = 0; q < NN; ++q) {
+                    const int rv = (int)rpix[q];
+                    const uint32_t dw = dp[q >> 1];
+                    const int dv = (q & 1) ? (int)(dw >> 16) : (int)(dw & 0xffffu);
+                    const int f = fwd_index<N>(t, q);
+                    const uint32_t fw = dp[f >> 1];
+                    const int fv = (f & 1) ? (int)(fw >> 16) : (int)(fw & 0xffffu);
+                    sA += rv;
+                    sA2 += rv * rv;
+                    sD += dv;
+                    X += (long long)rv * fv;
+                    const float val = __fsub_rn(rpix[q], (float)fv / 4.0f);
+                    Fh = __fadd_rn(Fh, __fmul_rn(val, val));
+                }
+                (void)F;
+                const double dist = (double)Fh / (double)(d.w * d.h);
+                write_fit(a.out[r], rg, d, t, (double)sA, (double)sA2, (double)sD * 0.25, (double)X * 0.25,
+                          (double)NN, a.smax, dist);
+                a.aux[r] = RangeAux{p, (uint32_t)(kAuxFallback | (hit ? kAuxHit : 0u))};
+            } else {
+                write_default(a.out[r], rg);
+                a.aux[r] = RangeAux{0u, (uint32_t)kAuxEmpty};
+            }
+        }
+    }
+}
+
+} // namespace fracenc

@@ -1,0 +1,165 @@
+/*
+ * fracenc.h — C ABI of the MI355X-native range×domain search engine.
+ *
+ * This is the drop-in boundary for the reference's hot path
+ *   Frac2::AbstractEncodingEngine2 / CpuEncodingEngine2 → TransformEstimator2::estimate
+ *   → TransformMatcher::match (sebsgit/fractencode encode/EncodingEngine2.hpp:50-112,
+ *   encode/TransformEstimator2.hpp:29-48, encode/transformmatcher.h:38-111).
+ * A caller owns the planes and grids; a context owns every device buffer.
+ * No torch or HIP types cross this boundary: plain pointers, sizes and status ints.
+ *
+ * Semantics (identical to the reference on the same inputs):
+ *  - domains are visited in the order given (the reference's createUniformGrid
+ *    order), ties in distance go to the earliest domain and, inside a domain,
+ *    to the later transform; the first candidate with distance <= rms_threshold
+ *    wins (early exit); distance is the reference's unfitted fp32 error;
+ *  - contrast / brightness follow TransformMatcher::match_generic bit-for-bit;
+ *  - results are returned in the order the ranges were given.
+ * All entry points return 0 on success and a negative FRAC_E* code on error;
+ * frac_last_error() gives the message.  Not thread-safe per context.
+ */
+#ifndef FRACENC_H
+#define FRACENC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FRAC_ABI_VERSION 1
+
+/* error codes */
+#define FRAC_OK 0
+#define FRAC_E_INVALID (-1)     /* bad argument / geometry the engine does not support   */
+#define FRAC_E_DEVICE (-2)      /* HIP runtime error                                     */
+#define FRAC_E_STATE (-3)       /* call order (e.g. run before planes/grids are set)     */
+#define FRAC_E_NOMEM (-4)       /* device or host allocation failed                      */
+
+/* engines (frac_params.engine) */
+#define FRAC_ENGINE_AUTO 0      /* fastest engine that supports the geometry             */
+#define FRAC_ENGINE_VALU 1      /* v_dot2_u32_u16 scalar-broadcast search                */
+#define FRAC_ENGINE_MFMA 2      /* f16 MFMA search with an exact integer epilogue        */
+
+/* flags (frac_params.flags) */
+#define FRAC_FLAG_TIMING 1u     /* record per-kernel device time with HIP events         */
+
+/* == Frac2::UniformGridItem (image/partition2.hpp:93-99): GridItemBase{origin, size}
+ *    + GridItemData{bb_classifierBin}; 20 bytes. category -1 = not classified
+ *    (recomputed on the item's own plane, as Classifier2::compare does). */
+typedef struct frac_grid_item {
+    uint32_t x, y, w, h;
+    int32_t category;
+} frac_grid_item;
+
+/* Search parameters; the Frac::encode_parameters_t fields that reach the search
+ * (encode/encode_parameters.h:5-14, encode/Encoder2.hpp:36). */
+typedef struct frac_params {
+    uint32_t transforms;    /* 4 = TransformMatcher::match's Id,R90,R180,R270; 8 = all of image/transform.h */
+    int32_t use_classifier; /* 0 = DummyClassifier, 1 = BrightnessBlocksClassifier2 gating           */
+    double rms_threshold;   /* TransformMatcher rmsThreshold (early-exit distance), default 0.0       */
+    double s_max;           /* TransformMatcher sMax (|contrast| clamp when > 0), default -1.0         */
+    uint32_t engine;        /* FRAC_ENGINE_*                                                           */
+    uint32_t flags;         /* FRAC_FLAG_*                                                             */
+} frac_params;
+
+/* == Frac::transform_score_t (encode/datatypes.h:8-13), 32 bytes */
+typedef struct frac_score {
+    double distance;
+    double contrast;
+    double brightness;
+    int32_t transform; /* Frac::TransformType */
+    int32_t _pad;
+} frac_score;
+
+/* == Frac::item_match_t (encode/datatypes.h:14-19), 48 bytes */
+typedef struct frac_match {
+    frac_score score;
+    uint32_t x, y;   /* winning domain origin */
+    uint32_t sw, sh; /* winning domain size (sourceItemSize); 0,0 when no domain was eligible */
+} frac_match;
+
+/* == Frac::encode_item_t (encode/datatypes.h:20-23), 64 bytes */
+typedef struct frac_encode_item {
+    uint32_t x, y, w, h; /* range */
+    frac_match match;
+} frac_encode_item;
+
+typedef struct frac_stats {
+    uint64_t rejected_mappings; /* == TransformEstimator2::rejectedMappings() for this search   */
+    uint64_t total_mappings;    /* nd * nr (Encoder2::encode_stats_t::totalMappings)              */
+    uint32_t hit_ranges;        /* ranges decided by the rms threshold                           */
+    uint32_t fallback_ranges;   /* ranges re-run in fp32 emulation (min error >= 2^24/16)        */
+    uint32_t empty_ranges;      /* ranges with no eligible domain (default record)               */
+    uint32_t engine;            /* engine that ran                                               */
+    double ms_device;           /* device time of the last run (FRAC_FLAG_TIMING), else 0        */
+    double ms_search;           /* device time of the search kernel alone                        */
+    double ms_prep;             /* domain pool / operand build                                   */
+    double ms_finish;           /* winner fit + fallback                                         */
+} frac_stats;
+
+typedef struct frac_ctx frac_ctx;
+
+int frac_abi_version(void);
+/* NULL on failure (message via frac_last_error(NULL)). */
+frac_ctx* frac_create(int device, const frac_params* params);
+void frac_destroy(frac_ctx* ctx);
+const char* frac_last_error(const frac_ctx* ctx);
+int frac_set_params(frac_ctx* ctx, const frac_params* params);
+
+/* Planes are uint8, row-major with the given stride (bytes). Copied to the device.
+ * frac_set_frame: source == target (what Encoder2 does, encode/Encoder2.hpp:36).
+ * frac_set_planes: distinct source (domain) and target (range) planes, as
+ * TransformEstimator2's constructor allows (encode/TransformEstimator2.hpp:15-21). */
+int frac_set_frame(frac_ctx* ctx, const uint8_t* plane, uint32_t w, uint32_t h, uint32_t stride);
+int frac_set_planes(frac_ctx* ctx, const uint8_t* src, uint32_t sw, uint32_t sh, uint32_t sstride,
+                    const uint8_t* tgt, uint32_t tw, uint32_t th, uint32_t tstride);
+/* Planes already in device memory (e.g. a torch tensor in HBM): copied device-to-device. */
+int frac_set_frame_device(frac_ctx* ctx, const void* d_plane, uint32_t w, uint32_t h, uint32_t stride);
+
+/* The domain pool (TransformEstimator2's sourceGrid) and the range list. */
+int frac_set_domains(frac_ctx* ctx, const frac_grid_item* domains, size_t nd);
+int frac_set_ranges(frac_ctx* ctx, const frac_grid_item* ranges, size_t nr);
+
+/* Launch the whole search for the current planes/grids on the context's stream
+ * (asynchronous).  frac_fetch waits for it and copies results/stats to the host. */
+int frac_run(frac_ctx* ctx);
+int frac_fetch(frac_ctx* ctx, frac_encode_item* out, frac_stats* stats);
+int frac_sync(frac_ctx* ctx);
+
+/* One-shot: set_ranges + run + fetch (the shape of AbstractEncodingEngine2::encode
+ * applied to a batch of range items). */
+int frac_search(frac_ctx* ctx, const frac_grid_item* ranges, size_t nr, frac_encode_item* out, frac_stats* stats);
+
+/* Use an external hipStream_t (passed as void*); NULL restores the context's own. */
+int frac_set_stream(frac_ctx* ctx, void* hip_stream);
+void* frac_get_stream(frac_ctx* ctx);
+/* Device pointer to the nr frac_encode_item results of the last run (valid until
+ * the next set_ranges / destroy); used for device-side gathers (RCCL). */
+const frac_encode_item* frac_device_results(frac_ctx* ctx);
+/* Asynchronous device-to-device copy of the last run's nr results into d_dst
+ * (ordered on the context's stream). */
+int frac_copy_results_device(frac_ctx* ctx, void* d_dst);
+
+/* ---- host helpers (no device needed) ------------------------------------ */
+/* createUniformGrid (image/partition2.hpp:109-135): returns the item count and
+ * writes min(count, cap) items (categories -1). */
+size_t frac_uniform_grid(uint32_t width, uint32_t height, uint32_t item_size, uint32_t item_offset,
+                         frac_grid_item* out, size_t cap);
+/* BrightnessBlocksClassifier2::preclassify over items (encode/Classifier2.cpp:64-68):
+ * writes each item's category computed on `plane`. */
+int frac_classify(const uint8_t* plane, uint32_t w, uint32_t h, uint32_t stride, frac_grid_item* items, size_t n);
+/* The ratio-2 sample permutation the kernels use: range pixel pix = y·n + x under
+ * transform t meets decimated domain cell frac_transform_index(n, t, pix)
+ * (image/sampler.h:21-38 with image/transform.h:96-109).  −1 on bad arguments. */
+int frac_transform_index(uint32_t n, uint32_t t, uint32_t pix);
+/* Largest integer S16 = 16·Σ(r − d̄)² whose reference distance (S16/16)/(4n²) is
+ * <= rms_threshold, or −1 (TransformMatcher::checkDistance, transformmatcher.h:32-34). */
+int64_t frac_hit_limit(double rms_threshold, uint32_t n);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* FRACENC_H */

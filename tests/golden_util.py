@@ -1,0 +1,51 @@
+"""Loading of the committed golden vectors (tests/golden/, made by tools/make_golden.py
+from the unmodified reference build)."""
+from __future__ import annotations
+
+import json
+import os
+
+import numpy as np
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+FIELDS = ("x", "y", "dx", "dy", "dw", "dh", "t", "dist", "s", "o")
+
+
+def manifest() -> dict:
+    with open(os.path.join(GOLD, "manifest.json")) as f:
+        return json.load(f)
+
+
+def plane(name: str) -> np.ndarray:
+    m = manifest()[name]
+    if name == "s1_4096":
+        from fractencode_amd.synth import value_noise
+        p = value_noise(4096, 4096, 1234)
+    elif name == "s1_2048":
+        from fractencode_amd.synth import value_noise
+        p = value_noise(4096, 4096, 1234)[:2048, :2048].copy()
+    else:
+        p = np.fromfile(os.path.join(GOLD, name + ".u8"), dtype=np.uint8).reshape(m["shape"])
+    from fractencode_amd.synth import sha256
+    assert sha256(p) == m["sha256"], f"fixture plane {name} drifted"
+    return p
+
+
+def golden(name: str):
+    z = np.load(os.path.join(GOLD, name + ".npz"))
+    meta = json.loads(bytes(z["meta"]).decode())
+    rec = {k: z[k] for k in FIELDS}
+    return rec, meta
+
+
+def selection(meta: dict, n_ranges: int):
+    sel = meta.get("sel")
+    if sel is None:
+        return None
+    if sel.startswith("arange("):
+        a, b, c = (int(v) for v in sel[len("arange("):-1].split(","))
+        return np.arange(a, b, c)
+    raise ValueError(sel)
+
+
+GOLDEN_NAMES = sorted(f[:-4] for f in os.listdir(GOLD) if f.endswith(".npz") and not f.endswith("_decode.npz"))

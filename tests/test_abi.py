@@ -1,0 +1,114 @@
+"""CPU checks of the C-ABI boundary (no compute calls on a device):
+the library loads, exports every symbol include/fracenc.h declares, the record
+layouts match the reference's structs, and the host helpers agree with the oracle.
+"""
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+import fractencode_amd as F
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "fracenc.h")
+
+
+def declared_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(frac_[a-z_0-9]+)\s*\(", text)))
+
+
+def test_library_exports_every_declared_symbol():
+    lib = F.lib()
+    names = declared_functions()
+    assert len(names) >= 20
+    missing = [n for n in names if not hasattr(lib, n)]
+    assert not missing, missing
+    assert lib.frac_abi_version() == 1
+
+
+def test_record_layouts_match_reference_structs(tmp_path):
+    # frac_* mirror Frac::transform_score_t / item_match_t / encode_item_t and
+    # Frac2::UniformGridItem (encode/datatypes.h:8-26, image/partition2.hpp:93-99)
+    src = tmp_path / "layout.c"
+    src.write_text(
+        '#include "fracenc.h"\n#include <stddef.h>\n'
+        "_Static_assert(sizeof(frac_grid_item) == 20, \"item\");\n"
+        "_Static_assert(sizeof(frac_score) == 32, \"score\");\n"
+        "_Static_assert(sizeof(frac_match) == 48, \"match\");\n"
+        "_Static_assert(sizeof(frac_encode_item) == 64, \"encode\");\n"
+        "_Static_assert(offsetof(frac_encode_item, match) == 16, \"match off\");\n"
+        "_Static_assert(offsetof(frac_match, x) == 32, \"x off\");\n"
+        "_Static_assert(offsetof(frac_score, transform) == 24, \"t off\");\n"
+        "int main(void) { return 0; }\n")
+    subprocess.check_call(["gcc", "-std=c11", "-I", os.path.join(ROOT, "include"), "-c", str(src), "-o",
+                           str(tmp_path / "layout.o")])
+    assert F.ENCODE_ITEM.itemsize == 64 and F.GRID_ITEM.itemsize == 20
+    assert F.ENCODE_ITEM.fields["distance"][1] == 16 and F.ENCODE_ITEM.fields["dx"][1] == 48
+
+
+@pytest.mark.parametrize("W,H,size,off", [(64, 64, 16, 8), (512, 512, 8, 8), (96, 64, 8, 4), (48, 80, 4, 2),
+                                          (64, 64, 64, 32)])
+def test_uniform_grid_matches_oracle(oracle, W, H, size, off):
+    g = F.create_uniform_grid(W, H, size, off)
+    o = oracle.uniform_grid(W, H, size, off)
+    assert len(g) == len(o)
+    for k in ("x", "y", "w", "h", "category"):
+        np.testing.assert_array_equal(g[k], o[k])
+
+
+def test_preclassify_matches_oracle(oracle):
+    from golden_util import plane
+    y = plane("lenna_y")
+    for size, off in [(8, 8), (16, 8), (4, 4), (32, 16)]:
+        items = F.create_uniform_grid(512, 512, size, off)
+        a = F.preclassify(y, items)["category"]
+        b = oracle.classify(y, oracle.uniform_grid(512, 512, size, off))["category"]
+        np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.parametrize("n", [2, 4, 8, 16])
+def test_transform_tables_are_the_reference_sampler(n):
+    # the kernel's permutation must equal SamplerBilinear's 2×2 block under each
+    # transform (image/sampler.h:21-38, image/transform.h:96-109) at ratio 2
+    lut = [(1, 0, 0, 0, 0, 1, 0, 0), (0, 1, 0, 0, -1, 0, 1, 0), (-1, 0, 1, 0, 0, -1, 0, 1), (0, -1, 0, 1, 1, 0, 0, 0),
+           (1, 0, 0, 0, 0, -1, 0, 1), (0, 1, 0, 0, 1, 0, 0, 0), (-1, 0, 1, 0, 0, 1, 0, 0), (0, -1, 0, 1, -1, 0, 1, 0)]
+    S = 2 * n
+    for t in range(8):
+        a = lut[t]
+        seen = set()
+        for pix in range(n * n):
+            x, y = pix % n, pix // n
+            lx, ly = 2 * x, 2 * y
+            px = a[0] * lx + a[1] * ly + a[2] * (S - 1) + a[3] * (S - 1)
+            py = a[4] * lx + a[5] * ly + a[6] * (S - 1) + a[7] * (S - 1)
+            pts = [(px, py), (px + a[0], py + a[4]), (px + a[1], py + a[5]), (px + a[0] + a[1], py + a[4] + a[5])]
+            x0 = min(p[0] for p in pts)
+            y0 = min(p[1] for p in pts)
+            assert x0 % 2 == 0 and y0 % 2 == 0
+            q = F.transform_index(n, t, pix)
+            assert q == (y0 // 2) * n + (x0 // 2), (t, pix)
+            seen.add(q)
+        assert len(seen) == n * n
+
+
+def test_hit_limit():
+    # dist = (S16/16)/(4n²) <= thr  (transformmatcher.h:32-34)
+    assert F.hit_limit(0.0, 8) == 0
+    assert F.hit_limit(-0.5, 8) == -1
+    assert F.hit_limit(float("nan"), 8) == -1
+    for thr in (0.25, 1.0, 10.0, 123.456):
+        for n in (2, 4, 8, 16):
+            H = F.hit_limit(thr, n)
+            assert (H / 16.0) / (4 * n * n) <= thr < ((H + 1) / 16.0) / (4 * n * n)
+
+
+def test_engine_without_device_fails_loudly():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("device present")
+    with pytest.raises(F.FracError):
+        F.Engine()

@@ -1,0 +1,214 @@
+"""GPU parity of the HIP search engine against the reference goldens and the oracle.
+
+Bar: bit-exact (domain, transform, distance, contrast, brightness) — the fit is
+exact in FP64 and the distance is the reference's fp32 value — plus the
+reference's rejected-mapping counts.  All calls go through the C ABI.
+"""
+import numpy as np
+import pytest
+
+import fractencode_amd as F
+from golden_util import FIELDS, GOLDEN_NAMES, golden, plane, selection
+
+pytestmark = pytest.mark.gpu
+
+# fixture name → engine support (the engine implements the ratio-2 path, n ∈ {2,4,8,16})
+RATIO2 = [n for n in GOLDEN_NAMES if n != "lenna_16to4"]
+ENGINES = [F.ENGINE_VALU]
+
+
+def as_oracle_fields(out):
+    return {"x": out["x"], "y": out["y"], "dx": out["dx"], "dy": out["dy"], "dw": out["sw"], "dh": out["sh"],
+            "t": out["transform"], "dist": out["distance"], "s": out["contrast"], "o": out["brightness"]}
+
+
+def run_engine(p, meta, engine, tgt=None, ranges_idx=None):
+    H, W = p.shape
+    doms = F.create_uniform_grid(W, H, meta["src"], meta["src"] // 2)
+    rngs = F.create_uniform_grid(W, H, meta["tgt"], meta["tgt"])
+    if meta["cls"]:
+        doms = F.preclassify(p, doms)
+        rngs = F.preclassify(p, rngs)
+    if ranges_idx is not None:
+        rngs = rngs[ranges_idx]
+    with F.Engine(0, meta["T"], meta["cls"], meta["thr"], meta["smax"], engine) as e:
+        e.set_frame(p)
+        e.set_domains(doms)
+        return e.search(rngs)
+
+
+def assert_same(got, want, what):
+    g = as_oracle_fields(got)
+    for k in FIELDS:
+        np.testing.assert_array_equal(g[k], want[k], err_msg=f"{what}: field {k}")
+
+
+@pytest.mark.parametrize("engine", ENGINES)
+@pytest.mark.parametrize("name", RATIO2)
+def test_engine_matches_reference_goldens(name, engine):
+    rec, meta = golden(name)
+    p = plane(meta["plane"])
+    H, W = p.shape
+    n_ranges = (W // meta["tgt"]) * (H // meta["tgt"])
+    sel = selection(meta, n_ranges)
+    out, st = run_engine(p, meta, engine, ranges_idx=sel)
+    assert_same(out, rec, name)
+    if sel is None:
+        assert st["rejected_mappings"] == meta["rejected"]
+
+
+def _random_plane(rng, W, H, kind):
+    if kind == "uniform":
+        return rng.integers(0, 256, (H, W), dtype=np.uint8)
+    if kind == "flat":
+        # many exact matches (threshold hits, ties)
+        return (rng.integers(0, 3, (H // 4, W // 4), dtype=np.uint8) * 60).repeat(4, 0).repeat(4, 1)
+    from fractencode_amd.synth import value_noise
+    return value_noise(W, H, int(rng.integers(1 << 30)))
+
+
+CASES = [
+    # W, H, n, T, classifier, thr, smax, kind
+    (64, 64, 8, 4, False, 0.0, -1.0, "uniform"),
+    (96, 64, 8, 8, False, 0.0, -1.0, "noise"),
+    (64, 96, 8, 4, True, 0.0, -1.0, "noise"),
+    (64, 64, 8, 8, True, 2.5, 0.7, "flat"),
+    (64, 64, 8, 4, False, 0.0, -1.0, "flat"),
+    (48, 48, 4, 4, False, 1.0, -1.0, "noise"),
+    (48, 32, 4, 8, True, 0.0, 2.0, "uniform"),
+    (32, 32, 2, 4, False, 0.0, -1.0, "noise"),
+    (32, 32, 2, 8, True, 0.0, -1.0, "flat"),
+    (96, 96, 16, 4, False, 0.0, -1.0, "noise"),
+    (128, 96, 16, 8, True, 30.0, -1.0, "uniform"),
+    (64, 64, 8, 4, False, 1e9, -1.0, "noise"),   # every candidate hits: all-fallback mode
+    (64, 64, 8, 8, False, 5000.0, -1.0, "uniform"),
+]
+
+
+@pytest.mark.parametrize("engine", ENGINES)
+@pytest.mark.parametrize("case", range(len(CASES)))
+def test_engine_matches_oracle_random(oracle, case, engine):
+    W, H, n, T, cls, thr, smax, kind = CASES[case]
+    rng = np.random.default_rng(1000 + case)
+    p = _random_plane(rng, W, H, kind)
+    meta = dict(src=2 * n, tgt=n, T=T, cls=cls, thr=thr, smax=smax)
+    out, st = run_engine(p, meta, engine)
+    doms = oracle.uniform_grid(W, H, 2 * n, n)
+    rngs = oracle.uniform_grid(W, H, n, n)
+    if cls:
+        doms = oracle.classify(p, doms)
+        rngs = oracle.classify(p, rngs)
+    want, rej, _ = oracle.estimate(p, doms, rngs, T=T, thr=thr, smax=smax, use_classifier=cls)
+    assert_same(out, {k: want[k] for k in FIELDS}, f"case {CASES[case]}")
+    assert st["rejected_mappings"] == rej
+
+
+@pytest.mark.parametrize("engine", ENGINES)
+def test_distinct_source_and_target_planes(engine):
+    # reference tests/TransformEstimatorTest.cpp:14-47 (source 8×8, target 4×4)
+    src = np.array([[1, 1, 2, 2, 40, 41, 50, 51], [1, 1, 2, 2, 40, 41, 50, 51], [3, 3, 4, 4, 70, 71, 80, 81],
+                    [3, 3, 4, 4, 70, 71, 80, 81], [10, 10, 10, 10, 0, 0, 0, 0], [11, 11, 11, 11, 1, 1, 1, 1],
+                    [10, 10, 10, 10, 0, 0, 0, 0], [11, 11, 11, 11, 1, 1, 1, 1]], np.uint8)
+    tgt = np.array([[40, 50, 2, 4], [70, 80, 1, 3], [0, 0, 10, 10], [1, 1, 11, 11]], np.uint8)
+    with F.Engine(0, 4, False, 0.0, 100.0, engine) as e:
+        e.set_planes(src, tgt)
+        e.set_domains(F.create_uniform_grid(8, 8, 4, 2))
+        out, _ = e.search(F.create_uniform_grid(4, 4, 2, 2))
+    got = {(int(r["x"]), int(r["y"])): (int(r["dx"]), int(r["dy"])) for r in out}
+    assert got == {(0, 0): (4, 0), (2, 0): (0, 0), (0, 2): (4, 4), (2, 2): (0, 4)}
+    # TransformMatcherTest.cpp:13-35: range (0,0) vs domain (0,0) is an exact Rotate_270 match
+    with F.Engine(0, 4, False, 0.0, 100.0, engine) as e:
+        s2 = np.array([[1, 1, 2, 2, 40, 41, 50, 51], [1, 1, 2, 2, 40, 41, 50, 51], [3, 3, 4, 4, 70, 71, 80, 81],
+                       [3, 3, 4, 4, 70, 71, 80, 81], [0] * 8, [1] * 8, [0] * 8, [1] * 8], np.uint8)
+        t2 = np.array([[2, 4, 40, 50], [1, 3, 70, 80], [0, 0, 0, 0], [1, 1, 1, 1]], np.uint8)
+        e.set_planes(s2, t2)
+        e.set_domains(np.array([(0, 0, 4, 4, -1)], dtype=F.GRID_ITEM))
+        out, _ = e.search(np.array([(0, 0, 2, 2, -1)], dtype=F.GRID_ITEM))
+    assert out["distance"][0] == 0.0 and out["transform"][0] == 3
+    assert out["contrast"][0] < 1.0 and out["brightness"][0] < 1.0
+
+
+@pytest.mark.parametrize("engine", ENGINES)
+def test_edge_cases(oracle, engine):
+    rng = np.random.default_rng(5)
+    p = rng.integers(0, 256, (64, 64), dtype=np.uint8)
+    rngs = F.create_uniform_grid(64, 64, 8, 8)
+    with F.Engine(0, 4, False, 0.0, -1.0, engine) as e:
+        e.set_frame(p)
+        # no domains at all: every range gets the default item_match_t (datatypes.h:8-19)
+        e.set_domains(np.zeros(0, dtype=F.GRID_ITEM))
+        out, st = e.search(rngs)
+        assert (out["distance"] == 100000.0).all() and (out["sw"] == 0).all() and st["empty_ranges"] == 64
+        # no ranges
+        e.set_domains(F.create_uniform_grid(64, 64, 16, 8))
+        out, st = e.search(np.zeros(0, dtype=F.GRID_ITEM))
+        assert len(out) == 0
+        # ragged range list in arbitrary order (results come back in that order)
+        perm = rng.permutation(len(rngs))[:37]
+        out, _ = e.search(rngs[perm])
+        want, _, _ = oracle.estimate(p, oracle.uniform_grid(64, 64, 16, 8), oracle.uniform_grid(64, 64, 8, 8)[perm])
+        assert_same(out, {k: want[k] for k in FIELDS}, "ragged")
+        # repeated runs are deterministic
+        out2, _ = e.search(rngs[perm])
+        assert out.tobytes() == out2.tobytes()
+    # classifier with a category that no domain has: rejected = nd for those ranges
+    doms = F.preclassify(p, F.create_uniform_grid(64, 64, 16, 8))
+    rg = F.preclassify(p, rngs)
+    doms = doms[doms["category"] != rg["category"][0]]
+    with F.Engine(0, 4, True, 0.0, -1.0, engine) as e:
+        e.set_frame(p)
+        e.set_domains(doms)
+        out, st = e.search(rg)
+    want, rej, _ = oracle.estimate(p, doms, rg, use_classifier=True)
+    assert_same(out, {k: want[k] for k in FIELDS}, "empty bucket")
+    assert st["rejected_mappings"] == rej and st["empty_ranges"] > 0
+
+
+@pytest.mark.parametrize("engine", ENGINES)
+def test_invalid_geometry_is_an_error(engine):
+    p = np.zeros((64, 64), np.uint8)
+    with F.Engine(0, 4, engine=engine) as e:
+        e.set_frame(p)
+        e.set_domains(F.create_uniform_grid(64, 64, 12, 6))  # ratio 12/8 is not the ratio-2 path
+        with pytest.raises(F.FracError):
+            e.search(F.create_uniform_grid(64, 64, 8, 8))
+        e.set_domains(F.create_uniform_grid(64, 64, 16, 8))
+        bad = np.array([(60, 60, 8, 8, -1)], dtype=F.GRID_ITEM)  # outside the plane
+        with pytest.raises(F.FracError):
+            e.search(bad)
+
+
+def _recompute_s16(p, out, n=8):
+    """Independent numpy recomputation of the exact error of each chosen (domain, t)."""
+    rx, ry, dx, dy, t = (out[k].astype(np.int64) for k in ("x", "y", "dx", "dy", "transform"))
+    yy, xx = np.divmod(np.arange(n * n), n)
+    r = p[ry[:, None] + yy[None, :], rx[:, None] + xx[None, :]].astype(np.int64)
+    fwd = np.array([[F.transform_index(n, tt, q) for q in range(n * n)] for tt in range(8)])
+    q = fwd[t]  # [N, n²] decimated cell met by each range pixel
+    qy, qx = np.divmod(q, n)
+    X0 = dx[:, None] + 2 * qx
+    Y0 = dy[:, None] + 2 * qy
+    pi = p.astype(np.int64)
+    D = pi[Y0, X0] + pi[Y0, X0 + 1] + pi[Y0 + 1, X0] + pi[Y0 + 1, X0 + 1]
+    return ((4 * r - D) ** 2).sum(1)
+
+
+@pytest.mark.parametrize("engine", ENGINES)
+def test_full_4096_frame(engine):
+    """C3 at full size: the 1,024 reference-sampled ranges match bit-exactly, and every
+    range's distance is the exact error of the (domain, transform) it reports."""
+    rec, meta = golden("s1_4096_sample")
+    p = plane("s1_4096")
+    doms = F.create_uniform_grid(4096, 4096, 16, 8)
+    rngs = F.create_uniform_grid(4096, 4096, 8, 8)
+    with F.Engine(0, 4, False, 0.0, -1.0, engine, timing=True) as e:
+        e.set_frame(p)
+        e.set_domains(doms)
+        out, st = e.search(rngs)
+    sel = selection(meta, len(rngs))
+    assert_same(out[sel], rec, "s1_4096 sample")
+    s16 = _recompute_s16(p, out)
+    exact = s16 < (1 << 24)
+    np.testing.assert_array_equal(out["distance"][exact], (s16[exact] / 16.0) / 256.0)
+    assert st["fallback_ranges"] == int((~exact).sum())
+    assert (out["sw"] == 16).all()

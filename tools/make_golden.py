@@ -1,0 +1,175 @@
+#!/usr/bin/env python3
+"""Generate the committed golden vectors under tests/golden/ from the REFERENCE.
+
+Runs only in the build container (needs /root/reference): builds
+oracle/_ref/libfracref.so from the unmodified reference sources
+(oracle/ref/Makefile) and records, per fixture, the reference's per-range
+winners.  Only data is written (raw planes and result arrays); no reference
+source travels.  Re-run with:  python tools/make_golden.py [--only NAME ...]
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import hashlib
+import json
+import os
+import subprocess
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from fractencode_amd.synth import value_noise, sha256  # noqa: E402
+
+GOLD = os.path.join(ROOT, "tests", "golden")
+REF_PNG = "/root/reference/tests/input/lenna512x512.png"
+
+
+class FrResult(C.Structure):
+    _fields_ = [("x", C.c_uint32), ("y", C.c_uint32), ("dx", C.c_uint32), ("dy", C.c_uint32),
+                ("dw", C.c_uint32), ("dh", C.c_uint32), ("transform", C.c_int32), ("pad", C.c_int32),
+                ("distance", C.c_double), ("contrast", C.c_double), ("brightness", C.c_double)]
+
+
+def load_ref():
+    subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle", "ref")])
+    lib = C.CDLL(os.path.join(ROOT, "oracle", "_ref", "libfracref.so"))
+    lib.fr_estimate.restype = C.c_int
+    lib.fr_estimate.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
+                                C.c_int, C.c_double, C.c_double, C.c_int, C.c_int, C.c_void_p, C.c_size_t,
+                                C.c_void_p, C.POINTER(C.c_uint64), C.c_double, C.POINTER(C.c_size_t)]
+    lib.fr_decode.restype = C.c_int
+    lib.fr_decode.argtypes = [C.c_void_p, C.c_size_t, C.c_uint32, C.c_uint32, C.c_uint32, C.c_int, C.c_double,
+                              C.c_void_p, C.POINTER(C.c_double)]
+    lib.fr_load_yuv.argtypes = [C.c_char_p, C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(C.c_uint32),
+                                C.POINTER(C.c_uint32)]
+    return lib
+
+
+def ref_estimate(lib, plane, src_size, tgt_size, T, thr=0.0, smax=-1.0, cls=False, sel=None, threads=8):
+    plane = np.ascontiguousarray(plane, dtype=np.uint8)
+    H, W = plane.shape
+    n_ranges = (W // tgt_size) * (H // tgt_size)
+    count = n_ranges if sel is None else len(sel)
+    out = (FrResult * count)()
+    rej = C.c_uint64(0)
+    done = C.c_size_t(0)
+    sel_arr = None if sel is None else np.ascontiguousarray(sel, dtype=np.uint32)
+    lib.fr_estimate(plane.ctypes.data, plane.ctypes.data, W, H, W, src_size, tgt_size, T, thr, smax, int(cls),
+                    threads, None if sel_arr is None else sel_arr.ctypes.data, count, out, C.byref(rej), 0.0,
+                    C.byref(done))
+    a = np.frombuffer(out, dtype=np.dtype([("x", "<u4"), ("y", "<u4"), ("dx", "<u4"), ("dy", "<u4"), ("dw", "<u4"),
+                                           ("dh", "<u4"), ("t", "<i4"), ("pad", "<i4"), ("dist", "<f8"),
+                                           ("s", "<f8"), ("o", "<f8")])).copy()
+    return a, int(rej.value)
+
+
+def save(name, plane_ref, rec, rejected, params, extra=None):
+    d = {k: rec[k] for k in ("x", "y", "dx", "dy", "dw", "dh", "t", "dist", "s", "o")}
+    meta = dict(params, rejected=rejected, plane=plane_ref)
+    if extra:
+        meta.update(extra)
+    d["meta"] = np.frombuffer(json.dumps(meta).encode(), dtype=np.uint8)
+    np.savez_compressed(os.path.join(GOLD, name + ".npz"), **d)
+    print(f"  {name}: {len(rec)} ranges, rejected={rejected}", flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", nargs="*")
+    args = ap.parse_args()
+    os.makedirs(GOLD, exist_ok=True)
+    lib = load_ref()
+    want = (lambda n: True) if not args.only else (lambda n: n in args.only)
+
+    # -- input planes (data only) --------------------------------------------
+    y = np.zeros((512, 512), np.uint8)
+    u = np.zeros((256, 256), np.uint8)
+    v = np.zeros((256, 256), np.uint8)
+    w = C.c_uint32()
+    h = C.c_uint32()
+    lib.fr_load_yuv(REF_PNG.encode(), y.ctypes.data, u.ctypes.data, v.ctypes.data, C.byref(w), C.byref(h))
+    assert (w.value, h.value) == (512, 512)
+    planes = {"lenna_y": y, "lenna_u": u, "lenna_v": v, "crop64": np.ascontiguousarray(y[256:320, 256:320])}
+    rng = np.random.default_rng(7)
+    inexact = rng.integers(0, 41, size=(64, 64), dtype=np.uint8)
+    inexact[0:8, 0:8] = 255
+    inexact[40:48, 24:32] = 250
+    planes["inexact64"] = inexact
+    yy, xx = np.mgrid[0:64, 0:64]
+    planes["checker64"] = np.where(((yy // 8) + (xx // 8)) % 2 == 0, 0, 255).astype(np.uint8)
+    for k, p in planes.items():
+        p.tofile(os.path.join(GOLD, k + ".u8"))
+    manifest = {k: {"shape": list(p.shape), "sha256": sha256(p)} for k, p in planes.items()}
+
+    # -- reference runs -------------------------------------------------------
+    jobs = [
+        ("crop64_t4", "crop64", dict(src=16, tgt=8, T=4)),
+        ("lenna_t4", "lenna_y", dict(src=16, tgt=8, T=4)),
+        ("lenna_t8", "lenna_y", dict(src=16, tgt=8, T=8)),
+        ("lenna_cls", "lenna_y", dict(src=16, tgt=8, T=4, cls=True)),
+        ("lenna_cls_t8", "lenna_y", dict(src=16, tgt=8, T=8, cls=True)),
+        ("lenna_thr10", "lenna_y", dict(src=16, tgt=8, T=4, thr=10.0)),
+        ("lenna_smax", "lenna_y", dict(src=16, tgt=8, T=4, smax=0.9)),
+        ("lenna_n4", "lenna_y", dict(src=8, tgt=4, T=4)),
+        ("lenna_n16", "lenna_y", dict(src=32, tgt=16, T=4)),
+        ("lenna_16to4", "lenna_y", dict(src=16, tgt=4, T=4)),
+        ("lenna_u_t4", "lenna_u", dict(src=16, tgt=8, T=4)),
+        ("lenna_v_t4", "lenna_v", dict(src=16, tgt=8, T=4)),
+        ("crop64_n2", "crop64", dict(src=4, tgt=2, T=4)),
+        ("crop64_n2_t8", "crop64", dict(src=4, tgt=2, T=8)),
+        ("crop64_cls", "crop64", dict(src=16, tgt=8, T=4, cls=True)),
+        ("inexact64_t8", "inexact64", dict(src=16, tgt=8, T=8)),
+        ("inexact64_t4", "inexact64", dict(src=16, tgt=8, T=4)),
+        ("checker64_t8", "checker64", dict(src=16, tgt=8, T=8)),
+        ("checker64_thr", "checker64", dict(src=16, tgt=8, T=4, thr=8200.0)),
+    ]
+    for name, pk, p in jobs:
+        if not want(name):
+            continue
+        t0 = time.time()
+        rec, rej = ref_estimate(lib, planes[pk], p["src"], p["tgt"], p["T"], p.get("thr", 0.0), p.get("smax", -1.0),
+                                p.get("cls", False))
+        params = dict(src=p["src"], tgt=p["tgt"], T=p["T"], thr=p.get("thr", 0.0), smax=p.get("smax", -1.0),
+                      cls=p.get("cls", False), sel=None)
+        save(name, pk, rec, rej, params, {"seconds": round(time.time() - t0, 2)})
+        if name == "lenna_t4":
+            dec = np.zeros((512, 512), np.uint8)
+            rms = C.c_double()
+            it = lib.fr_decode(rec.ctypes.data, len(rec), 8, 512, 512, -1, 1e-5, dec.ctypes.data, C.byref(rms))
+            np.savez_compressed(os.path.join(GOLD, "lenna_t4_decode.npz"), plane=dec,
+                                meta=np.frombuffer(json.dumps({"iterations": it, "rms": rms.value}).encode(),
+                                                   dtype=np.uint8))
+            print(f"  decode: {it} iterations rms={rms.value}")
+
+    # -- S1 4096^2 strided sample (C3 parity on a sample) ----------------------
+    if want("s1_4096_sample"):
+        t0 = time.time()
+        s1 = value_noise(4096, 4096, 1234)
+        manifest["s1_4096"] = {"shape": [4096, 4096], "sha256": sha256(s1), "generator": "value_noise(4096,4096,1234)"}
+        sel = np.arange(0, 262144, 256, dtype=np.uint32)  # 1,024 ranges, range index i*256
+        rec, rej = ref_estimate(lib, s1, 16, 8, 4, sel=sel)
+        save("s1_4096_sample", "s1_4096", rec, rej, dict(src=16, tgt=8, T=4, thr=0.0, smax=-1.0, cls=False,
+                                                         sel="arange(0,262144,256)"),
+             {"seconds": round(time.time() - t0, 2)})
+    if want("s1_2048_cls_sample"):
+        t0 = time.time()
+        s1 = value_noise(4096, 4096, 1234)[:2048, :2048].copy()
+        manifest["s1_2048"] = {"shape": [2048, 2048], "sha256": sha256(s1),
+                               "generator": "value_noise(4096,4096,1234)[:2048,:2048]"}
+        sel = np.arange(0, 65536, 64, dtype=np.uint32)
+        rec, rej = ref_estimate(lib, s1, 16, 8, 4, cls=True, sel=sel)
+        save("s1_2048_cls_sample", "s1_2048", rec, rej, dict(src=16, tgt=8, T=4, thr=0.0, smax=-1.0, cls=True,
+                                                             sel="arange(0,65536,64)"),
+             {"seconds": round(time.time() - t0, 2)})
+    path = os.path.join(GOLD, "manifest.json")
+    old = json.load(open(path)) if os.path.exists(path) else {}
+    old.update(manifest)
+    json.dump(old, open(path, "w"), indent=1, sort_keys=True)
+
+
+if __name__ == "__main__":
+    main()
