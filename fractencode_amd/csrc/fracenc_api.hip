@@ -14,6 +14,7 @@
 
 #include "fracenc_common.h"
 #include "fracenc_kernels.hip"
+#include "fracenc_mfma.hip"
 
 using namespace fracenc;
 
@@ -154,6 +155,19 @@ struct frac_ctx {
     DBuf<unsigned long long> d_best_key;
     DBuf<frac_encode_item> d_out;
     DBuf<RangeAux> d_aux;
+
+    // MFMA engine layout
+    uint32_t engine = FRAC_ENGINE_VALU;    // engine chosen for the current geometry
+    uint32_t nblocks = 0, ntiles = 0;
+    std::vector<int32_t> m_slot_range;     // [nblocks*32]
+    std::vector<uint32_t> m_range_slot;    // [nr]
+    std::vector<int32_t> m_tile_pos;       // [ntiles*32]
+    std::vector<uint4> m_work;             // per WG
+    std::vector<uint32_t> m_blk_ptr, m_blk_ent;
+    DBuf<int32_t> d_m_slot_range, d_m_tile_pos;
+    DBuf<uint32_t> d_m_range_slot, d_m_blk_ptr, d_m_blk_ent, d_m_rconst, d_m_dconst;
+    DBuf<uint4> d_m_work, d_m_dtiles, d_m_rfrags;
+    DBuf<uint2> d_m_entries;
 
     std::vector<RangeAux> h_aux;
     hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
@@ -320,6 +334,74 @@ int prepare(frac_ctx* c)
     c->hitH = compute_hit_limit(c->p.rms_threshold, (uint32_t)(4 * n * n));
     c->all_fallback = c->hitH >= kExactLimit;
 
+    // engine: the MFMA encoding is exact for n <= 8 (|Σ(r−128)(D4−510)| < 2^22)
+    if (c->p.engine == FRAC_ENGINE_MFMA && n > 8)
+        return c->fail(FRAC_E_INVALID, "the MFMA engine supports range sizes 2, 4 and 8");
+    c->engine = (c->p.engine == FRAC_ENGINE_VALU || n > 8) ? FRAC_ENGINE_VALU : FRAC_ENGINE_MFMA;
+    if (c->engine == FRAC_ENGINE_MFMA) {
+        // range blocks of 32 slots per bucket; domain tiles of 32 pool positions per bucket
+        c->m_slot_range.clear();
+        c->m_range_slot.assign(c->ranges.size(), 0);
+        std::vector<uint32_t> blk_first(nb, 0), blk_count(nb, 0);
+        for (int b = 0; b < nb; ++b) {
+            blk_first[b] = (uint32_t)(c->m_slot_range.size() / 32);
+            for (size_t i = 0; i < c->ranges.size(); ++i)
+                if (c->range_bucket[i] == b) {
+                    c->m_range_slot[i] = (uint32_t)c->m_slot_range.size();
+                    c->m_slot_range.push_back((int32_t)i);
+                }
+            while (c->m_slot_range.size() % 32)
+                c->m_slot_range.push_back(-1);
+            blk_count[b] = (uint32_t)(c->m_slot_range.size() / 32) - blk_first[b];
+        }
+        c->nblocks = (uint32_t)(c->m_slot_range.size() / 32);
+        c->m_tile_pos.clear();
+        std::vector<uint32_t> tile_first(nb, 0), tile_count(nb, 0);
+        for (int b = 0; b < nb; ++b) {
+            tile_first[b] = (uint32_t)(c->m_tile_pos.size() / 32);
+            for (uint32_t pp = c->bucket_begin[b]; pp < c->bucket_end[b]; ++pp)
+                c->m_tile_pos.push_back((int32_t)pp);
+            while (c->m_tile_pos.size() % 32)
+                c->m_tile_pos.push_back(-1);
+            tile_count[b] = (uint32_t)(c->m_tile_pos.size() / 32) - tile_first[b];
+        }
+        c->ntiles = (uint32_t)(c->m_tile_pos.size() / 32);
+        // work items: groups of up to 4 blocks of one bucket × splits of its tiles
+        size_t groups = 0;
+        for (int b = 0; b < nb; ++b)
+            if (tile_count[b])
+                groups += (blk_count[b] + 3) / 4;
+        const size_t target_wgs = 8192;
+        std::vector<std::vector<uint32_t>> blk_list(c->nblocks);
+        c->m_work.clear();
+        for (int b = 0; b < nb; ++b) {
+            if (!tile_count[b] || !blk_count[b])
+                continue;
+            size_t splits = groups ? (target_wgs + groups - 1) / groups : 1;
+            splits = std::max<size_t>(1, std::min<size_t>(splits, std::max<uint32_t>(1u, tile_count[b] / 4u)));
+            for (uint32_t g = 0; g < blk_count[b]; g += 4) {
+                const uint32_t nbk = std::min(4u, blk_count[b] - g);
+                for (size_t sp = 0; sp < splits; ++sp) {
+                    const uint32_t t0 = tile_first[b] + (uint32_t)((uint64_t)tile_count[b] * sp / splits);
+                    const uint32_t t1 = tile_first[b] + (uint32_t)((uint64_t)tile_count[b] * (sp + 1) / splits);
+                    if (t1 <= t0)
+                        continue;
+                    const uint32_t w = (uint32_t)c->m_work.size();
+                    c->m_work.push_back(make_uint4(blk_first[b] + g, nbk, t0, t1));
+                    for (uint32_t k = 0; k < nbk; ++k)
+                        blk_list[blk_first[b] + g + k].push_back(w * 4u + k);
+                }
+            }
+        }
+        c->m_blk_ptr.assign(c->nblocks + 1, 0);
+        c->m_blk_ent.clear();
+        for (uint32_t b = 0; b < c->nblocks; ++b) {
+            c->m_blk_ptr[b] = (uint32_t)c->m_blk_ent.size();
+            c->m_blk_ent.insert(c->m_blk_ent.end(), blk_list[b].begin(), blk_list[b].end());
+        }
+        c->m_blk_ptr[c->nblocks] = (uint32_t)c->m_blk_ent.size();
+    }
+
     const size_t nr = c->ranges.size(), P = c->porig.size();
     FRAC_HIP(c, c->d_doms.ensure(c->doms.size()));
     FRAC_HIP(c, c->d_ranges.ensure(nr));
@@ -349,8 +431,105 @@ int prepare(frac_ctx* c)
             c->fb_iota[i] = (uint32_t)i;
         FRAC_TRY(up(c->d_fb_list.ptr, c->fb_iota.data(), nr * sizeof(uint32_t)));
     }
+    if (c->engine == FRAC_ENGINE_MFMA) {
+        const int KS = (n * n + 15) / 16;
+        FRAC_HIP(c, c->d_m_slot_range.ensure(c->m_slot_range.size()));
+        FRAC_HIP(c, c->d_m_range_slot.ensure(nr));
+        FRAC_HIP(c, c->d_m_tile_pos.ensure(c->m_tile_pos.size()));
+        FRAC_HIP(c, c->d_m_work.ensure(c->m_work.size()));
+        FRAC_HIP(c, c->d_m_blk_ptr.ensure(c->m_blk_ptr.size()));
+        FRAC_HIP(c, c->d_m_blk_ent.ensure(c->m_blk_ent.size()));
+        FRAC_HIP(c, c->d_m_rconst.ensure((size_t)c->nblocks * 32));
+        FRAC_HIP(c, c->d_m_dconst.ensure((size_t)c->ntiles * 32));
+        FRAC_HIP(c, c->d_m_dtiles.ensure((size_t)c->ntiles * KS * 64));
+        FRAC_HIP(c, c->d_m_rfrags.ensure((size_t)c->nblocks * T * KS * 64));
+        FRAC_HIP(c, c->d_m_entries.ensure(c->m_work.size() * 4 * T * 64));
+        FRAC_TRY(up(c->d_m_slot_range.ptr, c->m_slot_range.data(), c->m_slot_range.size() * sizeof(int32_t)));
+        FRAC_TRY(up(c->d_m_range_slot.ptr, c->m_range_slot.data(), nr * sizeof(uint32_t)));
+        FRAC_TRY(up(c->d_m_tile_pos.ptr, c->m_tile_pos.data(), c->m_tile_pos.size() * sizeof(int32_t)));
+        FRAC_TRY(up(c->d_m_work.ptr, c->m_work.data(), c->m_work.size() * sizeof(uint4)));
+        FRAC_TRY(up(c->d_m_blk_ptr.ptr, c->m_blk_ptr.data(), c->m_blk_ptr.size() * sizeof(uint32_t)));
+        FRAC_TRY(up(c->d_m_blk_ent.ptr, c->m_blk_ent.data(), c->m_blk_ent.size() * sizeof(uint32_t)));
+    }
     c->h_aux.resize(nr);
     c->dirty = false;
+    return FRAC_OK;
+}
+
+template <int N, int T>
+void launch_search_mfma(frac_ctx* c, const MfmaSearchArgs& a)
+{
+    if (c->hitH >= 0)
+        search_mfma<N, T, true><<<(unsigned)c->m_work.size(), 256, 0, c->stream>>>(a);
+    else
+        search_mfma<N, T, false><<<(unsigned)c->m_work.size(), 256, 0, c->stream>>>(a);
+}
+
+template <int N>
+int launch_mfma(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride)
+{
+    const uint32_t nr = (uint32_t)c->ranges.size(), T = c->p.transforms;
+    if (c->ntiles) {
+        MfmaDomainPrepArgs d;
+        d.pool = c->d_pool.ptr;
+        d.negsd2 = c->d_negsd2.ptr;
+        d.tile_pos = c->d_m_tile_pos.ptr;
+        d.ntiles = c->ntiles;
+        d.dtiles = c->d_m_dtiles.ptr;
+        d.dconst = c->d_m_dconst.ptr;
+        mfma_domain_prep<N><<<(c->ntiles * 32 + 255) / 256, 256, 0, c->stream>>>(d);
+    }
+    if (c->nblocks) {
+        MfmaRangePrepArgs r;
+        r.tgt = dtgt;
+        r.tstride = tstride;
+        r.ranges = c->d_ranges.ptr;
+        r.slot_range = c->d_m_slot_range.ptr;
+        r.nblocks = c->nblocks;
+        r.T = T;
+        r.rfrags = c->d_m_rfrags.ptr;
+        r.rconst = c->d_m_rconst.ptr;
+        const size_t threads = (size_t)c->nblocks * T * MfmaGeom<N>::KS * 64;
+        mfma_range_prep<N><<<(unsigned)((threads + 255) / 256), 256, 0, c->stream>>>(r);
+    }
+    if (c->p.flags & FRAC_FLAG_TIMING)
+        FRAC_HIP(c, hipEventRecord(c->ev[1], c->stream));
+    if (!c->m_work.empty()) {
+        MfmaSearchArgs a;
+        a.dtiles = c->d_m_dtiles.ptr;
+        a.dconst = reinterpret_cast<const uint4*>(c->d_m_dconst.ptr);
+        a.rfrags = c->d_m_rfrags.ptr;
+        a.rconst = c->d_m_rconst.ptr;
+        a.work = c->d_m_work.ptr;
+        a.nwork = (uint32_t)c->m_work.size();
+        a.hitH = (uint32_t)std::max<int64_t>(c->hitH, 0);
+        a.entries = c->d_m_entries.ptr;
+        if (T == 8)
+            launch_search_mfma<N, 8>(c, a);
+        else
+            launch_search_mfma<N, 4>(c, a);
+    }
+    if (c->p.flags & FRAC_FLAG_TIMING)
+        FRAC_HIP(c, hipEventRecord(c->ev[2], c->stream));
+    if (nr) {
+        MfmaResolveArgs v;
+        v.tgt = dtgt;
+        v.tstride = tstride;
+        v.ranges = c->d_ranges.ptr;
+        v.range_slot = c->d_m_range_slot.ptr;
+        v.blk_ptr = c->d_m_blk_ptr.ptr;
+        v.blk_ent = c->d_m_blk_ent.ptr;
+        v.entries = c->d_m_entries.ptr;
+        v.rconst = c->d_m_rconst.ptr;
+        v.tile_pos = c->d_m_tile_pos.ptr;
+        v.pool = c->d_pool.ptr;
+        v.negsd2 = c->d_negsd2.ptr;
+        v.nr = nr;
+        v.T = T;
+        v.hitH = c->hitH;
+        v.best_key = c->d_best_key.ptr;
+        resolve_mfma<N><<<(nr + 255) / 256, 256, 0, c->stream>>>(v);
+    }
     return FRAC_OK;
 }
 
@@ -371,9 +550,14 @@ int launch_all(frac_ctx* c)
     if (P)
         pool_build<N><<<(P + 3) / 4, 256, 0, c->stream>>>(dsrc, c->d_sstride, c->d_doms.ptr, c->d_porig.ptr, P,
                                                           c->d_pool.ptr, c->d_negsd2.ptr);
-    if (timing)
+    const bool use_mfma = c->engine == FRAC_ENGINE_MFMA && !c->all_fallback;
+    if constexpr (N <= 8) {
+        if (use_mfma)
+            FRAC_TRY(launch_mfma<N>(c, dtgt, tstride));
+    }
+    if (timing && !use_mfma)
         FRAC_HIP(c, hipEventRecord(c->ev[1], c->stream));
-    if (!c->all_fallback && !c->work.empty()) {
+    if (!use_mfma && !c->all_fallback && !c->work.empty()) {
         SearchArgs a;
         a.tgt = dtgt;
         a.tstride = tstride;
@@ -411,7 +595,7 @@ int launch_all(frac_ctx* c)
                 search_valu<N, 4, false><<<grid, block, 0, c->stream>>>(a);
         }
     }
-    if (timing)
+    if (timing && !use_mfma)
         FRAC_HIP(c, hipEventRecord(c->ev[2], c->stream));
     if (!c->all_fallback && nr) {
         FitArgs f;
@@ -454,7 +638,7 @@ int launch_all(frac_ctx* c)
     if (timing)
         FRAC_HIP(c, hipEventRecord(c->ev[3], c->stream));
     FRAC_HIP(c, hipGetLastError());
-    c->engine_ran = FRAC_ENGINE_VALU;
+    c->engine_ran = use_mfma ? FRAC_ENGINE_MFMA : FRAC_ENGINE_VALU;
     return FRAC_OK;
 }
 
@@ -528,6 +712,17 @@ void frac_destroy(frac_ctx* c)
     c->d_best_key.release();
     c->d_out.release();
     c->d_aux.release();
+    c->d_m_slot_range.release();
+    c->d_m_tile_pos.release();
+    c->d_m_range_slot.release();
+    c->d_m_blk_ptr.release();
+    c->d_m_blk_ent.release();
+    c->d_m_rconst.release();
+    c->d_m_dconst.release();
+    c->d_m_work.release();
+    c->d_m_dtiles.release();
+    c->d_m_rfrags.release();
+    c->d_m_entries.release();
     for (auto& ev : c->ev)
         if (ev)
             (void)hipEventDestroy(ev);

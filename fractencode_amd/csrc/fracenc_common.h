@@ -59,14 +59,25 @@ __host__ __device__ constexpr int inv_index(int t, int q)
     return py * N + px;
 }
 
-// Selection key of one (range, domain) candidate, reduced by a u64 atomicMin:
-//   hit  (S16 <= H):  (0 << 63) | pool_position
-//   miss:             (1 << 63) | (S16 << 32) | pool_position
+// Selection key of one candidate, reduced with u64 min (atomicMin or in-thread):
+//   hit  (S16 <= H):  (0 << 63) | (pool_position << 3) | t
+//   miss:             (1 << 63) | (S16 << 27) | (pool_position << 3) | (T − 1 − t)
 // Pool positions preserve the reference's domain order inside a classifier bucket,
-// so min(key) = "first hit, else least error, ties to the earliest domain"
-// (encode/TransformEstimator2.hpp:34-41).  The transform is re-derived for the winner.
+// so min(key) = "first hit in (domain, transform) order, else least error with ties
+// to the earliest domain and then the later transform"
+// (encode/TransformEstimator2.hpp:34-41, encode/transformmatcher.h:55-67).
+// Engines that do not track t leave the low 3 bits 0; fit_winner re-derives t.
 constexpr unsigned long long kKeyNone = ~0ull;
 constexpr unsigned long long kKeyMiss = 1ull << 63;
+__host__ __device__ inline uint32_t key_pos(unsigned long long k) { return (uint32_t)((k >> 3) & 0xffffffu); }
+__host__ __device__ inline unsigned long long key_miss(uint64_t s16, uint32_t pos, uint32_t tcode)
+{
+    return kKeyMiss | ((unsigned long long)s16 << 27) | ((unsigned long long)pos << 3) | tcode;
+}
+__host__ __device__ inline unsigned long long key_hit(uint32_t pos, uint32_t t)
+{
+    return ((unsigned long long)pos << 3) | t;
+}
 
 // S16 = Σ(4r − D4)² is the reference's fp32 error ×16 (image/metrics.h:37-50);
 // the fp32 sum is exact iff S16 < 2^24.

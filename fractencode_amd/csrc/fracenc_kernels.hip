@@ -217,9 +217,9 @@ __global__ void __launch_bounds__(256) search_valu(SearchArgs a)
     if (live && best != INT_MIN) {
         unsigned long long key;
         if (HITS && best == INT_MAX)
-            key = (unsigned long long)bestp;
+            key = key_hit(bestp, 0);
         else
-            key = kKeyMiss | ((unsigned long long)(uint32_t)(Cr - best) << 32) | (unsigned long long)bestp;
+            key = key_miss((uint32_t)(Cr - best), bestp, 0);
         atomicMin(&a.best_key[ri], key);
     }
 }
@@ -310,7 +310,7 @@ __global__ void __launch_bounds__(256) fit_winner(FitArgs a)
         }
         return;
     }
-    const uint32_t p = (uint32_t)(key & 0xffffffffull);
+    const uint32_t p = key_pos(key);
     const bool hit = (key >> 63) == 0;
     const frac_grid_item d = a.doms[a.porig[p]];
     const uint32_t* dp = a.pool + (size_t)p * (NN / 2);

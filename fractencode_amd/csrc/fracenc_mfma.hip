@@ -1,0 +1,344 @@
+// fracenc_mfma.hip — f16 MFMA search engine (ratio-2 path, n ∈ {2, 4, 8}).
+//
+// The error of every (range, transform, domain) candidate is an all-pairs dot product
+// X = Σ_k copy_t[k]·D4[k], i.e. a GEMM with K = n².  It runs on v_mfma_f32_32x32x16_f16
+// with operands chosen so the fp32 accumulator is EXACT and its bit pattern is an
+// affine function of the integer result:
+//   A (rows, 32 domains per tile)         = D4 − 510            ∈ [−510, 510]   (exact in f16)
+//   B (cols, 32 ranges, one transform)    = 128 − copy_t         ∈ [−127, 128]
+//   C (init)                              = 1.5·2^23
+// Every partial sum lies in [2^23, 2^24) (|Σ| ≤ 64·128·510 < 2^22 for n ≤ 8) where fp32
+// has unit spacing, so acc is exact and bits(acc) = 0x4B400000 − Z with
+// Z = Σ (r − 128)(D4 − 510).  (Exactness measured on gfx950: tools/ubench.hip.)
+// Per candidate the epilogue is ONE v_lshl_add_u32:
+//   v = (bits << 3) + e'_d  =  S16 + c_r   (mod 2^32, true value in [0, 2^27))
+// with e'_d = ΣD4² − 1024·ΣD4 − 0x58000000 per domain and c_r a per-range constant, so
+// the min over domains of v is the min of the reference's error S16 (image/metrics.h).
+// Lanes keep per (transform) the running min over domain tiles and the first tile that
+// attained it (strict '<' in domain order, encode/TransformEstimator2.hpp:34); hits
+// (S16 <= H) collapse to 0.  resolve_mfma then pins the exact domain inside that tile.
+#include "fracenc_common.h"
+
+namespace fracenc {
+
+typedef _Float16 half8_t __attribute__((ext_vector_type(8)));
+typedef float floatx16_t __attribute__((ext_vector_type(16)));
+
+constexpr uint32_t kMfmaPadConst = 0x70000000u; // e' of padding domains: v ≈ 1.9e9, never wins
+constexpr int kTilesPerStage = 8;
+
+template <int N>
+struct MfmaGeom {
+    static constexpr int NN = N * N;
+    static constexpr int KS = (NN + 15) / 16; // K-steps of 16
+};
+
+// c_r: v − c_r = S16 for a range with pixel sum Σr and square sum Σr²
+// v = 2^25 − 8Z + ΣD4² − 1024ΣD4  and  −8Z = −8X + 4080Σr + 1024ΣD4 − 8·NN·65280
+//   ⇒ v = S16 − 16Σr² + 4080Σr + 2^25 − 8·NN·65280
+__host__ __device__ inline uint32_t mfma_range_const(int NN, int64_t sr, int64_t sr2)
+{
+    return (uint32_t)(int64_t)(-16 * sr2 + 4080 * sr + (1ll << 25) - 8ll * NN * 65280);
+}
+
+// ---------------------------------------------------------------------------
+// mfma_domain_prep: u16 pool → per 32-domain tile the A fragments (lane l holds row
+// l&31, k = 16s + 8(l>>5) + j) and the per-lane-half epilogue constants e'.
+// One thread per (tile, row).  Rows past a bucket's end are padding.
+// ---------------------------------------------------------------------------
+struct MfmaDomainPrepArgs {
+    const uint32_t* pool;       // [P][NN/2]
+    const int32_t* negsd2;      // [P]
+    const int32_t* tile_pos;    // [ntiles*32] pool position of each tile row (−1 = padding)
+    uint32_t ntiles;
+    uint4* dtiles;              // [ntiles][KS][64] 16 B
+    uint32_t* dconst;           // [ntiles][2][16]
+};
+
+template <int N>
+__global__ void __launch_bounds__(256) mfma_domain_prep(MfmaDomainPrepArgs a)
+{
+    constexpr int NN = N * N, KS = MfmaGeom<N>::KS;
+    const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid >= a.ntiles * 32u)
+        return;
+    const uint32_t tile = gid >> 5, row = gid & 31u;
+    const int p = a.tile_pos[gid];
+    int sumd = 0, sd2 = 0;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            _Float16 v8[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int k = 16 * s + 8 * h + j;
+                int dv = 510; // padding k (n = 2) and padding rows contribute 0
+                if (p >= 0 && k < NN) {
+                    const uint32_t w = a.pool[(size_t)p * (NN / 2) + (k >> 1)];
+                    dv = (k & 1) ? (int)(w >> 16) : (int)(w & 0xffffu);
+                    sumd += dv;
+                }
+                v8[j] = (_Float16)(dv - 510);
+            }
+            a.dtiles[((size_t)tile * KS + s) * 64 + row + 32 * h] = __builtin_bit_cast(uint4, v8);
+        }
+    }
+    if (p >= 0)
+        sd2 = -a.negsd2[p];
+    const uint32_t e = p >= 0 ? (uint32_t)(sd2 - 1024 * sumd) - 0x58000000u : kMfmaPadConst;
+    // row = (i&3) + 8(i>>2) + 4h  ⇔  h = (row>>2)&1, i = (row&3) + 4(row>>3)
+    const uint32_t h = (row >> 2) & 1u, i = (row & 3u) + 4u * (row >> 3);
+    a.dconst[(size_t)tile * 32 + h * 16 + i] = e;
+}
+
+// ---------------------------------------------------------------------------
+// mfma_range_prep: B fragments of every range block (32 range slots) and transform:
+// lane l holds col l&31 (range slot), k = 16s + 8(l>>5) + j, value 128 − copy_t[k]
+// with copy_t[k] = r[inv_t(k)].  One thread per (block, t, s, lane).
+// ---------------------------------------------------------------------------
+struct MfmaRangePrepArgs {
+    const uint8_t* tgt;
+    uint32_t tstride;
+    const frac_grid_item* ranges;
+    const int32_t* slot_range; // [nblocks*32]
+    uint32_t nblocks;
+    uint32_t T;
+    uint4* rfrags;             // [nblocks][T][KS][64]
+    uint32_t* rconst;          // [nblocks*32]
+};
+
+template <int N>
+__global__ void __launch_bounds__(256) mfma_range_prep(MfmaRangePrepArgs a)
+{
+    constexpr int NN = N * N, KS = MfmaGeom<N>::KS;
+    const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t per_block = a.T * KS * 64u;
+    if (gid >= a.nblocks * per_block)
+        return;
+    const uint32_t b = gid / per_block, rem = gid % per_block;
+    const uint32_t t = rem / (KS * 64u), s = (rem / 64u) % KS, lane = rem % 64u;
+    const uint32_t col = lane & 31u, h = lane >> 5;
+    const int ri = a.slot_range[b * 32 + col];
+    _Float16 v8[8];
+    if (ri >= 0) {
+        const frac_grid_item rg = a.ranges[ri];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int k = 16 * (int)s + 8 * (int)h + j;
+            int rv = 128;
+            if (k < NN) {
+                const int pix = inv_index<N>((int)t, k);
+                rv = a.tgt[(size_t)(rg.y + pix / N) * a.tstride + rg.x + (pix % N)];
+            }
+            v8[j] = (_Float16)(128 - rv);
+        }
+        if (t == 0 && s == 0 && h == 0) {
+            int64_t sr = 0, sr2 = 0;
+            for (int q = 0; q < NN; ++q) {
+                const int rv = a.tgt[(size_t)(rg.y + q / N) * a.tstride + rg.x + (q % N)];
+                sr += rv;
+                sr2 += rv * rv;
+            }
+            a.rconst[b * 32 + col] = mfma_range_const(NN, sr, sr2);
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            v8[j] = (_Float16)0.0f;
+        if (t == 0 && s == 0 && h == 0)
+            a.rconst[b * 32 + col] = 0;
+    }
+    a.rfrags[((size_t)(b * a.T + t) * KS + s) * 64 + lane] = __builtin_bit_cast(uint4, v8);
+}
+
+// ---------------------------------------------------------------------------
+// search_mfma<N, T, HITS>: workgroup = 4 waves = 4 range blocks of one bucket; the
+// domain tiles [tile_begin, tile_end) of that bucket are staged through LDS and shared.
+// ---------------------------------------------------------------------------
+struct MfmaSearchArgs {
+    const uint4* dtiles;
+    const uint4* dconst;   // [ntiles][8] (= [2][16] u32)
+    const uint4* rfrags;
+    const uint32_t* rconst;
+    const uint4* work;     // per WG: {first block, number of blocks (1..4), tile_begin, tile_end}
+    uint32_t nwork;
+    uint32_t hitH;         // valid when HITS
+    uint2* entries;        // [nwork*4][T][64] {min v (0 = hit), tile}
+};
+
+template <int N, int T, bool HITS>
+__global__ void __launch_bounds__(256) search_mfma(MfmaSearchArgs a)
+{
+    constexpr int KS = MfmaGeom<N>::KS;
+    __shared__ uint4 lds_a[kTilesPerStage * KS * 64];
+    __shared__ uint4 lds_c[kTilesPerStage * 8];
+    const uint4 wk = a.work[blockIdx.x];
+    const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    const bool active = wv < wk.y;
+    const uint32_t blk = wk.x + (active ? wv : 0u);
+
+    half8_t bf[T][KS];
+#pragma unroll
+    for (int t = 0; t < T; ++t)
+#pragma unroll
+        for (int s = 0; s < KS; ++s)
+            bf[t][s] = __builtin_bit_cast(half8_t, a.rfrags[((size_t)(blk * T + t) * KS + s) * 64 + lane]);
+    uint32_t hl = 0;
+    if constexpr (HITS)
+        hl = a.hitH + a.rconst[blk * 32 + (lane & 31u)];
+
+    floatx16_t cinit;
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+        cinit[i] = 12582912.0f;
+    uint32_t best[T], btile[T];
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+        best[t] = 0xffffffffu;
+        btile[t] = 0;
+    }
+    const uint32_t h = lane >> 5;
+    for (uint32_t tb = wk.z; tb < wk.w; tb += kTilesPerStage) {
+        const uint32_t nt = min((uint32_t)kTilesPerStage, wk.w - tb);
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < nt * KS * 64u; i += 256u)
+            lds_a[i] = a.dtiles[(size_t)tb * KS * 64 + i];
+        for (uint32_t i = threadIdx.x; i < nt * 8u; i += 256u)
+            lds_c[i] = a.dconst[(size_t)tb * 8 + i];
+        __syncthreads();
+        for (uint32_t q = 0; q < nt; ++q) {
+            half8_t af[KS];
+#pragma unroll
+            for (int s = 0; s < KS; ++s)
+                af[s] = __builtin_bit_cast(half8_t, lds_a[(q * KS + s) * 64 + lane]);
+            uint32_t e[16];
+#pragma unroll
+            for (int c4 = 0; c4 < 4; ++c4) {
+                const uint4 v = lds_c[q * 8 + h * 4 + c4];
+                e[4 * c4 + 0] = v.x;
+                e[4 * c4 + 1] = v.y;
+                e[4 * c4 + 2] = v.z;
+                e[4 * c4 + 3] = v.w;
+            }
+            const uint32_t tile = tb + q;
+#pragma unroll
+            for (int t = 0; t < T; ++t) {
+                floatx16_t acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[0], bf[t][0], cinit, 0, 0, 0);
+#pragma unroll
+                for (int s = 1; s < KS; ++s)
+                    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[s], bf[t][s], acc, 0, 0, 0);
+                uint32_t m = 0xffffffffu;
+#pragma unroll
+                for (int i = 0; i < 16; ++i)
+                    m = min(m, (__float_as_uint(acc[i]) << 3) + e[i]);
+                if constexpr (HITS)
+                    m = m <= hl ? 0u : m;
+                if (m < best[t]) {
+                    best[t] = m;
+                    btile[t] = tile;
+                }
+            }
+        }
+    }
+    if (active) {
+#pragma unroll
+        for (int t = 0; t < T; ++t)
+            a.entries[((size_t)(blockIdx.x * 4u + wv) * T + t) * 64 + lane] = make_uint2(best[t], btile[t]);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// resolve_mfma: one thread per range.  Combines the per-(split, transform, lane-half)
+// entries of its block: hits first (the first (domain, transform) in order), else the
+// minimum error with ties to the earliest domain and the later transform; the exact
+// domain inside a tile is re-derived with integer arithmetic.  Writes the selection
+// key consumed by fit_winner.
+// ---------------------------------------------------------------------------
+struct MfmaResolveArgs {
+    const uint8_t* tgt;
+    uint32_t tstride;
+    const frac_grid_item* ranges;
+    const uint32_t* range_slot; // [nr] slot of each range
+    const uint32_t* blk_ptr;    // CSR over blocks → entry bases (work*4 + wave)
+    const uint32_t* blk_ent;
+    const uint2* entries;
+    const uint32_t* rconst;     // [nblocks*32]
+    const int32_t* tile_pos;    // [ntiles*32]
+    const uint32_t* pool;
+    const int32_t* negsd2;
+    uint32_t nr;
+    uint32_t T;
+    int64_t hitH;               // −1: no hits
+    unsigned long long* best_key;
+};
+
+template <int N>
+__device__ inline int64_t s16_of(const uint8_t (&r)[N * N], const uint32_t* __restrict__ pool,
+                                 const int32_t* __restrict__ negsd2, int p, int t, int64_t sr2)
+{
+    constexpr int NN = N * N;
+    const uint32_t* dp = pool + (size_t)p * (NN / 2);
+    int64_t X = 0;
+    for (int q = 0; q < NN; ++q) {
+        const int f = fwd_index<N>(t, q);
+        const uint32_t w = dp[f >> 1];
+        X += (int64_t)r[q] * (int64_t)((f & 1) ? (w >> 16) : (w & 0xffffu));
+    }
+    return 16 * sr2 - 8 * X - (int64_t)negsd2[p];
+}
+
+template <int N>
+__global__ void __launch_bounds__(256) resolve_mfma(MfmaResolveArgs a)
+{
+    constexpr int NN = N * N;
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= a.nr)
+        return;
+    const uint32_t slot = a.range_slot[r];
+    const uint32_t blk = slot >> 5, col = slot & 31u;
+    const uint32_t e0 = a.blk_ptr[blk], e1 = a.blk_ptr[blk + 1];
+    if (e0 == e1)
+        return; // no eligible domain: best_key stays "none"
+    uint32_t vmin = 0xffffffffu;
+    for (uint32_t e = e0; e < e1; ++e)
+        for (uint32_t t = 0; t < a.T; ++t)
+            for (uint32_t h = 0; h < 2; ++h)
+                vmin = min(vmin, a.entries[((size_t)a.blk_ent[e] * a.T + t) * 64 + col + 32 * h].x);
+    if (vmin == 0xffffffffu)
+        return;
+    const frac_grid_item rg = a.ranges[r];
+    uint8_t px[NN];
+    int64_t sr2 = 0;
+    for (int q = 0; q < NN; ++q) {
+        px[q] = a.tgt[(size_t)(rg.y + q / N) * a.tstride + rg.x + (q % N)];
+        sr2 += (int64_t)px[q] * px[q];
+    }
+    const bool hit = vmin == 0 && a.hitH >= 0;
+    const int64_t target = (int64_t)vmin - (int64_t)a.rconst[slot]; // S16 of the best miss
+    unsigned long long bestk = kKeyNone;
+    for (uint32_t e = e0; e < e1; ++e)
+        for (uint32_t t = 0; t < a.T; ++t)
+            for (uint32_t h = 0; h < 2; ++h) {
+                const uint2 en = a.entries[((size_t)a.blk_ent[e] * a.T + t) * 64 + col + 32 * h];
+                if (en.x != vmin)
+                    continue;
+                // rows of this lane half in increasing order: (i&3) + 8(i>>2) + 4h
+                for (int i = 0; i < 16; ++i) {
+                    const int row = (i & 3) + 8 * (i >> 2) + 4 * (int)h;
+                    const int p = a.tile_pos[en.y * 32 + row];
+                    if (p < 0)
+                        continue;
+                    const int64_t s16 = s16_of<N>(px, a.pool, a.negsd2, p, (int)t, sr2);
+                    if (hit ? (s16 <= a.hitH) : (s16 == target)) {
+                        const unsigned long long k =
+                            hit ? key_hit((uint32_t)p, t) : key_miss((uint64_t)s16, (uint32_t)p, a.T - 1 - t);
+                        bestk = k < bestk ? k : bestk;
+                        break;
+                    }
+                }
+            }
+    a.best_key[r] = bestk;
+}
+
+} // namespace fracenc

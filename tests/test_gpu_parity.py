@@ -14,7 +14,7 @@ pytestmark = pytest.mark.gpu
 
 # fixture name → engine support (the engine implements the ratio-2 path, n ∈ {2,4,8,16})
 RATIO2 = [n for n in GOLDEN_NAMES if n != "lenna_16to4"]
-ENGINES = [F.ENGINE_VALU]
+ENGINES = [F.ENGINE_VALU, F.ENGINE_MFMA]
 
 
 def as_oracle_fields(out):
@@ -23,6 +23,8 @@ def as_oracle_fields(out):
 
 
 def run_engine(p, meta, engine, tgt=None, ranges_idx=None):
+    if engine == F.ENGINE_MFMA and meta["tgt"] > 8:
+        pytest.skip("the MFMA engine covers n <= 8 (n = 16 runs on the VALU engine)")
     H, W = p.shape
     doms = F.create_uniform_grid(W, H, meta["src"], meta["src"] // 2)
     rngs = F.create_uniform_grid(W, H, meta["tgt"], meta["tgt"])
@@ -212,3 +214,27 @@ def test_full_4096_frame(engine):
     np.testing.assert_array_equal(out["distance"][exact], (s16[exact] / 16.0) / 256.0)
     assert st["fallback_ranges"] == int((~exact).sum())
     assert (out["sw"] == 16).all()
+
+
+def test_mfma_rejects_n16():
+    p = np.zeros((64, 64), np.uint8)
+    with F.Engine(0, 4, engine=F.ENGINE_MFMA) as e:
+        e.set_frame(p)
+        e.set_domains(F.create_uniform_grid(64, 64, 32, 16))
+        with pytest.raises(F.FracError):
+            e.search(F.create_uniform_grid(64, 64, 16, 16))
+
+
+def test_engines_agree_on_stress_frame():
+    """VALU and MFMA engines on a uniform-noise 1024² frame (S2): identical records."""
+    from fractencode_amd.synth import uniform_noise
+    p = uniform_noise(1024, 1024, 42)
+    outs = []
+    for eng in (F.ENGINE_VALU, F.ENGINE_MFMA):
+        with F.Engine(0, 8, False, 0.0, -1.0, eng) as e:
+            e.set_frame(p)
+            e.set_domains(F.create_uniform_grid(1024, 1024, 16, 8))
+            out, st = e.search(F.create_uniform_grid(1024, 1024, 8, 8))
+            assert st["engine"] == eng
+            outs.append(out)
+    assert outs[0].tobytes() == outs[1].tobytes()
