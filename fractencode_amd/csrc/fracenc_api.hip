@@ -528,7 +528,7 @@ int launch_mfma(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride)
         v.T = T;
         v.hitH = c->hitH;
         v.best_key = c->d_best_key.ptr;
-        resolve_mfma<N><<<(nr + 255) / 256, 256, 0, c->stream>>>(v);
+        resolve_mfma<N><<<(nr + 3) / 4, 256, 0, c->stream>>>(v);
     }
     return FRAC_OK;
 }

@@ -25,7 +25,7 @@ typedef _Float16 half8_t __attribute__((ext_vector_type(8)));
 typedef float floatx16_t __attribute__((ext_vector_type(16)));
 
 constexpr uint32_t kMfmaPadConst = 0x70000000u; // e' of padding domains: v ≈ 1.9e9, never wins
-constexpr int kTilesPerStage = 8;
+constexpr int kTilesPerStage = 4; // domain tiles per LDS stage (double-buffered)
 
 template <int N>
 struct MfmaGeom {
@@ -167,12 +167,27 @@ struct MfmaSearchArgs {
     uint2* entries;        // [nwork*4][T][64] {min v (0 = hit), tile}
 };
 
+template <int KS>
+__device__ inline void stage_tiles(uint4* dst, const uint4* __restrict__ dtiles, const uint4* __restrict__ dconst,
+                                   uint32_t tb, uint32_t nt)
+{
+    // LDS-DMA (global_load_lds_dwordx4): the LDS image is lane-linear per wave, which is
+    // exactly this [A fragments | epilogue constants] stage layout.
+    const uint32_t na = nt * KS * 64u, ntot = na + nt * 8u;
+    const uint32_t lane = threadIdx.x & 63u;
+    for (uint32_t i = threadIdx.x; i < ntot; i += 256u) {
+        const uint4* src = i < na ? dtiles + (size_t)tb * KS * 64 + i : dconst + (size_t)tb * 8 + (i - na);
+        __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)src,
+                                         (__attribute__((address_space(3))) void*)(dst + (i - lane)), 16, 0, 0);
+    }
+}
+
 template <int N, int T, bool HITS>
 __global__ void __launch_bounds__(256) search_mfma(MfmaSearchArgs a)
 {
     constexpr int KS = MfmaGeom<N>::KS;
-    __shared__ uint4 lds_a[kTilesPerStage * KS * 64];
-    __shared__ uint4 lds_c[kTilesPerStage * 8];
+    constexpr int STAGE = kTilesPerStage * KS * 64 + kTilesPerStage * 8; // uint4 per stage
+    __shared__ uint4 lds[2 * STAGE]; // one LDS object (see cdna_hip_programming.md §5 item 4a)
     const uint4 wk = a.work[blockIdx.x];
     const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
     const bool active = wv < wk.y;
@@ -199,23 +214,28 @@ __global__ void __launch_bounds__(256) search_mfma(MfmaSearchArgs a)
         btile[t] = 0;
     }
     const uint32_t h = lane >> 5;
-    for (uint32_t tb = wk.z; tb < wk.w; tb += kTilesPerStage) {
+    const uint32_t nstage = (wk.w - wk.z + kTilesPerStage - 1) / kTilesPerStage;
+    stage_tiles<KS>(lds, a.dtiles, a.dconst, wk.z, min((uint32_t)kTilesPerStage, wk.w - wk.z));
+    for (uint32_t st = 0; st < nstage; ++st) {
+        const uint32_t tb = wk.z + st * kTilesPerStage;
         const uint32_t nt = min((uint32_t)kTilesPerStage, wk.w - tb);
-        __syncthreads();
-        for (uint32_t i = threadIdx.x; i < nt * KS * 64u; i += 256u)
-            lds_a[i] = a.dtiles[(size_t)tb * KS * 64 + i];
-        for (uint32_t i = threadIdx.x; i < nt * 8u; i += 256u)
-            lds_c[i] = a.dconst[(size_t)tb * 8 + i];
-        __syncthreads();
+        __syncthreads(); // stage st landed (vmcnt) in every wave; stage st−1's reads are done
+        if (st + 1 < nstage) {
+            const uint32_t tn = tb + kTilesPerStage;
+            stage_tiles<KS>(lds + ((st + 1) & 1u) * STAGE, a.dtiles, a.dconst, tn,
+                            min((uint32_t)kTilesPerStage, wk.w - tn));
+        }
+        const uint4* la = lds + (st & 1u) * STAGE;
+        const uint4* lc = la + nt * KS * 64u;
         for (uint32_t q = 0; q < nt; ++q) {
             half8_t af[KS];
 #pragma unroll
             for (int s = 0; s < KS; ++s)
-                af[s] = __builtin_bit_cast(half8_t, lds_a[(q * KS + s) * 64 + lane]);
+                af[s] = __builtin_bit_cast(half8_t, la[(q * KS + s) * 64 + lane]);
             uint32_t e[16];
 #pragma unroll
             for (int c4 = 0; c4 < 4; ++c4) {
-                const uint4 v = lds_c[q * 8 + h * 4 + c4];
+                const uint4 v = lc[q * 8 + h * 4 + c4];
                 e[4 * c4 + 0] = v.x;
                 e[4 * c4 + 1] = v.y;
                 e[4 * c4 + 2] = v.z;
@@ -273,72 +293,89 @@ struct MfmaResolveArgs {
     unsigned long long* best_key;
 };
 
-template <int N>
-__device__ inline int64_t s16_of(const uint8_t (&r)[N * N], const uint32_t* __restrict__ pool,
-                                 const int32_t* __restrict__ negsd2, int p, int t, int64_t sr2)
+__device__ inline int fwd_rt(const Aff& a, int N, int q)
 {
-    constexpr int NN = N * N;
-    const uint32_t* dp = pool + (size_t)p * (NN / 2);
-    int64_t X = 0;
-    for (int q = 0; q < NN; ++q) {
-        const int f = fwd_index<N>(t, q);
-        const uint32_t w = dp[f >> 1];
-        X += (int64_t)r[q] * (int64_t)((f & 1) ? (w >> 16) : (w & 0xffffu));
-    }
-    return 16 * sr2 - 8 * X - (int64_t)negsd2[p];
+    const int x = q % N, y = q / N;
+    return (a.a4 * x + a.a5 * y + (a.a6 + a.a7) * (N - 1)) * N + a.a0 * x + a.a1 * y + (a.a2 + a.a3) * (N - 1);
 }
 
+// One wave per range.  Lane l covers tile row i = l>>2 of a candidate entry's lane half
+// and pixel slice g = l&3 (n²/4 pixels), so the 16 rows of a tile are evaluated at once
+// with exact integers; a ballot picks the first row (domain order) that matches.
 template <int N>
 __global__ void __launch_bounds__(256) resolve_mfma(MfmaResolveArgs a)
 {
-    constexpr int NN = N * N;
-    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    constexpr int NN = N * N, PG = (NN + 3) / 4; // pixels per slice
+    const uint32_t r = blockIdx.x * 4u + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
     if (r >= a.nr)
         return;
     const uint32_t slot = a.range_slot[r];
     const uint32_t blk = slot >> 5, col = slot & 31u;
     const uint32_t e0 = a.blk_ptr[blk], e1 = a.blk_ptr[blk + 1];
-    if (e0 == e1)
-        return; // no eligible domain: best_key stays "none"
+    const uint32_t nent = (e1 - e0) * a.T * 2u;
     uint32_t vmin = 0xffffffffu;
-    for (uint32_t e = e0; e < e1; ++e)
-        for (uint32_t t = 0; t < a.T; ++t)
-            for (uint32_t h = 0; h < 2; ++h)
-                vmin = min(vmin, a.entries[((size_t)a.blk_ent[e] * a.T + t) * 64 + col + 32 * h].x);
-    if (vmin == 0xffffffffu)
-        return;
-    const frac_grid_item rg = a.ranges[r];
-    uint8_t px[NN];
-    int64_t sr2 = 0;
-    for (int q = 0; q < NN; ++q) {
-        px[q] = a.tgt[(size_t)(rg.y + q / N) * a.tstride + rg.x + (q % N)];
-        sr2 += (int64_t)px[q] * px[q];
+    for (uint32_t j = lane; j < nent; j += 64) {
+        const uint32_t e = e0 + j / (2u * a.T), t = (j >> 1) % a.T, h = j & 1u;
+        vmin = min(vmin, a.entries[((size_t)a.blk_ent[e] * a.T + t) * 64 + col + 32 * h].x);
     }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1)
+        vmin = min(vmin, (uint32_t)__shfl_xor((int)vmin, o, 64));
+    if (vmin == 0xffffffffu)
+        return; // no eligible domain: best_key stays "none"
+    const frac_grid_item rg = a.ranges[r];
+    const int i = lane >> 2, g = lane & 3;
+    int px[PG];
+    int64_t sr2 = 0;
+#pragma unroll
+    for (int u = 0; u < PG; ++u) {
+        const int q = g * PG + u;
+        px[u] = q < NN ? (int)a.tgt[(size_t)(rg.y + q / N) * a.tstride + rg.x + (q % N)] : 0;
+        sr2 += px[u] * px[u];
+    }
+    sr2 += __shfl_xor(sr2, 1, 64);
+    sr2 += __shfl_xor(sr2, 2, 64);
     const bool hit = vmin == 0 && a.hitH >= 0;
     const int64_t target = (int64_t)vmin - (int64_t)a.rconst[slot]; // S16 of the best miss
     unsigned long long bestk = kKeyNone;
-    for (uint32_t e = e0; e < e1; ++e)
-        for (uint32_t t = 0; t < a.T; ++t)
-            for (uint32_t h = 0; h < 2; ++h) {
-                const uint2 en = a.entries[((size_t)a.blk_ent[e] * a.T + t) * 64 + col + 32 * h];
-                if (en.x != vmin)
-                    continue;
-                // rows of this lane half in increasing order: (i&3) + 8(i>>2) + 4h
-                for (int i = 0; i < 16; ++i) {
-                    const int row = (i & 3) + 8 * (i >> 2) + 4 * (int)h;
-                    const int p = a.tile_pos[en.y * 32 + row];
-                    if (p < 0)
-                        continue;
-                    const int64_t s16 = s16_of<N>(px, a.pool, a.negsd2, p, (int)t, sr2);
-                    if (hit ? (s16 <= a.hitH) : (s16 == target)) {
-                        const unsigned long long k =
-                            hit ? key_hit((uint32_t)p, t) : key_miss((uint64_t)s16, (uint32_t)p, a.T - 1 - t);
-                        bestk = k < bestk ? k : bestk;
-                        break;
-                    }
+    for (uint32_t j = 0; j < nent; ++j) { // wave-uniform loop over entries
+        const uint32_t e = e0 + j / (2u * a.T), t = (j >> 1) % a.T, h = j & 1u;
+        const uint2 en = a.entries[((size_t)a.blk_ent[e] * a.T + t) * 64 + col + 32 * h];
+        if (en.x != vmin)
+            continue;
+        const int row = (i & 3) + 8 * (i >> 2) + 4 * (int)h;
+        const int p = a.tile_pos[en.y * 32 + row];
+        const Aff af = lut((int)t);
+        int64_t X = 0;
+        if (p >= 0) {
+            const uint32_t* dp = a.pool + (size_t)p * (NN / 2);
+#pragma unroll
+            for (int u = 0; u < PG; ++u) {
+                const int q = g * PG + u;
+                if (q < NN) {
+                    const int f = fwd_rt(af, N, q);
+                    const uint32_t w = dp[f >> 1];
+                    X += (int64_t)px[u] * (int64_t)((f & 1) ? (w >> 16) : (w & 0xffffu));
                 }
             }
-    a.best_key[r] = bestk;
+        }
+        X += __shfl_xor(X, 1, 64);
+        X += __shfl_xor(X, 2, 64);
+        const int64_t s16 = p >= 0 ? 16 * sr2 - 8 * X - (int64_t)a.negsd2[p] : 0;
+        const bool ok = p >= 0 && g == 0 && (hit ? (s16 <= a.hitH) : (s16 == target));
+        const unsigned long long mask = __ballot(ok);
+        if (mask) {
+            const int first = __ffsll((long long)mask) - 1; // lowest lane = lowest row of the half
+            const int64_t s16f = __shfl(s16, first, 64);
+            const int pf = __shfl(p, first, 64);
+            const unsigned long long k =
+                hit ? key_hit((uint32_t)pf, t) : key_miss((uint64_t)s16f, (uint32_t)pf, a.T - 1 - t);
+            bestk = k < bestk ? k : bestk;
+        }
+    }
+    if (lane == 0)
+        a.best_key[r] = bestk;
 }
 
 } // namespace fracenc
