@@ -86,6 +86,7 @@ def main():
     import torch.distributed as dist
 
     import fractencode_amd as F
+    from fractencode_amd.distributed import RECORD_BYTES, gather_records, shard_bounds, shard_capacity
     from fractencode_amd.synth import value_noise
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -104,8 +105,9 @@ def main():
     doms = F.create_uniform_grid(S, S, 16, 8)
     rngs = F.create_uniform_grid(S, S, 8, 8)
     nr_total = len(rngs)
-    per = (nr_total + world - 1) // world
-    mine = rngs[rank * per:min(nr_total, (rank + 1) * per)]
+    per = shard_capacity(nr_total, world)
+    start, stop = shard_bounds(nr_total, world, rank)
+    mine = rngs[start:stop]
     engine_id = {"auto": F.ENGINE_AUTO, "valu": F.ENGINE_VALU, "mfma": F.ENGINE_MFMA}[args.engine]
 
     stream = torch.cuda.current_stream(dev)
@@ -115,14 +117,13 @@ def main():
     eng.set_frame(d_frame)
     eng.set_domains(doms)
     eng.set_ranges(mine)
-    mine_bytes = torch.empty(per * 64, dtype=torch.uint8, device=dev)
-    gathered = torch.empty(world * per * 64, dtype=torch.uint8, device=dev) if world > 1 else None
+    mine_bytes = torch.zeros(per * RECORD_BYTES, dtype=torch.uint8, device=dev)
 
     def step():
         eng.run()
-        if world > 1:
+        if world > 1:  # RCCL all-gather of the 64-byte winner records (same stream)
             eng.copy_results_device(mine_bytes.data_ptr())
-            dist.all_gather_into_tensor(gathered, mine_bytes)
+            gather_records(mine_bytes, nr_total, world)
 
     for _ in range(args.warmup):
         step()
