@@ -8,6 +8,7 @@
 //   search order / ties    encode/TransformEstimator2.hpp:29-48
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -456,13 +457,44 @@ int prepare(frac_ctx* c)
     return FRAC_OK;
 }
 
+template <int N, int T, int VAR>
+void launch_search_mfma_v(frac_ctx* c, const MfmaSearchArgs& a)
+{
+    // H = 0 (the default threshold): a hit is S16 = 0, the smallest possible error, so
+    // the plain first-minimum search already finds the first hit
+    if (c->hitH > 0)
+        search_mfma<N, T, true, VAR><<<(unsigned)c->m_work.size(), 256, 0, c->stream>>>(a);
+    else
+        search_mfma<N, T, false, VAR><<<(unsigned)c->m_work.size(), 256, 0, c->stream>>>(a);
+}
+
+// FRAC_MFMA_VARIANT (tuning knob, read per run): schedule variant of search_mfma
+inline int mfma_variant()
+{
+    const char* v = getenv("FRAC_MFMA_VARIANT");
+    return v ? atoi(v) : kDefaultMfmaVariant;
+}
+
 template <int N, int T>
 void launch_search_mfma(frac_ctx* c, const MfmaSearchArgs& a)
 {
-    if (c->hitH >= 0)
-        search_mfma<N, T, true><<<(unsigned)c->m_work.size(), 256, 0, c->stream>>>(a);
-    else
-        search_mfma<N, T, false><<<(unsigned)c->m_work.size(), 256, 0, c->stream>>>(a);
+    switch (mfma_variant()) {
+    case 0: launch_search_mfma_v<N, T, 0>(c, a); break;
+    case 1: launch_search_mfma_v<N, T, 1>(c, a); break;
+    case 2: launch_search_mfma_v<N, T, 2>(c, a); break;
+    case 3: launch_search_mfma_v<N, T, 3>(c, a); break;
+    case 4: launch_search_mfma_v<N, T, 4>(c, a); break;
+    case 5: launch_search_mfma_v<N, T, 5>(c, a); break;
+    case 6: launch_search_mfma_v<N, T, 6>(c, a); break;
+    case 7: launch_search_mfma_v<N, T, 7>(c, a); break;
+    case 8: launch_search_mfma_v<N, T, 8>(c, a); break;   // ablation: 1-value epilogue
+    case 16: launch_search_mfma_v<N, T, 16>(c, a); break; // ablation: no MFMA
+    case 32: launch_search_mfma_v<N, T, 32>(c, a); break; // s_setprio around MFMA clusters
+    case 64: launch_search_mfma_v<N, T, 64>(c, a); break; // late epilogue-constant reads
+    case 96: launch_search_mfma_v<N, T, 96>(c, a); break;
+    case 98: launch_search_mfma_v<N, T, 98>(c, a); break;
+    default: launch_search_mfma_v<N, T, kDefaultMfmaVariant>(c, a); break;
+    }
 }
 
 template <int N>
@@ -522,6 +554,7 @@ int launch_mfma(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride)
         v.entries = c->d_m_entries.ptr;
         v.rconst = c->d_m_rconst.ptr;
         v.tile_pos = c->d_m_tile_pos.ptr;
+        v.ntiles = c->ntiles;
         v.pool = c->d_pool.ptr;
         v.negsd2 = c->d_negsd2.ptr;
         v.nr = nr;
@@ -570,7 +603,7 @@ int launch_all(frac_ctx* c)
         a.hitH = (int32_t)std::max<int64_t>(c->hitH, 0);
         a.best_key = c->d_best_key.ptr;
         const dim3 grid((a.nwork + 3) / 4), block(256);
-        const bool hits = c->hitH >= 0;
+        const bool hits = c->hitH > 0; // H = 0: the first maximum of w is the first hit
         if constexpr (N == 16) {
             if (hits)
                 search_valu<N, 1, true><<<grid, block, 0, c->stream>>>(a);

@@ -311,7 +311,9 @@ __global__ void __launch_bounds__(256) fit_winner(FitArgs a)
         return;
     }
     const uint32_t p = key_pos(key);
-    const bool hit = (key >> 63) == 0;
+    // a miss-format key whose error meets H is a hit too (engines skip the hit sentinel
+    // when H = 0, where a hit is the minimum error S16 = 0)
+    const bool hit = (key >> 63) == 0 || (a.hitH >= 0 && (int64_t)((key >> 27) & 0xffffffffull) <= a.hitH);
     const frac_grid_item d = a.doms[a.porig[p]];
     const uint32_t* dp = a.pool + (size_t)p * (NN / 2);
 

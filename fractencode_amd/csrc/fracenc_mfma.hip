@@ -26,6 +26,7 @@ typedef float floatx16_t __attribute__((ext_vector_type(16)));
 
 constexpr uint32_t kMfmaPadConst = 0x70000000u; // e' of padding domains: v ≈ 1.9e9, never wins
 constexpr int kTilesPerStage = 4; // domain tiles per LDS stage (double-buffered)
+constexpr int kDefaultMfmaVariant = 2; // two v_min3 chains (A/B: tools/ab_mfma.py)
 
 template <int N>
 struct MfmaGeom {
@@ -182,12 +183,134 @@ __device__ inline void stage_tiles(uint4* dst, const uint4* __restrict__ dtiles,
     }
 }
 
-template <int N, int T, bool HITS>
+template <int N, int T, bool PRIO = false>
+__device__ inline floatx16_t mfma_tile(const half8_t (&af)[MfmaGeom<N>::KS], const half8_t (&bt)[MfmaGeom<N>::KS],
+                                       const floatx16_t& cinit)
+{
+    if constexpr (PRIO)
+        __builtin_amdgcn_s_setprio(1);
+    floatx16_t acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[0], bt[0], cinit, 0, 0, 0);
+#pragma unroll
+    for (int s = 1; s < MfmaGeom<N>::KS; ++s)
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[s], bt[s], acc, 0, 0, 0);
+    if constexpr (PRIO)
+        __builtin_amdgcn_s_setprio(0);
+    return acc;
+}
+
+// v = (bits << 3) + e' for the 16 rows a lane holds, folded into the running min m
+// with two independent v_min3 chains (halves the dependency depth).
+template <bool TWO_CHAINS>
+__device__ inline uint32_t epilogue_min(const floatx16_t& acc, const uint32_t (&e)[16], uint32_t m)
+{
+    if constexpr (!TWO_CHAINS) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+            m = min(m, (__float_as_uint(acc[i]) << 3) + e[i]);
+        return m;
+    }
+    uint32_t m0 = m, m1 = 0xffffffffu;
+#pragma unroll
+    for (int i = 0; i < 16; i += 4) {
+        m0 = min(min(m0, (__float_as_uint(acc[i]) << 3) + e[i]), (__float_as_uint(acc[i + 1]) << 3) + e[i + 1]);
+        m1 = min(min(m1, (__float_as_uint(acc[i + 2]) << 3) + e[i + 2]), (__float_as_uint(acc[i + 3]) << 3) + e[i + 3]);
+    }
+    return min(m0, m1);
+}
+
+// Compute the nt tiles of one LDS stage: per tile the A fragments and epilogue constants
+// come from LDS; the T transforms are software-pipelined so the MFMAs of transform t+1
+// are in flight while the VALU epilogue of transform t runs.
+template <int N, int T, int VAR>
+__device__ inline void compute_stage(const uint4* __restrict__ la, uint32_t nt, uint32_t lane,
+                                     const half8_t (&bf)[T][MfmaGeom<N>::KS], const floatx16_t& cinit,
+                                     uint32_t (&cm)[T])
+{
+    constexpr int KS = MfmaGeom<N>::KS;
+    const uint4* lc = la + nt * KS * 64u;
+    const uint32_t h = lane >> 5;
+    for (uint32_t q = 0; q < nt; ++q) {
+        half8_t af[KS];
+#pragma unroll
+        for (int s = 0; s < KS; ++s)
+            af[s] = __builtin_bit_cast(half8_t, la[(q * KS + s) * 64 + lane]);
+        uint32_t e[16];
+        auto read_e = [&]() {
+#pragma unroll
+            for (int c4 = 0; c4 < 4; ++c4) {
+                const uint4 v = lc[q * 8 + h * 4 + c4];
+                e[4 * c4 + 0] = v.x;
+                e[4 * c4 + 1] = v.y;
+                e[4 * c4 + 2] = v.z;
+                e[4 * c4 + 3] = v.w;
+            }
+        };
+        constexpr bool PRIO = (VAR & 32) != 0, LATE_E = (VAR & 64) != 0;
+        if constexpr (LATE_E) {
+            // the first transform's MFMAs wait only for the A fragments; the epilogue
+            // constants are read while they run
+            const floatx16_t acc0 = mfma_tile<N, T, PRIO>(af, bf[0], cinit);
+            __builtin_amdgcn_sched_barrier(0);
+            read_e();
+            cm[0] = epilogue_min<(VAR & 2) != 0>(acc0, e, cm[0]);
+#pragma unroll
+            for (int t = 1; t < T; ++t)
+                cm[t] = epilogue_min<(VAR & 2) != 0>(mfma_tile<N, T, PRIO>(af, bf[t], cinit), e, cm[t]);
+            continue;
+        }
+        read_e();
+        if constexpr ((VAR & 1) != 0) {
+            floatx16_t prev = mfma_tile<N, T>(af, bf[0], cinit);
+#pragma unroll
+            for (int t = 1; t < T; ++t) {
+                const floatx16_t cur = mfma_tile<N, T>(af, bf[t], cinit);
+                cm[t - 1] = epilogue_min<(VAR & 2) != 0>(prev, e, cm[t - 1]);
+                prev = cur;
+            }
+            cm[T - 1] = epilogue_min<(VAR & 2) != 0>(prev, e, cm[T - 1]);
+        } else if constexpr ((VAR & 8) != 0) {
+            // ABLATION (tuning only, wrong results): epilogue cut to one value per transform
+#pragma unroll
+            for (int t = 0; t < T; ++t) {
+                const floatx16_t acc = mfma_tile<N, T>(af, bf[t], cinit);
+                cm[t] = min(cm[t], (__float_as_uint(acc[0]) << 3) + e[0]);
+                asm volatile("" ::"v"(acc));
+            }
+        } else if constexpr ((VAR & 16) != 0) {
+            // ABLATION (tuning only, wrong results): no MFMA, epilogue on operand bits
+#pragma unroll
+            for (int t = 0; t < T; ++t) {
+                floatx16_t acc;
+#pragma unroll
+                for (int i = 0; i < 16; ++i)
+                    acc[i] = __builtin_bit_cast(float, (uint32_t)__builtin_bit_cast(uint4, af[i & (KS - 1)]).x + i + t);
+                cm[t] = epilogue_min<false>(acc, e, cm[t]);
+            }
+        } else {
+#pragma unroll
+            for (int t = 0; t < T; ++t)
+                cm[t] = epilogue_min<(VAR & 2) != 0>(mfma_tile<N, T, PRIO>(af, bf[t], cinit), e, cm[t]);
+        }
+    }
+}
+
+// Schedule variant bits (A/B'd in one process by tools/ab_mfma.py):
+//   1: software-pipelined transforms (MFMAs of t+1 in flight during the epilogue of t)
+//   2: two independent v_min3 chains in the epilogue
+//   4: the two LDS stage buffers are distinct __shared__ objects (the LDS-DMA into one
+//      provably does not alias ds_reads of the other, so no vmcnt(0) before each tile)
+template <int N, int T, bool HITS, int VAR>
 __global__ void __launch_bounds__(256) search_mfma(MfmaSearchArgs a)
 {
     constexpr int KS = MfmaGeom<N>::KS;
     constexpr int STAGE = kTilesPerStage * KS * 64 + kTilesPerStage * 8; // uint4 per stage
-    __shared__ uint4 lds[2 * STAGE]; // one LDS object (see cdna_hip_programming.md §5 item 4a)
+    // two distinct LDS objects: the stage loop is unrolled by two so the LDS-DMA into
+    // one buffer provably does not alias the ds_reads of the other (no vmcnt(0) drain)
+    constexpr bool SPLIT = (VAR & 4) != 0;
+    __shared__ uint4 lds0[SPLIT ? STAGE : 2 * STAGE];
+    __shared__ uint4 lds1[SPLIT ? STAGE : 1];
+    uint4* const buf0 = lds0;
+    uint4* const buf1 = SPLIT ? lds1 : lds0 + STAGE;
     const uint4 wk = a.work[blockIdx.x];
     const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
     const bool active = wv < wk.y;
@@ -213,52 +336,48 @@ __global__ void __launch_bounds__(256) search_mfma(MfmaSearchArgs a)
         best[t] = 0xffffffffu;
         btile[t] = 0;
     }
-    const uint32_t h = lane >> 5;
-    const uint32_t nstage = (wk.w - wk.z + kTilesPerStage - 1) / kTilesPerStage;
-    stage_tiles<KS>(lds, a.dtiles, a.dconst, wk.z, min((uint32_t)kTilesPerStage, wk.w - wk.z));
-    for (uint32_t st = 0; st < nstage; ++st) {
-        const uint32_t tb = wk.z + st * kTilesPerStage;
-        const uint32_t nt = min((uint32_t)kTilesPerStage, wk.w - tb);
-        __syncthreads(); // stage st landed (vmcnt) in every wave; stage st−1's reads are done
-        if (st + 1 < nstage) {
-            const uint32_t tn = tb + kTilesPerStage;
-            stage_tiles<KS>(lds + ((st + 1) & 1u) * STAGE, a.dtiles, a.dconst, tn,
-                            min((uint32_t)kTilesPerStage, wk.w - tn));
+    auto finish_stage = [&](const uint32_t (&cm)[T], uint32_t tb) {
+#pragma unroll
+        for (int t = 0; t < T; ++t) {
+            uint32_t m = cm[t];
+            if constexpr (HITS)
+                m = m <= hl ? 0u : m; // any hit in the chunk: the first-hit chunk wins
+            if (m < best[t]) {
+                best[t] = m;
+                btile[t] = tb;
+            }
         }
-        const uint4* la = lds + (st & 1u) * STAGE;
-        const uint4* lc = la + nt * KS * 64u;
-        for (uint32_t q = 0; q < nt; ++q) {
-            half8_t af[KS];
+    };
+    const uint32_t nstage = (wk.w - wk.z + kTilesPerStage - 1) / kTilesPerStage;
+    auto stage_nt = [&](uint32_t st) { return min((uint32_t)kTilesPerStage, wk.w - (wk.z + st * kTilesPerStage)); };
+    if (nstage)
+        stage_tiles<KS>(buf0, a.dtiles, a.dconst, wk.z, stage_nt(0));
+    for (uint32_t st = 0; st < nstage; st += 2) {
+        // even stage: read lds0, prefetch stage st+1 into lds1
+        {
+            const uint32_t tb = wk.z + st * kTilesPerStage;
+            __syncthreads();
+            if (st + 1 < nstage)
+                stage_tiles<KS>(buf1, a.dtiles, a.dconst, tb + kTilesPerStage, stage_nt(st + 1));
+            uint32_t cm[T];
 #pragma unroll
-            for (int s = 0; s < KS; ++s)
-                af[s] = __builtin_bit_cast(half8_t, la[(q * KS + s) * 64 + lane]);
-            uint32_t e[16];
+            for (int t = 0; t < T; ++t)
+                cm[t] = 0xffffffffu;
+            compute_stage<N, T, VAR>(buf0, stage_nt(st), lane, bf, cinit, cm);
+            finish_stage(cm, tb);
+        }
+        if (st + 1 < nstage) {
+            // odd stage: read lds1, prefetch stage st+2 into lds0
+            const uint32_t tb = wk.z + (st + 1) * kTilesPerStage;
+            __syncthreads();
+            if (st + 2 < nstage)
+                stage_tiles<KS>(buf0, a.dtiles, a.dconst, tb + kTilesPerStage, stage_nt(st + 2));
+            uint32_t cm[T];
 #pragma unroll
-            for (int c4 = 0; c4 < 4; ++c4) {
-                const uint4 v = lc[q * 8 + h * 4 + c4];
-                e[4 * c4 + 0] = v.x;
-                e[4 * c4 + 1] = v.y;
-                e[4 * c4 + 2] = v.z;
-                e[4 * c4 + 3] = v.w;
-            }
-            const uint32_t tile = tb + q;
-#pragma unroll
-            for (int t = 0; t < T; ++t) {
-                floatx16_t acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[0], bf[t][0], cinit, 0, 0, 0);
-#pragma unroll
-                for (int s = 1; s < KS; ++s)
-                    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[s], bf[t][s], acc, 0, 0, 0);
-                uint32_t m = 0xffffffffu;
-#pragma unroll
-                for (int i = 0; i < 16; ++i)
-                    m = min(m, (__float_as_uint(acc[i]) << 3) + e[i]);
-                if constexpr (HITS)
-                    m = m <= hl ? 0u : m;
-                if (m < best[t]) {
-                    best[t] = m;
-                    btile[t] = tile;
-                }
-            }
+            for (int t = 0; t < T; ++t)
+                cm[t] = 0xffffffffu;
+            compute_stage<N, T, VAR>(buf1, stage_nt(st + 1), lane, bf, cinit, cm);
+            finish_stage(cm, tb);
         }
     }
     if (active) {
@@ -285,6 +404,7 @@ struct MfmaResolveArgs {
     const uint2* entries;
     const uint32_t* rconst;     // [nblocks*32]
     const int32_t* tile_pos;    // [ntiles*32]
+    uint32_t ntiles;
     const uint32_t* pool;
     const int32_t* negsd2;
     uint32_t nr;
@@ -336,8 +456,9 @@ __global__ void __launch_bounds__(256) resolve_mfma(MfmaResolveArgs a)
     }
     sr2 += __shfl_xor(sr2, 1, 64);
     sr2 += __shfl_xor(sr2, 2, 64);
-    const bool hit = vmin == 0 && a.hitH >= 0;
-    const int64_t target = (int64_t)vmin - (int64_t)a.rconst[slot]; // S16 of the best miss
+    const int64_t target = (int64_t)vmin - (int64_t)a.rconst[slot]; // best S16 (when vmin != sentinel)
+    // hits: the sentinel 0 (kernel run with H > 0), or a best error that meets H = 0
+    const bool hit = a.hitH >= 0 && (vmin == 0 || target <= a.hitH);
     unsigned long long bestk = kKeyNone;
     for (uint32_t j = 0; j < nent; ++j) { // wave-uniform loop over entries
         const uint32_t e = e0 + j / (2u * a.T), t = (j >> 1) % a.T, h = j & 1u;
@@ -345,33 +466,38 @@ __global__ void __launch_bounds__(256) resolve_mfma(MfmaResolveArgs a)
         if (en.x != vmin)
             continue;
         const int row = (i & 3) + 8 * (i >> 2) + 4 * (int)h;
-        const int p = a.tile_pos[en.y * 32 + row];
         const Aff af = lut((int)t);
-        int64_t X = 0;
-        if (p >= 0) {
-            const uint32_t* dp = a.pool + (size_t)p * (NN / 2);
+        // the entry names the first tile of the chunk that attained the minimum: scan the
+        // chunk's tiles in order; the first matching row is the earliest domain
+        for (uint32_t tile = en.y; tile < min(en.y + (uint32_t)kTilesPerStage, a.ntiles); ++tile) {
+            const int p = a.tile_pos[tile * 32 + row];
+            int64_t X = 0;
+            if (p >= 0) {
+                const uint32_t* dp = a.pool + (size_t)p * (NN / 2);
 #pragma unroll
-            for (int u = 0; u < PG; ++u) {
-                const int q = g * PG + u;
-                if (q < NN) {
-                    const int f = fwd_rt(af, N, q);
-                    const uint32_t w = dp[f >> 1];
-                    X += (int64_t)px[u] * (int64_t)((f & 1) ? (w >> 16) : (w & 0xffffu));
+                for (int u = 0; u < PG; ++u) {
+                    const int q = g * PG + u;
+                    if (q < NN) {
+                        const int f = fwd_rt(af, N, q);
+                        const uint32_t w = dp[f >> 1];
+                        X += (int64_t)px[u] * (int64_t)((f & 1) ? (w >> 16) : (w & 0xffffu));
+                    }
                 }
             }
-        }
-        X += __shfl_xor(X, 1, 64);
-        X += __shfl_xor(X, 2, 64);
-        const int64_t s16 = p >= 0 ? 16 * sr2 - 8 * X - (int64_t)a.negsd2[p] : 0;
-        const bool ok = p >= 0 && g == 0 && (hit ? (s16 <= a.hitH) : (s16 == target));
-        const unsigned long long mask = __ballot(ok);
-        if (mask) {
-            const int first = __ffsll((long long)mask) - 1; // lowest lane = lowest row of the half
-            const int64_t s16f = __shfl(s16, first, 64);
-            const int pf = __shfl(p, first, 64);
-            const unsigned long long k =
-                hit ? key_hit((uint32_t)pf, t) : key_miss((uint64_t)s16f, (uint32_t)pf, a.T - 1 - t);
-            bestk = k < bestk ? k : bestk;
+            X += __shfl_xor(X, 1, 64);
+            X += __shfl_xor(X, 2, 64);
+            const int64_t s16 = p >= 0 ? 16 * sr2 - 8 * X - (int64_t)a.negsd2[p] : 0;
+            const bool ok = p >= 0 && g == 0 && (hit ? (s16 <= a.hitH) : (s16 == target));
+            const unsigned long long mask = __ballot(ok);
+            if (mask) {
+                const int first = __ffsll((long long)mask) - 1; // lowest lane = lowest row of the half
+                const int64_t s16f = __shfl(s16, first, 64);
+                const int pf = __shfl(p, first, 64);
+                const unsigned long long k =
+                    hit ? key_hit((uint32_t)pf, t) : key_miss((uint64_t)s16f, (uint32_t)pf, a.T - 1 - t);
+                bestk = k < bestk ? k : bestk;
+                break;
+            }
         }
     }
     if (lane == 0)
