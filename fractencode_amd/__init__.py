@@ -86,6 +86,10 @@ def lib() -> C.CDLL:
             "frac_get_stream": (vp, [vp]),
             "frac_device_results": (vp, [vp]),
             "frac_copy_results_device": (i32, [vp, vp]),
+            "frac_decode": (i32, [vp, vp, sz, u32, u32, i32, C.c_double, vp, C.POINTER(C.c_int),
+                                  C.POINTER(C.c_double)]),
+            "frac_decode_results": (i32, [vp, u32, u32, i32, C.c_double, vp, C.POINTER(C.c_int),
+                                          C.POINTER(C.c_double)]),
             "frac_uniform_grid": (sz, [u32, u32, u32, u32, vp, sz]),
             "frac_classify": (i32, [vp, u32, u32, u32, vp, sz]),
             "frac_transform_index": (i32, [u32, u32, u32]),
@@ -238,6 +242,22 @@ class Engine:
     def copy_results_device(self, dst_ptr: int) -> None:
         """Async D2D copy of the last run's results (64 B each) to a device buffer."""
         self._check(lib().frac_copy_results_device(self._ctx, C.c_void_p(dst_ptr)))
+
+    def decode(self, items: np.ndarray | None, width: int, height: int, max_iter: int = -1, rms_eps: float = 1e-5,
+               initial: np.ndarray | None = None):
+        """Decoder2::decode on the GPU. items=None decodes the last run's results on the device.
+        Returns (plane, iterations, rms)."""
+        plane = np.zeros((height, width), np.uint8) if initial is None else np.ascontiguousarray(initial, np.uint8).copy()
+        it = C.c_int()
+        rms = C.c_double()
+        if items is None:
+            self._check(lib().frac_decode_results(self._ctx, width, height, max_iter, rms_eps, plane.ctypes.data,
+                                                  C.byref(it), C.byref(rms)))
+        else:
+            items = np.ascontiguousarray(items, dtype=ENCODE_ITEM)
+            self._check(lib().frac_decode(self._ctx, items.ctypes.data if len(items) else None, len(items), width,
+                                          height, max_iter, rms_eps, plane.ctypes.data, C.byref(it), C.byref(rms)))
+        return plane, it.value, rms.value
 
     def device_results_ptr(self) -> int:
         return lib().frac_device_results(self._ctx) or 0

@@ -16,6 +16,7 @@
 #include "fracenc_common.h"
 #include "fracenc_kernels.hip"
 #include "fracenc_mfma.hip"
+#include "fracenc_decode.hip"
 
 using namespace fracenc;
 
@@ -169,6 +170,12 @@ struct frac_ctx {
     DBuf<uint32_t> d_m_range_slot, d_m_blk_ptr, d_m_blk_ent, d_m_rconst, d_m_dconst;
     DBuf<uint4> d_m_work, d_m_dtiles, d_m_rfrags;
     DBuf<uint2> d_m_entries;
+
+    // decoder state
+    DBuf<uint8_t> d_dec_src, d_dec_tgt;
+    DBuf<frac_encode_item> d_dec_items;
+    DBuf<unsigned long long> d_dec_sum;
+    unsigned long long* h_dec_sum = nullptr; // pinned
 
     std::vector<RangeAux> h_aux;
     hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
@@ -756,6 +763,12 @@ void frac_destroy(frac_ctx* c)
     c->d_m_dtiles.release();
     c->d_m_rfrags.release();
     c->d_m_entries.release();
+    c->d_dec_src.release();
+    c->d_dec_tgt.release();
+    c->d_dec_items.release();
+    c->d_dec_sum.release();
+    if (c->h_dec_sum)
+        (void)hipHostFree(c->h_dec_sum);
     for (auto& ev : c->ev)
         if (ev)
             (void)hipEventDestroy(ev);
@@ -962,6 +975,92 @@ int frac_set_stream(frac_ctx* c, void* s)
 void* frac_get_stream(frac_ctx* c) { return c ? reinterpret_cast<void*>(c->stream) : nullptr; }
 
 const frac_encode_item* frac_device_results(frac_ctx* c) { return c ? c->d_out.ptr : nullptr; }
+
+static int decode_impl(frac_ctx* c, const frac_encode_item* d_items, size_t n, uint32_t w, uint32_t h, int max_iter,
+                       double eps, uint8_t* plane, int* iterations, double* rms)
+{
+    if (!plane || w == 0 || h == 0)
+        return c->fail(FRAC_E_INVALID, "decode: invalid plane");
+    const uint32_t stride = (w + 63u) & ~63u;
+    const size_t bytes = (size_t)stride * (h + 1);
+    FRAC_HIP(c, c->d_dec_src.ensure(bytes));
+    FRAC_HIP(c, c->d_dec_tgt.ensure(bytes));
+    FRAC_HIP(c, c->d_dec_sum.ensure(1));
+    if (!c->h_dec_sum)
+        FRAC_HIP(c, hipHostMalloc(reinterpret_cast<void**>(&c->h_dec_sum), sizeof(unsigned long long)));
+    // Decoder2::decode: source filled with 100, target = the caller's plane
+    FRAC_HIP(c, hipMemsetAsync(c->d_dec_src.ptr, 100, bytes, c->stream));
+    FRAC_HIP(c, hipMemsetAsync(c->d_dec_tgt.ptr, 0, bytes, c->stream));
+    FRAC_HIP(c, hipMemcpy2DAsync(c->d_dec_tgt.ptr, stride, plane, w, w, h, hipMemcpyHostToDevice, c->stream));
+    const int iters = max_iter < 0 ? 300 : max_iter;
+    DecodeArgs a;
+    a.src = c->d_dec_src.ptr;
+    a.tgt = c->d_dec_tgt.ptr;
+    a.stride = stride;
+    a.items = d_items;
+    a.n = (uint32_t)n;
+    const uint32_t rms_blocks = (uint32_t)std::min<size_t>(1024, ((size_t)w * h + 255) / 256);
+    int i = 0;
+    double r = 0.0;
+    for (; i < iters; ++i) {
+        if (n)
+            decode_apply<<<(unsigned)((n + 3) / 4), 256, 0, c->stream>>>(a);
+        FRAC_HIP(c, hipMemsetAsync(c->d_dec_sum.ptr, 0, sizeof(unsigned long long), c->stream));
+        decode_rms<<<rms_blocks, 256, 0, c->stream>>>(c->d_dec_src.ptr, c->d_dec_tgt.ptr, w, h, stride, c->d_dec_sum.ptr);
+        FRAC_HIP(c, hipMemcpyAsync(c->h_dec_sum, c->d_dec_sum.ptr, sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                                   c->stream));
+        FRAC_HIP(c, hipStreamSynchronize(c->stream));
+        // the reference accumulates in int32 (metrics.h:29): reproduce its wrap-around
+        const int32_t s32 = (int32_t)(uint32_t)(*c->h_dec_sum & 0xffffffffull);
+        r = (double)s32 / (double)((uint64_t)w * h);
+        if (r < eps)
+            break;
+        FRAC_HIP(c, hipMemcpyAsync(c->d_dec_src.ptr, c->d_dec_tgt.ptr, bytes, hipMemcpyDeviceToDevice, c->stream));
+    }
+    FRAC_HIP(c, hipMemcpy2DAsync(plane, w, c->d_dec_tgt.ptr, stride, w, h, hipMemcpyDeviceToHost, c->stream));
+    FRAC_HIP(c, hipStreamSynchronize(c->stream));
+    FRAC_HIP(c, hipGetLastError());
+    if (iterations)
+        *iterations = i;
+    if (rms)
+        *rms = r;
+    return FRAC_OK;
+}
+
+int frac_decode(frac_ctx* c, const frac_encode_item* items, size_t n, uint32_t w, uint32_t h, int max_iter,
+                double rms_eps, uint8_t* plane, int* iterations, double* rms)
+{
+    if (!c)
+        return FRAC_E_INVALID;
+    if (n && !items)
+        return c->fail(FRAC_E_INVALID, "decode: items is NULL");
+    for (size_t i = 0; i < n; ++i) {
+        const frac_encode_item& e = items[i];
+        if ((uint64_t)e.x + e.w > w || (uint64_t)e.y + e.h > h || e.match.score.transform < 0 ||
+            e.match.score.transform > 7 ||
+            (e.match.sw && ((uint64_t)e.match.x + e.match.sw > w || (uint64_t)e.match.y + e.match.sh > h)))
+            return c->fail(FRAC_E_INVALID, "decode: item outside the plane or bad transform");
+    }
+    FRAC_HIP(c, hipSetDevice(c->device));
+    FRAC_HIP(c, c->d_dec_items.ensure(n));
+    if (n)
+        FRAC_HIP(c, hipMemcpyAsync(c->d_dec_items.ptr, items, n * sizeof(frac_encode_item), hipMemcpyHostToDevice,
+                                   c->stream));
+    return decode_impl(c, c->d_dec_items.ptr, n, w, h, max_iter, rms_eps, plane, iterations, rms);
+}
+
+int frac_decode_results(frac_ctx* c, uint32_t w, uint32_t h, int max_iter, double rms_eps, uint8_t* plane,
+                        int* iterations, double* rms)
+{
+    if (!c)
+        return FRAC_E_INVALID;
+    if (!c->ran)
+        return c->fail(FRAC_E_STATE, "decode: frac_run has not been called");
+    if (c->src.w > w || c->src.h > h || c->tgt.w > w || c->tgt.h > h)
+        return c->fail(FRAC_E_INVALID, "decode: plane smaller than the encoded planes");
+    FRAC_HIP(c, hipSetDevice(c->device));
+    return decode_impl(c, c->d_out.ptr, c->ranges.size(), w, h, max_iter, rms_eps, plane, iterations, rms);
+}
 
 int frac_copy_results_device(frac_ctx* c, void* d_dst)
 {

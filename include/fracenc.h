@@ -142,6 +142,17 @@ const frac_encode_item* frac_device_results(frac_ctx* ctx);
  * (ordered on the context's stream). */
 int frac_copy_results_device(frac_ctx* ctx, void* d_dst);
 
+/* Decoder2::decode (encode/Encoder2.hpp:67-99) on the device.  `plane` (w×h, row
+ * stride w) holds the decoder's initial target (main.cpp:171-173 zero-fills it) and
+ * receives the decoded image; the source starts filled with 100.  Items must not
+ * overlap; items without a domain (size 0) are skipped.  max_iter < 0 means 300.
+ * Writes the iteration count and the final rms exactly as Decoder2 reports them. */
+int frac_decode(frac_ctx* ctx, const frac_encode_item* items, size_t n, uint32_t w, uint32_t h, int max_iter,
+                double rms_eps, uint8_t* plane, int* iterations, double* rms);
+/* The same for the last frac_run's results, which stay on the device. */
+int frac_decode_results(frac_ctx* ctx, uint32_t w, uint32_t h, int max_iter, double rms_eps, uint8_t* plane,
+                        int* iterations, double* rms);
+
 /* ---- host helpers (no device needed) ------------------------------------ */
 /* createUniformGrid (image/partition2.hpp:109-135): returns the item count and
  * writes min(count, cap) items (categories -1). */

@@ -89,9 +89,10 @@ def estimate(src: np.ndarray, domains: np.ndarray, ranges: np.ndarray, T: int = 
     return out, int(rej.value), int(done.value)
 
 
-def decode(records: np.ndarray, range_size: int, W: int, H: int, max_iter: int = -1, eps: float = 1e-5):
+def decode(records: np.ndarray, range_size: int, W: int, H: int, max_iter: int = -1, eps: float = 1e-5,
+           initial: np.ndarray | None = None):
     records = np.ascontiguousarray(records, dtype=RESULT_DTYPE)
-    plane = np.zeros((H, W), np.uint8)
+    plane = np.zeros((H, W), np.uint8) if initial is None else np.ascontiguousarray(initial, np.uint8).copy()
     rms = C.c_double()
     it = lib().or_decode(records.ctypes.data, len(records), range_size, W, H, max_iter, eps, plane.ctypes.data,
                          C.byref(rms))
@@ -109,6 +110,20 @@ def ref_lib():
                                   C.c_size_t, C.c_void_p, C.POINTER(C.c_uint64), C.c_double, C.POINTER(C.c_size_t)]
         _ref = L
     return _ref
+
+
+def ref_quantize(vmin: float, vmax: float, bits: int, values: np.ndarray):
+    """Frac::Quantizerd of the REFERENCE build: (codes u64, dequantized f64), or None when absent."""
+    L = ref_lib()
+    if L is None:
+        return None
+    L.fr_quantize.restype = C.c_int
+    L.fr_quantize.argtypes = [C.c_double, C.c_double, C.c_int, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p]
+    v = np.ascontiguousarray(values, dtype=np.float64)
+    q = np.zeros(len(v), np.uint64)
+    back = np.zeros(len(v), np.float64)
+    L.fr_quantize(vmin, vmax, bits, v.ctypes.data, len(v), q.ctypes.data, back.ctypes.data)
+    return q, back
 
 
 def ref_estimate(plane: np.ndarray, src_size: int, tgt_size: int, T: int = 4, thr: float = 0.0, smax: float = -1.0,

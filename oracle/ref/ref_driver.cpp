@@ -22,6 +22,7 @@
 #include "encode/Classifier2.hpp"
 #include "encode/Encoder2.hpp"
 #include "encode/transformmatcher.h"
+#include "encode/Quantizer.hpp"
 #include "image/ImageIO.hpp"
 #include "image/partition2.hpp"
 
@@ -204,6 +205,17 @@ int fr_decode(const fr_result* recs, size_t n, uint32_t tgt_size, uint32_t w, ui
     if (out_rms)
         *out_rms = stats.rms;
     return stats.iterations;
+}
+
+// Frac::Quantizer<double> (encode/Quantizer.hpp:7-45): quantized() and value() of n values.
+int fr_quantize(double vmin, double vmax, int bits, const double* v, size_t n, uint64_t* q, double* back)
+{
+    Frac::Quantizerd qz(vmin, vmax, bits);
+    for (size_t i = 0; i < n; ++i) {
+        q[i] = qz.quantized(v[i]);
+        back[i] = qz.value(q[i]);
+    }
+    return 0;
 }
 
 } // extern "C"

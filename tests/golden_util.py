@@ -48,4 +48,30 @@ def selection(meta: dict, n_ranges: int):
     raise ValueError(sel)
 
 
-GOLDEN_NAMES = sorted(f[:-4] for f in os.listdir(GOLD) if f.endswith(".npz") and not f.endswith("_decode.npz"))
+GOLDEN_NAMES = sorted(f[:-4] for f in os.listdir(GOLD)
+                      if f.endswith(".npz") and not f.endswith(("_decode.npz", "_quant.npz")))
+
+
+_MAP = (("x", "x"), ("y", "y"), ("dx", "dx"), ("dy", "dy"), ("sw", "dw"), ("sh", "dh"), ("transform", "t"),
+        ("distance", "dist"), ("contrast", "s"), ("brightness", "o"))
+
+
+def encode_items(rec: dict, range_size: int) -> np.ndarray:
+    """Golden / oracle per-range records → encode_item_t records (fractencode_amd.ENCODE_ITEM)."""
+    from fractencode_amd import ENCODE_ITEM
+
+    out = np.zeros(len(rec["x"]), dtype=ENCODE_ITEM)
+    for a, b in _MAP:
+        out[a] = rec[b]
+    out["w"] = out["h"] = range_size
+    return out
+
+
+def oracle_records(items: np.ndarray) -> np.ndarray:
+    """encode_item_t records → the oracle's result records (oracle.RESULT_DTYPE)."""
+    from oracle.oracle import RESULT_DTYPE
+
+    out = np.zeros(len(items), dtype=RESULT_DTYPE)
+    for a, b in _MAP:
+        out[b] = items[a]
+    return out

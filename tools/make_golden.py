@@ -44,6 +44,8 @@ def load_ref():
     lib.fr_decode.restype = C.c_int
     lib.fr_decode.argtypes = [C.c_void_p, C.c_size_t, C.c_uint32, C.c_uint32, C.c_uint32, C.c_int, C.c_double,
                               C.c_void_p, C.POINTER(C.c_double)]
+    lib.fr_quantize.restype = C.c_int
+    lib.fr_quantize.argtypes = [C.c_double, C.c_double, C.c_int, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p]
     lib.fr_load_yuv.argtypes = [C.c_char_p, C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(C.c_uint32),
                                 C.POINTER(C.c_uint32)]
     return lib
@@ -137,6 +139,17 @@ def main():
                       cls=p.get("cls", False), sel=None)
         save(name, pk, rec, rej, params, {"seconds": round(time.time() - t0, 2)})
         if name == "lenna_t4":
+            # Frac::Quantizer on (s, o) with main.cpp:120-121's bit depths (5 / 7)
+            qd = {}
+            for key, bits in (("s", 5), ("o", 7)):
+                v = np.ascontiguousarray(rec[key], dtype=np.float64)
+                q = np.zeros(len(v), np.uint64)
+                back = np.zeros(len(v), np.float64)
+                lib.fr_quantize(float(v.min()), float(v.max()), bits, v.ctypes.data, len(v), q.ctypes.data,
+                                back.ctypes.data)
+                qd["q_" + key], qd["v_" + key] = q, back
+            np.savez_compressed(os.path.join(GOLD, "lenna_t4_quant.npz"), **qd)
+            print("  quantizer golden written")
             dec = np.zeros((512, 512), np.uint8)
             rms = C.c_double()
             it = lib.fr_decode(rec.ctypes.data, len(rec), 8, 512, 512, -1, 1e-5, dec.ctypes.data, C.byref(rms))
