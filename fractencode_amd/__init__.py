@@ -90,6 +90,8 @@ def lib() -> C.CDLL:
                                   C.POINTER(C.c_double)]),
             "frac_decode_results": (i32, [vp, u32, u32, i32, C.c_double, vp, C.POINTER(C.c_int),
                                           C.POINTER(C.c_double)]),
+            "frac_rgb_to_yuv_device": (i32, [vp, vp, u32, u32, u32, vp, u32, vp, u32, vp, u32]),
+            "frac_rgb_to_yuv": (i32, [vp, vp, u32, u32, u32, vp, vp, vp]),
             "frac_uniform_grid": (sz, [u32, u32, u32, u32, vp, sz]),
             "frac_classify": (i32, [vp, u32, u32, u32, vp, sz]),
             "frac_transform_index": (i32, [u32, u32, u32]),
@@ -258,6 +260,37 @@ class Engine:
             self._check(lib().frac_decode(self._ctx, items.ctypes.data if len(items) else None, len(items), width,
                                           height, max_iter, rms_eps, plane.ctypes.data, C.byref(it), C.byref(rms)))
         return plane, it.value, rms.value
+
+    def rgb_to_yuv(self, rgb):
+        """ImageIO::rgb2yuv on the device (image/ImageIO.cpp:43-58).
+
+        rgb: numpy uint8 [H, W, 3] → numpy (Y [H, W], U [H/2, W/2], V [H/2, W/2]); or a CUDA
+        uint8 tensor [H, W, 3] (rows may be strided) → CUDA tensors, enqueued on this
+        engine's stream and synchronised before returning."""
+        if hasattr(rgb, "is_cuda") and rgb.is_cuda:
+            import torch
+
+            assert rgb.dtype == torch.uint8 and rgb.dim() == 3 and rgb.shape[2] == 3
+            assert rgb.stride(2) == 1 and rgb.stride(1) == 3, "pixels must be packed RGB"
+            H, W = rgb.shape[0], rgb.shape[1]
+            y = torch.empty((H, W), dtype=torch.uint8, device=rgb.device)
+            u = torch.empty((H // 2, W // 2), dtype=torch.uint8, device=rgb.device)
+            v = torch.empty_like(u)
+            torch.cuda.current_stream(rgb.device).synchronize()  # rgb must be ready before our stream reads it
+            self._check(lib().frac_rgb_to_yuv_device(self._ctx, C.c_void_p(rgb.data_ptr()), W, H, rgb.stride(0),
+                                                     C.c_void_p(y.data_ptr()), W, C.c_void_p(u.data_ptr()),
+                                                     max(W // 2, 1), C.c_void_p(v.data_ptr()), max(W // 2, 1)))
+            self.sync()
+            return y, u, v
+        rgb = np.ascontiguousarray(rgb, dtype=np.uint8)
+        assert rgb.ndim == 3 and rgb.shape[2] == 3
+        H, W = rgb.shape[:2]
+        y = np.zeros((H, W), np.uint8)
+        u = np.zeros((H // 2, W // 2), np.uint8)
+        v = np.zeros((H // 2, W // 2), np.uint8)
+        self._check(lib().frac_rgb_to_yuv(self._ctx, rgb.ctypes.data, W, H, 3 * W, y.ctypes.data, u.ctypes.data,
+                                          v.ctypes.data))
+        return y, u, v
 
     def device_results_ptr(self) -> int:
         return lib().frac_device_results(self._ctx) or 0

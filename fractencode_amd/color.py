@@ -1,0 +1,88 @@
+"""Colour frames: main.cpp's --color mode on the device.
+
+The reference loads a PNG, converts it with ImageIO::rgb2yuv (image/ImageIO.cpp:43-58)
+and encodes the three planes independently, each with its own grids and classifier
+(main.cpp:184-196 → encode_image2, main.cpp:142-180).  Here the RGB frame is uploaded
+once, converted on the device (frac_rgb_to_yuv_device), and the Y, U and V searches
+are enqueued on three engines with their own HIP streams so the small chroma searches
+overlap the luma search instead of running after it.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import ENGINE_AUTO, Engine, create_uniform_grid, preclassify
+
+PLANES = ("Y", "U", "V")
+
+
+class ColorEncoder:
+    """Three-plane encoder.  load(rgb) → run() → sync() → fetch(), engines reused across frames."""
+
+    def __init__(self, device: int = 0, range_size: int = 8, domain_size: int | None = None, transforms: int = 4,
+                 use_classifier: bool = False, rms_threshold: float = 0.0, s_max: float = -1.0,
+                 engine: int = ENGINE_AUTO, timing: bool = False):
+        self.device = device
+        self.range_size = range_size
+        self.domain_size = domain_size or 2 * range_size
+        self.use_classifier = use_classifier
+        self.engines = [Engine(device, transforms, use_classifier, rms_threshold, s_max, engine, timing) for _ in PLANES]
+        self.planes = None
+        self.ranges = None
+
+    def close(self) -> None:
+        for e in self.engines:
+            e.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def load(self, rgb) -> None:
+        """rgb: numpy uint8 [H, W, 3] or a CUDA uint8 tensor [H, W, 3]; converted on the device."""
+        import torch
+
+        if not (hasattr(rgb, "is_cuda") and rgb.is_cuda):
+            rgb = torch.from_numpy(np.ascontiguousarray(rgb, dtype=np.uint8)).to(f"cuda:{self.device}")
+        planes = self.engines[0].rgb_to_yuv(rgb)
+        self.planes = planes
+        self.ranges = []
+        n, d = self.range_size, self.domain_size
+        for e, p in zip(self.engines, planes):
+            H, W = p.shape
+            e.set_frame(p)
+            doms = create_uniform_grid(W, H, d, d // 2)
+            rngs = create_uniform_grid(W, H, n, n)
+            if self.use_classifier:
+                host = p.cpu().numpy()
+                doms, rngs = preclassify(host, doms), preclassify(host, rngs)
+            e.set_domains(doms)
+            e.set_ranges(rngs)
+            self.ranges.append(rngs)
+
+    def run(self) -> None:
+        """Enqueue the three searches (asynchronous; each engine on its own stream)."""
+        for e in self.engines:
+            e.run()
+
+    def sync(self) -> None:
+        for e in self.engines:
+            e.sync()
+
+    def fetch(self):
+        """[(encode items, stats)] for Y, U, V."""
+        return [e.fetch() for e in self.engines]
+
+    def host_planes(self):
+        return [p.cpu().numpy() for p in self.planes]
+
+
+def encode_color(rgb, **kw):
+    """Convert + encode one RGB frame; returns ([Y, U, V] host planes, [(items, stats)] per plane)."""
+    with ColorEncoder(**kw) as enc:
+        enc.load(rgb)
+        enc.run()
+        enc.sync()
+        return enc.host_planes(), enc.fetch()

@@ -17,6 +17,7 @@
 #include "fracenc_kernels.hip"
 #include "fracenc_mfma.hip"
 #include "fracenc_decode.hip"
+#include "fracenc_color.hip"
 
 using namespace fracenc;
 
@@ -172,7 +173,7 @@ struct frac_ctx {
     DBuf<uint2> d_m_entries;
 
     // decoder state
-    DBuf<uint8_t> d_dec_src, d_dec_tgt;
+    DBuf<uint8_t> d_dec_src, d_dec_tgt, d_color;
     DBuf<frac_encode_item> d_dec_items;
     DBuf<unsigned long long> d_dec_sum;
     unsigned long long* h_dec_sum = nullptr; // pinned
@@ -764,6 +765,7 @@ void frac_destroy(frac_ctx* c)
     c->d_m_rfrags.release();
     c->d_m_entries.release();
     c->d_dec_src.release();
+    c->d_color.release();
     c->d_dec_tgt.release();
     c->d_dec_items.release();
     c->d_dec_sum.release();
@@ -975,6 +977,68 @@ int frac_set_stream(frac_ctx* c, void* s)
 void* frac_get_stream(frac_ctx* c) { return c ? reinterpret_cast<void*>(c->stream) : nullptr; }
 
 const frac_encode_item* frac_device_results(frac_ctx* c) { return c ? c->d_out.ptr : nullptr; }
+
+int frac_rgb_to_yuv_device(frac_ctx* c, const void* d_rgb, uint32_t w, uint32_t h, uint32_t rgb_stride, void* d_y,
+                           uint32_t y_stride, void* d_u, uint32_t u_stride, void* d_v, uint32_t v_stride)
+{
+    if (!c)
+        return FRAC_E_INVALID;
+    if (w == 0 || h == 0)
+        return FRAC_OK;
+    if (!d_rgb || !d_y || ((w >= 2 && h >= 2) && (!d_u || !d_v)) || rgb_stride < 3ull * w || y_stride < w ||
+        (w >= 2 && h >= 2 && (u_stride < w / 2 || v_stride < w / 2)))
+        return c->fail(FRAC_E_INVALID, "rgb_to_yuv: invalid plane pointers or strides");
+    FRAC_HIP(c, hipSetDevice(c->device));
+    ColorArgs a;
+    a.rgb = static_cast<const uint8_t*>(d_rgb);
+    a.w = w;
+    a.h = h;
+    a.rgb_stride = rgb_stride;
+    a.y = static_cast<uint8_t*>(d_y);
+    a.ys = y_stride;
+    a.u = static_cast<uint8_t*>(d_u);
+    a.us = u_stride;
+    a.v = static_cast<uint8_t*>(d_v);
+    a.vs = v_stride;
+    if (color_fast_path(a)) {
+        const size_t n = (size_t)(w / 4) * (h / 2);
+        rgb2yuv_quads4<<<(unsigned)((n + 255) / 256), 256, 0, c->stream>>>(a);
+    } else {
+        const size_t n = (size_t)((w + 1) / 2) * ((h + 1) / 2);
+        rgb2yuv_generic<<<(unsigned)((n + 255) / 256), 256, 0, c->stream>>>(a);
+    }
+    FRAC_HIP(c, hipGetLastError());
+    return FRAC_OK;
+}
+
+int frac_rgb_to_yuv(frac_ctx* c, const uint8_t* rgb, uint32_t w, uint32_t h, uint32_t rgb_stride, uint8_t* y,
+                    uint8_t* u, uint8_t* v)
+{
+    if (!c)
+        return FRAC_E_INVALID;
+    if (w == 0 || h == 0)
+        return FRAC_OK;
+    if (!rgb || !y || (w >= 2 && h >= 2 && (!u || !v)) || rgb_stride < 3ull * w)
+        return c->fail(FRAC_E_INVALID, "rgb_to_yuv: invalid buffers");
+    FRAC_HIP(c, hipSetDevice(c->device));
+    const uint32_t cw = w / 2, ch = h / 2;
+    const uint32_t ys = (w + 63u) & ~63u, cs = (cw + 63u) & ~63u;
+    const size_t rgb_bytes = (size_t)rgb_stride * h, y_bytes = (size_t)ys * h, c_bytes = (size_t)cs * std::max(ch, 1u);
+    FRAC_HIP(c, c->d_color.ensure(rgb_bytes + y_bytes + 2 * c_bytes));
+    uint8_t* d_rgb = c->d_color.ptr;
+    uint8_t* d_y = d_rgb + rgb_bytes;
+    uint8_t* d_u = d_y + y_bytes;
+    uint8_t* d_v = d_u + c_bytes;
+    FRAC_HIP(c, hipMemcpyAsync(d_rgb, rgb, rgb_bytes, hipMemcpyHostToDevice, c->stream));
+    FRAC_TRY(frac_rgb_to_yuv_device(c, d_rgb, w, h, rgb_stride, d_y, ys, d_u, cs, d_v, cs));
+    FRAC_HIP(c, hipMemcpy2DAsync(y, w, d_y, ys, w, h, hipMemcpyDeviceToHost, c->stream));
+    if (cw && ch) {
+        FRAC_HIP(c, hipMemcpy2DAsync(u, cw, d_u, cs, cw, ch, hipMemcpyDeviceToHost, c->stream));
+        FRAC_HIP(c, hipMemcpy2DAsync(v, cw, d_v, cs, cw, ch, hipMemcpyDeviceToHost, c->stream));
+    }
+    FRAC_HIP(c, hipStreamSynchronize(c->stream));
+    return FRAC_OK;
+}
 
 static int decode_impl(frac_ctx* c, const frac_encode_item* d_items, size_t n, uint32_t w, uint32_t h, int max_iter,
                        double eps, uint8_t* plane, int* iterations, double* rms)

@@ -153,6 +153,18 @@ int frac_decode(frac_ctx* ctx, const frac_encode_item* items, size_t n, uint32_t
 int frac_decode_results(frac_ctx* ctx, uint32_t w, uint32_t h, int max_iter, double rms_eps, uint8_t* plane,
                         int* iterations, double* rms);
 
+/* ---- frame loader: colour conversion (ImageIO::rgb2yuv, image/ImageIO.cpp:43-58) ----
+ * Packed RGB (w×h, rgb_stride bytes per row) → Y (w×h) and U, V (w/2 × h/2, the odd
+ * pixel of each 2×2 quad), bit-exact with the built reference (FMA-contracted weights).
+ * Replaces the conversion inside ImageIO::loadImage (ImageIO.cpp:60-66); the PNG decode
+ * itself stays on the host.  _device: all pointers are device pointers, the work is
+ * enqueued on the ctx stream (call frac_sync before reading).  The host variant uploads,
+ * converts on the device and downloads. */
+int frac_rgb_to_yuv_device(frac_ctx* ctx, const void* d_rgb, uint32_t w, uint32_t h, uint32_t rgb_stride, void* d_y,
+                           uint32_t y_stride, void* d_u, uint32_t u_stride, void* d_v, uint32_t v_stride);
+int frac_rgb_to_yuv(frac_ctx* ctx, const uint8_t* rgb, uint32_t w, uint32_t h, uint32_t rgb_stride, uint8_t* y,
+                    uint8_t* u, uint8_t* v);
+
 /* ---- host helpers (no device needed) ------------------------------------ */
 /* createUniformGrid (image/partition2.hpp:109-135): returns the item count and
  * writes min(count, cap) items (categories -1). */

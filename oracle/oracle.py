@@ -99,6 +99,21 @@ def decode(records: np.ndarray, range_size: int, W: int, H: int, max_iter: int =
     return plane, it, rms.value
 
 
+def rgb2yuv(rgb: np.ndarray):
+    """ImageIO::rgb2yuv restated (fracoracle.c or_rgb2yuv) → (Y [H, W], U, V [H/2, W/2])."""
+    rgb = np.ascontiguousarray(rgb, dtype=np.uint8)
+    H, W = rgb.shape[:2]
+    y = np.zeros((H, W), np.uint8)
+    cs = W // 2 + 1
+    u = np.zeros(((H + 1) // 2, cs), np.uint8)
+    v = np.zeros_like(u)
+    L = lib()
+    L.or_rgb2yuv.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p, C.c_uint32, C.c_void_p,
+                             C.c_uint32, C.c_void_p, C.c_uint32]
+    L.or_rgb2yuv(rgb.ctypes.data, W, H, 3 * W, y.ctypes.data, W, u.ctypes.data, cs, v.ctypes.data, cs)
+    return y, np.ascontiguousarray(u[:H // 2, :W // 2]), np.ascontiguousarray(v[:H // 2, :W // 2])
+
+
 def ref_lib():
     """The reference build (oracle/_ref/libfracref.so) or None when absent."""
     global _ref

@@ -207,6 +207,18 @@ int fr_decode(const fr_result* recs, size_t n, uint32_t tgt_size, uint32_t w, ui
     return stats.iterations;
 }
 
+// ImageIO::rgb2yuv (image/ImageIO.cpp:43-58) on a caller-supplied packed RGB buffer.
+int fr_rgb2yuv(const uint8_t* rgb, uint32_t w, uint32_t h, uint32_t rgb_stride, uint8_t* y, uint32_t ys, uint8_t* u,
+               uint32_t us, uint8_t* v, uint32_t vs)
+{
+    const std::ptrdiff_t uvh = (h + 1) / 2;
+    ImageIO::rgb2yuv({rgb, static_cast<std::ptrdiff_t>(size_t(rgb_stride) * h)}, w, h, rgb_stride,
+                     {y, static_cast<std::ptrdiff_t>(size_t(ys) * h)}, ys,
+                     {u, static_cast<std::ptrdiff_t>(size_t(us) * uvh)}, us,
+                     {v, static_cast<std::ptrdiff_t>(size_t(vs) * uvh)}, vs);
+    return 0;
+}
+
 // Frac::Quantizer<double> (encode/Quantizer.hpp:7-45): quantized() and value() of n values.
 int fr_quantize(double vmin, double vmax, int bits, const double* v, size_t n, uint64_t* q, double* back)
 {

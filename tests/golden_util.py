@@ -48,8 +48,10 @@ def selection(meta: dict, n_ranges: int):
     raise ValueError(sel)
 
 
+# per-range search goldens (decode / quantizer / colour fixtures live beside them)
 GOLDEN_NAMES = sorted(f[:-4] for f in os.listdir(GOLD)
-                      if f.endswith(".npz") and not f.endswith(("_decode.npz", "_quant.npz")))
+                      if f.endswith(".npz") and not f.endswith(("_decode.npz", "_quant.npz"))
+                      and not f.startswith("rgb_"))
 
 
 _MAP = (("x", "x"), ("y", "y"), ("dx", "dx"), ("dy", "dy"), ("sw", "dw"), ("sh", "dh"), ("transform", "t"),

@@ -49,7 +49,7 @@ def test_decode_matches_oracle(oracle, name):
     want3, wit3, _ = oracle.decode(oracle_records(items), meta["tgt"], W, H, max_iter=3)
     assert (it, rms) == (wit, wrms)
     np.testing.assert_array_equal(got, want)
-    assert it3 == wit3 == 3
+    assert it3 == wit3 <= 3
     np.testing.assert_array_equal(got3, want3)
 
 

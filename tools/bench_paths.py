@@ -1,0 +1,155 @@
+#!/usr/bin/env python3
+"""Measurements for the rows around the headline search, one JSON line each:
+
+  rgb2yuv   frame loader colour conversion (C5 frame, 4096² RGB): HBM-bound, 4.5 B/pixel
+  c5        colour frame: device rgb2yuv + Y/U/V searches on three streams, range-blocks/s
+  c4        2048² S1 crop with the classifier pre-pass on: range-blocks/s
+  decode    Decoder2 on the GPU for the C3 winners: ms per iteration, HBM bytes per iteration
+  stream    FRC1 pack of the C3 winners (host, numpy): ms
+
+Run on the GPU box:  python tools/bench_paths.py [--only rgb2yuv c5 ...] [--steps K]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def timed(fn, steps, warmup, sync):
+    for _ in range(warmup):
+        fn()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    sync()
+    return (time.perf_counter() - t0) / steps
+
+
+def s1_rgb(size: int) -> np.ndarray:
+    from fractencode_amd.synth import value_noise
+
+    return np.stack([value_noise(size, size, 1234 + k) for k in range(3)], -1)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", nargs="*")
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    args = ap.parse_args()
+    want = (lambda k: True) if not args.only else (lambda k: k in args.only)
+
+    import torch
+
+    import fractencode_amd as F
+    from fractencode_amd import codec
+    from fractencode_amd.color import ColorEncoder
+    from fractencode_amd.synth import value_noise
+
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(0)
+    sync = torch.cuda.synchronize
+
+    if want("rgb2yuv") or want("c5"):
+        rgb = torch.from_numpy(s1_rgb(4096)).to(dev)
+    if want("rgb2yuv"):
+        with F.Engine(0) as e:
+            e.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+            H, W = rgb.shape[:2]
+            y = torch.empty((H, W), dtype=torch.uint8, device=dev)
+            u = torch.empty((H // 2, W // 2), dtype=torch.uint8, device=dev)
+            v = torch.empty_like(u)
+            lib = F.lib()
+            import ctypes as C
+
+            def conv():
+                lib.frac_rgb_to_yuv_device(e._ctx, C.c_void_p(rgb.data_ptr()), W, H, 3 * W, C.c_void_p(y.data_ptr()),
+                                           W, C.c_void_p(u.data_ptr()), W // 2, C.c_void_p(v.data_ptr()), W // 2)
+
+            for _ in range(3):
+                conv()
+            sync()
+            ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            n = 50
+            ev0.record()
+            for _ in range(n):
+                conv()
+            ev1.record()
+            sync()
+            ms = ev0.elapsed_time(ev1) / n
+        nbytes = H * W * 3 + H * W + 2 * (H // 2) * (W // 2)
+        print(json.dumps({"path": "rgb2yuv", "frame": f"{W}x{H} RGB", "kernel_ms": round(ms, 4),
+                          "algorithmic_bytes": nbytes, "achieved_gbs": round(nbytes / ms / 1e6, 1),
+                          "peak_gbs": 8000.0, "frac": round(nbytes / ms / 1e6 / 8000.0, 4)}), flush=True)
+
+    if want("c5"):
+        with ColorEncoder(0, 8, 16, 4, timing=True) as enc:
+            def step():
+                enc.load(rgb)
+                enc.run()
+
+            sec = timed(step, args.steps, args.warmup, enc.sync)
+            res = enc.fetch()
+            nr = sum(len(r) for r in enc.ranges)
+            sec_run = timed(enc.run, args.steps, args.warmup, enc.sync)
+        print(json.dumps({"path": "c5", "workload": "C5: S1 RGB 4096² (seeds 1234/1235/1236) → Y 4096², U/V 2048², "
+                                                    "8x8 ranges, T=4, exhaustive",
+                          "ranges": nr, "ms_per_frame_incl_load": round(sec * 1e3, 3),
+                          "ms_per_frame_search": round(sec_run * 1e3, 3),
+                          "range_blocks_per_s": round(nr / sec_run, 1),
+                          "plane_search_ms": [round(st["ms_search"], 3) for _, st in res]}), flush=True)
+
+    if want("c4"):
+        frame = value_noise(4096, 4096, 1234)[:2048, :2048].copy()
+        doms = F.preclassify(frame, F.create_uniform_grid(2048, 2048, 16, 8))
+        rngs = F.preclassify(frame, F.create_uniform_grid(2048, 2048, 8, 8))
+        with F.Engine(0, 4, True, timing=True) as e:
+            e.set_frame(frame)
+            e.set_domains(doms)
+            e.set_ranges(rngs)
+            sec = timed(e.run, args.steps, args.warmup, e.sync)
+            _, st = e.fetch()
+        print(json.dumps({"path": "c4", "workload": "C4: S1 2048² crop, classifier on, 8x8 ranges, T=4",
+                          "ranges": len(rngs), "ms_per_frame": round(sec * 1e3, 3),
+                          "range_blocks_per_s": round(len(rngs) / sec, 1),
+                          "rejected_mappings": st["rejected_mappings"], "total_mappings": st["total_mappings"],
+                          "engine": st["engine"], "ms_search": round(st["ms_search"], 3)}), flush=True)
+
+    if want("decode") or want("stream"):
+        frame = value_noise(4096, 4096, 1234)
+        with F.Engine(0, 4) as e:
+            e.set_frame(frame)
+            e.set_domains(F.create_uniform_grid(4096, 4096, 16, 8))
+            out, _ = e.search(F.create_uniform_grid(4096, 4096, 8, 8))
+            if want("decode"):
+                t0 = time.perf_counter()
+                dec, it, rms = e.decode(None, 4096, 4096)
+                sec = time.perf_counter() - t0
+                # per iteration: the gather reads 4 source bytes per target pixel through L2 (algorithmic:
+                # 1 source + 1 target byte per pixel), the rms pass reads 2 planes, then a 1-plane copy
+                per_it = 4096 * 4096 * (1 + 1 + 2 + 2)
+                print(json.dumps({"path": "decode", "frame": "4096x4096 (C3 winners)", "iterations": it,
+                                  "rms": rms, "ms_total": round(sec * 1e3, 3),
+                                  "ms_per_iteration": round(sec * 1e3 / max(it, 1), 4),
+                                  "algorithmic_bytes_per_iteration": per_it,
+                                  "psnr_db": round(codec.psnr(frame, dec), 3)}), flush=True)
+            if want("stream"):
+                t0 = time.perf_counter()
+                buf = codec.pack_stream(out, 4096, 4096, 8)
+                sec = time.perf_counter() - t0
+                print(json.dumps({"path": "stream", "ranges": len(out), "bytes": len(buf),
+                                  "bits_per_range": round(8 * (len(buf) - codec.HEADER.size) / len(out), 3),
+                                  "pack_ms_host": round(sec * 1e3, 2)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

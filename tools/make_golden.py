@@ -46,6 +46,8 @@ def load_ref():
                               C.c_void_p, C.POINTER(C.c_double)]
     lib.fr_quantize.restype = C.c_int
     lib.fr_quantize.argtypes = [C.c_double, C.c_double, C.c_int, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p]
+    lib.fr_rgb2yuv.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p, C.c_uint32, C.c_void_p,
+                               C.c_uint32, C.c_void_p, C.c_uint32]
     lib.fr_load_yuv.argtypes = [C.c_char_p, C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(C.c_uint32),
                                 C.POINTER(C.c_uint32)]
     return lib
@@ -67,6 +69,25 @@ def ref_estimate(lib, plane, src_size, tgt_size, T, thr=0.0, smax=-1.0, cls=Fals
                                            ("dh", "<u4"), ("t", "<i4"), ("pad", "<i4"), ("dist", "<f8"),
                                            ("s", "<f8"), ("o", "<f8")])).copy()
     return a, int(rej.value)
+
+
+def ref_rgb2yuv(lib, rgb):
+    """ImageIO::rgb2yuv of the reference build → (Y [H,W], U, V [H/2, W/2])."""
+    rgb = np.ascontiguousarray(rgb, dtype=np.uint8)
+    H, W = rgb.shape[:2]
+    y = np.zeros((H, W), np.uint8)
+    cs = W // 2 + 1  # the reference writes the odd trailing column / row's chroma past the plane
+    u = np.zeros(((H + 1) // 2, cs), np.uint8)
+    v = np.zeros_like(u)
+    lib.fr_rgb2yuv(rgb.ctypes.data, W, H, 3 * W, y.ctypes.data, W, u.ctypes.data, cs, v.ctypes.data, cs)
+    return y, np.ascontiguousarray(u[:H // 2, :W // 2]), np.ascontiguousarray(v[:H // 2, :W // 2])
+
+
+def all_colours_rgb(chunk: int) -> np.ndarray:
+    """Chunk k (of 4) of the 2^24 colours, colour c on the 2×2 block at ((c%2048)·2, (c//2048)·2)."""
+    c = np.arange(chunk << 22, (chunk + 1) << 22, dtype=np.uint32).reshape(2048, 2048)
+    rgb = np.stack([(c >> 16) & 255, (c >> 8) & 255, c & 255], -1).astype(np.uint8)
+    return np.repeat(np.repeat(rgb, 2, 0), 2, 1)
 
 
 def save(name, plane_ref, rec, rejected, params, extra=None):
@@ -103,6 +124,25 @@ def main():
     planes["inexact64"] = inexact
     yy, xx = np.mgrid[0:64, 0:64]
     planes["checker64"] = np.where(((yy // 8) + (xx // 8)) % 2 == 0, 0, 255).astype(np.uint8)
+    # Lenna RGB (the reference's own test input, decoded losslessly; checked against the
+    # reference loader's planes below) and a seeded synthetic RGB frame with odd sizes
+    from PIL import Image
+    lrgb = np.asarray(Image.open(REF_PNG).convert("RGB"), dtype=np.uint8)
+    ly, lu, lv = ref_rgb2yuv(lib, lrgb)
+    assert (ly == y).all() and (lu == u).all() and (lv == v).all(), "PIL decode differs from stb_image"
+    planes["lenna_rgb"] = lrgb
+    if want("color"):
+        srgb = np.random.default_rng(11).integers(0, 256, size=(67, 101, 3), dtype=np.uint8)
+        sy, su, sv = ref_rgb2yuv(lib, srgb)
+        np.savez_compressed(os.path.join(GOLD, "rgb_synth_yuv.npz"), rgb=srgb, y=sy, u=su, v=sv)
+        # all 2^24 colours: digest of the reference's Y/U/V per chunk (the data itself is 48 MB)
+        digests = []
+        for k in range(4):
+            cy, cu, cv = ref_rgb2yuv(lib, all_colours_rgb(k))
+            digests.append({"y": sha256(np.ascontiguousarray(cy[::2, ::2])), "u": sha256(cu), "v": sha256(cv)})
+        with open(os.path.join(GOLD, "rgb_all_colours.json"), "w") as f:
+            json.dump({"layout": "tools/make_golden.py:all_colours_rgb", "chunks": digests}, f, indent=1)
+        print("  colour goldens written")
     for k, p in planes.items():
         p.tofile(os.path.join(GOLD, k + ".u8"))
     manifest = {k: {"shape": list(p.shape), "sha256": sha256(p)} for k, p in planes.items()}
