@@ -41,6 +41,8 @@ def parse():
     ap.add_argument("--transforms", type=int, default=4)
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of CPU-baseline sampling (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--alt-steps", type=int, default=2,
+                    help="steps of the VALU engine (north_star's no-MFMA formulation) reported beside (0 = skip)")
     return ap.parse_args()
 
 
@@ -110,7 +112,10 @@ def main():
     mine = rngs[start:stop]
     engine_id = {"auto": F.ENGINE_AUTO, "valu": F.ENGINE_VALU, "mfma": F.ENGINE_MFMA}[args.engine]
 
-    stream = torch.cuda.current_stream(dev)
+    # one dedicated stream for the engine and the RCCL gather, so the all-gather is ordered after
+    # the record copy (the legacy null stream cannot be handed to the library: NULL = its own stream)
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
     eng = F.Engine(dev.index, args.transforms, False, 0.0, -1.0, engine_id, timing=True)
     eng.set_stream(stream.cuda_stream)
     d_frame = torch.from_numpy(frame).to(dev)  # the frame is resident in HBM before timing
@@ -194,6 +199,27 @@ def main():
     if traffic:
         line["roofline"]["hbm_gbs"] = round(traffic / (avg_search_ms * 1e-3) / 1e9, 3)
         line["roofline"]["hbm_frac"] = round(line["roofline"]["hbm_gbs"] / HBM_PEAK_GBS, 6)
+    if world == 1 and engine_name == "mfma" and args.alt_steps > 0:
+        # the same workload on the VALU engine (packed-u16 v_dot2, no MFMA), measured the same way
+        with F.Engine(dev.index, args.transforms, False, 0.0, -1.0, F.ENGINE_VALU, timing=True) as alt:
+            alt.set_stream(stream.cuda_stream)
+            alt.set_frame(d_frame)
+            alt.set_domains(doms)
+            alt.set_ranges(mine)
+            alt.run()
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            for _ in range(args.alt_steps):
+                alt.run()
+            torch.cuda.synchronize(dev)
+            alt_sec = (time.perf_counter() - t0) / args.alt_steps
+            _, ast = alt.fetch()
+        alt_ach = ops_per_launch / (ast["ms_search"] * 1e-3) / 1e12
+        line["alt_engines"] = {"valu": {
+            "value": round(nr_total / alt_sec, 1), "ms_per_step": round(alt_sec * 1e3, 3), "steps": args.alt_steps,
+            "dtype": "u16", "roofline": {"bound": "valu", "achieved": round(alt_ach, 2), "peak": VALU_PEAK_TOPS,
+                                         "unit": "TOP/s", "frac": round(alt_ach / VALU_PEAK_TOPS, 4),
+                                         "kernel_ms": round(ast["ms_search"], 3)}}}
     if rank == 0 and world == 1 and args.cpu_budget > 0:
         threads = args.cpu_threads or min(16, os.cpu_count() or 1)
         line["cpu_baseline"] = cpu_baseline(frame, args.cpu_budget, threads)

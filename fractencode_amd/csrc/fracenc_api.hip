@@ -16,6 +16,7 @@
 #include "fracenc_common.h"
 #include "fracenc_kernels.hip"
 #include "fracenc_mfma.hip"
+#include "fracenc_dft.hip"
 #include "fracenc_decode.hip"
 #include "fracenc_color.hip"
 
@@ -505,10 +506,88 @@ void launch_search_mfma(frac_ctx* c, const MfmaSearchArgs& a)
     }
 }
 
+// FRAC_MFMA_DFT (tuning knob, read per run): 0 selects the direct n=8, T=4 MFMA search
+// instead of the rotation-group Fourier form (fracenc_dft.hip)
+inline bool mfma_dft_enabled()
+{
+    const char* v = getenv("FRAC_MFMA_DFT");
+    return v ? atoi(v) != 0 : true;
+}
+
+// n = 8, T = 4: the C4-Fourier search (6 MFMAs per 32×32 tile pair instead of 16)
+inline int launch_dft(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride)
+{
+    const uint32_t nr = (uint32_t)c->ranges.size();
+    MfmaDomainPrepArgs d;
+    d.pool = c->d_pool.ptr;
+    d.negsd2 = c->d_negsd2.ptr;
+    d.tile_pos = c->d_m_tile_pos.ptr;
+    d.ntiles = c->ntiles;
+    d.dtiles = c->d_m_dtiles.ptr;
+    d.dconst = c->d_m_dconst.ptr;
+    if (c->ntiles)
+        dft_domain_prep<<<(c->ntiles * 32 + 255) / 256, 256, 0, c->stream>>>(d);
+    MfmaRangePrepArgs r;
+    r.tgt = dtgt;
+    r.tstride = tstride;
+    r.ranges = c->d_ranges.ptr;
+    r.slot_range = c->d_m_slot_range.ptr;
+    r.nblocks = c->nblocks;
+    r.T = 4;
+    r.rfrags = c->d_m_rfrags.ptr;
+    r.rconst = c->d_m_rconst.ptr;
+    if (c->nblocks)
+        dft_range_prep<<<(c->nblocks * 32 + 255) / 256, 256, 0, c->stream>>>(r);
+    if (c->p.flags & FRAC_FLAG_TIMING)
+        FRAC_HIP(c, hipEventRecord(c->ev[1], c->stream));
+    if (!c->m_work.empty()) {
+        MfmaSearchArgs a;
+        a.dtiles = c->d_m_dtiles.ptr;
+        a.dconst = reinterpret_cast<const uint4*>(c->d_m_dconst.ptr);
+        a.rfrags = c->d_m_rfrags.ptr;
+        a.rconst = c->d_m_rconst.ptr;
+        a.work = c->d_m_work.ptr;
+        a.nwork = (uint32_t)c->m_work.size();
+        a.hitH = (uint32_t)std::max<int64_t>(c->hitH, 0);
+        a.entries = c->d_m_entries.ptr;
+        if (c->hitH > 0)
+            search_dft<true, 0><<<(unsigned)c->m_work.size(), 256, 0, c->stream>>>(a);
+        else
+            search_dft<false, 0><<<(unsigned)c->m_work.size(), 256, 0, c->stream>>>(a);
+    }
+    if (c->p.flags & FRAC_FLAG_TIMING)
+        FRAC_HIP(c, hipEventRecord(c->ev[2], c->stream));
+    if (nr) {
+        MfmaResolveArgs v;
+        v.tgt = dtgt;
+        v.tstride = tstride;
+        v.ranges = c->d_ranges.ptr;
+        v.range_slot = c->d_m_range_slot.ptr;
+        v.blk_ptr = c->d_m_blk_ptr.ptr;
+        v.blk_ent = c->d_m_blk_ent.ptr;
+        v.entries = c->d_m_entries.ptr;
+        v.rconst = c->d_m_rconst.ptr;
+        v.tile_pos = c->d_m_tile_pos.ptr;
+        v.ntiles = c->ntiles;
+        v.pool = c->d_pool.ptr;
+        v.negsd2 = c->d_negsd2.ptr;
+        v.nr = nr;
+        v.T = 4;
+        v.hitH = c->hitH;
+        v.best_key = c->d_best_key.ptr;
+        resolve_dft<<<(nr + 3) / 4, 256, 0, c->stream>>>(v);
+    }
+    return FRAC_OK;
+}
+
 template <int N>
 int launch_mfma(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride)
 {
     const uint32_t nr = (uint32_t)c->ranges.size(), T = c->p.transforms;
+    if constexpr (N == 8) {
+        if (T == 4 && mfma_dft_enabled())
+            return launch_dft(c, dtgt, tstride);
+    }
     if (c->ntiles) {
         MfmaDomainPrepArgs d;
         d.pool = c->d_pool.ptr;

@@ -238,3 +238,51 @@ def test_engines_agree_on_stress_frame():
             assert st["engine"] == eng
             outs.append(out)
     assert outs[0].tobytes() == outs[1].tobytes()
+
+
+DFT_CASES = [
+    # W, H, classifier, thr, smax, kind — n = 8, T = 4 (the C4-Fourier MFMA path)
+    (128, 128, False, 0.0, -1.0, "uniform"),
+    (128, 96, True, 0.0, -1.0, "noise"),
+    (96, 96, False, 2.5, -1.0, "flat"),      # threshold hits (first hit in (domain, t) order)
+    (96, 64, True, 0.0, 0.5, "flat"),        # exact matches, ties across transforms
+    (64, 64, False, 0.0, -1.0, "flat"),
+    (160, 96, False, 40.0, -1.0, "noise"),
+]
+
+
+@pytest.mark.parametrize("dft", ["1", "0"])
+@pytest.mark.parametrize("case", range(len(DFT_CASES)))
+def test_mfma_fourier_and_direct_match_oracle(oracle, monkeypatch, case, dft):
+    monkeypatch.setenv("FRAC_MFMA_DFT", dft)
+    W, H, cls, thr, smax, kind = DFT_CASES[case]
+    rng = np.random.default_rng(2000 + case)
+    p = _random_plane(rng, W, H, kind)
+    meta = dict(src=16, tgt=8, T=4, cls=cls, thr=thr, smax=smax)
+    out, st = run_engine(p, meta, F.ENGINE_MFMA)
+    doms = oracle.uniform_grid(W, H, 16, 8)
+    rngs = oracle.uniform_grid(W, H, 8, 8)
+    if cls:
+        doms = oracle.classify(p, doms)
+        rngs = oracle.classify(p, rngs)
+    want, rej, _ = oracle.estimate(p, doms, rngs, T=4, thr=thr, smax=smax, use_classifier=cls)
+    assert_same(out, {k: want[k] for k in FIELDS}, f"dft={dft} case {DFT_CASES[case]}")
+    assert st["rejected_mappings"] == rej
+
+
+def test_fourier_direct_and_valu_agree_on_stress_frame(monkeypatch):
+    """n = 8, T = 4 on a uniform-noise 1024² frame: C4-Fourier MFMA, direct MFMA and VALU
+    engines give identical records."""
+    from fractencode_amd.synth import uniform_noise
+    p = uniform_noise(1024, 1024, 43)
+    outs = []
+    for eng, dft in ((F.ENGINE_VALU, "1"), (F.ENGINE_MFMA, "0"), (F.ENGINE_MFMA, "1")):
+        monkeypatch.setenv("FRAC_MFMA_DFT", dft)
+        with F.Engine(0, 4, False, 0.0, -1.0, eng) as e:
+            e.set_frame(p)
+            e.set_domains(F.create_uniform_grid(1024, 1024, 16, 8))
+            out, st = e.search(F.create_uniform_grid(1024, 1024, 8, 8))
+            assert st["engine"] == eng
+            outs.append(out)
+    assert outs[0].tobytes() == outs[1].tobytes()
+    assert outs[0].tobytes() == outs[2].tobytes()

@@ -1,6 +1,9 @@
 #!/usr/bin/env python3
-"""Interleaved in-process A/B of search_mfma schedule variants (FRAC_MFMA_VARIANT) on the C3
-frame; prints per-variant median/min search-kernel ms (library HIP events)."""
+"""Interleaved in-process A/B of MFMA search variants on the C3 frame; prints per-variant
+median/min search-kernel and finish (resolve + fit) ms (library HIP events).
+Variants: "d" = the C4-Fourier search (FRAC_MFMA_DFT=1, default), an integer v = the direct
+search_mfma with FRAC_MFMA_VARIANT=v (FRAC_MFMA_DFT=0).
+usage: tools/ab_mfma.py d,2 [rounds]"""
 import os
 import sys
 
@@ -10,7 +13,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import fractencode_amd as F  # noqa: E402
 from fractencode_amd.synth import value_noise  # noqa: E402
 
-variants = [int(v) for v in (sys.argv[1].split(",") if len(sys.argv) > 1 else ["0", "1", "2"])]
+variants = sys.argv[1].split(",") if len(sys.argv) > 1 else ["d", "2"]
 rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 5
 S = int(os.environ.get("AB_SIZE", "4096"))
 p = value_noise(S, S, 1234)
@@ -20,17 +23,21 @@ with F.Engine(0, 4, False, 0.0, -1.0, F.ENGINE_MFMA, timing=True) as e:
     e.set_domains(F.create_uniform_grid(S, S, 16, 8))
     e.set_ranges(F.create_uniform_grid(S, S, 8, 8))
     res = {v: [] for v in variants}
+    fin = {v: [] for v in variants}
     for r in range(rounds + 1):
         for v in variants:
-            os.environ["FRAC_MFMA_VARIANT"] = str(v)
+            os.environ["FRAC_MFMA_DFT"] = "1" if v == "d" else "0"
+            os.environ["FRAC_MFMA_VARIANT"] = "2" if v == "d" else v
             e.run()
             out, st = e.fetch()
             if ref is None:
                 ref = out.tobytes()
-            if v < 8:  # 8, 16 are ablations (results intentionally wrong)
+            if v == "d" or int(v) < 8:  # 8, 16 are ablations (results intentionally wrong)
                 assert out.tobytes() == ref, f"variant {v} differs"
             if r:
                 res[v].append(st["ms_search"])
+                fin[v].append(st["ms_finish"])
     for v in variants:
         a = np.array(res[v])
-        print(f"variant {v}: search median {np.median(a):.3f} ms  min {a.min():.3f} ms  (n={len(a)})", flush=True)
+        print(f"variant {v}: search median {np.median(a):.3f} ms  min {a.min():.3f} ms  finish median "
+              f"{np.median(fin[v]):.3f} ms  (n={len(a)})", flush=True)
