@@ -175,6 +175,8 @@ struct frac_ctx {
 
     // decoder state
     DBuf<uint8_t> d_dec_src, d_dec_tgt, d_color;
+    DBuf<uint2> d_dft_tguard;
+    DBuf<uint32_t> d_dft_rguard;
     DBuf<frac_encode_item> d_dec_items;
     DBuf<unsigned long long> d_dec_sum;
     unsigned long long* h_dec_sum = nullptr; // pinned
@@ -525,8 +527,12 @@ inline int launch_dft(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride)
     d.ntiles = c->ntiles;
     d.dtiles = c->d_m_dtiles.ptr;
     d.dconst = c->d_m_dconst.ptr;
+    FRAC_HIP(c, c->d_dft_tguard.ensure(std::max<size_t>(c->ntiles, 1)));
+    FRAC_HIP(c, c->d_dft_rguard.ensure(std::max<size_t>(c->nblocks, 1)));
+    FRAC_HIP(c, hipMemsetAsync(c->d_dft_tguard.ptr, 0, c->ntiles * sizeof(uint2), c->stream));
+    FRAC_HIP(c, hipMemsetAsync(c->d_dft_rguard.ptr, 0, c->nblocks * sizeof(uint32_t), c->stream));
     if (c->ntiles)
-        dft_domain_prep<<<(c->ntiles * 32 + 255) / 256, 256, 0, c->stream>>>(d);
+        dft_domain_prep<<<(c->ntiles * 32 + 255) / 256, 256, 0, c->stream>>>(d, c->d_dft_tguard.ptr);
     MfmaRangePrepArgs r;
     r.tgt = dtgt;
     r.tstride = tstride;
@@ -537,7 +543,7 @@ inline int launch_dft(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride)
     r.rfrags = c->d_m_rfrags.ptr;
     r.rconst = c->d_m_rconst.ptr;
     if (c->nblocks)
-        dft_range_prep<<<(c->nblocks * 32 + 255) / 256, 256, 0, c->stream>>>(r);
+        dft_range_prep<<<(c->nblocks * 32 + 255) / 256, 256, 0, c->stream>>>(r, c->d_dft_rguard.ptr);
     if (c->p.flags & FRAC_FLAG_TIMING)
         FRAC_HIP(c, hipEventRecord(c->ev[1], c->stream));
     if (!c->m_work.empty()) {
@@ -550,10 +556,23 @@ inline int launch_dft(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride)
         a.nwork = (uint32_t)c->m_work.size();
         a.hitH = (uint32_t)std::max<int64_t>(c->hitH, 0);
         a.entries = c->d_m_entries.ptr;
-        if (c->hitH > 0)
-            search_dft<true, 0><<<(unsigned)c->m_work.size(), 256, 0, c->stream>>>(a);
-        else
-            search_dft<false, 0><<<(unsigned)c->m_work.size(), 256, 0, c->stream>>>(a);
+        DftArgs da;
+        da.m = a;
+        da.rguard = c->d_dft_rguard.ptr;
+        da.tguard = c->d_dft_tguard.ptr;
+        const unsigned nwg = (unsigned)c->m_work.size();
+        const bool exact_only = mfma_variant() == 1; // A/B knob: guard disabled
+        if (c->hitH > 0) {
+            if (exact_only)
+                search_dft<true, 1><<<nwg, 256, 0, c->stream>>>(da);
+            else
+                search_dft<true, 0><<<nwg, 256, 0, c->stream>>>(da);
+        } else {
+            if (exact_only)
+                search_dft<false, 1><<<nwg, 256, 0, c->stream>>>(da);
+            else
+                search_dft<false, 0><<<nwg, 256, 0, c->stream>>>(da);
+        }
     }
     if (c->p.flags & FRAC_FLAG_TIMING)
         FRAC_HIP(c, hipEventRecord(c->ev[2], c->stream));
@@ -845,6 +864,8 @@ void frac_destroy(frac_ctx* c)
     c->d_m_entries.release();
     c->d_dec_src.release();
     c->d_color.release();
+    c->d_dft_tguard.release();
+    c->d_dft_rguard.release();
     c->d_dec_tgt.release();
     c->d_dec_items.release();
     c->d_dec_sum.release();

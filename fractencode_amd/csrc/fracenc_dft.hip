@@ -7,34 +7,40 @@
 //
 //   Z_t = Σ_p a(p)·b(g^t p) = Σ_o Σ_k a_{o,k}·b_{o,k+t}           (cyclic correlation)
 //
-// The length-4 DFT diagonalises it.  With per-orbit components
-//   Â0 = Σa, Â2 = a0−a1+a2−a3, α = a0−a2, β = a1−a3   (range; B̂0, B̂2, γ, δ for the domain)
-// and the four products  P0 = ΣÂ0B̂0,  P2 = ΣÂ2B̂2,  Pr = Σ(αγ+βδ),  Pi = Σ(βγ−αδ):
+// Per orbit let s = x0 + x2, u = x1 + x3, α = a0 − a2, β = a1 − a3, γ = b0 − b2, δ = b1 − b3.
+// The length-4 DFT of the correlation gives, with
+//   U = Σ(s_a s_b + u_a u_b),  U' = Σ(s_a u_b + u_a s_b),  Pr = Σ(αγ + βδ),  Pi = Σ(βγ − αδ):
 //
-//   4Z_0 = A + 2Pr,  4Z_2 = A − 2Pr,  4Z_1 = B − 2Pi,  4Z_3 = B + 2Pi,   A = P0+P2, B = P0−P2
+//   2Z_0 = U + Pr,  2Z_2 = U − Pr,  2Z_1 = U' − Pi,  2Z_3 = U' + Pi
 //
-// so  max_t 4Z_t = max(A + 2|Pr|, B + 2|Pi|)  and the least error over the four transforms is
+// so  2·max_t Z_t = max(U + |Pr|, U' + |Pi|)  and, with S16 = Σ(4r − D4)² = 16Σa² − 8Z + Σb²,
+// the chunk statistic tracked per lane is the maximum over domains of
 //
-//   S16_min − 16Σa² = w = Σb² − 2·max_t 4Z_t          (S16 = Σ(4r − D4)² = 16Σa² − 8Z + Σb²)
+//   y = 8·max_t Z_t − Σb²  =  16Σa² − min_t S16                      (one GEMM per tile)
 //
-// Cost per (32 domains × 32 ranges): 6 MFMA 32x32x16 (P0, P2: K=16; Pr, Pi: K=32) instead
-// of T·n²/16 = 16, and 6.5 VALU per (range, domain) instead of 4 × 1.5.
+// Cost per (32 domains × 32 ranges): 8 MFMA 32x32x16 (U, U', Pr, Pi with K = 32) instead of
+// the direct T·n²/16 = 16, and 3 VALU per (range, domain) on the fast path (below) instead
+// of 4 transforms × 1.5.
 //
 // Exactness (f16 operands, f32 accumulate, all values integers):
-//   operands  |Â0| ≤ 512, |Â2| ≤ 510, |α|,|β| ≤ 255;  |B̂0| ≤ 2048, |B̂2| ≤ 2040, |γ|,|δ| ≤ 1020
-//             — integers of magnitude ≤ 2048 are exact in f16;
-//   products  every partial sum of P0, P2 (16 terms ≤ 2^20) and Pr, Pi (32 terms ≤ 2^18)
-//             is an integer of magnitude ≤ 2^24: exact in any accumulation order;
-//   epilogue  A = 2Σ(s_a s_b + u_a u_b) (s = x0+x2, u = x1+x3) is an even integer, |A| ≤ 2^24,
-//             likewise B; A ± 2Pr and B ± 2Pi are 4Z_t with |4Z_t| ≤ 4·64·128·512 = 2^24:
-//             each op's exact result is representable, so every step is exact;
-//             w = fma(m, −2, Σb²) is exact whenever |w| ≤ 2^24, which holds for every
-//             candidate in the exact regime S16 < 2^24 (w = S16 − 16Σa², 16Σa² ≤ 2^24).
-//   Candidates with S16 ≥ 2^24 may round, but rounding is monotone: w ≥ 2^24 − 16Σa² (an
-//   exactly representable bound) stays ≥ it, so they never beat or tie an exact-regime
-//   candidate, and a range whose minimum reaches that bound is sent to the fp32 fallback
-//   (App. A.3), exactly as the direct engine does.
-// The per-lane chunk minimum of w and the tile it appeared in feed resolve_dft, which
+//   operands  |s_a|,|u_a| ≤ 256, |4s_a| ≤ 1024, |α|,|β| ≤ 255; |s_b|,|u_b| ≤ 1024,
+//             |γ|,|δ| ≤ 1020 — integers of magnitude ≤ 2048 are exact in f16;
+//   products  every partial sum of U, U' (32 terms ≤ 2^18) and Pr, Pi (32 terms ≤ 2^18) is
+//             an integer of magnitude ≤ 2^23: exact in any accumulation order.
+//   fast path (per (range block, domain tile) guard 4·max R1·max D∞ + max Σb² ≤ 2^24, with
+//             R1 = Σ_o(|s_a| + |u_a|) and D∞ = max_o(|s_b|, |u_b|); ≈93 % of tile pairs on S1):
+//             the MFMA starts from C = −Σb² and accumulates 4U (range operands ×4), every
+//             partial sum bounded by the guard, so Ũ = 4U − Σb² is exact; then
+//             y = max(fma(|Pr|, 4, Ũ), fma(|Pi|, 4, Ũ'))  — 2 fma + a shared v_max3.
+//   exact path (guard fails): U, U' from C = 0; 2max Z = max(U + |Pr|, U' + |Pi|) (≤ 2^23,
+//             exact); y = fma(that, 4, −Σb²).
+//   Both:     y is exact whenever |y| ≤ 2^24, which holds for every candidate in the exact
+//             regime S16 < 2^24 (y = 16Σa² − S16, 16Σa² ≤ 2^24).  Candidates with S16 ≥ 2^24
+//             may round, but rounding is monotone: their y ≤ 16Σa² − 2^24 (exactly
+//             representable) stays ≤ it, so they never beat or tie an exact-regime candidate,
+//             and a range whose maximum reaches that bound goes to the fp32 fallback
+//             (App. A.3), as with the direct engine.
+// The per-lane chunk maximum of y and the tile it appeared in feed resolve_dft, which
 // re-derives the exact (domain, transform) inside the chunk with integer arithmetic.
 #include "fracenc_common.h"
 
@@ -92,16 +98,24 @@ constexpr bool orbits4_valid()
 
 static_assert(orbits4_valid<8>(), "the reference's rotations must be the powers of Rotate_90 with 4-orbits");
 constexpr Orbits4<8> kOrb8 = make_orbits4<8>();
-constexpr float kDftPadConst = 1.0e30f; // Σb² of padding rows: w ≈ 1e30 never wins
+constexpr float kDftPadY = -1.0e30f; // −Σb² of padding rows: y ≈ −1e30 never wins
+constexpr int kDftRangeFrags = 7;     // s, u, 4s, 4u, α, β, −α
+
+struct DftArgs {
+    MfmaSearchArgs m;
+    uint32_t* rguard;     // [nblocks]  max over the block's ranges of R1 = Σ_o(|s_a| + |u_a|)
+    uint2* tguard;        // [ntiles]   {max 4·D∞, max Σb²} over the tile's valid rows
+};
 
 // ---------------------------------------------------------------------------
-// dft_domain_prep: pool (u16 D4) → per 32-domain tile the A fragments of the four
-// K-steps [B̂0 | B̂2 | γ | δ] (lane l: row l&31, orbit 8(l>>5) + j) and Σb² per row
-// in the [2][16] lane-half layout of the epilogue.  One thread per (tile, row).
+// dft_domain_prep: pool (u16 D4) → per 32-domain tile the A fragments of the four K-steps
+// [s_b | u_b | γ | δ] (lane l: row l&31, orbit 8(l>>5) + j), −Σb² per row in the [2][16]
+// lane-half layout of the epilogue, and the tile's fast-path guard terms.
+// One thread per (tile, row).
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) dft_domain_prep(MfmaDomainPrepArgs a)
+__global__ void __launch_bounds__(256) dft_domain_prep(MfmaDomainPrepArgs a, uint2* __restrict__ tguard)
 {
-    constexpr int N = 8, NN = 64, NO = 16;
+    constexpr int NN = 64, NO = 16;
     const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
     if (gid >= a.ntiles * 32u)
         return;
@@ -119,11 +133,14 @@ __global__ void __launch_bounds__(256) dft_domain_prep(MfmaDomainPrepArgs a)
     for (int k = 0; k < NN; ++k)
         sb2 += b[k] * b[k];
     _Float16 comp[4][NO];
+    int dinf = 0;
 #pragma unroll
     for (int o = 0; o < NO; ++o) {
         const int b0 = b[kOrb8.p[o][0]], b1 = b[kOrb8.p[o][1]], b2 = b[kOrb8.p[o][2]], b3 = b[kOrb8.p[o][3]];
-        comp[0][o] = (_Float16)(b0 + b1 + b2 + b3);
-        comp[1][o] = (_Float16)(b0 - b1 + b2 - b3);
+        const int sb = b0 + b2, ub = b1 + b3;
+        dinf = max(dinf, max(abs(sb), abs(ub)));
+        comp[0][o] = (_Float16)sb;
+        comp[1][o] = (_Float16)ub;
         comp[2][o] = (_Float16)(b0 - b2);
         comp[3][o] = (_Float16)(b1 - b3);
     }
@@ -137,20 +154,23 @@ __global__ void __launch_bounds__(256) dft_domain_prep(MfmaDomainPrepArgs a)
                 v8[j] = comp[s][8 * h + j];
             a.dtiles[((size_t)tile * 4 + s) * 64 + row + 32 * h] = __builtin_bit_cast(uint4, v8);
         }
-    const float e = p >= 0 ? (float)sb2 : kDftPadConst; // Σb² ≤ 64·512² = 2^24: exact
+    const float ny = p >= 0 ? -(float)sb2 : kDftPadY; // Σb² ≤ 64·512² = 2^24: exact
     const uint32_t h = (row >> 2) & 1u, i = (row & 3u) + 4u * (row >> 3);
-    a.dconst[(size_t)tile * 32 + h * 16 + i] = __float_as_uint(e);
-    (void)N;
+    a.dconst[(size_t)tile * 32 + h * 16 + i] = __float_as_uint(ny);
+    if (p >= 0) {
+        atomicMax(&tguard[tile].x, (uint32_t)(4 * dinf));
+        atomicMax(&tguard[tile].y, (uint32_t)sb2);
+    }
 }
 
 // ---------------------------------------------------------------------------
-// dft_range_prep: per range block the six B fragments
-//   f0 = Â0, f1 = Â2  (K=16 each),  Pr: [f2 = α | f3 = β],  Pi: [f4 = β | f5 = −α]
-// (lane l: range slot l&31, orbit 8(l>>5) + j) and 16Σa² per slot.  One thread per slot.
+// dft_range_prep: per range block the seven distinct B fragments
+//   f0 = s_a, f1 = u_a, f2 = 4s_a, f3 = 4u_a, f4 = α, f5 = β, f6 = −α
+// (lane l: range slot l&31, orbit 8(l>>5) + j); U = [f0|f1], U' = [f1|f0] (×4: f2, f3),
+// Pr = [f4|f5], Pi = [f5|f6] against the domain K-steps [s_b|u_b], [γ|δ].  Also 16Σa² per
+// slot and the block's guard term max R1.  One thread per slot.
 // ---------------------------------------------------------------------------
-constexpr int kDftRangeFrags = 6;
-
-__global__ void __launch_bounds__(256) dft_range_prep(MfmaRangePrepArgs a)
+__global__ void __launch_bounds__(256) dft_range_prep(MfmaRangePrepArgs a, uint32_t* __restrict__ rguard)
 {
     constexpr int N = 8, NN = 64, NO = 16;
     const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
@@ -173,15 +193,19 @@ __global__ void __launch_bounds__(256) dft_range_prep(MfmaRangePrepArgs a)
             av[q] = 0;
     }
     _Float16 comp[kDftRangeFrags][NO];
+    int r1 = 0;
 #pragma unroll
     for (int o = 0; o < NO; ++o) {
         const int a0 = av[kOrb8.p[o][0]], a1 = av[kOrb8.p[o][1]], a2 = av[kOrb8.p[o][2]], a3 = av[kOrb8.p[o][3]];
-        comp[0][o] = (_Float16)(a0 + a1 + a2 + a3);
-        comp[1][o] = (_Float16)(a0 - a1 + a2 - a3);
-        comp[2][o] = (_Float16)(a0 - a2);
-        comp[3][o] = (_Float16)(a1 - a3);
-        comp[4][o] = (_Float16)(a1 - a3);
-        comp[5][o] = (_Float16)(a2 - a0);
+        const int sa = a0 + a2, ua = a1 + a3;
+        r1 += abs(sa) + abs(ua);
+        comp[0][o] = (_Float16)sa;
+        comp[1][o] = (_Float16)ua;
+        comp[2][o] = (_Float16)(4 * sa);
+        comp[3][o] = (_Float16)(4 * ua);
+        comp[4][o] = (_Float16)(a0 - a2);
+        comp[5][o] = (_Float16)(a1 - a3);
+        comp[6][o] = (_Float16)(a2 - a0);
     }
 #pragma unroll
     for (int f = 0; f < kDftRangeFrags; ++f)
@@ -194,74 +218,92 @@ __global__ void __launch_bounds__(256) dft_range_prep(MfmaRangePrepArgs a)
             a.rfrags[((size_t)b * kDftRangeFrags + f) * 64 + col + 32 * h] = __builtin_bit_cast(uint4, v8);
         }
     a.rconst[gid] = ri >= 0 ? (uint32_t)(16 * sa2) : 0u; // 16Σa² ≤ 2^24
+    atomicMax(&rguard[b], (uint32_t)r1);
 }
 
 // ---------------------------------------------------------------------------
-// search_dft<HITS>: the search_mfma work decomposition (workgroup = 4 waves = 4 range
+// search_dft<HITS, VAR>: the search_mfma work decomposition (workgroup = 4 waves = 4 range
 // blocks of one bucket, domain tiles staged through LDS, 4 tiles per double-buffered
-// stage); per lane the chunk minimum of w over its 16 rows × the stage's tiles and all
-// four transforms.  Entries: [nwork*4][64] {float bits of min w (−inf = hit), tile}.
+// stage); per lane the chunk maximum of y over its 16 rows × the stage's tiles (all four
+// transforms folded in).  Entries: [nwork*4][64] {float bits of max y (+inf = hit), tile}.
+// VAR 1: exact path only (A/B of the guard).
 // ---------------------------------------------------------------------------
-__device__ inline float dft_row(float p0, float p2, float pr, float pi, float sb2)
+__device__ inline floatx16_t mfma2(const half8_t& a0, const half8_t& b0, const half8_t& a1, const half8_t& b1,
+                                   const floatx16_t& c)
 {
-    const float A = p0 + p2, B = p0 - p2;
-    const float x1 = __builtin_fmaf(__builtin_fabsf(pr), 2.0f, A); // max(4Z_0, 4Z_2)
-    const float x2 = __builtin_fmaf(__builtin_fabsf(pi), 2.0f, B); // max(4Z_1, 4Z_3)
-    return __builtin_fmaf(__builtin_fmaxf(x1, x2), -2.0f, sb2);    // min_t S16 − 16Σa²
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, b1, __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, b0, c, 0, 0, 0),
+                                                  0, 0, 0);
 }
 
 template <int VAR>
-__device__ inline float dft_tile_min(const half8_t (&af)[4], const half8_t (&bf)[kDftRangeFrags], const float (&e)[16],
-                                     float m)
+__device__ inline float dft_tile_max(const half8_t (&af)[4], const half8_t (&bf)[kDftRangeFrags],
+                                     const floatx16_t& ny, bool fast, float m)
 {
     const floatx16_t z = {};
-    const floatx16_t p0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[0], bf[0], z, 0, 0, 0);
-    const floatx16_t p2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[1], bf[1], z, 0, 0, 0);
-    floatx16_t pr = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[2], bf[2], z, 0, 0, 0);
-    floatx16_t pi = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[2], bf[4], z, 0, 0, 0);
-    pr = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[3], bf[3], pr, 0, 0, 0);
-    pi = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[3], bf[5], pi, 0, 0, 0);
-    float m0 = m, m1 = __builtin_inff();
+    // af: [s_b, u_b, γ, δ];  bf: [s_a, u_a, 4s_a, 4u_a, α, β, −α]
+    const floatx16_t pr = mfma2(af[2], bf[4], af[3], bf[5], z);
+    const floatx16_t pi = mfma2(af[2], bf[5], af[3], bf[6], z);
+    float m0 = m, m1 = -__builtin_inff();
+    if ((VAR & 1) == 0 && fast) {
+        const floatx16_t u = mfma2(af[0], bf[2], af[1], bf[3], ny);  // 4U − Σb²
+        const floatx16_t v = mfma2(af[0], bf[3], af[1], bf[2], ny);  // 4U' − Σb²
 #pragma unroll
-    for (int i = 0; i < 16; i += 4) {
-        m0 = __builtin_fminf(__builtin_fminf(m0, dft_row(p0[i], p2[i], pr[i], pi[i], e[i])),
-                             dft_row(p0[i + 1], p2[i + 1], pr[i + 1], pi[i + 1], e[i + 1]));
-        m1 = __builtin_fminf(__builtin_fminf(m1, dft_row(p0[i + 2], p2[i + 2], pr[i + 2], pi[i + 2], e[i + 2])),
-                             dft_row(p0[i + 3], p2[i + 3], pr[i + 3], pi[i + 3], e[i + 3]));
+        for (int i = 0; i < 16; i += 2) {
+            m0 = __builtin_fmaxf(m0, __builtin_fmaxf(__builtin_fmaf(__builtin_fabsf(pr[i]), 4.0f, u[i]),
+                                                     __builtin_fmaf(__builtin_fabsf(pi[i]), 4.0f, v[i])));
+            m1 = __builtin_fmaxf(m1, __builtin_fmaxf(__builtin_fmaf(__builtin_fabsf(pr[i + 1]), 4.0f, u[i + 1]),
+                                                     __builtin_fmaf(__builtin_fabsf(pi[i + 1]), 4.0f, v[i + 1])));
+        }
+    } else {
+        const floatx16_t u = mfma2(af[0], bf[0], af[1], bf[1], z);   // U
+        const floatx16_t v = mfma2(af[0], bf[1], af[1], bf[0], z);   // U'
+#pragma unroll
+        for (int i = 0; i < 16; i += 2) {
+            const float y0 = __builtin_fmaf(
+                __builtin_fmaxf(u[i] + __builtin_fabsf(pr[i]), v[i] + __builtin_fabsf(pi[i])), 4.0f, ny[i]);
+            const float y1 = __builtin_fmaf(
+                __builtin_fmaxf(u[i + 1] + __builtin_fabsf(pr[i + 1]), v[i + 1] + __builtin_fabsf(pi[i + 1])), 4.0f,
+                ny[i + 1]);
+            m0 = __builtin_fmaxf(m0, __builtin_fmaxf(y0, y1));
+        }
     }
-    (void)VAR;
-    return __builtin_fminf(m0, m1);
+    return __builtin_fmaxf(m0, m1);
 }
 
 template <int VAR>
 __device__ inline float dft_compute_stage(const uint4* __restrict__ la, uint32_t nt, uint32_t lane,
-                                          const half8_t (&bf)[kDftRangeFrags])
+                                          const half8_t (&bf)[kDftRangeFrags], uint32_t tb,
+                                          const uint2* __restrict__ tguard, uint32_t r1)
 {
     const uint4* lc = la + nt * 4u * 64u;
     const uint32_t h = lane >> 5;
-    float cm = __builtin_inff();
+    float cm = -__builtin_inff();
     for (uint32_t q = 0; q < nt; ++q) {
         half8_t af[4];
 #pragma unroll
         for (int s = 0; s < 4; ++s)
             af[s] = __builtin_bit_cast(half8_t, la[(q * 4 + s) * 64 + lane]);
-        float e[16];
+        floatx16_t ny;
 #pragma unroll
         for (int c4 = 0; c4 < 4; ++c4) {
             const uint4 v = lc[q * 8 + h * 4 + c4];
-            e[4 * c4 + 0] = __uint_as_float(v.x);
-            e[4 * c4 + 1] = __uint_as_float(v.y);
-            e[4 * c4 + 2] = __uint_as_float(v.z);
-            e[4 * c4 + 3] = __uint_as_float(v.w);
+            ny[4 * c4 + 0] = __uint_as_float(v.x);
+            ny[4 * c4 + 1] = __uint_as_float(v.y);
+            ny[4 * c4 + 2] = __uint_as_float(v.z);
+            ny[4 * c4 + 3] = __uint_as_float(v.w);
         }
-        cm = dft_tile_min<VAR>(af, bf, e, cm);
+        // wave-uniform guard: every partial sum of 4U − Σb² stays within 2^24
+        const uint2 g = tguard[tb + q];
+        const bool fast = (uint64_t)r1 * g.x + g.y <= (uint64_t)kExactLimit;
+        cm = dft_tile_max<VAR>(af, bf, ny, fast, cm);
     }
     return cm;
 }
 
 template <bool HITS, int VAR>
-__global__ void __launch_bounds__(256) search_dft(MfmaSearchArgs a)
+__global__ void __launch_bounds__(256) search_dft(DftArgs d)
 {
+    const MfmaSearchArgs& a = d.m;
     constexpr int KS = 4;
     constexpr int STAGE = kTilesPerStage * KS * 64 + kTilesPerStage * 8;
     __shared__ uint4 lds0[STAGE];
@@ -270,21 +312,22 @@ __global__ void __launch_bounds__(256) search_dft(MfmaSearchArgs a)
     const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
     const bool active = wv < wk.y;
     const uint32_t blk = wk.x + (active ? wv : 0u);
+    const uint32_t r1 = __builtin_amdgcn_readfirstlane(d.rguard[blk]);
 
     half8_t bf[kDftRangeFrags];
 #pragma unroll
     for (int f = 0; f < kDftRangeFrags; ++f)
         bf[f] = __builtin_bit_cast(half8_t, a.rfrags[((size_t)blk * kDftRangeFrags + f) * 64 + lane]);
     float hl = 0.0f;
-    if constexpr (HITS) // S16 ≤ H  ⇔  w ≤ H − 16Σa²  (both exact integers below 2^24)
-        hl = (float)((int32_t)a.hitH - (int32_t)a.rconst[blk * 32 + (lane & 31u)]);
+    if constexpr (HITS) // S16 ≤ H  ⇔  y ≥ 16Σa² − H  (exact integers below 2^24)
+        hl = (float)((int32_t)a.rconst[blk * 32 + (lane & 31u)] - (int32_t)a.hitH);
 
-    float best = __builtin_inff();
+    float best = -__builtin_inff();
     uint32_t btile = 0;
     auto finish_stage = [&](float cm, uint32_t tb) {
         if constexpr (HITS)
-            cm = cm <= hl ? -__builtin_inff() : cm; // any hit in the chunk: the first-hit chunk wins
-        if (cm < best) {
+            cm = cm >= hl ? __builtin_inff() : cm; // any hit in the chunk: the first-hit chunk wins
+        if (cm > best) {
             best = cm;
             btile = tb;
         }
@@ -299,14 +342,14 @@ __global__ void __launch_bounds__(256) search_dft(MfmaSearchArgs a)
             __syncthreads();
             if (st + 1 < nstage)
                 stage_tiles<KS>(lds1, a.dtiles, a.dconst, tb + kTilesPerStage, stage_nt(st + 1));
-            finish_stage(dft_compute_stage<VAR>(lds0, stage_nt(st), lane, bf), tb);
+            finish_stage(dft_compute_stage<VAR>(lds0, stage_nt(st), lane, bf, tb, d.tguard, r1), tb);
         }
         if (st + 1 < nstage) {
             const uint32_t tb = wk.z + (st + 1) * kTilesPerStage;
             __syncthreads();
             if (st + 2 < nstage)
                 stage_tiles<KS>(lds0, a.dtiles, a.dconst, tb + kTilesPerStage, stage_nt(st + 2));
-            finish_stage(dft_compute_stage<VAR>(lds1, stage_nt(st + 1), lane, bf), tb);
+            finish_stage(dft_compute_stage<VAR>(lds1, stage_nt(st + 1), lane, bf, tb, d.tguard, r1), tb);
         }
     }
     if (active)
@@ -315,8 +358,8 @@ __global__ void __launch_bounds__(256) search_dft(MfmaSearchArgs a)
 
 // ---------------------------------------------------------------------------
 // resolve_dft: one wave per range (resolve_mfma's lane map: tile row i = l>>2, pixel
-// slice g = l&3).  The least entry w over the block's splits and lane halves gives the
-// target error S16 = w + 16Σa² (exact regime) or flags the range for the fp32 fallback;
+// slice g = l&3).  The greatest entry y over the block's splits and lane halves gives the
+// target error S16 = 16Σa² − y (exact regime) or flags the range for the fp32 fallback;
 // the chunk(s) holding it are re-evaluated with exact integers for all four transforms,
 // keeping the least selection key (first hit in (domain, transform) order, else least
 // error with ties to the earliest domain, then the later transform).
@@ -332,18 +375,20 @@ __global__ void __launch_bounds__(256) resolve_dft(MfmaResolveArgs a)
     const uint32_t blk = slot >> 5, col = slot & 31u;
     const uint32_t e0 = a.blk_ptr[blk], e1 = a.blk_ptr[blk + 1];
     const uint32_t nent = (e1 - e0) * 2u;
-    float vmin = __builtin_inff();
+    float vmax = -__builtin_inff();
     for (uint32_t j = lane; j < nent; j += 64)
-        vmin = __builtin_fminf(vmin, __uint_as_float(a.entries[(size_t)a.blk_ent[e0 + j / 2] * 64 + col + 32 * (j & 1)].x));
+        vmax = __builtin_fmaxf(vmax,
+                               __uint_as_float(a.entries[(size_t)a.blk_ent[e0 + j / 2] * 64 + col + 32 * (j & 1)].x));
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1)
-        vmin = __builtin_fminf(vmin, __shfl_xor(vmin, o, 64));
-    if (!(vmin < 1.0e29f))
+        vmax = __builtin_fmaxf(vmax, __shfl_xor(vmax, o, 64));
+    if (!(vmax > -1.0e29f))
         return; // only padding rows: no eligible domain, best_key stays "none"
     const int64_t sa16 = (int64_t)a.rconst[slot];
-    const bool exact = vmin < (float)(kExactLimit - sa16);
-    const int64_t target = exact && vmin != -__builtin_inff() ? (int64_t)vmin + sa16 : -1;
-    const bool hit = a.hitH >= 0 && (vmin == -__builtin_inff() || (target >= 0 && target <= a.hitH));
+    const bool sentinel = vmax == __builtin_inff();
+    const bool exact = sentinel || vmax > (float)(sa16 - kExactLimit);
+    const int64_t target = exact && !sentinel ? sa16 - (int64_t)vmax : -1;
+    const bool hit = a.hitH >= 0 && (sentinel || (target >= 0 && target <= a.hitH));
     const frac_grid_item rg = a.ranges[r];
     const int i = lane >> 2, g = lane & 3;
     int px[PG];
@@ -357,7 +402,7 @@ __global__ void __launch_bounds__(256) resolve_dft(MfmaResolveArgs a)
     sr2 += __shfl_xor(sr2, 1, 64);
     sr2 += __shfl_xor(sr2, 2, 64);
     unsigned long long bestk = kKeyNone;
-    const uint32_t vbits = __float_as_uint(vmin);
+    const uint32_t vbits = __float_as_uint(vmax);
     for (uint32_t j = 0; j < nent; ++j) { // wave-uniform loop over entries
         const uint2 en = a.entries[(size_t)a.blk_ent[e0 + j / 2] * 64 + col + 32 * (j & 1)];
         if (en.x != vbits)
