@@ -166,8 +166,12 @@ struct frac_ctx {
     std::vector<int32_t> m_slot_range;     // [nblocks*32]
     std::vector<uint32_t> m_range_slot;    // [nr]
     std::vector<int32_t> m_tile_pos;       // [ntiles*32]
-    std::vector<uint4> m_work;             // per WG
+    std::vector<uint4> m_work;             // per WG (4 range blocks: search_mfma)
     std::vector<uint32_t> m_blk_ptr, m_blk_ent;
+    std::vector<uint4> m8_work;            // per WG (8 range blocks: search_dft)
+    std::vector<uint32_t> m8_blk_ptr, m8_blk_ent;
+    DBuf<uint4> d_m8_work;
+    DBuf<uint32_t> d_m8_blk_ptr, d_m8_blk_ent;
     DBuf<int32_t> d_m_slot_range, d_m_tile_pos;
     DBuf<uint32_t> d_m_range_slot, d_m_blk_ptr, d_m_blk_ent, d_m_rconst, d_m_dconst;
     DBuf<uint4> d_m_work, d_m_dtiles, d_m_rfrags;
@@ -378,40 +382,51 @@ int prepare(frac_ctx* c)
             tile_count[b] = (uint32_t)(c->m_tile_pos.size() / 32) - tile_first[b];
         }
         c->ntiles = (uint32_t)(c->m_tile_pos.size() / 32);
-        // work items: groups of up to 4 blocks of one bucket × splits of its tiles
-        size_t groups = 0;
-        for (int b = 0; b < nb; ++b)
-            if (tile_count[b])
-                groups += (blk_count[b] + 3) / 4;
-        const size_t target_wgs = 8192;
-        std::vector<std::vector<uint32_t>> blk_list(c->nblocks);
-        c->m_work.clear();
-        for (int b = 0; b < nb; ++b) {
-            if (!tile_count[b] || !blk_count[b])
-                continue;
-            size_t splits = groups ? (target_wgs + groups - 1) / groups : 1;
-            splits = std::max<size_t>(1, std::min<size_t>(splits, std::max<uint32_t>(1u, tile_count[b] / 4u)));
-            for (uint32_t g = 0; g < blk_count[b]; g += 4) {
-                const uint32_t nbk = std::min(4u, blk_count[b] - g);
-                for (size_t sp = 0; sp < splits; ++sp) {
-                    const uint32_t t0 = tile_first[b] + (uint32_t)((uint64_t)tile_count[b] * sp / splits);
-                    const uint32_t t1 = tile_first[b] + (uint32_t)((uint64_t)tile_count[b] * (sp + 1) / splits);
-                    if (t1 <= t0)
-                        continue;
-                    const uint32_t w = (uint32_t)c->m_work.size();
-                    c->m_work.push_back(make_uint4(blk_first[b] + g, nbk, t0, t1));
-                    for (uint32_t k = 0; k < nbk; ++k)
-                        blk_list[blk_first[b] + g + k].push_back(w * 4u + k);
+        // work items: groups of up to BPW blocks of one bucket × splits of its tiles, plus the
+        // CSR map block → entry bases (work·BPW + wave) the resolve kernels read
+        auto build_work = [&](uint32_t bpw, size_t target_wgs, std::vector<uint4>& work,
+                              std::vector<uint32_t>& blk_ptr, std::vector<uint32_t>& blk_ent) {
+            size_t groups = 0;
+            for (int b = 0; b < nb; ++b)
+                if (tile_count[b])
+                    groups += (blk_count[b] + bpw - 1) / bpw;
+            std::vector<std::vector<uint32_t>> blk_list(c->nblocks);
+            work.clear();
+            for (int b = 0; b < nb; ++b) {
+                if (!tile_count[b] || !blk_count[b])
+                    continue;
+                size_t splits = groups ? (target_wgs + groups - 1) / groups : 1;
+                splits = std::max<size_t>(1, std::min<size_t>(splits, std::max<uint32_t>(1u, tile_count[b] / 4u)));
+                for (uint32_t g = 0; g < blk_count[b]; g += bpw) {
+                    const uint32_t nbk = std::min(bpw, blk_count[b] - g);
+                    for (size_t sp = 0; sp < splits; ++sp) {
+                        const uint32_t t0 = tile_first[b] + (uint32_t)((uint64_t)tile_count[b] * sp / splits);
+                        const uint32_t t1 = tile_first[b] + (uint32_t)((uint64_t)tile_count[b] * (sp + 1) / splits);
+                        if (t1 <= t0)
+                            continue;
+                        const uint32_t w = (uint32_t)work.size();
+                        work.push_back(make_uint4(blk_first[b] + g, nbk, t0, t1));
+                        for (uint32_t k = 0; k < nbk; ++k)
+                            blk_list[blk_first[b] + g + k].push_back(w * bpw + k);
+                    }
                 }
             }
+            blk_ptr.assign(c->nblocks + 1, 0);
+            blk_ent.clear();
+            for (uint32_t b = 0; b < c->nblocks; ++b) {
+                blk_ptr[b] = (uint32_t)blk_ent.size();
+                blk_ent.insert(blk_ent.end(), blk_list[b].begin(), blk_list[b].end());
+            }
+            blk_ptr[c->nblocks] = (uint32_t)blk_ent.size();
+        };
+        build_work(4, 8192, c->m_work, c->m_blk_ptr, c->m_blk_ent);
+        if (n == 8 && c->p.transforms == 4)
+            build_work(kDftBlocksPerWG, 8192 / kDftBlocksPerWG * 4, c->m8_work, c->m8_blk_ptr, c->m8_blk_ent);
+        else {
+            c->m8_work.clear();
+            c->m8_blk_ptr.clear();
+            c->m8_blk_ent.clear();
         }
-        c->m_blk_ptr.assign(c->nblocks + 1, 0);
-        c->m_blk_ent.clear();
-        for (uint32_t b = 0; b < c->nblocks; ++b) {
-            c->m_blk_ptr[b] = (uint32_t)c->m_blk_ent.size();
-            c->m_blk_ent.insert(c->m_blk_ent.end(), blk_list[b].begin(), blk_list[b].end());
-        }
-        c->m_blk_ptr[c->nblocks] = (uint32_t)c->m_blk_ent.size();
     }
 
     const size_t nr = c->ranges.size(), P = c->porig.size();
@@ -455,7 +470,15 @@ int prepare(frac_ctx* c)
         FRAC_HIP(c, c->d_m_dconst.ensure((size_t)c->ntiles * 32));
         FRAC_HIP(c, c->d_m_dtiles.ensure((size_t)c->ntiles * KS * 64));
         FRAC_HIP(c, c->d_m_rfrags.ensure((size_t)c->nblocks * T * KS * 64));
-        FRAC_HIP(c, c->d_m_entries.ensure(c->m_work.size() * 4 * T * 64));
+        FRAC_HIP(c, c->d_m_entries.ensure(std::max(c->m_work.size() * 4 * T, c->m8_work.size() * kDftBlocksPerWG) * 64));
+        if (!c->m8_blk_ptr.empty()) { // built for n = 8, T = 4 (search_dft); may have no work
+            FRAC_HIP(c, c->d_m8_work.ensure(std::max<size_t>(c->m8_work.size(), 1)));
+            FRAC_HIP(c, c->d_m8_blk_ptr.ensure(c->m8_blk_ptr.size()));
+            FRAC_HIP(c, c->d_m8_blk_ent.ensure(c->m8_blk_ent.size()));
+            FRAC_TRY(up(c->d_m8_work.ptr, c->m8_work.data(), c->m8_work.size() * sizeof(uint4)));
+            FRAC_TRY(up(c->d_m8_blk_ptr.ptr, c->m8_blk_ptr.data(), c->m8_blk_ptr.size() * sizeof(uint32_t)));
+            FRAC_TRY(up(c->d_m8_blk_ent.ptr, c->m8_blk_ent.data(), c->m8_blk_ent.size() * sizeof(uint32_t)));
+        }
         FRAC_TRY(up(c->d_m_slot_range.ptr, c->m_slot_range.data(), c->m_slot_range.size() * sizeof(int32_t)));
         FRAC_TRY(up(c->d_m_range_slot.ptr, c->m_range_slot.data(), nr * sizeof(uint32_t)));
         FRAC_TRY(up(c->d_m_tile_pos.ptr, c->m_tile_pos.data(), c->m_tile_pos.size() * sizeof(int32_t)));
@@ -546,32 +569,54 @@ inline int launch_dft(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride)
         dft_range_prep<<<(c->nblocks * 32 + 255) / 256, 256, 0, c->stream>>>(r, c->d_dft_rguard.ptr);
     if (c->p.flags & FRAC_FLAG_TIMING)
         FRAC_HIP(c, hipEventRecord(c->ev[1], c->stream));
-    if (!c->m_work.empty()) {
+    // FRAC_MFMA_VARIANT for this path (A/B knob): default = exact form in 8-wave workgroups;
+    // 1 = exact form in 4-wave workgroups, 3 = guarded fast path (4 waves), odd values ≥ 9 =
+    // ablations of variant 1 (tuning only: wrong results)
+    const int var = mfma_variant();
+    const bool four = var == 1 || var == 3 || (var >= 9 && (var & 1));
+    const std::vector<uint4>& work = four ? c->m_work : c->m8_work;
+    if (!work.empty()) {
         MfmaSearchArgs a;
         a.dtiles = c->d_m_dtiles.ptr;
         a.dconst = reinterpret_cast<const uint4*>(c->d_m_dconst.ptr);
         a.rfrags = c->d_m_rfrags.ptr;
         a.rconst = c->d_m_rconst.ptr;
-        a.work = c->d_m_work.ptr;
-        a.nwork = (uint32_t)c->m_work.size();
+        a.work = four ? c->d_m_work.ptr : c->d_m8_work.ptr;
+        a.nwork = (uint32_t)work.size();
         a.hitH = (uint32_t)std::max<int64_t>(c->hitH, 0);
         a.entries = c->d_m_entries.ptr;
         DftArgs da;
         da.m = a;
         da.rguard = c->d_dft_rguard.ptr;
         da.tguard = c->d_dft_tguard.ptr;
-        const unsigned nwg = (unsigned)c->m_work.size();
-        const bool exact_only = mfma_variant() == 1; // A/B knob: guard disabled
-        if (c->hitH > 0) {
-            if (exact_only)
+        const unsigned nwg = (unsigned)work.size();
+        const bool hits = c->hitH > 0;
+        constexpr uint32_t W8 = kDftBlocksPerWG;
+        if (!four) {
+            if (hits)
+                search_dft<true, 1, W8><<<nwg, 64 * W8, 0, c->stream>>>(da);
+            else
+                search_dft<false, 1, W8><<<nwg, 64 * W8, 0, c->stream>>>(da);
+        } else if (var == 1) {
+            if (hits)
                 search_dft<true, 1><<<nwg, 256, 0, c->stream>>>(da);
             else
-                search_dft<true, 0><<<nwg, 256, 0, c->stream>>>(da);
-        } else {
-            if (exact_only)
                 search_dft<false, 1><<<nwg, 256, 0, c->stream>>>(da);
+        } else if (var == 3) {
+            if (hits)
+                search_dft<true, 0><<<nwg, 256, 0, c->stream>>>(da);
             else
                 search_dft<false, 0><<<nwg, 256, 0, c->stream>>>(da);
+        } else {
+            switch (var) {
+            case 9: search_dft<false, 9><<<nwg, 256, 0, c->stream>>>(da); break;     // MFMA-only
+            case 17: search_dft<false, 17><<<nwg, 256, 0, c->stream>>>(da); break;   // VALU-only
+            case 41: search_dft<false, 41><<<nwg, 256, 0, c->stream>>>(da); break;   // MFMA-only, no LDS reads
+            case 73: search_dft<false, 73><<<nwg, 256, 0, c->stream>>>(da); break;   // MFMA-only, no DMA/barrier
+            case 105: search_dft<false, 105><<<nwg, 256, 0, c->stream>>>(da); break; // MFMA-only, neither
+            case 65: search_dft<false, 65><<<nwg, 256, 0, c->stream>>>(da); break;   // full, no DMA/barrier
+            default: search_dft<false, 1><<<nwg, 256, 0, c->stream>>>(da); break;
+            }
         }
     }
     if (c->p.flags & FRAC_FLAG_TIMING)
@@ -582,8 +627,8 @@ inline int launch_dft(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride)
         v.tstride = tstride;
         v.ranges = c->d_ranges.ptr;
         v.range_slot = c->d_m_range_slot.ptr;
-        v.blk_ptr = c->d_m_blk_ptr.ptr;
-        v.blk_ent = c->d_m_blk_ent.ptr;
+        v.blk_ptr = four ? c->d_m_blk_ptr.ptr : c->d_m8_blk_ptr.ptr;
+        v.blk_ent = four ? c->d_m_blk_ent.ptr : c->d_m8_blk_ent.ptr;
         v.entries = c->d_m_entries.ptr;
         v.rconst = c->d_m_rconst.ptr;
         v.tile_pos = c->d_m_tile_pos.ptr;
@@ -859,6 +904,9 @@ void frac_destroy(frac_ctx* c)
     c->d_m_rconst.release();
     c->d_m_dconst.release();
     c->d_m_work.release();
+    c->d_m8_work.release();
+    c->d_m8_blk_ptr.release();
+    c->d_m8_blk_ent.release();
     c->d_m_dtiles.release();
     c->d_m_rfrags.release();
     c->d_m_entries.release();

@@ -241,6 +241,31 @@ __device__ inline float dft_tile_max(const half8_t (&af)[4], const half8_t (&bf)
 {
     const floatx16_t z = {};
     // af: [s_b, u_b, γ, δ];  bf: [s_a, u_a, 4s_a, 4u_a, α, β, −α]
+    if constexpr ((VAR & 16) != 0) {
+        // ABLATION (tuning only, wrong results): the exact epilogue on fake accumulators
+        floatx16_t u, v, pr, pi;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const float b = __builtin_bit_cast(float, __builtin_bit_cast(uint4, af[i & 3]).x);
+            u[i] = b + (float)i;
+            v[i] = b - (float)i;
+            pr[i] = b * 0.5f;
+            pi[i] = ny[i];
+        }
+        float m2 = m;
+#pragma unroll
+        for (int i = 0; i < 16; i += 2) {
+            const float y0 = __builtin_fmaf(
+                __builtin_fmaxf(u[i] + __builtin_fabsf(pr[i]), v[i] + __builtin_fabsf(pi[i])), 4.0f, ny[i]);
+            const float y1 = __builtin_fmaf(__builtin_fmaxf(u[i + 1] + __builtin_fabsf(pr[i + 1]),
+                                                            v[i + 1] + __builtin_fabsf(pi[i + 1])),
+                                            4.0f, ny[i + 1]);
+            m2 = __builtin_fmaxf(m2, __builtin_fmaxf(y0, y1));
+        }
+        (void)bf;
+        (void)fast;
+        return m2;
+    }
     const floatx16_t pr = mfma2(af[2], bf[4], af[3], bf[5], z);
     const floatx16_t pi = mfma2(af[2], bf[5], af[3], bf[6], z);
     float m0 = m, m1 = -__builtin_inff();
@@ -254,6 +279,11 @@ __device__ inline float dft_tile_max(const half8_t (&af)[4], const half8_t (&bf)
             m1 = __builtin_fmaxf(m1, __builtin_fmaxf(__builtin_fmaf(__builtin_fabsf(pr[i + 1]), 4.0f, u[i + 1]),
                                                      __builtin_fmaf(__builtin_fabsf(pi[i + 1]), 4.0f, v[i + 1])));
         }
+    } else if constexpr ((VAR & 8) != 0) {
+        // ABLATION (tuning only, wrong results): MFMAs with a one-value epilogue
+        const floatx16_t u = mfma2(af[0], bf[0], af[1], bf[1], z);
+        const floatx16_t v = mfma2(af[0], bf[1], af[1], bf[0], z);
+        m0 = __builtin_fmaxf(m0, u[0] + v[0] + pr[0] + pi[0] + ny[0]);
     } else {
         const floatx16_t u = mfma2(af[0], bf[0], af[1], bf[1], z);   // U
         const floatx16_t v = mfma2(af[0], bf[1], af[1], bf[0], z);   // U'
@@ -279,14 +309,16 @@ __device__ inline float dft_compute_stage(const uint4* __restrict__ la, uint32_t
     const uint32_t h = lane >> 5;
     float cm = -__builtin_inff();
     for (uint32_t q = 0; q < nt; ++q) {
+        // ABLATION bit 32 (tuning only, wrong results): every tile reuses tile 0's operands
+        const uint32_t qq = (VAR & 32) ? 0u : q;
         half8_t af[4];
 #pragma unroll
         for (int s = 0; s < 4; ++s)
-            af[s] = __builtin_bit_cast(half8_t, la[(q * 4 + s) * 64 + lane]);
+            af[s] = __builtin_bit_cast(half8_t, la[(qq * 4 + s) * 64 + lane]);
         floatx16_t ny;
 #pragma unroll
         for (int c4 = 0; c4 < 4; ++c4) {
-            const uint4 v = lc[q * 8 + h * 4 + c4];
+            const uint4 v = lc[qq * 8 + h * 4 + c4];
             ny[4 * c4 + 0] = __uint_as_float(v.x);
             ny[4 * c4 + 1] = __uint_as_float(v.y);
             ny[4 * c4 + 2] = __uint_as_float(v.z);
@@ -300,8 +332,10 @@ __device__ inline float dft_compute_stage(const uint4* __restrict__ la, uint32_t
     return cm;
 }
 
-template <bool HITS, int VAR>
-__global__ void __launch_bounds__(256) search_dft(DftArgs d)
+constexpr uint32_t kDftBlocksPerWG = 8; // waves (range blocks) sharing one LDS domain stage
+
+template <bool HITS, int VAR, uint32_t WAVES = 4>
+__global__ void __launch_bounds__(64 * WAVES) search_dft(DftArgs d)
 {
     const MfmaSearchArgs& a = d.m;
     constexpr int KS = 4;
@@ -334,26 +368,30 @@ __global__ void __launch_bounds__(256) search_dft(DftArgs d)
     };
     const uint32_t nstage = (wk.w - wk.z + kTilesPerStage - 1) / kTilesPerStage;
     auto stage_nt = [&](uint32_t st) { return min((uint32_t)kTilesPerStage, wk.w - (wk.z + st * kTilesPerStage)); };
+    // ABLATION bit 64 (tuning only, wrong results): no LDS-DMA / barrier after the first stages
+    constexpr bool NODMA = (VAR & 64) != 0;
     if (nstage)
-        stage_tiles<KS>(lds0, a.dtiles, a.dconst, wk.z, stage_nt(0));
+        stage_tiles<KS, 64 * WAVES>(lds0, a.dtiles, a.dconst, wk.z, stage_nt(0));
     for (uint32_t st = 0; st < nstage; st += 2) {
         {
             const uint32_t tb = wk.z + st * kTilesPerStage;
-            __syncthreads();
-            if (st + 1 < nstage)
-                stage_tiles<KS>(lds1, a.dtiles, a.dconst, tb + kTilesPerStage, stage_nt(st + 1));
+            if (!NODMA || st < 2)
+                __syncthreads();
+            if (st + 1 < nstage && (!NODMA || st == 0))
+                stage_tiles<KS, 64 * WAVES>(lds1, a.dtiles, a.dconst, tb + kTilesPerStage, stage_nt(st + 1));
             finish_stage(dft_compute_stage<VAR>(lds0, stage_nt(st), lane, bf, tb, d.tguard, r1), tb);
         }
         if (st + 1 < nstage) {
             const uint32_t tb = wk.z + (st + 1) * kTilesPerStage;
-            __syncthreads();
-            if (st + 2 < nstage)
-                stage_tiles<KS>(lds0, a.dtiles, a.dconst, tb + kTilesPerStage, stage_nt(st + 2));
+            if (!NODMA || st < 2)
+                __syncthreads();
+            if (st + 2 < nstage && !NODMA)
+                stage_tiles<KS, 64 * WAVES>(lds0, a.dtiles, a.dconst, tb + kTilesPerStage, stage_nt(st + 2));
             finish_stage(dft_compute_stage<VAR>(lds1, stage_nt(st + 1), lane, bf, tb, d.tguard, r1), tb);
         }
     }
     if (active)
-        a.entries[(size_t)(blockIdx.x * 4u + wv) * 64 + lane] = make_uint2(__float_as_uint(best), btile);
+        a.entries[(size_t)(blockIdx.x * WAVES + wv) * 64 + lane] = make_uint2(__float_as_uint(best), btile);
 }
 
 // ---------------------------------------------------------------------------

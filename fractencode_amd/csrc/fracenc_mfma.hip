@@ -168,7 +168,7 @@ struct MfmaSearchArgs {
     uint2* entries;        // [nwork*4][T][64] {min v (0 = hit), tile}
 };
 
-template <int KS>
+template <int KS, uint32_t NTHREADS = 256>
 __device__ inline void stage_tiles(uint4* dst, const uint4* __restrict__ dtiles, const uint4* __restrict__ dconst,
                                    uint32_t tb, uint32_t nt)
 {
@@ -176,7 +176,7 @@ __device__ inline void stage_tiles(uint4* dst, const uint4* __restrict__ dtiles,
     // exactly this [A fragments | epilogue constants] stage layout.
     const uint32_t na = nt * KS * 64u, ntot = na + nt * 8u;
     const uint32_t lane = threadIdx.x & 63u;
-    for (uint32_t i = threadIdx.x; i < ntot; i += 256u) {
+    for (uint32_t i = threadIdx.x; i < ntot; i += NTHREADS) {
         const uint4* src = i < na ? dtiles + (size_t)tb * KS * 64 + i : dconst + (size_t)tb * 8 + (i - na);
         __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)src,
                                          (__attribute__((address_space(3))) void*)(dst + (i - lane)), 16, 0, 0);

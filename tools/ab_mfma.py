@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
 """Interleaved in-process A/B of MFMA search variants on the C3 frame; prints per-variant
 median/min search-kernel and finish (resolve + fit) ms (library HIP events).
-Variants: "d" = the C4-Fourier search (FRAC_MFMA_DFT=1, default), "e" = the same with its
-guarded fast path disabled (exact path only), an integer v = the direct
+Variants: "d" = the C4-Fourier search (FRAC_MFMA_DFT=1, default: software-pipelined exact
+form), "e" = its unpipelined exact form, "g" = the guarded fast-path form, "p" = pipelined with a forced interleave, "em"/"ev" = MFMA-only / VALU-only ablations of "e", an integer v = the direct
 search_mfma with FRAC_MFMA_VARIANT=v (FRAC_MFMA_DFT=0).
 usage: tools/ab_mfma.py d,2 [rounds]"""
 import os
@@ -27,13 +27,14 @@ with F.Engine(0, 4, False, 0.0, -1.0, F.ENGINE_MFMA, timing=True) as e:
     fin = {v: [] for v in variants}
     for r in range(rounds + 1):
         for v in variants:
-            os.environ["FRAC_MFMA_DFT"] = "1" if v in ("d", "e") else "0"
-            os.environ["FRAC_MFMA_VARIANT"] = {"d": "2", "e": "1"}.get(v, v)
+            os.environ["FRAC_MFMA_DFT"] = "1" if not v.isdigit() else "0"
+            os.environ["FRAC_MFMA_VARIANT"] = {"d": "2", "e": "1", "g": "3", "p": "4", "em": "9", "ev": "17", "emL": "41", "emB": "73",
+                                              "em0": "105", "eB": "65"}.get(v, v)
             e.run()
             out, st = e.fetch()
             if ref is None:
                 ref = out.tobytes()
-            if v in ("d", "e") or int(v) < 8:  # 8, 16 are ablations (results intentionally wrong)
+            if v in ("d", "e", "g", "p") or (v.isdigit() and int(v) < 8):  # 8, 16 are ablations (results intentionally wrong)
                 assert out.tobytes() == ref, f"variant {v} differs"
             if r:
                 res[v].append(st["ms_search"])
