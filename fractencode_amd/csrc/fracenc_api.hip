@@ -592,7 +592,27 @@ inline int launch_dft(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride)
         const unsigned nwg = (unsigned)work.size();
         const bool hits = c->hitH > 0;
         constexpr uint32_t W8 = kDftBlocksPerWG;
-        if (!four) {
+        if (!four && var >= 200) { // ablations of the 8-wave exact form (tuning only, wrong results)
+            switch (var) {
+            case 201: search_dft<false, 9, W8><<<nwg, 64 * W8, 0, c->stream>>>(da); break;   // MFMA-only
+            case 202: search_dft<false, 73, W8><<<nwg, 64 * W8, 0, c->stream>>>(da); break;  // MFMA-only, no DMA/bar
+            case 203: search_dft<false, 265, W8><<<nwg, 64 * W8, 0, c->stream>>>(da); break; // MFMA-only, no DMA
+            case 204: search_dft<false, 521, W8><<<nwg, 64 * W8, 0, c->stream>>>(da); break; // MFMA-only, no barrier
+            case 205: search_dft<false, 257, W8><<<nwg, 64 * W8, 0, c->stream>>>(da); break; // full, no DMA
+            case 206: search_dft<false, 513, W8><<<nwg, 64 * W8, 0, c->stream>>>(da); break; // full, no barrier
+            default: search_dft<false, 65, W8><<<nwg, 64 * W8, 0, c->stream>>>(da); break;  // full, no DMA/bar
+            }
+        } else if (!four && var == 6) { // register staging instead of LDS-DMA
+            if (hits)
+                search_dft_rs<true, W8><<<nwg, 64 * W8, 0, c->stream>>>(da);
+            else
+                search_dft_rs<false, W8><<<nwg, 64 * W8, 0, c->stream>>>(da);
+        } else if (!four && var == 5) { // 8-tile LDS stages
+            if (hits)
+                search_dft<true, 1, W8, 8><<<nwg, 64 * W8, 0, c->stream>>>(da);
+            else
+                search_dft<false, 1, W8, 8><<<nwg, 64 * W8, 0, c->stream>>>(da);
+        } else if (!four) {
             if (hits)
                 search_dft<true, 1, W8><<<nwg, 64 * W8, 0, c->stream>>>(da);
             else

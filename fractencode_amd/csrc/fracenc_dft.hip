@@ -303,12 +303,13 @@ __device__ inline float dft_tile_max(const half8_t (&af)[4], const half8_t (&bf)
 template <int VAR>
 __device__ inline float dft_compute_stage(const uint4* __restrict__ la, uint32_t nt, uint32_t lane,
                                           const half8_t (&bf)[kDftRangeFrags], uint32_t tb,
-                                          const uint2* __restrict__ tguard, uint32_t r1)
+                                          const uint2* __restrict__ tguard, uint32_t r1, uint32_t q0 = 0,
+                                          uint32_t q1 = ~0u)
 {
     const uint4* lc = la + nt * 4u * 64u;
     const uint32_t h = lane >> 5;
     float cm = -__builtin_inff();
-    for (uint32_t q = 0; q < nt; ++q) {
+    for (uint32_t q = q0; q < min(q1, nt); ++q) {
         // ABLATION bit 32 (tuning only, wrong results): every tile reuses tile 0's operands
         const uint32_t qq = (VAR & 32) ? 0u : q;
         half8_t af[4];
@@ -334,11 +335,12 @@ __device__ inline float dft_compute_stage(const uint4* __restrict__ la, uint32_t
 
 constexpr uint32_t kDftBlocksPerWG = 8; // waves (range blocks) sharing one LDS domain stage
 
-template <bool HITS, int VAR, uint32_t WAVES = 4>
+template <bool HITS, int VAR, uint32_t WAVES = 4, uint32_t TPS = kTilesPerStage>
 __global__ void __launch_bounds__(64 * WAVES) search_dft(DftArgs d)
 {
     const MfmaSearchArgs& a = d.m;
     constexpr int KS = 4;
+    constexpr uint32_t kTilesPerStage = TPS; // LDS stage; chunks stay 4 tiles (resolve_dft)
     constexpr int STAGE = kTilesPerStage * KS * 64 + kTilesPerStage * 8;
     __shared__ uint4 lds0[STAGE];
     __shared__ uint4 lds1[STAGE];
@@ -368,27 +370,108 @@ __global__ void __launch_bounds__(64 * WAVES) search_dft(DftArgs d)
     };
     const uint32_t nstage = (wk.w - wk.z + kTilesPerStage - 1) / kTilesPerStage;
     auto stage_nt = [&](uint32_t st) { return min((uint32_t)kTilesPerStage, wk.w - (wk.z + st * kTilesPerStage)); };
-    // ABLATION bit 64 (tuning only, wrong results): no LDS-DMA / barrier after the first stages
+    // ABLATION bits (tuning only, wrong results): 64 no LDS-DMA and no barrier after the first
+    // stages; 256 no LDS-DMA (barriers kept); 512 no barrier (LDS-DMA kept)
     constexpr bool NODMA = (VAR & 64) != 0;
+    constexpr bool SKIPDMA = NODMA || (VAR & 256) != 0, SKIPBAR = NODMA || (VAR & 512) != 0;
     if (nstage)
         stage_tiles<KS, 64 * WAVES>(lds0, a.dtiles, a.dconst, wk.z, stage_nt(0));
     for (uint32_t st = 0; st < nstage; st += 2) {
         {
             const uint32_t tb = wk.z + st * kTilesPerStage;
-            if (!NODMA || st < 2)
+            if (!SKIPBAR || st < 2)
                 __syncthreads();
-            if (st + 1 < nstage && (!NODMA || st == 0))
+            if (st + 1 < nstage && (!SKIPDMA || st == 0))
                 stage_tiles<KS, 64 * WAVES>(lds1, a.dtiles, a.dconst, tb + kTilesPerStage, stage_nt(st + 1));
-            finish_stage(dft_compute_stage<VAR>(lds0, stage_nt(st), lane, bf, tb, d.tguard, r1), tb);
+            for (uint32_t c0 = 0; c0 < stage_nt(st); c0 += 4)
+                finish_stage(dft_compute_stage<VAR>(lds0, stage_nt(st), lane, bf, tb, d.tguard, r1, c0, c0 + 4),
+                             tb + c0);
         }
         if (st + 1 < nstage) {
             const uint32_t tb = wk.z + (st + 1) * kTilesPerStage;
-            if (!NODMA || st < 2)
+            if (!SKIPBAR || st < 2)
                 __syncthreads();
-            if (st + 2 < nstage && !NODMA)
+            if (st + 2 < nstage && !SKIPDMA)
                 stage_tiles<KS, 64 * WAVES>(lds0, a.dtiles, a.dconst, tb + kTilesPerStage, stage_nt(st + 2));
-            finish_stage(dft_compute_stage<VAR>(lds1, stage_nt(st + 1), lane, bf, tb, d.tguard, r1), tb);
+            for (uint32_t c0 = 0; c0 < stage_nt(st + 1); c0 += 4)
+                finish_stage(
+                    dft_compute_stage<VAR>(lds1, stage_nt(st + 1), lane, bf, tb, d.tguard, r1, c0, c0 + 4), tb + c0);
         }
+    }
+    if (active)
+        a.entries[(size_t)(blockIdx.x * WAVES + wv) * 64 + lane] = make_uint2(__float_as_uint(best), btile);
+}
+
+// ---------------------------------------------------------------------------
+// search_dft_rs<HITS, WAVES>: search_dft's exact form with register staging instead of
+// LDS-DMA: while tile q of the current stage is computed, each thread holds one 16-B piece
+// of the next stage in registers (global_load at the start of the tile, ds_write at its
+// end, so the L2 latency hides behind the tile's MFMAs); one barrier per 4-tile stage.
+// ---------------------------------------------------------------------------
+template <bool HITS, uint32_t WAVES>
+__global__ void __launch_bounds__(64 * WAVES) search_dft_rs(DftArgs d)
+{
+    const MfmaSearchArgs& a = d.m;
+    constexpr uint32_t KS = 4, TPS = kTilesPerStage, NT = 64 * WAVES;
+    constexpr uint32_t STAGE = TPS * KS * 64 + TPS * 8;     // uint4 per stage
+    constexpr uint32_t PPT = (STAGE + NT - 1) / NT;         // pieces per thread and stage
+    static_assert(PPT <= TPS, "one staged piece per tile");
+    __shared__ uint4 lds[2][STAGE];
+    const uint4 wk = a.work[blockIdx.x];
+    const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    const bool active = wv < wk.y;
+    const uint32_t blk = wk.x + (active ? wv : 0u);
+
+    half8_t bf[kDftRangeFrags];
+#pragma unroll
+    for (int f = 0; f < kDftRangeFrags; ++f)
+        bf[f] = __builtin_bit_cast(half8_t, a.rfrags[((size_t)blk * kDftRangeFrags + f) * 64 + lane]);
+    float hl = 0.0f;
+    if constexpr (HITS)
+        hl = (float)((int32_t)a.rconst[blk * 32 + (lane & 31u)] - (int32_t)a.hitH);
+
+    float best = -__builtin_inff();
+    uint32_t btile = 0;
+    const uint32_t nstage = (wk.w - wk.z + TPS - 1) / TPS;
+    auto stage_nt = [&](uint32_t st) { return min(TPS, wk.w - (wk.z + st * TPS)); };
+    // piece i of the stage starting at tile tb with nt tiles: [A fragments | row constants]
+    auto piece_src = [&](uint32_t tb, uint32_t nt, uint32_t i) -> const uint4* {
+        const uint32_t na = nt * KS * 64u;
+        return i < na ? a.dtiles + (size_t)tb * KS * 64 + i : a.dconst + (size_t)tb * 8 + (i - na);
+    };
+    if (nstage) {
+        const uint32_t nt0 = stage_nt(0), ntot0 = nt0 * (KS * 64u + 8u);
+        for (uint32_t i = threadIdx.x; i < ntot0; i += NT)
+            lds[0][i] = *piece_src(wk.z, nt0, i);
+    }
+    // drain every global load here (vmcnt(0)): inside the loop the only outstanding load is
+    // the staged piece, so the MFMAs never wait on it
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+    __syncthreads();
+    for (uint32_t st = 0; st < nstage; ++st) {
+        const uint32_t cur = st & 1u, tb = wk.z + st * TPS, nt = stage_nt(st);
+        const bool more = st + 1 < nstage;
+        const uint32_t tbn = tb + TPS, ntn = more ? stage_nt(st + 1) : 0u, ntotn = ntn * (KS * 64u + 8u);
+        float cm = -__builtin_inff();
+        for (uint32_t q = 0; q < nt; ++q) {
+            // wave-uniform: the stage's pieces, the last one repeated by the tail threads
+            const bool stage_piece = more && q < PPT;
+            const uint32_t i = min(threadIdx.x + q * NT, ntotn - 1u);
+            uint4 reg;
+            if (stage_piece)
+                reg = *piece_src(tbn, ntn, i); // re-read by every range group: default cache policy
+            cm = __builtin_fmaxf(cm, dft_compute_stage<1>(lds[cur], nt, lane, bf, tb, d.tguard, 0u, q, q + 1));
+            asm volatile("" ::"v"(cm)); // the tile's epilogue completes before the ds_write below
+            if (stage_piece)
+                lds[cur ^ 1u][i] = reg;
+        }
+        if constexpr (HITS)
+            cm = cm >= hl ? __builtin_inff() : cm;
+        if (cm > best) {
+            best = cm;
+            btile = tb;
+        }
+        __syncthreads();
     }
     if (active)
         a.entries[(size_t)(blockIdx.x * WAVES + wv) * 64 + lane] = make_uint2(__float_as_uint(best), btile);
