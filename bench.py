@@ -171,7 +171,7 @@ def main():
         bound, peak, unit = "mfma", MFMA_F16_PEAK_TFLOPS, "TFLOP/s"
     else:
         bound, peak, unit = "valu", VALU_PEAK_TOPS, "TOP/s"
-    traffic = load_traffic(engine_name)
+    traffic = load_traffic(F.FORM_NAMES.get(st["search_form"], engine_name))
     line = {
         "metric": METRIC,
         "value": round(value, 1),
@@ -192,10 +192,17 @@ def main():
                      "frac": round(achieved / peak, 4), "traffic": traffic,
                      "kernel": "search", "kernel_ms": round(avg_search_ms, 3),
                      "ops_per_launch": ops_per_launch},
+        "search_form": F.FORM_NAMES.get(st["search_form"], "?"),
         "phases_ms": {"prep": round(st["ms_prep"], 3), "search": round(st["ms_search"], 3),
                       "finish": round(st["ms_finish"], 3)},
         "fallback_ranges": st["fallback_ranges"],
     }
+    if st["matrix_flops"]:
+        # the matrix-core work the search actually issued (the Fourier form needs 3/8 of the
+        # §8(d) direct-form count): the hardware utilisation beside the algorithmic figure
+        issued = st["matrix_flops"] / (avg_search_ms * 1e-3) / 1e12
+        line["roofline"]["issued"] = {"flops_per_launch": st["matrix_flops"], "achieved": round(issued, 2),
+                                      "frac": round(issued / MFMA_F16_PEAK_TFLOPS, 4)}
     if traffic:
         line["roofline"]["hbm_gbs"] = round(traffic / (avg_search_ms * 1e-3) / 1e9, 3)
         line["roofline"]["hbm_frac"] = round(line["roofline"]["hbm_gbs"] / HBM_PEAK_GBS, 6)

@@ -30,6 +30,8 @@ ENCODE_ITEM = np.dtype([("x", "<u4"), ("y", "<u4"), ("w", "<u4"), ("h", "<u4"),
 assert GRID_ITEM.itemsize == 20 and ENCODE_ITEM.itemsize == 64
 
 ENGINE_AUTO, ENGINE_VALU, ENGINE_MFMA = 0, 1, 2
+FORM_DOT2, FORM_DIRECT, FORM_FOURIER = 0, 1, 2
+FORM_NAMES = {FORM_DOT2: "dot2", FORM_DIRECT: "direct", FORM_FOURIER: "fourier"}
 FLAG_TIMING = 1
 
 # Frac::TransformType (image/transform.h:16-25)
@@ -46,7 +48,8 @@ class FracStats(C.Structure):
     _fields_ = [("rejected_mappings", C.c_uint64), ("total_mappings", C.c_uint64), ("hit_ranges", C.c_uint32),
                 ("fallback_ranges", C.c_uint32), ("empty_ranges", C.c_uint32), ("engine", C.c_uint32),
                 ("ms_device", C.c_double), ("ms_search", C.c_double), ("ms_prep", C.c_double),
-                ("ms_finish", C.c_double)]
+                ("ms_finish", C.c_double), ("search_form", C.c_uint32), ("pad_", C.c_uint32),
+                ("matrix_flops", C.c_uint64)]
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -189,6 +189,8 @@ struct frac_ctx {
     hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
     bool ran = false;
     uint32_t engine_ran = FRAC_ENGINE_VALU;
+    uint32_t form_ran = FRAC_FORM_DOT2;
+    uint64_t flops_ran = 0;
 
     int fail(int code, const std::string& msg)
     {
@@ -575,6 +577,10 @@ inline int launch_dft(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride)
     const int var = mfma_variant();
     const bool four = var == 1 || var == 3 || (var >= 9 && (var & 1));
     const std::vector<uint4>& work = four ? c->m_work : c->m8_work;
+    c->form_ran = FRAC_FORM_FOURIER;
+    c->flops_ran = 0;
+    for (const uint4& w : work) // 8 MFMA 32x32x16 (32768 flops each) per (range block, domain tile)
+        c->flops_ran += (uint64_t)w.y * (w.w - w.z) * 8ull * 32768ull;
     if (!work.empty()) {
         MfmaSearchArgs a;
         a.dtiles = c->d_m_dtiles.ptr;
@@ -697,6 +703,10 @@ int launch_mfma(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride)
     }
     if (c->p.flags & FRAC_FLAG_TIMING)
         FRAC_HIP(c, hipEventRecord(c->ev[1], c->stream));
+    c->form_ran = FRAC_FORM_DIRECT;
+    c->flops_ran = 0;
+    for (const uint4& w : c->m_work) // T·KS MFMA 32x32x16 per (range block, domain tile)
+        c->flops_ran += (uint64_t)w.y * (w.w - w.z) * T * MfmaGeom<N>::KS * 32768ull;
     if (!c->m_work.empty()) {
         MfmaSearchArgs a;
         a.dtiles = c->d_m_dtiles.ptr;
@@ -843,6 +853,10 @@ int launch_all(frac_ctx* c)
         FRAC_HIP(c, hipEventRecord(c->ev[3], c->stream));
     FRAC_HIP(c, hipGetLastError());
     c->engine_ran = use_mfma ? FRAC_ENGINE_MFMA : FRAC_ENGINE_VALU;
+    if (!use_mfma) {
+        c->form_ran = FRAC_FORM_DOT2;
+        c->flops_ran = 0;
+    }
     return FRAC_OK;
 }
 
@@ -1091,6 +1105,8 @@ int frac_fetch(frac_ctx* c, frac_encode_item* out, frac_stats* stats)
         std::memset(stats, 0, sizeof(*stats));
         stats->total_mappings = (uint64_t)c->doms.size() * nr;
         stats->engine = c->engine_ran;
+        stats->search_form = c->form_ran;
+        stats->matrix_flops = c->flops_ran;
         const uint64_t nd = c->doms.size();
         for (size_t r = 0; r < nr; ++r) {
             const RangeAux& ax = c->h_aux[r];

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define FRAC_ABI_VERSION 1
+#define FRAC_ABI_VERSION 2
 
 /* error codes */
 #define FRAC_OK 0
@@ -97,7 +97,15 @@ typedef struct frac_stats {
     double ms_search;           /* device time of the search kernel alone                        */
     double ms_prep;             /* domain pool / operand build                                   */
     double ms_finish;           /* winner fit + fallback                                         */
+    uint32_t search_form;       /* FRAC_FORM_*: how the search kernel computed the candidates     */
+    uint32_t pad_;
+    uint64_t matrix_flops;      /* MFMA flops the search issued (0 for the VALU engine)          */
 } frac_stats;
+
+/* frac_stats.search_form */
+#define FRAC_FORM_DOT2 0    /* VALU engine: packed-u16 v_dot2 per (range, transform, domain)       */
+#define FRAC_FORM_DIRECT 1  /* MFMA engine: one f16 GEMM per transform (n²·T MACs per pair)        */
+#define FRAC_FORM_FOURIER 2 /* MFMA engine, n = 8, T = 4: rotation-group Fourier form (96 MACs)    */
 
 typedef struct frac_ctx frac_ctx;
 

@@ -2,6 +2,7 @@
 the library loads, exports every symbol include/fracenc.h declares, the record
 layouts match the reference's structs, and the host helpers agree with the oracle.
 """
+import ctypes as C
 import os
 import re
 import subprocess
@@ -27,7 +28,7 @@ def test_library_exports_every_declared_symbol():
     assert len(names) >= 20
     missing = [n for n in names if not hasattr(lib, n)]
     assert not missing, missing
-    assert lib.frac_abi_version() == 1
+    assert lib.frac_abi_version() == 2
 
 
 def test_record_layouts_match_reference_structs(tmp_path):
@@ -43,6 +44,8 @@ def test_record_layouts_match_reference_structs(tmp_path):
         "_Static_assert(offsetof(frac_encode_item, match) == 16, \"match off\");\n"
         "_Static_assert(offsetof(frac_match, x) == 32, \"x off\");\n"
         "_Static_assert(offsetof(frac_score, transform) == 24, \"t off\");\n"
+        f"_Static_assert(sizeof(frac_stats) == {C.sizeof(F.FracStats)}, \"stats (ctypes mirror)\");\n"
+        f"_Static_assert(offsetof(frac_stats, matrix_flops) == {F.FracStats.matrix_flops.offset}, \"flops off\");\n"
         "int main(void) { return 0; }\n")
     subprocess.check_call(["gcc", "-std=c11", "-I", os.path.join(ROOT, "include"), "-c", str(src), "-o",
                            str(tmp_path / "layout.o")])

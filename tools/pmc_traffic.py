@@ -1,0 +1,34 @@
+#!/usr/bin/env python3
+"""Writes profiles/pmc_search.json from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (separate
+runs, kB per dispatch) of bench.py: HBM-side bytes per search launch, FETCH_SIZE doubled on gfx950
+(MI355X_MICROARCH.md §HBM: 16-B/lane streaming reads are tallied at half their bytes).
+usage: tools/pmc_traffic.py FORM KERNEL_PREFIX FETCH_CSV WRITE_CSV SOURCE_NOTE"""
+import collections
+import csv
+import json
+import os
+import sys
+
+form, prefix, fcsv, wcsv, note = sys.argv[1:6]
+
+
+def avg(path):
+    tot, disp = 0.0, set()
+    for r in csv.DictReader(open(path)):
+        if r["Kernel_Name"].startswith(prefix):
+            tot += float(r["Counter_Value"])
+            disp.add(r["Dispatch_Id"])
+    return tot / max(1, len(disp)), len(disp)
+
+
+f, nf = avg(fcsv)
+w, nw = avg(wcsv)
+path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "pmc_search.json")
+d = json.load(open(path)) if os.path.exists(path) else {}
+d["_doc"] = ("HBM-side bytes per search launch from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes, "
+             "kB units), corrected per MI355X_MICROARCH.md §HBM: FETCH_SIZE doubled on gfx950, WRITE_SIZE as "
+             "reported.  Keyed by frac_stats.search_form.")
+d[form] = {"kernel": prefix, "fetch_size_kb": round(f, 1), "write_size_kb": round(w, 1), "dispatches": [nf, nw],
+           "hbm_bytes_per_launch": int(round((2 * f + w) * 1024)), "source": note}
+json.dump(d, open(path, "w"), indent=1)
+print(json.dumps(d[form]))
