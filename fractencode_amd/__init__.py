@@ -93,6 +93,7 @@ def lib() -> C.CDLL:
                                   C.POINTER(C.c_double)]),
             "frac_decode_results": (i32, [vp, u32, u32, i32, C.c_double, vp, C.POINTER(C.c_int),
                                           C.POINTER(C.c_double)]),
+            "frac_classify_items": (i32, [vp, vp, sz, i32]),
             "frac_rgb_to_yuv_device": (i32, [vp, vp, u32, u32, u32, vp, u32, vp, u32, vp, u32]),
             "frac_rgb_to_yuv": (i32, [vp, vp, u32, u32, u32, vp, vp, vp]),
             "frac_uniform_grid": (sz, [u32, u32, u32, u32, vp, sz]),
@@ -263,6 +264,14 @@ class Engine:
             self._check(lib().frac_decode(self._ctx, items.ctypes.data if len(items) else None, len(items), width,
                                           height, max_iter, rms_eps, plane.ctypes.data, C.byref(it), C.byref(rms)))
         return plane, it.value, rms.value
+
+    def classify(self, items: np.ndarray, target_plane: bool = False) -> np.ndarray:
+        """BrightnessBlocksClassifier2 categories of `items` computed on the device plane set by
+        set_frame / set_planes (returns a copy with the categories filled in)."""
+        items = np.ascontiguousarray(items, dtype=GRID_ITEM).copy()
+        self._check(lib().frac_classify_items(self._ctx, items.ctypes.data if len(items) else None, len(items),
+                                              int(target_plane)))
+        return items
 
     def rgb_to_yuv(self, rgb):
         """ImageIO::rgb2yuv on the device (image/ImageIO.cpp:43-58).

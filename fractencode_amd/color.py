@@ -11,7 +11,7 @@ from __future__ import annotations
 
 import numpy as np
 
-from . import ENGINE_AUTO, Engine, create_uniform_grid, preclassify
+from . import ENGINE_AUTO, Engine, create_uniform_grid
 
 PLANES = ("Y", "U", "V")
 
@@ -53,11 +53,10 @@ class ColorEncoder:
         for e, p in zip(self.engines, planes):
             H, W = p.shape
             e.set_frame(p)
+            # categories −1: with the classifier on, the engine classifies every item on the
+            # device plane (main.cpp:155-162 preclassifies both grids on the same plane)
             doms = create_uniform_grid(W, H, d, d // 2)
             rngs = create_uniform_grid(W, H, n, n)
-            if self.use_classifier:
-                host = p.cpu().numpy()
-                doms, rngs = preclassify(host, doms), preclassify(host, rngs)
             e.set_domains(doms)
             e.set_ranges(rngs)
             self.ranges.append(rngs)

@@ -19,6 +19,7 @@
 #include "fracenc_dft.hip"
 #include "fracenc_decode.hip"
 #include "fracenc_color.hip"
+#include "fracenc_classify.hip"
 
 using namespace fracenc;
 
@@ -180,6 +181,9 @@ struct frac_ctx {
     // decoder state
     DBuf<uint8_t> d_dec_src, d_dec_tgt, d_color;
     DBuf<uint2> d_dft_tguard;
+    DBuf<frac_grid_item> d_cls_items;
+    DBuf<uint32_t> d_cls_list;
+    DBuf<int32_t> d_cls_out;
     DBuf<uint32_t> d_dft_rguard;
     DBuf<frac_encode_item> d_dec_items;
     DBuf<unsigned long long> d_dec_sum;
@@ -233,6 +237,35 @@ int check_params(const frac_params* p, std::string& msg)
     return FRAC_OK;
 }
 
+// Categories of items[list[k]] on the device plane (classify_items); synchronous.
+int classify_on_device(frac_ctx* c, const std::vector<frac_grid_item>& items, const std::vector<uint32_t>& list,
+                       const uint8_t* dplane, uint32_t dstride, std::vector<int32_t>& out)
+{
+    out.assign(list.size(), -1);
+    if (list.empty())
+        return FRAC_OK;
+    FRAC_HIP(c, c->d_cls_items.ensure(items.size()));
+    FRAC_HIP(c, c->d_cls_list.ensure(list.size()));
+    FRAC_HIP(c, c->d_cls_out.ensure(list.size()));
+    FRAC_HIP(c, hipMemcpyAsync(c->d_cls_items.ptr, items.data(), items.size() * sizeof(frac_grid_item),
+                               hipMemcpyHostToDevice, c->stream));
+    FRAC_HIP(c, hipMemcpyAsync(c->d_cls_list.ptr, list.data(), list.size() * sizeof(uint32_t), hipMemcpyHostToDevice,
+                               c->stream));
+    ClassifyArgs a;
+    a.plane = dplane;
+    a.stride = dstride;
+    a.items = c->d_cls_items.ptr;
+    a.list = c->d_cls_list.ptr;
+    a.n = (uint32_t)list.size();
+    a.out = c->d_cls_out.ptr;
+    classify_items<<<(unsigned)((list.size() + 3) / 4), 256, 0, c->stream>>>(a);
+    FRAC_HIP(c, hipGetLastError());
+    FRAC_HIP(c, hipMemcpyAsync(out.data(), c->d_cls_out.ptr, list.size() * sizeof(int32_t), hipMemcpyDeviceToHost,
+                               c->stream));
+    FRAC_HIP(c, hipStreamSynchronize(c->stream));
+    return FRAC_OK;
+}
+
 int upload_plane(frac_ctx* c, const HostPlane& hp, DBuf<uint8_t>& d, uint32_t& dstride)
 {
     dstride = (hp.w + 63u) & ~63u;
@@ -275,18 +308,27 @@ int prepare(frac_ctx* c)
     std::vector<int32_t> dbk(c->doms.size(), 0);
     c->range_bucket.assign(c->ranges.size(), 0);
     if (c->p.use_classifier) {
-        for (size_t i = 0; i < c->doms.size(); ++i) {
-            int cat = c->doms[i].category;
-            if (cat == -1)
-                cat = category(c->src, c->doms[i]);
-            dbk[i] = cat + 1;
-        }
-        for (size_t i = 0; i < c->ranges.size(); ++i) {
-            int cat = c->ranges[i].category;
-            if (cat == -1)
-                cat = category(c->tgt, c->ranges[i]);
-            c->range_bucket[i] = cat + 1;
-        }
+        // a stored −1 is recomputed on the item's own plane (BrightnessBlocksClassifier2::compare,
+        // encode/Classifier2.cpp:70-81) — on the device (fracenc_classify.hip)
+        std::vector<uint32_t> dl, rl;
+        for (size_t i = 0; i < c->doms.size(); ++i)
+            if (c->doms[i].category == -1)
+                dl.push_back((uint32_t)i);
+        for (size_t i = 0; i < c->ranges.size(); ++i)
+            if (c->ranges[i].category == -1)
+                rl.push_back((uint32_t)i);
+        std::vector<int32_t> dcat, rcat;
+        FRAC_TRY(classify_on_device(c, c->doms, dl, c->d_src.ptr, c->d_sstride, dcat));
+        FRAC_TRY(classify_on_device(c, c->ranges, rl, c->same_plane ? c->d_src.ptr : c->d_tgt.ptr,
+                                    c->same_plane ? c->d_sstride : c->d_tstride, rcat));
+        for (size_t i = 0; i < c->doms.size(); ++i)
+            dbk[i] = c->doms[i].category + 1;
+        for (size_t k = 0; k < dl.size(); ++k)
+            dbk[dl[k]] = dcat[k] + 1;
+        for (size_t i = 0; i < c->ranges.size(); ++i)
+            c->range_bucket[i] = c->ranges[i].category + 1;
+        for (size_t k = 0; k < rl.size(); ++k)
+            c->range_bucket[rl[k]] = rcat[k] + 1;
         for (size_t i = 0; i < c->doms.size(); ++i)
             if (dbk[i] < 0 || dbk[i] >= nb)
                 return c->fail(FRAC_E_INVALID, "domain category outside -1..5");
@@ -947,6 +989,9 @@ void frac_destroy(frac_ctx* c)
     c->d_dec_src.release();
     c->d_color.release();
     c->d_dft_tguard.release();
+    c->d_cls_items.release();
+    c->d_cls_list.release();
+    c->d_cls_out.release();
     c->d_dft_rguard.release();
     c->d_dec_tgt.release();
     c->d_dec_items.release();
@@ -1020,11 +1065,10 @@ int frac_set_frame_device(frac_ctx* c, const void* d_plane, uint32_t w, uint32_t
     if (!d_plane || w == 0 || h == 0 || stride < w)
         return c->fail(FRAC_E_INVALID, "invalid device plane");
     FRAC_HIP(c, hipSetDevice(c->device));
-    // host copy for the classifier's category pre-pass (host-side, as in the reference)
+    // the frame stays on the device: the classifier pre-pass runs there too
     c->src.w = w;
     c->src.h = h;
-    c->src.data.resize((size_t)w * h);
-    FRAC_HIP(c, hipMemcpy2DAsync(c->src.data.data(), w, d_plane, stride, w, h, hipMemcpyDeviceToHost, c->stream));
+    c->src.data.clear();
     c->d_sstride = (w + 63u) & ~63u;
     FRAC_HIP(c, c->d_src.ensure((size_t)c->d_sstride * (h + 1)));
     FRAC_HIP(c, hipMemcpy2DAsync(c->d_src.ptr, c->d_sstride, d_plane, stride, w, h, hipMemcpyDeviceToDevice, c->stream));
@@ -1161,6 +1205,32 @@ int frac_set_stream(frac_ctx* c, void* s)
 void* frac_get_stream(frac_ctx* c) { return c ? reinterpret_cast<void*>(c->stream) : nullptr; }
 
 const frac_encode_item* frac_device_results(frac_ctx* c) { return c ? c->d_out.ptr : nullptr; }
+
+int frac_classify_items(frac_ctx* c, frac_grid_item* items, size_t n, int target_plane)
+{
+    if (!c)
+        return FRAC_E_INVALID;
+    if (n && !items)
+        return c->fail(FRAC_E_INVALID, "classify: items is NULL");
+    if (!c->planes_set)
+        return c->fail(FRAC_E_STATE, "classify: no frame set");
+    const bool tgt = target_plane != 0 && !c->same_plane;
+    const HostPlane& hp = tgt ? c->tgt : c->src;
+    std::vector<frac_grid_item> v(items, items + n);
+    std::vector<uint32_t> list(n);
+    for (size_t i = 0; i < n; ++i) {
+        if ((uint64_t)v[i].x + v[i].w > hp.w || (uint64_t)v[i].y + v[i].h > hp.h)
+            return c->fail(FRAC_E_INVALID, "classify: item outside the plane");
+        list[i] = (uint32_t)i;
+    }
+    FRAC_HIP(c, hipSetDevice(c->device));
+    std::vector<int32_t> cat;
+    FRAC_TRY(classify_on_device(c, v, list, tgt ? c->d_tgt.ptr : c->d_src.ptr, tgt ? c->d_tstride : c->d_sstride,
+                                cat));
+    for (size_t i = 0; i < n; ++i)
+        items[i].category = cat[i];
+    return FRAC_OK;
+}
 
 int frac_rgb_to_yuv_device(frac_ctx* c, const void* d_rgb, uint32_t w, uint32_t h, uint32_t rgb_stride, void* d_y,
                            uint32_t y_stride, void* d_u, uint32_t u_stride, void* d_v, uint32_t v_stride)

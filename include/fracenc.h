@@ -161,6 +161,13 @@ int frac_decode(frac_ctx* ctx, const frac_encode_item* items, size_t n, uint32_t
 int frac_decode_results(frac_ctx* ctx, uint32_t w, uint32_t h, int max_iter, double rms_eps, uint8_t* plane,
                         int* iterations, double* rms);
 
+/* ---- classifier pre-pass on the device (BrightnessBlocksClassifier2::preclassify,
+ * encode/Classifier2.cpp:55-68, as main.cpp:155-162 runs it at grid build) ----
+ * Writes the category (0..5 or -1) of each item, computed on the context's source plane
+ * (target_plane = 0) or target plane (1) already on the device.  frac_run does the same
+ * internally for any item whose stored category is -1 when use_classifier is set. */
+int frac_classify_items(frac_ctx* ctx, frac_grid_item* items, size_t n, int target_plane);
+
 /* ---- frame loader: colour conversion (ImageIO::rgb2yuv, image/ImageIO.cpp:43-58) ----
  * Packed RGB (w×h, rgb_stride bytes per row) → Y (w×h) and U, V (w/2 × h/2, the odd
  * pixel of each 2×2 quad), bit-exact with the built reference (FMA-contracted weights).

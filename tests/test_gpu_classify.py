@@ -1,0 +1,68 @@
+"""Classifier pre-pass on the device (fracenc_classify.hip) against the oracle and the
+reference's ClassifierTest known answers; the engine's internal −1 recomputation gives
+the same search results as host-preclassified grids."""
+import numpy as np
+import pytest
+
+import fractencode_amd as F
+from golden_util import FIELDS, golden, plane
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("size,off", [(2, 2), (4, 2), (8, 8), (16, 8), (32, 16), (64, 32), (7, 3), (5, 5)])
+def test_device_classify_matches_oracle(oracle, size, off):
+    y = plane("lenna_y")
+    items = F.create_uniform_grid(512, 512, size, off)
+    with F.Engine(0) as e:
+        e.set_frame(y)
+        got = e.classify(items)
+    want = oracle.classify(y, items)
+    np.testing.assert_array_equal(got["category"], want["category"])
+
+
+def test_device_classify_reference_kat():
+    # reference tests/ClassifierTest.cpp:24-50 on the Lenna Y plane
+    y = plane("lenna_y")
+    cases = [(204, 78, 2, 0), (242, 242, 2, 1), (6, 6, 2, 2), (82, 226, 2, 3), (418, 486, 2, 4), (384, 250, 2, 5),
+             (136, 40, 2, -1), (184, 96, 8, 0), (472, 96, 8, -1), (320, 224, 16, 4), (416, 256, 16, -1),
+             (384, 224, 32, -1), (64, 320, 32, 5), (64, 0, 64, 0), (128, 320, 64, 5)]
+    items = np.zeros(len(cases), dtype=F.GRID_ITEM)
+    for i, (x, yy, s, _) in enumerate(cases):
+        items[i] = (x, yy, s, s, -1)
+    with F.Engine(0) as e:
+        e.set_frame(y)
+        got = e.classify(items)
+    assert list(got["category"]) == [c for *_, c in cases]
+
+
+@pytest.mark.parametrize("engine", [F.ENGINE_VALU, F.ENGINE_MFMA])
+def test_engine_classifies_unlabelled_items_on_device(engine):
+    # categories −1 + use_classifier: the engine's device pre-pass reproduces the
+    # reference goldens made with host-preclassified grids (main.cpp:155-162)
+    rec, meta = golden("lenna_cls")
+    p = plane("lenna_y")
+    with F.Engine(0, 4, True, 0.0, -1.0, engine) as e:
+        e.set_frame(p)
+        e.set_domains(F.create_uniform_grid(512, 512, 16, 8))
+        out, st = e.search(F.create_uniform_grid(512, 512, 8, 8))
+    got = {"x": out["x"], "y": out["y"], "dx": out["dx"], "dy": out["dy"], "dw": out["sw"], "dh": out["sh"],
+           "t": out["transform"], "dist": out["distance"], "s": out["contrast"], "o": out["brightness"]}
+    for k in FIELDS:
+        np.testing.assert_array_equal(got[k], rec[k], err_msg=k)
+    assert st["rejected_mappings"] == meta["rejected"]
+
+
+def test_device_frame_classifier_without_host_copy():
+    # a CUDA-tensor frame never comes back to the host; the classifier still runs
+    import torch
+
+    rec, meta = golden("lenna_cls")
+    p = plane("lenna_y")
+    with F.Engine(0, 4, True) as e:
+        e.set_frame(torch.from_numpy(p).cuda())
+        e.set_domains(F.create_uniform_grid(512, 512, 16, 8))
+        out, st = e.search(F.create_uniform_grid(512, 512, 8, 8))
+    np.testing.assert_array_equal(out["dx"], rec["dx"])
+    np.testing.assert_array_equal(out["transform"], rec["t"])
+    assert st["rejected_mappings"] == meta["rejected"]

@@ -87,3 +87,35 @@ def test_color_encoder_matches_reference_planes(oracle, engine):
         assert (it, rms) == (wit, wrms)
         np.testing.assert_array_equal(dec, want)
         assert codec.psnr(p, dec) > 25.0
+
+
+def test_color_encoder_with_classifier(oracle):
+    # Y against the reference's classifier golden; U and V against the oracle (the engine
+    # classifies every plane's grids on the device)
+    from fractencode_amd.color import ColorEncoder
+
+    with ColorEncoder(0, 8, 16, 4, use_classifier=True) as enc:
+        enc.load(plane("lenna_rgb"))
+        enc.run()
+        enc.sync()
+        results = enc.fetch()
+        planes = enc.host_planes()
+    rec, meta = golden("lenna_cls")
+    out, st = results[0]
+    np.testing.assert_array_equal(out["dx"], rec["dx"])
+    np.testing.assert_array_equal(out["dy"], rec["dy"])
+    np.testing.assert_array_equal(out["transform"], rec["t"])
+    np.testing.assert_array_equal(out["distance"], rec["dist"])
+    assert st["rejected_mappings"] == meta["rejected"]
+    for (out, st), p in zip(results[1:], planes[1:]):
+        H, W = p.shape
+        doms = oracle.classify(p, oracle.uniform_grid(W, H, 16, 8))
+        rngs = oracle.classify(p, oracle.uniform_grid(W, H, 8, 8))
+        want, rej, _ = oracle.estimate(p, doms, rngs, T=4, use_classifier=True)
+        np.testing.assert_array_equal(out["dx"], want["dx"])
+        np.testing.assert_array_equal(out["dy"], want["dy"])
+        np.testing.assert_array_equal(out["transform"], want["t"])
+        np.testing.assert_array_equal(out["distance"], want["dist"])
+        np.testing.assert_array_equal(out["contrast"], want["s"])
+        np.testing.assert_array_equal(out["brightness"], want["o"])
+        assert st["rejected_mappings"] == rej
