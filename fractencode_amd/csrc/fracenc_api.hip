@@ -650,11 +650,6 @@ inline int launch_dft(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride)
             case 206: search_dft<false, 513, W8><<<nwg, 64 * W8, 0, c->stream>>>(da); break; // full, no barrier
             default: search_dft<false, 65, W8><<<nwg, 64 * W8, 0, c->stream>>>(da); break;  // full, no DMA/bar
             }
-        } else if (!four && var == 6) { // register staging instead of LDS-DMA
-            if (hits)
-                search_dft_rs<true, W8><<<nwg, 64 * W8, 0, c->stream>>>(da);
-            else
-                search_dft_rs<false, W8><<<nwg, 64 * W8, 0, c->stream>>>(da);
         } else if (!four && var == 5) { // 8-tile LDS stages
             if (hits)
                 search_dft<true, 1, W8, 8><<<nwg, 64 * W8, 0, c->stream>>>(da);

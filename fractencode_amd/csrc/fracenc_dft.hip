@@ -309,6 +309,16 @@ __device__ inline float dft_compute_stage(const uint4* __restrict__ la, uint32_t
     const uint4* lc = la + nt * 4u * 64u;
     const uint32_t h = lane >> 5;
     float cm = -__builtin_inff();
+    // the chunk's fast-path guards, loaded up front (wave-uniform scalar loads)
+    uint32_t gfast = 0;
+    if constexpr ((VAR & 1) == 0) {
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k)
+            if (q0 + k < min(q1, nt)) {
+                const uint2 g = tguard[tb + q0 + k];
+                gfast |= ((uint64_t)r1 * g.x + g.y <= (uint64_t)kExactLimit) ? (1u << k) : 0u;
+            }
+    }
     for (uint32_t q = q0; q < min(q1, nt); ++q) {
         // ABLATION bit 32 (tuning only, wrong results): every tile reuses tile 0's operands
         const uint32_t qq = (VAR & 32) ? 0u : q;
@@ -326,8 +336,7 @@ __device__ inline float dft_compute_stage(const uint4* __restrict__ la, uint32_t
             ny[4 * c4 + 3] = __uint_as_float(v.w);
         }
         // wave-uniform guard: every partial sum of 4U − Σb² stays within 2^24
-        const uint2 g = tguard[tb + q];
-        const bool fast = (uint64_t)r1 * g.x + g.y <= (uint64_t)kExactLimit;
+        const bool fast = (gfast >> (q - q0)) & 1u;
         cm = dft_tile_max<VAR>(af, bf, ny, fast, cm);
     }
     return cm;
@@ -397,81 +406,6 @@ __global__ void __launch_bounds__(64 * WAVES) search_dft(DftArgs d)
                 finish_stage(
                     dft_compute_stage<VAR>(lds1, stage_nt(st + 1), lane, bf, tb, d.tguard, r1, c0, c0 + 4), tb + c0);
         }
-    }
-    if (active)
-        a.entries[(size_t)(blockIdx.x * WAVES + wv) * 64 + lane] = make_uint2(__float_as_uint(best), btile);
-}
-
-// ---------------------------------------------------------------------------
-// search_dft_rs<HITS, WAVES>: search_dft's exact form with register staging instead of
-// LDS-DMA: while tile q of the current stage is computed, each thread holds one 16-B piece
-// of the next stage in registers (global_load at the start of the tile, ds_write at its
-// end, so the L2 latency hides behind the tile's MFMAs); one barrier per 4-tile stage.
-// ---------------------------------------------------------------------------
-template <bool HITS, uint32_t WAVES>
-__global__ void __launch_bounds__(64 * WAVES) search_dft_rs(DftArgs d)
-{
-    const MfmaSearchArgs& a = d.m;
-    constexpr uint32_t KS = 4, TPS = kTilesPerStage, NT = 64 * WAVES;
-    constexpr uint32_t STAGE = TPS * KS * 64 + TPS * 8;     // uint4 per stage
-    constexpr uint32_t PPT = (STAGE + NT - 1) / NT;         // pieces per thread and stage
-    static_assert(PPT <= TPS, "one staged piece per tile");
-    __shared__ uint4 lds[2][STAGE];
-    const uint4 wk = a.work[blockIdx.x];
-    const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
-    const bool active = wv < wk.y;
-    const uint32_t blk = wk.x + (active ? wv : 0u);
-
-    half8_t bf[kDftRangeFrags];
-#pragma unroll
-    for (int f = 0; f < kDftRangeFrags; ++f)
-        bf[f] = __builtin_bit_cast(half8_t, a.rfrags[((size_t)blk * kDftRangeFrags + f) * 64 + lane]);
-    float hl = 0.0f;
-    if constexpr (HITS)
-        hl = (float)((int32_t)a.rconst[blk * 32 + (lane & 31u)] - (int32_t)a.hitH);
-
-    float best = -__builtin_inff();
-    uint32_t btile = 0;
-    const uint32_t nstage = (wk.w - wk.z + TPS - 1) / TPS;
-    auto stage_nt = [&](uint32_t st) { return min(TPS, wk.w - (wk.z + st * TPS)); };
-    // piece i of the stage starting at tile tb with nt tiles: [A fragments | row constants]
-    auto piece_src = [&](uint32_t tb, uint32_t nt, uint32_t i) -> const uint4* {
-        const uint32_t na = nt * KS * 64u;
-        return i < na ? a.dtiles + (size_t)tb * KS * 64 + i : a.dconst + (size_t)tb * 8 + (i - na);
-    };
-    if (nstage) {
-        const uint32_t nt0 = stage_nt(0), ntot0 = nt0 * (KS * 64u + 8u);
-        for (uint32_t i = threadIdx.x; i < ntot0; i += NT)
-            lds[0][i] = *piece_src(wk.z, nt0, i);
-    }
-    // drain every global load here (vmcnt(0)): inside the loop the only outstanding load is
-    // the staged piece, so the MFMAs never wait on it
-    __builtin_amdgcn_s_waitcnt(0x0F70);
-    __syncthreads();
-    for (uint32_t st = 0; st < nstage; ++st) {
-        const uint32_t cur = st & 1u, tb = wk.z + st * TPS, nt = stage_nt(st);
-        const bool more = st + 1 < nstage;
-        const uint32_t tbn = tb + TPS, ntn = more ? stage_nt(st + 1) : 0u, ntotn = ntn * (KS * 64u + 8u);
-        float cm = -__builtin_inff();
-        for (uint32_t q = 0; q < nt; ++q) {
-            // wave-uniform: the stage's pieces, the last one repeated by the tail threads
-            const bool stage_piece = more && q < PPT;
-            const uint32_t i = min(threadIdx.x + q * NT, ntotn - 1u);
-            uint4 reg;
-            if (stage_piece)
-                reg = *piece_src(tbn, ntn, i); // re-read by every range group: default cache policy
-            cm = __builtin_fmaxf(cm, dft_compute_stage<1>(lds[cur], nt, lane, bf, tb, d.tguard, 0u, q, q + 1));
-            asm volatile("" ::"v"(cm)); // the tile's epilogue completes before the ds_write below
-            if (stage_piece)
-                lds[cur ^ 1u][i] = reg;
-        }
-        if constexpr (HITS)
-            cm = cm >= hl ? __builtin_inff() : cm;
-        if (cm > best) {
-            best = cm;
-            btile = tb;
-        }
-        __syncthreads();
     }
     if (active)
         a.entries[(size_t)(blockIdx.x * WAVES + wv) * 64 + lane] = make_uint2(__float_as_uint(best), btile);
