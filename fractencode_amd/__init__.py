@@ -55,6 +55,10 @@ class FracStats(C.Structure):
         return {k: getattr(self, k) for k, _ in self._fields_}
 
 
+class FracQuadtreeParams(C.Structure):
+    _fields_ = [("max_size", C.c_uint32), ("min_size", C.c_uint32), ("split_distance", C.c_double)]
+
+
 class FracError(RuntimeError):
     pass
 
@@ -94,6 +98,8 @@ def lib() -> C.CDLL:
             "frac_decode_results": (i32, [vp, u32, u32, i32, C.c_double, vp, C.POINTER(C.c_int),
                                           C.POINTER(C.c_double)]),
             "frac_classify_items": (i32, [vp, vp, sz, i32]),
+            "frac_encode_quadtree": (i32, [vp, C.POINTER(FracQuadtreeParams), vp, sz, C.POINTER(sz),
+                                           C.POINTER(FracStats)]),
             "frac_rgb_to_yuv_device": (i32, [vp, vp, u32, u32, u32, vp, u32, vp, u32, vp, u32]),
             "frac_rgb_to_yuv": (i32, [vp, vp, u32, u32, u32, vp, vp, vp]),
             "frac_uniform_grid": (sz, [u32, u32, u32, u32, vp, sz]),
@@ -163,6 +169,7 @@ class Engine:
             raise FracError("frac_create failed: " + last_error())
         self._nr = 0
         self._keep = []
+        self._frame_wh = (0, 0)
 
     def close(self) -> None:
         if getattr(self, "_ctx", None):
@@ -200,6 +207,7 @@ class Engine:
 
     def set_frame(self, plane) -> None:
         """Source == target plane (Encoder2).  numpy uint8 [H, W] or a CUDA torch tensor."""
+        self._frame_wh = (int(plane.shape[1]), int(plane.shape[0]))
         if hasattr(plane, "is_cuda") and plane.is_cuda:
             assert plane.dtype.itemsize == 1 and plane.dim() == 2
             self._check(lib().frac_set_frame_device(self._ctx, C.c_void_p(plane.data_ptr()), plane.shape[1],
@@ -210,6 +218,7 @@ class Engine:
                                          plane.shape[1]))
 
     def set_planes(self, source: np.ndarray, target: np.ndarray) -> None:
+        self._frame_wh = (int(source.shape[1]), int(source.shape[0]))
         s = np.ascontiguousarray(source, dtype=np.uint8)
         t = np.ascontiguousarray(target, dtype=np.uint8)
         self._check(lib().frac_set_planes(self._ctx, s.ctypes.data, s.shape[1], s.shape[0], s.shape[1], t.ctypes.data,
@@ -264,6 +273,20 @@ class Engine:
             self._check(lib().frac_decode(self._ctx, items.ctypes.data if len(items) else None, len(items), width,
                                           height, max_iter, rms_eps, plane.ctypes.data, C.byref(it), C.byref(rms)))
         return plane, it.value, rms.value
+
+    def encode_quadtree(self, max_size: int = 16, min_size: int = 4, split_distance: float = 10.0):
+        """Quadtree partition of the frame set on this engine (frac_encode_quadtree): ranges of
+        max_size split into quadrants while their best distance exceeds split_distance, down to
+        min_size.  Returns (encode items of mixed sizes, summed stats dict)."""
+        qp = FracQuadtreeParams(max_size, min_size, split_distance)
+        n = C.c_size_t(0)
+        st = FracStats()
+        # one pass with a worst-case capacity: every range at min_size
+        W, H = self._frame_wh
+        cap = (W // min_size) * (H // min_size)
+        out = np.zeros(max(cap, 1), dtype=ENCODE_ITEM)
+        self._check(lib().frac_encode_quadtree(self._ctx, C.byref(qp), out.ctypes.data, cap, C.byref(n), C.byref(st)))
+        return out[: n.value].copy(), st.as_dict()
 
     def classify(self, items: np.ndarray, target_plane: bool = False) -> np.ndarray:
         """BrightnessBlocksClassifier2 categories of `items` computed on the device plane set by

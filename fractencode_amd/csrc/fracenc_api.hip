@@ -1201,6 +1201,73 @@ void* frac_get_stream(frac_ctx* c) { return c ? reinterpret_cast<void*>(c->strea
 
 const frac_encode_item* frac_device_results(frac_ctx* c) { return c ? c->d_out.ptr : nullptr; }
 
+int frac_encode_quadtree(frac_ctx* c, const frac_quadtree_params* qp, frac_encode_item* out, size_t cap,
+                         size_t* n_out, frac_stats* stats)
+{
+    if (!c)
+        return FRAC_E_INVALID;
+    if (!qp || !n_out)
+        return c->fail(FRAC_E_INVALID, "quadtree: params and n_out are required");
+    auto valid = [](uint32_t v) { return v == 2 || v == 4 || v == 8 || v == 16; };
+    if (!valid(qp->max_size) || !valid(qp->min_size) || qp->min_size > qp->max_size)
+        return c->fail(FRAC_E_INVALID, "quadtree: sizes must be 2, 4, 8 or 16 with min_size <= max_size");
+    if (!c->planes_set)
+        return c->fail(FRAC_E_STATE, "quadtree: no frame set");
+    const uint32_t W = c->src.w, H = c->src.h;
+    if (!c->same_plane && (c->tgt.w != W || c->tgt.h != H))
+        return c->fail(FRAC_E_INVALID, "quadtree: source and target planes must have one size");
+    auto grid = [&](uint32_t size, uint32_t off) {
+        std::vector<frac_grid_item> g(frac_uniform_grid(W, H, size, off, nullptr, 0));
+        if (!g.empty())
+            frac_uniform_grid(W, H, size, off, g.data(), g.size());
+        return g;
+    };
+    std::vector<frac_grid_item> pending = grid(qp->max_size, qp->max_size);
+    std::vector<frac_encode_item> emitted;
+    frac_stats total{};
+    for (uint32_t n = qp->max_size; !pending.empty() && n >= qp->min_size; n /= 2) {
+        const std::vector<frac_grid_item> doms = grid(2 * n, n);
+        FRAC_TRY(frac_set_domains(c, doms.data(), doms.size()));
+        FRAC_TRY(frac_set_ranges(c, pending.data(), pending.size()));
+        FRAC_TRY(frac_run(c));
+        std::vector<frac_encode_item> res(pending.size());
+        frac_stats st{};
+        FRAC_TRY(frac_fetch(c, res.data(), &st));
+        total.rejected_mappings += st.rejected_mappings;
+        total.total_mappings += st.total_mappings;
+        total.hit_ranges += st.hit_ranges;
+        total.fallback_ranges += st.fallback_ranges;
+        total.empty_ranges += st.empty_ranges;
+        total.engine = st.engine;
+        total.ms_device += st.ms_device;
+        total.ms_search += st.ms_search;
+        total.ms_prep += st.ms_prep;
+        total.ms_finish += st.ms_finish;
+        total.search_form = st.search_form;
+        total.matrix_flops += st.matrix_flops;
+        std::vector<frac_grid_item> next;
+        for (size_t i = 0; i < res.size(); ++i) {
+            const frac_grid_item& r = pending[i];
+            if (n > qp->min_size && res[i].match.score.distance > qp->split_distance) {
+                const uint32_t h = n / 2;
+                next.push_back(frac_grid_item{r.x, r.y, h, h, -1});
+                next.push_back(frac_grid_item{r.x + h, r.y, h, h, -1});
+                next.push_back(frac_grid_item{r.x, r.y + h, h, h, -1});
+                next.push_back(frac_grid_item{r.x + h, r.y + h, h, h, -1});
+            } else {
+                emitted.push_back(res[i]);
+            }
+        }
+        pending.swap(next);
+    }
+    *n_out = emitted.size();
+    if (out)
+        std::memcpy(out, emitted.data(), std::min(cap, emitted.size()) * sizeof(frac_encode_item));
+    if (stats)
+        *stats = total;
+    return FRAC_OK;
+}
+
 int frac_classify_items(frac_ctx* c, frac_grid_item* items, size_t n, int target_plane)
 {
     if (!c)

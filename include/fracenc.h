@@ -161,6 +161,25 @@ int frac_decode(frac_ctx* ctx, const frac_encode_item* items, size_t n, uint32_t
 int frac_decode_results(frac_ctx* ctx, uint32_t w, uint32_t h, int max_iter, double rms_eps, uint8_t* plane,
                         int* iterations, double* rms);
 
+/* ---- quadtree partition (C4 config; the reference parses --quadtree but never builds one,
+ * main.cpp:75-76, so the partition rule is this library's, parity pinned per level) ----
+ * Level sizes max_size, max_size/2, ..., min_size (each 2, 4, 8 or 16).  Level-0 ranges are
+ * createUniformGrid(W, H, max_size, max_size); every level searches domains
+ * createUniformGrid(W, H, 2n, n) of the frame set on ctx (classifier and threshold as in the
+ * ctx params; -1 categories are computed on the device).  A range whose best distance exceeds
+ * split_distance and whose size exceeds min_size is replaced by its four quadrants (top-left,
+ * top-right, bottom-left, bottom-right) at the next level; every other range is emitted.
+ * Output order: by level, then in search order (children follow their parent's order).
+ * Returns FRAC_OK and the item count in *n_out; writes min(count, cap) items (out may be NULL
+ * to query the count — the search still runs).  stats (optional) sums the levels. */
+typedef struct frac_quadtree_params {
+    uint32_t max_size;
+    uint32_t min_size;
+    double split_distance;
+} frac_quadtree_params;
+int frac_encode_quadtree(frac_ctx* ctx, const frac_quadtree_params* qp, frac_encode_item* out, size_t cap,
+                         size_t* n_out, frac_stats* stats);
+
 /* ---- classifier pre-pass on the device (BrightnessBlocksClassifier2::preclassify,
  * encode/Classifier2.cpp:55-68, as main.cpp:155-162 runs it at grid build) ----
  * Writes the category (0..5 or -1) of each item, computed on the context's source plane

@@ -114,6 +114,22 @@ def rgb2yuv(rgb: np.ndarray):
     return y, np.ascontiguousarray(u[:H // 2, :W // 2]), np.ascontiguousarray(v[:H // 2, :W // 2])
 
 
+def decode_sized(records: np.ndarray, sizes: np.ndarray, W: int, H: int, max_iter: int = -1, eps: float = 1e-5,
+                 initial: np.ndarray | None = None):
+    """Decoder2 over records with a range size each (quadtree encodings)."""
+    records = np.ascontiguousarray(records, dtype=RESULT_DTYPE)
+    sizes = np.ascontiguousarray(sizes, dtype=np.uint32)
+    plane = np.zeros((H, W), np.uint8) if initial is None else np.ascontiguousarray(initial, np.uint8).copy()
+    rms = C.c_double()
+    L = lib()
+    L.or_decode_sized.restype = C.c_int
+    L.or_decode_sized.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_uint32, C.c_uint32, C.c_uint32, C.c_int,
+                                  C.c_double, C.c_void_p, C.POINTER(C.c_double)]
+    it = L.or_decode_sized(records.ctypes.data, sizes.ctypes.data, len(records), 0, W, H, max_iter, eps,
+                           plane.ctypes.data, C.byref(rms))
+    return plane, it, rms.value
+
+
 def ref_lib():
     """The reference build (oracle/_ref/libfracref.so) or None when absent."""
     global _ref
@@ -159,3 +175,39 @@ def ref_estimate(plane: np.ndarray, src_size: int, tgt_size: int, T: int = 4, th
                   int(use_classifier), threads, None if sel_arr is None else sel_arr.ctypes.data, count,
                   out.ctypes.data, C.byref(rej), budget_s, C.byref(done))
     return out, int(rej.value), int(done.value)
+
+
+def quadtree(plane: np.ndarray, max_size: int, min_size: int, split_distance: float, T: int = 4,
+             use_classifier: bool = False, thr: float = 0.0, smax: float = -1.0):
+    """The quadtree rule of include/fracenc.h (frac_encode_quadtree) restated on the oracle: per
+    level n, ranges searched against createUniformGrid(W, H, 2n, n); a range whose distance
+    exceeds split_distance (n > min_size) is replaced by its four quadrants.  No reference
+    exists (main.cpp:75-76 ignores --quadtree); each level's search is the pinned oracle."""
+    plane = np.ascontiguousarray(plane, dtype=np.uint8)
+    H, W = plane.shape
+    pending = uniform_grid(W, H, max_size, max_size)
+    out = []
+    n = max_size
+    while len(pending) and n >= min_size:
+        doms = uniform_grid(W, H, 2 * n, n)
+        rngs = pending
+        if use_classifier:
+            doms = classify(plane, doms)
+            rngs = classify(plane, rngs)
+        res, _, _ = estimate(plane, doms, rngs, T=T, thr=thr, smax=smax, use_classifier=use_classifier)
+        nxt = []
+        for i, r in enumerate(res):
+            if n > min_size and r["dist"] > split_distance:
+                h = n // 2
+                x, y = int(pending[i]["x"]), int(pending[i]["y"])
+                nxt += [(x, y, h, h, -1), (x + h, y, h, h, -1), (x, y + h, h, h, -1), (x + h, y + h, h, h, -1)]
+            else:
+                out.append((r, n))
+        pending = np.array(nxt, dtype=ITEM_DTYPE)
+        n //= 2
+    recs = np.zeros(len(out), dtype=RESULT_DTYPE)
+    sizes = np.zeros(len(out), dtype=np.uint32)
+    for i, (r, sz) in enumerate(out):
+        recs[i] = r
+        sizes[i] = sz
+    return recs, sizes

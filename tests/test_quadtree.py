@@ -1,0 +1,64 @@
+"""Quadtree partition (include/fracenc.h frac_encode_quadtree).  The reference parses
+--quadtree and never builds one (main.cpp:75-76): the rule is this library's, so parity is
+against the oracle's restatement of the same rule (oracle.quadtree), whose every level is the
+reference-pinned search; the level searches themselves are pinned by lenna_n4 / lenna_n16.
+CPU: properties of the oracle partition.  GPU: the engine equals the oracle item for item,
+and the mixed-size decode equals the oracle decoder."""
+import numpy as np
+import pytest
+
+import fractencode_amd as F
+from golden_util import plane
+
+
+def _coverage(recs, sizes, W, H, max_size):
+    cov = np.zeros((H, W), np.int32)
+    for r, s in zip(recs, sizes):
+        cov[r["y"]:r["y"] + s, r["x"]:r["x"] + s] += 1
+    return cov
+
+
+@pytest.mark.parametrize("split", [0.0, 2.0, 1e9])
+def test_oracle_quadtree_partition_properties(oracle, split):
+    p = plane("crop64")
+    recs, sizes = oracle.quadtree(p, 16, 4, split)
+    cov = _coverage(recs, sizes, 64, 64, 16)
+    assert (cov == 1).all()  # the leaves tile the frame exactly once
+    if split == 1e9:
+        assert (sizes == 16).all() and len(recs) == 16
+    if split == 0.0:  # only exact matches stop the split
+        assert (recs["dist"][sizes > 4] == 0.0).all()
+    assert set(np.unique(sizes)) <= {4, 8, 16}
+
+
+def _as_oracle(items):
+    from oracle.oracle import RESULT_DTYPE
+
+    out = np.zeros(len(items), dtype=RESULT_DTYPE)
+    for a, b in (("x", "x"), ("y", "y"), ("dx", "dx"), ("dy", "dy"), ("sw", "dw"), ("sh", "dh"), ("transform", "t"),
+                 ("distance", "dist"), ("contrast", "s"), ("brightness", "o")):
+        out[b] = items[a]
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cls", [False, True])
+@pytest.mark.parametrize("split", [1.0, 8.0])
+def test_gpu_quadtree_matches_oracle(oracle, cls, split):
+    p = plane("lenna_y")
+    with F.Engine(0, 4, cls) as e:
+        e.set_frame(p)
+        items, st = e.encode_quadtree(16, 4, split)
+        want, sizes = oracle.quadtree(p, 16, 4, split, use_classifier=cls)
+        got = _as_oracle(items)
+        for k in want.dtype.names:
+            if k != "pad":
+                np.testing.assert_array_equal(got[k], want[k], err_msg=k)
+        np.testing.assert_array_equal(items["w"], sizes)
+        assert (_coverage(want, sizes, 512, 512, 16) == 1).all()
+        dec, it, rms = e.decode(items, 512, 512)
+    wdec, wit, wrms = oracle.decode_sized(want, sizes, 512, 512)
+    assert (it, rms) == (wit, wrms)
+    np.testing.assert_array_equal(dec, wdec)
+    from fractencode_amd.codec import psnr
+    assert psnr(p, dec) > 25.0

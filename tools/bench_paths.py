@@ -4,6 +4,7 @@
   rgb2yuv   frame loader colour conversion (C5 frame, 4096² RGB): HBM-bound, 4.5 B/pixel
   c5        colour frame: device rgb2yuv + Y/U/V searches on three streams, range-blocks/s
   c4        2048² S1 crop with the classifier pre-pass on: range-blocks/s
+  c4q       the same with the quadtree partition 16/8/4: ms per frame, items per size
   decode    Decoder2 on the GPU for the C3 winners: ms per iteration, HBM bytes per iteration
   stream    FRC1 pack of the C3 winners (host, numpy): ms
 
@@ -125,6 +126,26 @@ def main():
                           "range_blocks_per_s": round(len(rngs) / sec, 1),
                           "rejected_mappings": st["rejected_mappings"], "total_mappings": st["total_mappings"],
                           "engine": st["engine"], "ms_search": round(st["ms_search"], 3)}), flush=True)
+
+    if want("c4q"):
+        # C4 with the quadtree partition (16/8/4): the whole multi-level encode per frame
+        frame = value_noise(4096, 4096, 1234)[:2048, :2048].copy()
+        res = {}
+        for split in (0.05, 0.5):
+            with F.Engine(0, 4, True, timing=True) as e:
+                e.set_frame(frame)
+                e.encode_quadtree(16, 4, split)
+                t0 = time.perf_counter()
+                for _ in range(args.steps):
+                    items, st = e.encode_quadtree(16, 4, split)
+                sec = (time.perf_counter() - t0) / args.steps
+            sizes, counts = np.unique(items["w"], return_counts=True)
+            res[str(split)] = {"ms_per_frame": round(sec * 1e3, 3), "items": int(len(items)),
+                               "items_by_size": {int(a): int(b) for a, b in zip(sizes, counts)},
+                               "items_per_s": round(len(items) / sec, 1), "ms_search_sum": round(st["ms_search"], 3)}
+        print(json.dumps({"path": "c4q", "workload": "C4: S1 2048² crop, classifier on, quadtree 16/8/4 "
+                                                     "(split when distance > threshold), T=4", "by_threshold": res}),
+              flush=True)
 
     if want("decode") or want("stream"):
         frame = value_noise(4096, 4096, 1234)
