@@ -446,16 +446,24 @@ __global__ void __launch_bounds__(256) resolve_dft(MfmaResolveArgs a)
     const bool hit = a.hitH >= 0 && (sentinel || (target >= 0 && target <= a.hitH));
     const frac_grid_item rg = a.ranges[r];
     const int i = lane >> 2, g = lane & 3;
-    int px[PG];
-    int64_t sr2 = 0;
+    // the range's pixel q on lane q; lane (i, g) then holds, per transform, the inverse-
+    // permuted pixels of decimated cells k ∈ [16g, 16g + 16) as packed u16 pairs, so that
+    // X_t = Σ_k r[inv_t(k)]·D4[k] is 8 v_dot2_u32_u16 against two dwordx4 of the pool
+    const int rv = (int)a.tgt[(size_t)(rg.y + lane / N) * a.tstride + rg.x + (lane % N)];
+    int sr2 = rv * rv;
 #pragma unroll
-    for (int u = 0; u < PG; ++u) {
-        const int q = g * PG + u;
-        px[u] = (int)a.tgt[(size_t)(rg.y + q / N) * a.tstride + rg.x + (q % N)];
-        sr2 += px[u] * px[u];
-    }
-    sr2 += __shfl_xor(sr2, 1, 64);
-    sr2 += __shfl_xor(sr2, 2, 64);
+    for (int o = 32; o > 0; o >>= 1)
+        sr2 += __shfl_xor(sr2, o, 64);
+    uint32_t pk[T][PG / 2];
+#pragma unroll
+    for (int t = 0; t < T; ++t)
+#pragma unroll
+        for (int j = 0; j < PG / 2; ++j) {
+            const int k = g * PG + 2 * j;
+            const uint32_t lo = (uint32_t)__shfl(rv, inv_index<N>(t, k), 64);
+            const uint32_t hi = (uint32_t)__shfl(rv, inv_index<N>(t, k + 1), 64);
+            pk[t][j] = lo | (hi << 16);
+        }
     unsigned long long bestk = kKeyNone;
     const uint32_t vbits = __float_as_uint(vmax);
     for (uint32_t j = 0; j < nent; ++j) { // wave-uniform loop over entries
@@ -476,23 +484,26 @@ __global__ void __launch_bounds__(256) resolve_dft(MfmaResolveArgs a)
         }
         for (uint32_t tile = en.y; tile < min(en.y + (uint32_t)kTilesPerStage, a.ntiles); ++tile) {
             const int p = a.tile_pos[tile * 32 + row];
+            uint32_t dv[PG / 2] = {};
+            if (p >= 0) {
+                const uint4* dp = reinterpret_cast<const uint4*>(a.pool + (size_t)p * (NN / 2) + g * (PG / 2));
+                const uint4 d0 = dp[0], d1 = dp[1];
+                dv[0] = d0.x, dv[1] = d0.y, dv[2] = d0.z, dv[3] = d0.w;
+                dv[4] = d1.x, dv[5] = d1.y, dv[6] = d1.z, dv[7] = d1.w;
+            }
+            const int nsd2 = p >= 0 ? a.negsd2[p] : 0;
             unsigned long long tk = kKeyNone;
 #pragma unroll
             for (int t = 0; t < T; ++t) {
-                const Aff af = lut(t);
-                int64_t X = 0;
-                if (p >= 0) {
-                    const uint32_t* dp = a.pool + (size_t)p * (NN / 2);
+                uint32_t X = 0;
 #pragma unroll
-                    for (int u = 0; u < PG; ++u) {
-                        const int f = fwd_rt(af, N, g * PG + u);
-                        const uint32_t w = dp[f >> 1];
-                        X += (int64_t)px[u] * (int64_t)((f & 1) ? (w >> 16) : (w & 0xffffu));
-                    }
-                }
-                X += __shfl_xor(X, 1, 64);
-                X += __shfl_xor(X, 2, 64);
-                const int64_t s16 = p >= 0 ? 16 * sr2 - 8 * X - (int64_t)a.negsd2[p] : 0;
+                for (int q = 0; q < PG / 2; ++q)
+                    X = __builtin_amdgcn_udot2(__builtin_bit_cast(ushort2_t, pk[t][q]),
+                                               __builtin_bit_cast(ushort2_t, dv[q]), X, false);
+                X += (uint32_t)__shfl_xor((int)X, 1, 64);
+                X += (uint32_t)__shfl_xor((int)X, 2, 64);
+                // S16 = 16Σr² − 8X + ΣD4² ≤ 64·1020² < 2^31: exact in int32
+                const int64_t s16 = p >= 0 ? (int64_t)(16 * sr2 - 8 * (int32_t)X - nsd2) : 0;
                 const bool ok = p >= 0 && g == 0 && (hit ? (s16 <= a.hitH) : (s16 == target));
                 const unsigned long long mask = __ballot(ok);
                 if (mask) {
