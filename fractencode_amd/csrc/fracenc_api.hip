@@ -464,8 +464,12 @@ int prepare(frac_ctx* c)
             blk_ptr[c->nblocks] = (uint32_t)blk_ent.size();
         };
         build_work(4, 8192, c->m_work, c->m_blk_ptr, c->m_blk_ent);
-        if (n == 8 && c->p.transforms == 4)
-            build_work(kDftBlocksPerWG, 8192 / kDftBlocksPerWG * 4, c->m8_work, c->m8_blk_ptr, c->m8_blk_ent);
+        if (n == 8 && c->p.transforms == 4) {
+            // FRAC_DFT_WGS (tuning knob): target workgroup count of the Fourier search
+            const char* tw = getenv("FRAC_DFT_WGS");
+            const size_t wgs = tw ? (size_t)std::max(1, atoi(tw)) : 8192 / kDftBlocksPerWG * 4;
+            build_work(kDftBlocksPerWG, wgs, c->m8_work, c->m8_blk_ptr, c->m8_blk_ent);
+        }
         else {
             c->m8_work.clear();
             c->m8_blk_ptr.clear();
