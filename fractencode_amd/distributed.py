@@ -58,7 +58,11 @@ def encode_sharded(engine, ranges: np.ndarray, rank: int, world: int, device=Non
         torch.cuda.synchronize(local.device)  # the zero-fill must land before the engine's copy
     engine.set_ranges(ranges[start:stop])
     engine.run()
-    if stop > start:
-        engine.copy_results_device(local.data_ptr())
-    engine.sync()
+    if local.is_cuda:  # nccl: records stay on the device (frac_copy_results_device)
+        if stop > start:
+            engine.copy_results_device(local.data_ptr())
+        engine.sync()
+    elif stop > start:  # gloo: host records
+        out, _ = engine.fetch()
+        local[: (stop - start) * RECORD_BYTES] = torch.from_numpy(np.ascontiguousarray(out).view(np.uint8))
     return records_from_bytes(gather_records(local, len(ranges), world, group))

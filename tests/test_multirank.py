@@ -46,6 +46,9 @@ class OracleEngine:
     def copy_results_device(self, ptr):
         C.memmove(ptr, self.rec.ctypes.data, self.rec.nbytes)
 
+    def fetch(self):
+        return self.rec, {}
+
     def sync(self):
         pass
 
@@ -96,3 +99,42 @@ def test_gloo_sharded_search_matches_single_rank(tmp_path, oracle, world):
     np.testing.assert_array_equal(full["distance"], want["dist"])
     np.testing.assert_array_equal(full["contrast"], want["s"])
     np.testing.assert_array_equal(full["brightness"], want["o"])
+
+
+def _gpu_worker(rank, world, port, path):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import torch.distributed as dist
+
+    import fractencode_amd as F
+    from fractencode_amd.distributed import encode_sharded
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    y = np.fromfile(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "lenna_y.u8"),
+                    dtype=np.uint8).reshape(512, 512)
+    with F.Engine(0, 4) as e:  # every rank's engine on GPU 0 (one-GPU box)
+        e.set_frame(y)
+        e.set_domains(F.create_uniform_grid(512, 512, 16, 8))
+        full = encode_sharded(e, F.create_uniform_grid(512, 512, 8, 8), rank, world)
+    if rank == 0:
+        np.save(path, full)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_two_ranks_with_hip_engines_match_reference(tmp_path):
+    """world-size-2 ranks, each a real HIP engine, shard Lenna's ranges; the gathered records
+    equal the reference golden (lenna_t4)."""
+    from golden_util import FIELDS, golden
+
+    path = str(tmp_path / "full.npy")
+    mp.spawn(_gpu_worker, args=(2, _free_port(), path), nprocs=2, join=True)
+    full = np.load(path)
+    rec, _ = golden("lenna_t4")
+    got = {"x": full["x"], "y": full["y"], "dx": full["dx"], "dy": full["dy"], "dw": full["sw"], "dh": full["sh"],
+           "t": full["transform"], "dist": full["distance"], "s": full["contrast"], "o": full["brightness"]}
+    for k in FIELDS:
+        np.testing.assert_array_equal(got[k], rec[k], err_msg=k)
