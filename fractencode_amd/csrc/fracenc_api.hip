@@ -180,6 +180,9 @@ struct frac_ctx {
 
     // decoder state
     DBuf<uint8_t> d_dec_src, d_dec_tgt, d_color;
+    DBuf<unsigned long long> d_dec_part;
+    DBuf<DecodeState> d_dec_state;
+    DecodeState* h_dec_state = nullptr;
     DBuf<uint2> d_dft_tguard;
     DBuf<frac_grid_item> d_cls_items;
     DBuf<uint32_t> d_cls_list;
@@ -987,6 +990,10 @@ void frac_destroy(frac_ctx* c)
     c->d_m_entries.release();
     c->d_dec_src.release();
     c->d_color.release();
+    c->d_dec_part.release();
+    c->d_dec_state.release();
+    if (c->h_dec_state)
+        (void)hipHostFree(c->h_dec_state);
     c->d_dft_tguard.release();
     c->d_cls_items.release();
     c->d_cls_list.release();
@@ -1360,11 +1367,101 @@ int frac_rgb_to_yuv(frac_ctx* c, const uint8_t* rgb, uint32_t w, uint32_t h, uin
     return FRAC_OK;
 }
 
+// Do the items (x, y, w, h) cover the w×h plane exactly once?  Checked on a bitmap of cells of
+// the smallest item size (every item a multiple of it, aligned), so O(cells), not O(pixels).
+static bool covers_exactly(const std::vector<frac_grid_item>& rects, uint32_t w, uint32_t h)
+{
+    if (rects.empty())
+        return false;
+    uint32_t g = ~0u;
+    for (const auto& r : rects) {
+        if (r.w == 0 || r.w != r.h)
+            return false;
+        g = std::min(g, r.w);
+    }
+    if (w % g || h % g)
+        return false;
+    const uint32_t cw = w / g, ch = h / g;
+    std::vector<uint8_t> cell((size_t)cw * ch, 0);
+    size_t covered = 0;
+    for (const auto& r : rects) {
+        if (r.x % g || r.y % g || r.w % g || (uint64_t)r.x + r.w > w || (uint64_t)r.y + r.h > h)
+            return false;
+        for (uint32_t y = r.y / g; y < (r.y + r.h) / g; ++y)
+            for (uint32_t x = r.x / g; x < (r.x + r.w) / g; ++x) {
+                if (cell[(size_t)y * cw + x]++)
+                    return false;
+                ++covered;
+            }
+    }
+    return covered == cell.size();
+}
+
+// Fused decode (fracenc_decode.hip decode_fused / decode_check): the items tile the plane.
+static int decode_fused_impl(frac_ctx* c, const frac_encode_item* d_items, size_t n, uint32_t w, uint32_t h,
+                             int iters, double eps, uint8_t* plane, int* iterations, double* rms)
+{
+    const uint32_t stride = (w + 63u) & ~63u;
+    const size_t bytes = (size_t)stride * (h + 1);
+    FRAC_HIP(c, c->d_dec_src.ensure(bytes));
+    FRAC_HIP(c, c->d_dec_tgt.ensure(bytes));
+    const uint32_t nblk = (uint32_t)((n + 3) / 4);
+    FRAC_HIP(c, c->d_dec_part.ensure(std::max<uint32_t>(nblk, 1)));
+    FRAC_HIP(c, c->d_dec_state.ensure(1));
+    if (!c->h_dec_state)
+        FRAC_HIP(c, hipHostMalloc(reinterpret_cast<void**>(&c->h_dec_state), sizeof(DecodeState)));
+    uint8_t* buf[2] = {c->d_dec_src.ptr, c->d_dec_tgt.ptr};
+    FRAC_HIP(c, hipMemsetAsync(buf[0], 100, bytes, c->stream)); // Decoder2: source filled with 100
+    FRAC_HIP(c, hipMemsetAsync(buf[1], 0, bytes, c->stream));
+    FRAC_HIP(c, hipMemcpy2DAsync(buf[1], stride, plane, w, w, h, hipMemcpyHostToDevice, c->stream));
+    FRAC_HIP(c, hipMemsetAsync(c->d_dec_state.ptr, 0, sizeof(DecodeState), c->stream));
+    DecodeArgs a;
+    a.stride = stride;
+    a.items = d_items;
+    a.n = (uint32_t)n;
+    constexpr int kChunk = 8; // iterations enqueued between host checks of the convergence flag
+    int enq = 0;
+    while (enq < iters) {
+        const int stop = std::min(iters, enq + kChunk);
+        for (; enq < stop; ++enq) {
+            a.src = buf[enq & 1];
+            a.tgt = buf[(enq + 1) & 1];
+            decode_fused<<<nblk, 256, 0, c->stream>>>(a, c->d_dec_state.ptr, c->d_dec_part.ptr);
+            decode_check<<<1, 256, 0, c->stream>>>(c->d_dec_part.ptr, nblk, (uint64_t)w * h, eps, enq, iters - 1,
+                                                   c->d_dec_state.ptr);
+        }
+        FRAC_HIP(c, hipMemcpyAsync(c->h_dec_state, c->d_dec_state.ptr, sizeof(DecodeState), hipMemcpyDeviceToHost,
+                                   c->stream));
+        FRAC_HIP(c, hipStreamSynchronize(c->stream));
+        if (c->h_dec_state->done)
+            break;
+    }
+    int it = 0;
+    double r = 0.0;
+    if (iters > 0) {
+        it = c->h_dec_state->iterations;
+        r = c->h_dec_state->rms;
+    }
+    // the final target: step `it` when the loop broke there, else step iters − 1
+    const int last = iters > 0 ? (c->h_dec_state->done ? it : iters - 1) : -1;
+    const uint8_t* fin = last >= 0 ? buf[(last + 1) & 1] : buf[1];
+    FRAC_HIP(c, hipMemcpy2DAsync(plane, w, fin, stride, w, h, hipMemcpyDeviceToHost, c->stream));
+    FRAC_HIP(c, hipStreamSynchronize(c->stream));
+    FRAC_HIP(c, hipGetLastError());
+    if (iterations)
+        *iterations = it;
+    if (rms)
+        *rms = r;
+    return FRAC_OK;
+}
+
 static int decode_impl(frac_ctx* c, const frac_encode_item* d_items, size_t n, uint32_t w, uint32_t h, int max_iter,
-                       double eps, uint8_t* plane, int* iterations, double* rms)
+                       double eps, uint8_t* plane, int* iterations, double* rms, bool fused = false)
 {
     if (!plane || w == 0 || h == 0)
         return c->fail(FRAC_E_INVALID, "decode: invalid plane");
+    if (fused && getenv("FRAC_DECODE_UNFUSED") == nullptr)
+        return decode_fused_impl(c, d_items, n, w, h, max_iter < 0 ? 300 : max_iter, eps, plane, iterations, rms);
     const uint32_t stride = (w + 63u) & ~63u;
     const size_t bytes = (size_t)stride * (h + 1);
     FRAC_HIP(c, c->d_dec_src.ensure(bytes));
@@ -1430,7 +1527,14 @@ int frac_decode(frac_ctx* c, const frac_encode_item* items, size_t n, uint32_t w
     if (n)
         FRAC_HIP(c, hipMemcpyAsync(c->d_dec_items.ptr, items, n * sizeof(frac_encode_item), hipMemcpyHostToDevice,
                                    c->stream));
-    return decode_impl(c, c->d_dec_items.ptr, n, w, h, max_iter, rms_eps, plane, iterations, rms);
+    std::vector<frac_grid_item> rects(n);
+    bool all_domains = true;
+    for (size_t i = 0; i < n; ++i) {
+        rects[i] = frac_grid_item{items[i].x, items[i].y, items[i].w, items[i].h, -1};
+        all_domains = all_domains && items[i].match.sw != 0 && items[i].match.sh != 0;
+    }
+    const bool fused = all_domains && covers_exactly(rects, w, h);
+    return decode_impl(c, c->d_dec_items.ptr, n, w, h, max_iter, rms_eps, plane, iterations, rms, fused);
 }
 
 int frac_decode_results(frac_ctx* c, uint32_t w, uint32_t h, int max_iter, double rms_eps, uint8_t* plane,
@@ -1443,7 +1547,20 @@ int frac_decode_results(frac_ctx* c, uint32_t w, uint32_t h, int max_iter, doubl
     if (c->src.w > w || c->src.h > h || c->tgt.w > w || c->tgt.h > h)
         return c->fail(FRAC_E_INVALID, "decode: plane smaller than the encoded planes");
     FRAC_HIP(c, hipSetDevice(c->device));
-    return decode_impl(c, c->d_out.ptr, c->ranges.size(), w, h, max_iter, rms_eps, plane, iterations, rms);
+    // the fused form needs every range written: no empty (domain-less) record among the results
+    bool fused = covers_exactly(c->ranges, w, h);
+    if (fused && !c->ranges.empty()) {
+        c->h_aux.resize(c->ranges.size());
+        FRAC_HIP(c, hipMemcpyAsync(c->h_aux.data(), c->d_aux.ptr, c->ranges.size() * sizeof(RangeAux),
+                                   hipMemcpyDeviceToHost, c->stream));
+        FRAC_HIP(c, hipStreamSynchronize(c->stream));
+        for (const RangeAux& x : c->h_aux)
+            if (x.flags & kAuxEmpty) {
+                fused = false;
+                break;
+            }
+    }
+    return decode_impl(c, c->d_out.ptr, c->ranges.size(), w, h, max_iter, rms_eps, plane, iterations, rms, fused);
 }
 
 int frac_copy_results_device(frac_ctx* c, void* d_dst)

@@ -83,4 +83,86 @@ __global__ void __launch_bounds__(256) decode_rms(const uint8_t* __restrict__ sr
         atomicAdd(sum, part[0] + part[1] + part[2] + part[3]);
 }
 
+// ---------------------------------------------------------------------------
+// Fused form, used when the items tile the plane exactly (every pixel written once per
+// iteration by an item with a domain): the rms of step i is Σ over the written pixels of
+// (source − new target)², so it is accumulated while writing (per-block partial sums, no
+// second pass), the source ← target copy becomes a buffer swap, and the convergence test
+// (Encoder2.hpp:84-86, with the reference's int32 sum, metrics.h:27) runs on the device, so
+// the host only checks a flag every few iterations.  After convergence the remaining
+// enqueued iterations exit at their first instruction.
+// ---------------------------------------------------------------------------
+struct DecodeState {
+    int32_t done;       // 1 once rms < eps
+    int32_t iterations; // Decoder2's returned count
+    double rms;
+};
+
+__global__ void __launch_bounds__(256) decode_fused(DecodeArgs a, const DecodeState* __restrict__ st,
+                                                    unsigned long long* __restrict__ partial)
+{
+    if (st->done)
+        return;
+    const uint32_t it = blockIdx.x * 4u + (threadIdx.x >> 6);
+    const uint32_t lane = threadIdx.x & 63u;
+    unsigned long long acc = 0;
+    if (it < a.n) {
+        const frac_encode_item e = a.items[it];
+        const uint32_t sw = e.match.sw, sh = e.match.sh;
+        const double s = e.match.score.contrast, o = e.match.score.brightness;
+        const int t = e.match.score.transform;
+        for (uint32_t q = lane; q < e.w * e.h; q += 64) {
+            const uint32_t x = q % e.w, y = q / e.w;
+            const uint32_t sx = (x * sw) / e.w, sy = (y * sh) / e.h;
+            const double smp = (double)sample_sum_dev(a.src, a.stride, e.match.x, e.match.y, sw, sh, sx, sy, t) / 4.0;
+            const double v = __fma_rn(s, smp, o);
+            const uint8_t nv = v < 0.0 ? 0 : v > 255 ? 255 : (uint8_t)v;
+            const size_t off = (size_t)(e.y + y) * a.stride + e.x + x;
+            const int d = (int)a.src[off] - (int)nv;
+            acc += (unsigned long long)(d * d);
+            a.tgt[off] = nv;
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1)
+        acc += __shfl_xor(acc, o, 64);
+    __shared__ unsigned long long part[4];
+    if (lane == 0)
+        part[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0)
+        partial[blockIdx.x] = part[0] + part[1] + part[2] + part[3];
+}
+
+// one block: Σ partials → rms of step `step` exactly as the reference (int32 sum / area)
+__global__ void __launch_bounds__(256) decode_check(const unsigned long long* __restrict__ partial, uint32_t nparts,
+                                                    uint64_t area, double eps, int32_t step, int32_t last_step,
+                                                    DecodeState* __restrict__ st)
+{
+    if (st->done)
+        return;
+    unsigned long long acc = 0;
+    for (uint32_t i = threadIdx.x; i < nparts; i += 256)
+        acc += partial[i];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1)
+        acc += __shfl_xor(acc, o, 64);
+    __shared__ unsigned long long part[4];
+    if ((threadIdx.x & 63) == 0)
+        part[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned long long sum = part[0] + part[1] + part[2] + part[3];
+        const int32_t s32 = (int32_t)(uint32_t)(sum & 0xffffffffull);
+        const double r = (double)s32 / (double)area;
+        st->rms = r;
+        if (r < eps) {
+            st->done = 1;
+            st->iterations = step;
+        } else if (step == last_step) {
+            st->iterations = step + 1;
+        }
+    }
+}
+
 } // namespace fracenc

@@ -127,3 +127,24 @@ def test_decode_rejects_bad_items():
             e.decode(bad, 64, 64)
         with pytest.raises(F.FracError):
             e.decode(None, 64, 64)  # nothing ran yet
+
+
+@pytest.mark.parametrize("name", ["lenna_t4", "lenna_n4", "crop64_n2_t8"])
+def test_fused_and_stepwise_decoders_agree(monkeypatch, name):
+    # the fused decoder (exact coverage: rms accumulated while writing, buffer swap, device-side
+    # convergence test) against the step-by-step form, including bounded iteration counts
+    rec, meta = golden(name)
+    p = plane(meta["plane"])
+    H, W = p.shape
+    items = encode_items(rec, meta["tgt"])
+    outs = []
+    for unfused in ("", "1"):
+        if unfused:
+            monkeypatch.setenv("FRAC_DECODE_UNFUSED", "1")
+        else:
+            monkeypatch.delenv("FRAC_DECODE_UNFUSED", raising=False)
+        with F.Engine(0, 4) as e:
+            outs.append([e.decode(items, W, H, max_iter=m) for m in (-1, 0, 1, 2, 9)])
+    for (a, ia, ra), (b, ib, rb) in zip(*outs):
+        assert (ia, ra) == (ib, rb)
+        np.testing.assert_array_equal(a, b)
