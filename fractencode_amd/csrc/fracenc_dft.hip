@@ -466,57 +466,67 @@ __global__ void __launch_bounds__(256) resolve_dft(MfmaResolveArgs a)
         }
     unsigned long long bestk = kKeyNone;
     const uint32_t vbits = __float_as_uint(vmax);
-    for (uint32_t j = 0; j < nent; ++j) { // wave-uniform loop over entries
-        const uint2 en = a.entries[(size_t)a.blk_ent[e0 + j / 2] * 64 + col + 32 * (j & 1)];
-        if (en.x != vbits)
-            continue;
-        const int row = (i & 3) + 8 * (i >> 2) + 4 * (int)(j & 1);
-        if (!exact) {
-            // fp32 fallback regime: every candidate has S16 ≥ 2^24; any valid domain of the
-            // bucket routes the range to fallback_fp32 through fit_winner
-            const int p = a.tile_pos[en.y * 32 + row];
-            const unsigned long long mask = __ballot(p >= 0 && g == 0);
-            if (mask) {
-                const int pf = __shfl(p, __ffsll((long long)mask) - 1, 64);
-                bestk = min(bestk, key_miss((uint64_t)kExactLimit, (uint32_t)pf, 0));
-            }
-            continue;
-        }
-        for (uint32_t tile = en.y; tile < min(en.y + (uint32_t)kTilesPerStage, a.ntiles); ++tile) {
-            const int p = a.tile_pos[tile * 32 + row];
-            uint32_t dv[PG / 2] = {};
-            if (p >= 0) {
-                const uint4* dp = reinterpret_cast<const uint4*>(a.pool + (size_t)p * (NN / 2) + g * (PG / 2));
-                const uint4 d0 = dp[0], d1 = dp[1];
-                dv[0] = d0.x, dv[1] = d0.y, dv[2] = d0.z, dv[3] = d0.w;
-                dv[4] = d1.x, dv[5] = d1.y, dv[6] = d1.z, dv[7] = d1.w;
-            }
-            const int nsd2 = p >= 0 ? a.negsd2[p] : 0;
-            unsigned long long tk = kKeyNone;
-#pragma unroll
-            for (int t = 0; t < T; ++t) {
-                uint32_t X = 0;
-#pragma unroll
-                for (int q = 0; q < PG / 2; ++q)
-                    X = __builtin_amdgcn_udot2(__builtin_bit_cast(ushort2_t, pk[t][q]),
-                                               __builtin_bit_cast(ushort2_t, dv[q]), X, false);
-                X += (uint32_t)__shfl_xor((int)X, 1, 64);
-                X += (uint32_t)__shfl_xor((int)X, 2, 64);
-                // S16 = 16Σr² − 8X + ΣD4² ≤ 64·1020² < 2^31: exact in int32
-                const int64_t s16 = p >= 0 ? (int64_t)(16 * sr2 - 8 * (int32_t)X - nsd2) : 0;
-                const bool ok = p >= 0 && g == 0 && (hit ? (s16 <= a.hitH) : (s16 == target));
-                const unsigned long long mask = __ballot(ok);
+    // only the entries holding the maximum are re-evaluated (usually one): the lanes test 64
+    // entries at a time and the wave walks the ballot of matches, so the cost does not grow
+    // with the number of domain splits (many splits per block when ranges are sharded)
+    for (uint32_t c0 = 0; c0 < nent; c0 += 64) {
+        const uint32_t jl = c0 + (uint32_t)lane;
+        const uint2 enl = jl < nent ? a.entries[(size_t)a.blk_ent[e0 + jl / 2] * 64 + col + 32 * (jl & 1)]
+                                    : make_uint2(0u, 0u);
+        unsigned long long match = __ballot(jl < nent && enl.x == vbits);
+        while (match) {
+            const int src = __ffsll((long long)match) - 1;
+            match &= match - 1;
+            const uint32_t j = c0 + (uint32_t)src;
+            const uint2 en = make_uint2(vbits, (uint32_t)__shfl((int)enl.y, src, 64));
+            const int row = (i & 3) + 8 * (i >> 2) + 4 * (int)(j & 1);
+            if (!exact) {
+                // fp32 fallback regime: every candidate has S16 ≥ 2^24; any valid domain of the
+                // bucket routes the range to fallback_fp32 through fit_winner
+                const int p = a.tile_pos[en.y * 32 + row];
+                const unsigned long long mask = __ballot(p >= 0 && g == 0);
                 if (mask) {
-                    const int first = __ffsll((long long)mask) - 1;
-                    const int pf = __shfl(p, first, 64);
-                    const unsigned long long k =
-                        hit ? key_hit((uint32_t)pf, t) : key_miss((uint64_t)target, (uint32_t)pf, T - 1 - t);
-                    tk = k < tk ? k : tk;
+                    const int pf = __shfl(p, __ffsll((long long)mask) - 1, 64);
+                    bestk = min(bestk, key_miss((uint64_t)kExactLimit, (uint32_t)pf, 0));
                 }
+                continue;
             }
-            if (tk != kKeyNone) {
-                bestk = tk < bestk ? tk : bestk;
-                break;
+            for (uint32_t tile = en.y; tile < min(en.y + (uint32_t)kTilesPerStage, a.ntiles); ++tile) {
+                const int p = a.tile_pos[tile * 32 + row];
+                uint32_t dv[PG / 2] = {};
+                if (p >= 0) {
+                    const uint4* dp = reinterpret_cast<const uint4*>(a.pool + (size_t)p * (NN / 2) + g * (PG / 2));
+                    const uint4 d0 = dp[0], d1 = dp[1];
+                    dv[0] = d0.x, dv[1] = d0.y, dv[2] = d0.z, dv[3] = d0.w;
+                    dv[4] = d1.x, dv[5] = d1.y, dv[6] = d1.z, dv[7] = d1.w;
+                }
+                const int nsd2 = p >= 0 ? a.negsd2[p] : 0;
+                unsigned long long tk = kKeyNone;
+#pragma unroll
+                for (int t = 0; t < T; ++t) {
+                    uint32_t X = 0;
+#pragma unroll
+                    for (int q = 0; q < PG / 2; ++q)
+                        X = __builtin_amdgcn_udot2(__builtin_bit_cast(ushort2_t, pk[t][q]),
+                                                   __builtin_bit_cast(ushort2_t, dv[q]), X, false);
+                    X += (uint32_t)__shfl_xor((int)X, 1, 64);
+                    X += (uint32_t)__shfl_xor((int)X, 2, 64);
+                    // S16 = 16Σr² − 8X + ΣD4² ≤ 64·1020² < 2^31: exact in int32
+                    const int64_t s16 = p >= 0 ? (int64_t)(16 * sr2 - 8 * (int32_t)X - nsd2) : 0;
+                    const bool ok = p >= 0 && g == 0 && (hit ? (s16 <= a.hitH) : (s16 == target));
+                    const unsigned long long mask = __ballot(ok);
+                    if (mask) {
+                        const int first = __ffsll((long long)mask) - 1;
+                        const int pf = __shfl(p, first, 64);
+                        const unsigned long long k =
+                            hit ? key_hit((uint32_t)pf, t) : key_miss((uint64_t)target, (uint32_t)pf, T - 1 - t);
+                        tk = k < tk ? k : tk;
+                    }
+                }
+                if (tk != kKeyNone) {
+                    bestk = tk < bestk ? tk : bestk;
+                    break;
+                }
             }
         }
     }
