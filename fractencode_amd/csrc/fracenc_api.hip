@@ -605,8 +605,15 @@ inline int launch_dft(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride)
     FRAC_HIP(c, c->d_dft_rguard.ensure(std::max<size_t>(c->nblocks, 1)));
     FRAC_HIP(c, hipMemsetAsync(c->d_dft_tguard.ptr, 0, c->ntiles * sizeof(uint2), c->stream));
     FRAC_HIP(c, hipMemsetAsync(c->d_dft_rguard.ptr, 0, c->nblocks * sizeof(uint32_t), c->stream));
+    DftDomainBuildArgs b;
+    b.src = c->d_src.ptr;
+    b.sstride = c->d_sstride;
+    b.doms = c->d_doms.ptr;
+    b.porig = c->d_porig.ptr;
+    b.pool = c->d_pool.ptr;
+    b.negsd2 = c->d_negsd2.ptr;
     if (c->ntiles)
-        dft_domain_prep<<<(c->ntiles * 32 + 255) / 256, 256, 0, c->stream>>>(d, c->d_dft_tguard.ptr);
+        dft_domain_build<<<(c->ntiles * 32 + 255) / 256, 256, 0, c->stream>>>(d, b, c->d_dft_tguard.ptr);
     MfmaRangePrepArgs r;
     r.tgt = dtgt;
     r.tstride = tstride;
@@ -804,11 +811,15 @@ int launch_all(frac_ctx* c)
     if (nr)
         FRAC_HIP(c, hipMemsetAsync(c->d_best_key.ptr, 0xff, nr * sizeof(unsigned long long), c->stream));
     const uint32_t fbc = c->all_fallback ? nr : 0u;
-    FRAC_HIP(c, hipMemcpyAsync(c->d_fb_count.ptr, &fbc, sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
-    if (P)
+    // a device-side fill, not an H2D copy from pageable host memory (which serialises the host
+    // with the stream)
+    FRAC_HIP(c, hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(c->d_fb_count.ptr), (int)fbc, 1, c->stream));
+    const bool use_mfma = c->engine == FRAC_ENGINE_MFMA && !c->all_fallback;
+    // the Fourier path builds the pool in its fused domain pass (dft_domain_build)
+    const bool fused_pool = N == 8 && use_mfma && c->p.transforms == 4 && mfma_dft_enabled();
+    if (P && !fused_pool)
         pool_build<N><<<(P + 3) / 4, 256, 0, c->stream>>>(dsrc, c->d_sstride, c->d_doms.ptr, c->d_porig.ptr, P,
                                                           c->d_pool.ptr, c->d_negsd2.ptr);
-    const bool use_mfma = c->engine == FRAC_ENGINE_MFMA && !c->all_fallback;
     if constexpr (N <= 8) {
         if (use_mfma)
             FRAC_TRY(launch_mfma<N>(c, dtgt, tstride));

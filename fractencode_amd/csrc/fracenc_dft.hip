@@ -108,12 +108,33 @@ struct DftArgs {
 };
 
 // ---------------------------------------------------------------------------
-// dft_domain_prep: pool (u16 D4) → per 32-domain tile the A fragments of the four K-steps
-// [s_b | u_b | γ | δ] (lane l: row l&31, orbit 8(l>>5) + j), −Σb² per row in the [2][16]
-// lane-half layout of the epilogue, and the tile's fast-path guard terms.
-// One thread per (tile, row).
+// dft_domain_build: pool_build + dft_domain_prep in one pass for the Fourier path.  One
+// thread per (tile, row) = per pool position: the 2×2 sums come straight from the plane
+// (SamplerBilinear's integer sum, image/sampler.h:21-38, as pool_build), two cells per
+// 32-bit word — (w & 0x00ff00ff) + ((w >> 8) & 0x00ff00ff) over the word of both rows is
+// the packed u16 pair the pool stores — and the same registers feed the tile fragments.
+// Outputs: the pool and −ΣD4² (read by resolve_dft, fit_winner and fallback_fp32); per
+// 32-domain tile the A fragments of the four K-steps [s_b | u_b | γ | δ] (lane l: row l&31,
+// orbit 8(l>>5) + j), −Σb² per row in the [2][16] lane-half layout of the epilogue, and the
+// tile's fast-path guard terms.  Every pool position sits in exactly one tile row.
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) dft_domain_prep(MfmaDomainPrepArgs a, uint2* __restrict__ tguard)
+struct DftDomainBuildArgs {
+    const uint8_t* src;
+    uint32_t sstride;
+    const frac_grid_item* doms;
+    const uint32_t* porig;      // pool position → domain index
+    uint32_t* pool;             // [P][32] packed u16 pairs of D4
+    int32_t* negsd2;            // [P]
+};
+
+__device__ inline uint32_t pair_sums(uint32_t w0, uint32_t w1)
+{
+    constexpr uint32_t M = 0x00ff00ffu;
+    return (w0 & M) + ((w0 >> 8) & M) + (w1 & M) + ((w1 >> 8) & M);
+}
+
+__global__ void __launch_bounds__(256) dft_domain_build(MfmaDomainPrepArgs a, DftDomainBuildArgs s,
+                                                        uint2* __restrict__ tguard)
 {
     constexpr int NN = 64, NO = 16;
     const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
@@ -121,13 +142,54 @@ __global__ void __launch_bounds__(256) dft_domain_prep(MfmaDomainPrepArgs a, uin
         return;
     const uint32_t tile = gid >> 5, row = gid & 31u;
     const int p = a.tile_pos[gid];
+    uint32_t w[NN / 2];
+    if (p >= 0) {
+        const frac_grid_item d = s.doms[s.porig[p]];
+        const uint8_t* base = s.src + (size_t)d.y * s.sstride + d.x;
+        if ((((uintptr_t)base | s.sstride) & 7u) == 0) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                // 16 bytes per row: two 8-byte loads (domain origins are 8-byte aligned, not 16)
+                const uint2* r0 = reinterpret_cast<const uint2*>(base + (size_t)(2 * i) * s.sstride);
+                const uint2* r1 = reinterpret_cast<const uint2*>(base + (size_t)(2 * i + 1) * s.sstride);
+                const uint2 a0 = r0[0], a1 = r0[1], b0 = r1[0], b1 = r1[1];
+                w[4 * i + 0] = pair_sums(a0.x, b0.x);
+                w[4 * i + 1] = pair_sums(a0.y, b0.y);
+                w[4 * i + 2] = pair_sums(a1.x, b1.x);
+                w[4 * i + 3] = pair_sums(a1.y, b1.y);
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < NN / 2; ++k) {
+                const uint8_t* q = base + (size_t)(2 * (k / 4)) * s.sstride + 4 * (k % 4);
+                const uint32_t w0 = q[0] | (q[1] << 8) | (q[2] << 16) | ((uint32_t)q[3] << 24);
+                const uint8_t* q1 = q + s.sstride;
+                const uint32_t w1 = q1[0] | (q1[1] << 8) | (q1[2] << 16) | ((uint32_t)q1[3] << 24);
+                w[k] = pair_sums(w0, w1);
+            }
+        }
+        uint4* pw = reinterpret_cast<uint4*>(s.pool + (size_t)p * (NN / 2));
+        int sq = 0;
+#pragma unroll
+        for (int k = 0; k < NN / 2; ++k) {
+            const int lo = (int)(w[k] & 0xffffu), hi = (int)(w[k] >> 16);
+            sq += lo * lo + hi * hi;
+        }
+#pragma unroll
+        for (int k = 0; k < NN / 8; ++k)
+            pw[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
+        s.negsd2[p] = -sq;
+    } else {
+#pragma unroll
+        for (int k = 0; k < NN / 2; ++k)
+            w[k] = 0x02000200u; // padding: b = 0
+    }
     int b[NN];
     int sb2 = 0;
 #pragma unroll
     for (int k = 0; k < NN / 2; ++k) {
-        const uint32_t w = p >= 0 ? a.pool[(size_t)p * (NN / 2) + k] : 0x02000200u; // padding: b = 0
-        b[2 * k] = (int)(w & 0xffffu) - 512;
-        b[2 * k + 1] = (int)(w >> 16) - 512;
+        b[2 * k] = (int)(w[k] & 0xffffu) - 512;
+        b[2 * k + 1] = (int)(w[k] >> 16) - 512;
     }
 #pragma unroll
     for (int k = 0; k < NN; ++k)
@@ -145,16 +207,16 @@ __global__ void __launch_bounds__(256) dft_domain_prep(MfmaDomainPrepArgs a, uin
         comp[3][o] = (_Float16)(b1 - b3);
     }
 #pragma unroll
-    for (int s = 0; s < 4; ++s)
+    for (int st = 0; st < 4; ++st)
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             _Float16 v8[8];
 #pragma unroll
             for (int j = 0; j < 8; ++j)
-                v8[j] = comp[s][8 * h + j];
-            a.dtiles[((size_t)tile * 4 + s) * 64 + row + 32 * h] = __builtin_bit_cast(uint4, v8);
+                v8[j] = comp[st][8 * h + j];
+            a.dtiles[((size_t)tile * 4 + st) * 64 + row + 32 * h] = __builtin_bit_cast(uint4, v8);
         }
-    const float ny = p >= 0 ? -(float)sb2 : kDftPadY; // Σb² ≤ 64·512² = 2^24: exact
+    const float ny = p >= 0 ? -(float)sb2 : kDftPadY;
     const uint32_t h = (row >> 2) & 1u, i = (row & 3u) + 4u * (row >> 3);
     a.dconst[(size_t)tile * 32 + h * 16 + i] = __float_as_uint(ny);
     if (p >= 0) {
