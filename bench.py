@@ -207,26 +207,37 @@ def main():
         line["roofline"]["hbm_gbs"] = round(traffic / (avg_search_ms * 1e-3) / 1e9, 3)
         line["roofline"]["hbm_frac"] = round(line["roofline"]["hbm_gbs"] / HBM_PEAK_GBS, 6)
     if world == 1 and engine_name == "mfma" and args.alt_steps > 0:
-        # the same workload on the VALU engine (packed-u16 v_dot2, no MFMA), measured the same way
-        with F.Engine(dev.index, args.transforms, False, 0.0, -1.0, F.ENGINE_VALU, timing=True) as alt:
-            alt.set_stream(stream.cuda_stream)
-            alt.set_frame(d_frame)
-            alt.set_domains(doms)
-            alt.set_ranges(mine)
-            alt.run()
-            torch.cuda.synchronize(dev)
-            t0 = time.perf_counter()
-            for _ in range(args.alt_steps):
+        # the same workload on the other engines, measured the same way: the VALU engine (packed-u16
+        # v_dot2, north_star's no-MFMA formulation, exhaustive) and the SEA engine (successive
+        # elimination: identical records, most candidates skipped by an exact bound, data-dependent)
+        line["alt_engines"] = {}
+        for alt_name, alt_id in (("valu", F.ENGINE_VALU), ("sea", F.ENGINE_SEA)):
+            with F.Engine(dev.index, args.transforms, False, 0.0, -1.0, alt_id, timing=True) as alt:
+                alt.set_stream(stream.cuda_stream)
+                alt.set_frame(d_frame)
+                alt.set_domains(doms)
+                alt.set_ranges(mine)
                 alt.run()
-            torch.cuda.synchronize(dev)
-            alt_sec = (time.perf_counter() - t0) / args.alt_steps
-            _, ast = alt.fetch()
-        alt_ach = ops_per_launch / (ast["ms_search"] * 1e-3) / 1e12
-        line["alt_engines"] = {"valu": {
-            "value": round(nr_total / alt_sec, 1), "ms_per_step": round(alt_sec * 1e3, 3), "steps": args.alt_steps,
-            "dtype": "u16", "roofline": {"bound": "valu", "achieved": round(alt_ach, 2), "peak": VALU_PEAK_TOPS,
-                                         "unit": "TOP/s", "frac": round(alt_ach / VALU_PEAK_TOPS, 4),
-                                         "kernel_ms": round(ast["ms_search"], 3)}}}
+                torch.cuda.synchronize(dev)
+                t0 = time.perf_counter()
+                for _ in range(args.alt_steps):
+                    alt.run()
+                torch.cuda.synchronize(dev)
+                alt_sec = (time.perf_counter() - t0) / args.alt_steps
+                alt_out, ast = alt.fetch()
+            entry = {"value": round(nr_total / alt_sec, 1), "ms_per_step": round(alt_sec * 1e3, 3),
+                     "steps": args.alt_steps, "dtype": "u16",
+                     "phases_ms": {"prep": round(ast["ms_prep"], 3), "search": round(ast["ms_search"], 3),
+                                   "finish": round(ast["ms_finish"], 3)}}
+            if alt_name == "valu":
+                alt_ach = ops_per_launch / (ast["ms_search"] * 1e-3) / 1e12
+                entry["roofline"] = {"bound": "valu", "achieved": round(alt_ach, 2), "peak": VALU_PEAK_TOPS,
+                                     "unit": "TOP/s", "frac": round(alt_ach / VALU_PEAK_TOPS, 4),
+                                     "kernel_ms": round(ast["ms_search"], 3)}
+            else:
+                main_out, _ = eng.fetch()
+                entry["records_identical_to_exhaustive"] = bool(alt_out.tobytes() == main_out.tobytes())
+            line["alt_engines"][alt_name] = entry
     if rank == 0 and world == 1 and args.cpu_budget > 0:
         threads = args.cpu_threads or min(16, os.cpu_count() or 1)
         line["cpu_baseline"] = cpu_baseline(frame, args.cpu_budget, threads)

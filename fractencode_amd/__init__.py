@@ -29,9 +29,9 @@ ENCODE_ITEM = np.dtype([("x", "<u4"), ("y", "<u4"), ("w", "<u4"), ("h", "<u4"),
                         ("dx", "<u4"), ("dy", "<u4"), ("sw", "<u4"), ("sh", "<u4")])
 assert GRID_ITEM.itemsize == 20 and ENCODE_ITEM.itemsize == 64
 
-ENGINE_AUTO, ENGINE_VALU, ENGINE_MFMA = 0, 1, 2
-FORM_DOT2, FORM_DIRECT, FORM_FOURIER = 0, 1, 2
-FORM_NAMES = {FORM_DOT2: "dot2", FORM_DIRECT: "direct", FORM_FOURIER: "fourier"}
+ENGINE_AUTO, ENGINE_VALU, ENGINE_MFMA, ENGINE_SEA = 0, 1, 2, 3
+FORM_DOT2, FORM_DIRECT, FORM_FOURIER, FORM_SEA = 0, 1, 2, 3
+FORM_NAMES = {FORM_DOT2: "dot2", FORM_DIRECT: "direct", FORM_FOURIER: "fourier", FORM_SEA: "sea"}
 FLAG_TIMING = 1
 
 # Frac::TransformType (image/transform.h:16-25)
@@ -72,6 +72,14 @@ def lib() -> C.CDLL:
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise FracError(f"{LIB_PATH} not built: run __graft_entry__.build() (no CPU fallback exists)")
+        # One HIP runtime per process: PyTorch bundles its own libamdhip64 (soname libamdhip64.so.7,
+        # file name libamdhip64.so).  Loaded first, it also serves this library (same soname), so
+        # torch streams and device tensors are valid here; loaded second, torch would open a second
+        # runtime that finds no device.  Import torch (when installed) before the library.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = C.CDLL(LIB_PATH)
         vp, u32, i32, sz = C.c_void_p, C.c_uint32, C.c_int, C.c_size_t
         sig = {

@@ -20,6 +20,7 @@
 #include "fracenc_decode.hip"
 #include "fracenc_color.hip"
 #include "fracenc_classify.hip"
+#include "fracenc_sea.hip"
 
 using namespace fracenc;
 
@@ -188,6 +189,12 @@ struct frac_ctx {
     DBuf<uint32_t> d_cls_list;
     DBuf<int32_t> d_cls_out;
     DBuf<uint32_t> d_dft_rguard;
+    // SEA engine: sort keys/values (double-buffered for the radix sort), sorted entries
+    DBuf<uint32_t> d_sea_dkey, d_sea_dkey2, d_sea_dpos, d_sea_dpos2, d_sea_rkey, d_sea_rkey2, d_sea_rord,
+        d_sea_rord2, d_sea_bend, d_sea_spool;
+    DBuf<SeaEntry> d_sea_ent;
+    DBuf<uint8_t> d_sea_tmp;
+    size_t sea_tmp_bytes = 0;
     DBuf<frac_encode_item> d_dec_items;
     DBuf<unsigned long long> d_dec_sum;
     unsigned long long* h_dec_sum = nullptr; // pinned
@@ -233,7 +240,7 @@ int check_params(const frac_params* p, std::string& msg)
         msg = "transforms must be 4 or 8";
         return FRAC_E_INVALID;
     }
-    if (p->engine > FRAC_ENGINE_MFMA) {
+    if (p->engine > FRAC_ENGINE_SEA) {
         msg = "unknown engine";
         return FRAC_E_INVALID;
     }
@@ -400,7 +407,11 @@ int prepare(frac_ctx* c)
     // engine: the MFMA encoding is exact for n <= 8 (|Σ(r−128)(D4−510)| < 2^22)
     if (c->p.engine == FRAC_ENGINE_MFMA && n > 8)
         return c->fail(FRAC_E_INVALID, "the MFMA engine supports range sizes 2, 4 and 8");
-    c->engine = (c->p.engine == FRAC_ENGINE_VALU || n > 8) ? FRAC_ENGINE_VALU : FRAC_ENGINE_MFMA;
+    if (c->p.engine == FRAC_ENGINE_SEA && n > 8)
+        return c->fail(FRAC_E_INVALID, "the SEA engine supports range sizes 2, 4 and 8");
+    c->engine = (c->p.engine == FRAC_ENGINE_VALU || n > 8) ? FRAC_ENGINE_VALU
+                : c->p.engine == FRAC_ENGINE_SEA       ? FRAC_ENGINE_SEA
+                                                       : FRAC_ENGINE_MFMA;
     if (c->engine == FRAC_ENGINE_MFMA) {
         // range blocks of 32 slots per bucket; domain tiles of 32 pool positions per bucket
         c->m_slot_range.clear();
@@ -508,6 +519,31 @@ int prepare(frac_ctx* c)
         for (size_t i = 0; i < nr; ++i)
             c->fb_iota[i] = (uint32_t)i;
         FRAC_TRY(up(c->d_fb_list.ptr, c->fb_iota.data(), nr * sizeof(uint32_t)));
+    }
+    if (c->engine == FRAC_ENGINE_SEA) {
+        if (c->bucket_end.size() > (size_t)kSeaMaxBuckets)
+            return c->fail(FRAC_E_INVALID, "SEA: too many classifier buckets");
+        FRAC_HIP(c, c->d_sea_dkey.ensure(std::max<size_t>(P, 1)));
+        FRAC_HIP(c, c->d_sea_dkey2.ensure(std::max<size_t>(P, 1)));
+        FRAC_HIP(c, c->d_sea_dpos.ensure(std::max<size_t>(P, 1)));
+        FRAC_HIP(c, c->d_sea_dpos2.ensure(std::max<size_t>(P, 1)));
+        FRAC_HIP(c, c->d_sea_ent.ensure(std::max<size_t>(P, 1)));
+        FRAC_HIP(c, c->d_sea_spool.ensure(std::max<size_t>(P * (size_t)(n * n / 2), 1)));
+        FRAC_HIP(c, c->d_sea_rkey.ensure(std::max<size_t>(nr, 1)));
+        FRAC_HIP(c, c->d_sea_rkey2.ensure(std::max<size_t>(nr, 1)));
+        FRAC_HIP(c, c->d_sea_rord.ensure(std::max<size_t>(nr, 1)));
+        FRAC_HIP(c, c->d_sea_rord2.ensure(std::max<size_t>(nr, 1)));
+        FRAC_HIP(c, c->d_sea_bend.ensure(kSeaMaxBuckets));
+        FRAC_TRY(up(c->d_sea_bend.ptr, c->bucket_end.data(), c->bucket_end.size() * sizeof(uint32_t)));
+        size_t t1 = 0, t2 = 0;
+        FRAC_HIP(c, hipcub::DeviceRadixSort::SortPairs(nullptr, t1, c->d_sea_dkey.ptr, c->d_sea_dkey2.ptr,
+                                                        c->d_sea_dpos.ptr, c->d_sea_dpos2.ptr, (int)P, 0, 20,
+                                                        c->stream));
+        FRAC_HIP(c, hipcub::DeviceRadixSort::SortPairs(nullptr, t2, c->d_sea_rkey.ptr, c->d_sea_rkey2.ptr,
+                                                        c->d_sea_rord.ptr, c->d_sea_rord2.ptr, (int)nr, 0, 17,
+                                                        c->stream));
+        c->sea_tmp_bytes = std::max<size_t>(std::max(t1, t2), 1);
+        FRAC_HIP(c, c->d_sea_tmp.ensure(c->sea_tmp_bytes));
     }
     if (c->engine == FRAC_ENGINE_MFMA) {
         const int KS = (n * n + 15) / 16;
@@ -798,6 +834,58 @@ int launch_mfma(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride)
     return FRAC_OK;
 }
 
+// SEA engine (fracenc_sea.hip): domain keys → radix sort (bucket, ΣD4) → sorted entries;
+// range keys → radix sort by ΣR; then one wave per range writes best_key.
+template <int N>
+int launch_sea(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool timing)
+{
+    const uint32_t nr = (uint32_t)c->ranges.size(), P = (uint32_t)c->porig.size();
+    if (P) {
+        sea_domain_keys<N><<<(P + 255) / 256, 256, 0, c->stream>>>(c->d_pool.ptr, P, c->d_sea_bend.ptr,
+                                                                   (uint32_t)c->bucket_end.size(), c->d_sea_dkey.ptr,
+                                                                   c->d_sea_dpos.ptr);
+        size_t tb = c->sea_tmp_bytes;
+        FRAC_HIP(c, hipcub::DeviceRadixSort::SortPairs(c->d_sea_tmp.ptr, tb, c->d_sea_dkey.ptr, c->d_sea_dkey2.ptr,
+                                                        c->d_sea_dpos.ptr, c->d_sea_dpos2.ptr, (int)P, 0, 20,
+                                                        c->stream));
+        const uint32_t pieces = (N * N / 2 + 3) / 4;
+        sea_domain_entries<N><<<(P * pieces + 255) / 256, 256, 0, c->stream>>>(
+            c->d_sea_dkey2.ptr, c->d_sea_dpos2.ptr, c->d_negsd2.ptr, c->d_pool.ptr, P, c->d_sea_ent.ptr,
+            c->d_sea_spool.ptr);
+    }
+    if (nr) {
+        sea_range_keys<N><<<(nr + 255) / 256, 256, 0, c->stream>>>(dtgt, tstride, c->d_ranges.ptr, nr,
+                                                                    c->d_sea_rkey.ptr, c->d_sea_rord.ptr);
+        size_t tb = c->sea_tmp_bytes;
+        FRAC_HIP(c, hipcub::DeviceRadixSort::SortPairs(c->d_sea_tmp.ptr, tb, c->d_sea_rkey.ptr, c->d_sea_rkey2.ptr,
+                                                        c->d_sea_rord.ptr, c->d_sea_rord2.ptr, (int)nr, 0, 17,
+                                                        c->stream));
+    }
+    if (timing)
+        FRAC_HIP(c, hipEventRecord(c->ev[1], c->stream));
+    if (nr) {
+        SeaArgs a;
+        a.tgt = dtgt;
+        a.tstride = tstride;
+        a.ranges = c->d_ranges.ptr;
+        a.rbucket = c->d_rbucket.ptr;
+        a.rorder = c->d_sea_rord2.ptr;
+        a.ent = c->d_sea_ent.ptr;
+        a.spool = c->d_sea_spool.ptr;
+        a.negsd2 = c->d_negsd2.ptr;
+        a.nr = nr;
+        a.hitH = c->hitH;
+        a.best_key = c->d_best_key.ptr;
+        if (c->p.transforms == 8)
+            sea_search<N, 8><<<(nr + 3) / 4, 256, 0, c->stream>>>(a);
+        else
+            sea_search<N, 4><<<(nr + 3) / 4, 256, 0, c->stream>>>(a);
+    }
+    c->form_ran = FRAC_FORM_SEA;
+    c->flops_ran = 0;
+    return FRAC_OK;
+}
+
 template <int N>
 int launch_all(frac_ctx* c)
 {
@@ -820,13 +908,17 @@ int launch_all(frac_ctx* c)
     if (P && !fused_pool)
         pool_build<N><<<(P + 3) / 4, 256, 0, c->stream>>>(dsrc, c->d_sstride, c->d_doms.ptr, c->d_porig.ptr, P,
                                                           c->d_pool.ptr, c->d_negsd2.ptr);
+    const bool use_sea = c->engine == FRAC_ENGINE_SEA && !c->all_fallback;
     if constexpr (N <= 8) {
         if (use_mfma)
             FRAC_TRY(launch_mfma<N>(c, dtgt, tstride));
+        if (use_sea)
+            FRAC_TRY(launch_sea<N>(c, dtgt, tstride, timing));
     }
-    if (timing && !use_mfma)
+    const bool use_valu = !use_mfma && !use_sea;
+    if (timing && use_valu)
         FRAC_HIP(c, hipEventRecord(c->ev[1], c->stream));
-    if (!use_mfma && !c->all_fallback && !c->work.empty()) {
+    if (use_valu && !c->all_fallback && !c->work.empty()) {
         SearchArgs a;
         a.tgt = dtgt;
         a.tstride = tstride;
@@ -907,8 +999,8 @@ int launch_all(frac_ctx* c)
     if (timing)
         FRAC_HIP(c, hipEventRecord(c->ev[3], c->stream));
     FRAC_HIP(c, hipGetLastError());
-    c->engine_ran = use_mfma ? FRAC_ENGINE_MFMA : FRAC_ENGINE_VALU;
-    if (!use_mfma) {
+    c->engine_ran = use_mfma ? FRAC_ENGINE_MFMA : use_sea ? FRAC_ENGINE_SEA : FRAC_ENGINE_VALU;
+    if (use_valu) {
         c->form_ran = FRAC_FORM_DOT2;
         c->flops_ran = 0;
     }
@@ -998,6 +1090,18 @@ void frac_destroy(frac_ctx* c)
     c->d_m8_blk_ent.release();
     c->d_m_dtiles.release();
     c->d_m_rfrags.release();
+    c->d_sea_dkey.release();
+    c->d_sea_dkey2.release();
+    c->d_sea_dpos.release();
+    c->d_sea_dpos2.release();
+    c->d_sea_rkey.release();
+    c->d_sea_rkey2.release();
+    c->d_sea_rord.release();
+    c->d_sea_rord2.release();
+    c->d_sea_bend.release();
+    c->d_sea_spool.release();
+    c->d_sea_ent.release();
+    c->d_sea_tmp.release();
     c->d_m_entries.release();
     c->d_dec_src.release();
     c->d_color.release();

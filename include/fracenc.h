@@ -41,6 +41,8 @@ extern "C" {
 #define FRAC_ENGINE_AUTO 0      /* fastest engine that supports the geometry             */
 #define FRAC_ENGINE_VALU 1      /* v_dot2_u32_u16 scalar-broadcast search                */
 #define FRAC_ENGINE_MFMA 2      /* f16 MFMA search with an exact integer epilogue        */
+#define FRAC_ENGINE_SEA 3       /* successive elimination: exact per-candidate bound skips   */
+                                /* domains that cannot win; same result, data-dependent cost */
 
 /* flags (frac_params.flags) */
 #define FRAC_FLAG_TIMING 1u     /* record per-kernel device time with HIP events         */
@@ -106,6 +108,7 @@ typedef struct frac_stats {
 #define FRAC_FORM_DOT2 0    /* VALU engine: packed-u16 v_dot2 per (range, transform, domain)       */
 #define FRAC_FORM_DIRECT 1  /* MFMA engine: one f16 GEMM per transform (n²·T MACs per pair)        */
 #define FRAC_FORM_FOURIER 2 /* MFMA engine, n = 8, T = 4: rotation-group Fourier form (96 MACs)    */
+#define FRAC_FORM_SEA 3     /* SEA engine: bound-pruned exact evaluation (v_dot2)                */
 
 typedef struct frac_ctx frac_ctx;
 

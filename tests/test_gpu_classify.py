@@ -36,7 +36,7 @@ def test_device_classify_reference_kat():
     assert list(got["category"]) == [c for *_, c in cases]
 
 
-@pytest.mark.parametrize("engine", [F.ENGINE_VALU, F.ENGINE_MFMA])
+@pytest.mark.parametrize("engine", [F.ENGINE_VALU, F.ENGINE_MFMA, F.ENGINE_SEA])
 def test_engine_classifies_unlabelled_items_on_device(engine):
     # categories −1 + use_classifier: the engine's device pre-pass reproduces the
     # reference goldens made with host-preclassified grids (main.cpp:155-162)

@@ -14,7 +14,7 @@ pytestmark = pytest.mark.gpu
 
 # fixture name → engine support (the engine implements the ratio-2 path, n ∈ {2,4,8,16})
 RATIO2 = [n for n in GOLDEN_NAMES if n != "lenna_16to4"]
-ENGINES = [F.ENGINE_VALU, F.ENGINE_MFMA]
+ENGINES = [F.ENGINE_VALU, F.ENGINE_MFMA, F.ENGINE_SEA]
 
 
 def as_oracle_fields(out):
@@ -23,8 +23,8 @@ def as_oracle_fields(out):
 
 
 def run_engine(p, meta, engine, tgt=None, ranges_idx=None):
-    if engine == F.ENGINE_MFMA and meta["tgt"] > 8:
-        pytest.skip("the MFMA engine covers n <= 8 (n = 16 runs on the VALU engine)")
+    if engine in (F.ENGINE_MFMA, F.ENGINE_SEA) and meta["tgt"] > 8:
+        pytest.skip("the MFMA and SEA engines cover n <= 8 (n = 16 runs on the VALU engine)")
     H, W = p.shape
     doms = F.create_uniform_grid(W, H, meta["src"], meta["src"] // 2)
     rngs = F.create_uniform_grid(W, H, meta["tgt"], meta["tgt"])
@@ -216,9 +216,10 @@ def test_full_4096_frame(engine):
     assert (out["sw"] == 16).all()
 
 
-def test_mfma_rejects_n16():
+@pytest.mark.parametrize("engine", [F.ENGINE_MFMA, F.ENGINE_SEA])
+def test_mfma_and_sea_reject_n16(engine):
     p = np.zeros((64, 64), np.uint8)
-    with F.Engine(0, 4, engine=F.ENGINE_MFMA) as e:
+    with F.Engine(0, 4, engine=engine) as e:
         e.set_frame(p)
         e.set_domains(F.create_uniform_grid(64, 64, 32, 16))
         with pytest.raises(F.FracError):
@@ -226,11 +227,12 @@ def test_mfma_rejects_n16():
 
 
 def test_engines_agree_on_stress_frame():
-    """VALU and MFMA engines on a uniform-noise 1024² frame (S2): identical records."""
+    """VALU, MFMA and SEA engines on a uniform-noise 1024² frame (S2, where the SEA bound is
+    loose): identical records."""
     from fractencode_amd.synth import uniform_noise
     p = uniform_noise(1024, 1024, 42)
     outs = []
-    for eng in (F.ENGINE_VALU, F.ENGINE_MFMA):
+    for eng in (F.ENGINE_VALU, F.ENGINE_MFMA, F.ENGINE_SEA):
         with F.Engine(0, 8, False, 0.0, -1.0, eng) as e:
             e.set_frame(p)
             e.set_domains(F.create_uniform_grid(1024, 1024, 16, 8))
@@ -238,6 +240,7 @@ def test_engines_agree_on_stress_frame():
             assert st["engine"] == eng
             outs.append(out)
     assert outs[0].tobytes() == outs[1].tobytes()
+    assert outs[0].tobytes() == outs[2].tobytes()
 
 
 DFT_CASES = [
@@ -276,7 +279,7 @@ def test_fourier_direct_and_valu_agree_on_stress_frame(monkeypatch):
     from fractencode_amd.synth import uniform_noise
     p = uniform_noise(1024, 1024, 43)
     outs = []
-    for eng, dft in ((F.ENGINE_VALU, "1"), (F.ENGINE_MFMA, "0"), (F.ENGINE_MFMA, "1")):
+    for eng, dft in ((F.ENGINE_VALU, "1"), (F.ENGINE_MFMA, "0"), (F.ENGINE_MFMA, "1"), (F.ENGINE_SEA, "1")):
         monkeypatch.setenv("FRAC_MFMA_DFT", dft)
         with F.Engine(0, 4, False, 0.0, -1.0, eng) as e:
             e.set_frame(p)
@@ -286,3 +289,4 @@ def test_fourier_direct_and_valu_agree_on_stress_frame(monkeypatch):
             outs.append(out)
     assert outs[0].tobytes() == outs[1].tobytes()
     assert outs[0].tobytes() == outs[2].tobytes()
+    assert outs[0].tobytes() == outs[3].tobytes()
