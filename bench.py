@@ -237,6 +237,7 @@ def main():
             else:
                 main_out, _ = eng.fetch()
                 entry["records_identical_to_exhaustive"] = bool(alt_out.tobytes() == main_out.tobytes())
+                entry["evaluated_frac"] = round(ast["evaluated_mappings"] / (len(mine) * n_d), 6)
             line["alt_engines"][alt_name] = entry
     if rank == 0 and world == 1 and args.cpu_budget > 0:
         threads = args.cpu_threads or min(16, os.cpu_count() or 1)

@@ -49,7 +49,7 @@ class FracStats(C.Structure):
                 ("fallback_ranges", C.c_uint32), ("empty_ranges", C.c_uint32), ("engine", C.c_uint32),
                 ("ms_device", C.c_double), ("ms_search", C.c_double), ("ms_prep", C.c_double),
                 ("ms_finish", C.c_double), ("search_form", C.c_uint32), ("pad_", C.c_uint32),
-                ("matrix_flops", C.c_uint64)]
+                ("matrix_flops", C.c_uint64), ("evaluated_mappings", C.c_uint64)]
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_}

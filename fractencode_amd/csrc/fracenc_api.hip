@@ -194,6 +194,9 @@ struct frac_ctx {
         d_sea_rord2, d_sea_bend, d_sea_spool;
     DBuf<SeaEntry> d_sea_ent;
     DBuf<uint8_t> d_sea_tmp;
+    DBuf<unsigned long long> d_sea_count; // candidates the SEA search evaluated
+    uint64_t eligible_pairs = 0;          // Σ over ranges of its bucket's domain count
+    uint64_t evaluated_ran = 0;           // frac_stats.evaluated_mappings of the last run
     size_t sea_tmp_bytes = 0;
     DBuf<frac_encode_item> d_dec_items;
     DBuf<unsigned long long> d_dec_sum;
@@ -401,6 +404,9 @@ int prepare(frac_ctx* c)
                     c->work.push_back(make_uint4(bl.first, pb, pe, g));
             }
     }
+    c->eligible_pairs = 0;
+    for (size_t i = 0; i < c->ranges.size(); ++i)
+        c->eligible_pairs += c->rbucket[i].y - c->rbucket[i].x;
     c->hitH = compute_hit_limit(c->p.rms_threshold, (uint32_t)(4 * n * n));
     c->all_fallback = c->hitH >= kExactLimit;
 
@@ -534,6 +540,7 @@ int prepare(frac_ctx* c)
         FRAC_HIP(c, c->d_sea_rord.ensure(std::max<size_t>(nr, 1)));
         FRAC_HIP(c, c->d_sea_rord2.ensure(std::max<size_t>(nr, 1)));
         FRAC_HIP(c, c->d_sea_bend.ensure(kSeaMaxBuckets));
+        FRAC_HIP(c, c->d_sea_count.ensure(1));
         FRAC_TRY(up(c->d_sea_bend.ptr, c->bucket_end.data(), c->bucket_end.size() * sizeof(uint32_t)));
         size_t t1 = 0, t2 = 0;
         FRAC_HIP(c, hipcub::DeviceRadixSort::SortPairs(nullptr, t1, c->d_sea_dkey.ptr, c->d_sea_dkey2.ptr,
@@ -863,6 +870,7 @@ int launch_sea(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool timing)
     }
     if (timing)
         FRAC_HIP(c, hipEventRecord(c->ev[1], c->stream));
+    FRAC_HIP(c, hipMemsetAsync(c->d_sea_count.ptr, 0, sizeof(unsigned long long), c->stream));
     if (nr) {
         SeaArgs a;
         a.tgt = dtgt;
@@ -876,6 +884,7 @@ int launch_sea(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool timing)
         a.nr = nr;
         a.hitH = c->hitH;
         a.best_key = c->d_best_key.ptr;
+        a.evaluated = c->d_sea_count.ptr;
         if (c->p.transforms == 8)
             sea_search<N, 8><<<(nr + 3) / 4, 256, 0, c->stream>>>(a);
         else
@@ -1000,6 +1009,7 @@ int launch_all(frac_ctx* c)
         FRAC_HIP(c, hipEventRecord(c->ev[3], c->stream));
     FRAC_HIP(c, hipGetLastError());
     c->engine_ran = use_mfma ? FRAC_ENGINE_MFMA : use_sea ? FRAC_ENGINE_SEA : FRAC_ENGINE_VALU;
+    c->evaluated_ran = c->all_fallback ? 0 : c->eligible_pairs; // SEA: read back at fetch
     if (use_valu) {
         c->form_ran = FRAC_FORM_DOT2;
         c->flops_ran = 0;
@@ -1100,6 +1110,7 @@ void frac_destroy(frac_ctx* c)
     c->d_sea_rord2.release();
     c->d_sea_bend.release();
     c->d_sea_spool.release();
+    c->d_sea_count.release();
     c->d_sea_ent.release();
     c->d_sea_tmp.release();
     c->d_m_entries.release();
@@ -1265,13 +1276,21 @@ int frac_fetch(frac_ctx* c, frac_encode_item* out, frac_stats* stats)
     if (nr)
         FRAC_HIP(c, hipMemcpyAsync(c->h_aux.data(), c->d_aux.ptr, nr * sizeof(RangeAux), hipMemcpyDeviceToHost,
                                    c->stream));
+    unsigned long long sea_count = 0;
+    const bool sea_ran = c->engine_ran == FRAC_ENGINE_SEA;
+    if (sea_ran)
+        FRAC_HIP(c, hipMemcpyAsync(&sea_count, c->d_sea_count.ptr, sizeof(sea_count), hipMemcpyDeviceToHost,
+                                   c->stream));
     FRAC_HIP(c, hipStreamSynchronize(c->stream));
+    if (sea_ran)
+        c->evaluated_ran = sea_count;
     if (stats) {
         std::memset(stats, 0, sizeof(*stats));
         stats->total_mappings = (uint64_t)c->doms.size() * nr;
         stats->engine = c->engine_ran;
         stats->search_form = c->form_ran;
         stats->matrix_flops = c->flops_ran;
+        stats->evaluated_mappings = c->evaluated_ran;
         const uint64_t nd = c->doms.size();
         for (size_t r = 0; r < nr; ++r) {
             const RangeAux& ax = c->h_aux[r];
@@ -1371,6 +1390,7 @@ int frac_encode_quadtree(frac_ctx* c, const frac_quadtree_params* qp, frac_encod
         total.ms_finish += st.ms_finish;
         total.search_form = st.search_form;
         total.matrix_flops += st.matrix_flops;
+        total.evaluated_mappings += st.evaluated_mappings;
         std::vector<frac_grid_item> next;
         for (size_t i = 0; i < res.size(); ++i) {
             const frac_grid_item& r = pending[i];

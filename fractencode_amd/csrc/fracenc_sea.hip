@@ -125,6 +125,7 @@ struct SeaArgs {
     uint32_t nr;
     int64_t hitH;             // −1: no hits
     unsigned long long* best_key; // [nr]
+    unsigned long long* evaluated; // Σ candidates evaluated exactly (frac_stats.evaluated_mappings)
 };
 
 constexpr uint32_t kSeaSeed = 16; // first step: the 16 candidates nearest in ΣD4 seed the bound
@@ -193,6 +194,7 @@ __global__ void __launch_bounds__(256) sea_search(SeaArgs a)
     const double H = a.hitH >= 0 ? (double)a.hitH : -1.0;
     double bound = __builtin_inf(); // max(U, H): candidates with LB above it cannot win
     unsigned long long bestk = kKeyNone;
+    uint32_t nevals = 0;
     uint32_t L = lo, Rt = lo; // visited [L, Rt)
     bool lopen = L > seg.x, ropen = Rt < seg.y;
     // the next step's window: up to `want` candidates split over the open sides
@@ -220,6 +222,7 @@ __global__ void __launch_bounds__(256) sea_search(SeaArgs a)
             list[wv][rank] = idx;
         __builtin_amdgcn_wave_barrier();
         const int ns = __popcll(sm);
+        nevals += (uint32_t)ns;
         // speculative prefetch of the next step (both sides assumed to stay open) and of the
         // entries just outside the window that decide whether they do
         const uint32_t L1 = L - nl, R1 = Rt + nrt;
@@ -323,8 +326,10 @@ __global__ void __launch_bounds__(256) sea_search(SeaArgs a)
             e = valid ? a.ent[idx] : SeaEntry{0.0, 0u, 0u};
         }
     }
-    if (lane == 0)
+    if (lane == 0) {
         a.best_key[r] = bestk;
+        atomicAdd(a.evaluated, (unsigned long long)nevals);
+    }
 }
 
 } // namespace fracenc

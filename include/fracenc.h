@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define FRAC_ABI_VERSION 2
+#define FRAC_ABI_VERSION 3
 
 /* error codes */
 #define FRAC_OK 0
@@ -102,6 +102,8 @@ typedef struct frac_stats {
     uint32_t search_form;       /* FRAC_FORM_*: how the search kernel computed the candidates     */
     uint32_t pad_;
     uint64_t matrix_flops;      /* MFMA flops the search issued (0 for the VALU engine)          */
+    uint64_t evaluated_mappings; /* (range, domain) pairs whose error was computed: every eligible */
+                                 /* pair for the exhaustive engines, the bound's survivors (SEA)   */
 } frac_stats;
 
 /* frac_stats.search_form */

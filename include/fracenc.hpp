@@ -204,6 +204,7 @@ public:
                     sum.engine = st.engine;
                     sum.search_form = st.search_form;
                     sum.matrix_flops += st.matrix_flops;
+                    sum.evaluated_mappings += st.evaluated_mappings;
                 }
             } catch (const std::exception& ex) {
                 std::lock_guard<std::mutex> lk(m);

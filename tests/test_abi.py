@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol():
     assert len(names) >= 20
     missing = [n for n in names if not hasattr(lib, n)]
     assert not missing, missing
-    assert lib.frac_abi_version() == 2
+    assert lib.frac_abi_version() == 3
 
 
 def test_record_layouts_match_reference_structs(tmp_path):
@@ -46,6 +46,8 @@ def test_record_layouts_match_reference_structs(tmp_path):
         "_Static_assert(offsetof(frac_score, transform) == 24, \"t off\");\n"
         f"_Static_assert(sizeof(frac_stats) == {C.sizeof(F.FracStats)}, \"stats (ctypes mirror)\");\n"
         f"_Static_assert(offsetof(frac_stats, matrix_flops) == {F.FracStats.matrix_flops.offset}, \"flops off\");\n"
+        f"_Static_assert(offsetof(frac_stats, evaluated_mappings) == {F.FracStats.evaluated_mappings.offset}, "
+        "\"evaluated off\");\n"
         "int main(void) { return 0; }\n")
     subprocess.check_call(["gcc", "-std=c11", "-I", os.path.join(ROOT, "include"), "-c", str(src), "-o",
                            str(tmp_path / "layout.o")])

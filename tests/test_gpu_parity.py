@@ -290,3 +290,22 @@ def test_fourier_direct_and_valu_agree_on_stress_frame(monkeypatch):
     assert outs[0].tobytes() == outs[1].tobytes()
     assert outs[0].tobytes() == outs[2].tobytes()
     assert outs[0].tobytes() == outs[3].tobytes()
+
+
+def test_sea_skips_most_candidates_with_identical_records():
+    """Lenna Y, n = 8, T = 8: the SEA engine evaluates a small fraction of the candidates the
+    exhaustive engines do, and returns the same records."""
+    p = plane("lenna_y")
+    doms = F.create_uniform_grid(512, 512, 16, 8)
+    rngs = F.create_uniform_grid(512, 512, 8, 8)
+    res = {}
+    for eng in (F.ENGINE_MFMA, F.ENGINE_SEA):
+        with F.Engine(0, 8, False, 0.0, -1.0, eng) as e:
+            e.set_frame(p)
+            e.set_domains(doms)
+            res[eng] = e.search(rngs)
+    (a, sa), (b, sb) = res[F.ENGINE_MFMA], res[F.ENGINE_SEA]
+    assert a.tobytes() == b.tobytes()
+    assert sa["evaluated_mappings"] == len(doms) * len(rngs)
+    assert 0 < sb["evaluated_mappings"] < 0.2 * sa["evaluated_mappings"]
+    assert sb["search_form"] == F.FORM_SEA
