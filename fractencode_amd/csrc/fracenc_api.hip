@@ -193,6 +193,7 @@ struct frac_ctx {
     DBuf<uint32_t> d_sea_dkey, d_sea_dkey2, d_sea_dpos, d_sea_dpos2, d_sea_rkey, d_sea_rkey2, d_sea_rord,
         d_sea_rord2, d_sea_bend, d_sea_spool;
     DBuf<SeaEntry> d_sea_ent;
+    DBuf<int32_t> d_sea_snegsd2;
     DBuf<uint8_t> d_sea_tmp;
     DBuf<unsigned long long> d_sea_count; // candidates the SEA search evaluated
     uint64_t eligible_pairs = 0;          // Σ over ranges of its bucket's domain count
@@ -534,6 +535,7 @@ int prepare(frac_ctx* c)
         FRAC_HIP(c, c->d_sea_dpos.ensure(std::max<size_t>(P, 1)));
         FRAC_HIP(c, c->d_sea_dpos2.ensure(std::max<size_t>(P, 1)));
         FRAC_HIP(c, c->d_sea_ent.ensure(std::max<size_t>(P, 1)));
+        FRAC_HIP(c, c->d_sea_snegsd2.ensure(std::max<size_t>(P, 1)));
         FRAC_HIP(c, c->d_sea_spool.ensure(std::max<size_t>(P * (size_t)(n * n / 2), 1)));
         FRAC_HIP(c, c->d_sea_rkey.ensure(std::max<size_t>(nr, 1)));
         FRAC_HIP(c, c->d_sea_rkey2.ensure(std::max<size_t>(nr, 1)));
@@ -858,7 +860,7 @@ int launch_sea(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool timing)
         const uint32_t pieces = (N * N / 2 + 3) / 4;
         sea_domain_entries<N><<<(P * pieces + 255) / 256, 256, 0, c->stream>>>(
             c->d_sea_dkey2.ptr, c->d_sea_dpos2.ptr, c->d_negsd2.ptr, c->d_pool.ptr, P, c->d_sea_ent.ptr,
-            c->d_sea_spool.ptr);
+            c->d_sea_spool.ptr, c->d_sea_snegsd2.ptr);
     }
     if (nr) {
         sea_range_keys<N><<<(nr + 255) / 256, 256, 0, c->stream>>>(dtgt, tstride, c->d_ranges.ptr, nr,
@@ -880,7 +882,7 @@ int launch_sea(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool timing)
         a.rorder = c->d_sea_rord2.ptr;
         a.ent = c->d_sea_ent.ptr;
         a.spool = c->d_sea_spool.ptr;
-        a.negsd2 = c->d_negsd2.ptr;
+        a.snegsd2 = c->d_sea_snegsd2.ptr;
         a.nr = nr;
         a.hitH = c->hitH;
         a.best_key = c->d_best_key.ptr;
@@ -1111,6 +1113,7 @@ void frac_destroy(frac_ctx* c)
     c->d_sea_bend.release();
     c->d_sea_spool.release();
     c->d_sea_count.release();
+    c->d_sea_snegsd2.release();
     c->d_sea_ent.release();
     c->d_sea_tmp.release();
     c->d_m_entries.release();

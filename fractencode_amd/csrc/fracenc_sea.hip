@@ -65,15 +65,17 @@ __global__ void __launch_bounds__(256) sea_domain_keys(const uint32_t* __restric
     pos[p] = p;
 }
 
-// sorted (key, pos) → entries {cD, SD, pos} and the pool rows in the same order (spool), so a
-// window of candidates is a contiguous stretch of memory shared by ranges of similar ΣR.
+// sorted (key, pos) → entries {cD, SD, pos}, and in the same order the pool rows (spool: a
+// window of candidates is a contiguous stretch of memory shared by ranges of similar ΣR) and
+// −ΣD4² (snegsd2).
 // One thread per (entry, 16-byte piece of its row).
 template <int N>
 __global__ void __launch_bounds__(256) sea_domain_entries(const uint32_t* __restrict__ key,
                                                           const uint32_t* __restrict__ pos,
                                                           const int32_t* __restrict__ negsd2,
                                                           const uint32_t* __restrict__ pool, uint32_t P,
-                                                          SeaEntry* __restrict__ ent, uint32_t* __restrict__ spool)
+                                                          SeaEntry* __restrict__ ent, uint32_t* __restrict__ spool,
+                                                          int32_t* __restrict__ snegsd2)
 {
     constexpr int64_t NN = N * N;
     constexpr uint32_t K2 = N * N / 2, PIECES = (K2 + 3) / 4;
@@ -92,6 +94,7 @@ __global__ void __launch_bounds__(256) sea_domain_entries(const uint32_t* __rest
     e.sd = (uint32_t)sd;
     e.pos = p;
     ent[i] = e;
+    snegsd2[i] = negsd2[p];
 }
 
 // per range: sort key ΣR = 4Σr (range order for locality only)
@@ -121,14 +124,15 @@ struct SeaArgs {
     const uint32_t* rorder;   // [nr] ranges in ΣR order
     const SeaEntry* ent;      // [P] per bucket sorted by ΣD4
     const uint32_t* spool;    // [P][n²/2] pool rows in entry order
-    const int32_t* negsd2;    // [P] by pool position
+    const int32_t* snegsd2;   // [P] −ΣD4² in entry order
     uint32_t nr;
     int64_t hitH;             // −1: no hits
     unsigned long long* best_key; // [nr]
     unsigned long long* evaluated; // Σ candidates evaluated exactly (frac_stats.evaluated_mappings)
 };
 
-constexpr uint32_t kSeaSeed = 16; // first step: the 16 candidates nearest in ΣD4 seed the bound
+constexpr uint32_t kSeaSeed = 16;  // first step: the 16 candidates nearest in ΣD4 seed the bound
+constexpr uint32_t kSeaStep = 128; // later steps: two candidates per lane
 
 template <int N, int T>
 __global__ void __launch_bounds__(256) sea_search(SeaArgs a)
@@ -139,7 +143,10 @@ __global__ void __launch_bounds__(256) sea_search(SeaArgs a)
     constexpr int C = NN / G;           // cells per slice
     constexpr int W = C / 2;            // packed words per slice
     static_assert(C % 2 == 0 && NN <= 64, "n ∈ {2, 4, 8}");
-    __shared__ uint32_t list[4][64];
+    // survivors of the current step: sorted index, pool position (for the key), −ΣD4²
+    __shared__ uint32_t l_idx[4][kSeaStep];
+    __shared__ uint32_t l_pos[4][kSeaStep];
+    __shared__ int32_t l_nsd[4][kSeaStep];
     const uint32_t wv = threadIdx.x >> 6;
     const uint32_t w = blockIdx.x * 4u + wv;
     const int lane = threadIdx.x & 63;
@@ -197,54 +204,71 @@ __global__ void __launch_bounds__(256) sea_search(SeaArgs a)
     uint32_t nevals = 0;
     uint32_t L = lo, Rt = lo; // visited [L, Rt)
     bool lopen = L > seg.x, ropen = Rt < seg.y;
-    // the next step's window: up to `want` candidates split over the open sides
-    auto plan = [&](uint32_t want, uint32_t& nl, uint32_t& nrt) {
-        nl = lopen ? (ropen ? want / 2 : want) : 0u;
-        nl = min(nl, L - seg.x);
-        nrt = ropen ? min(want - nl, seg.y - Rt) : 0u;
-        if (lopen && nl + nrt < want) // right side short: take more from the left
-            nl = min(want - nrt, L - seg.x);
+    // the window of a step: up to `want` candidates split over the open sides
+    auto plan = [&](uint32_t want, uint32_t cl, uint32_t cr_, bool lo_, bool ro_, uint32_t& nl, uint32_t& nrt) {
+        nl = lo_ ? (ro_ ? want / 2 : want) : 0u;
+        nl = min(nl, cl - seg.x);
+        nrt = ro_ ? min(want - nl, seg.y - cr_) : 0u;
+        if (lo_ && nl + nrt < want) // right side short: take more from the left
+            nl = min(want - nrt, cl - seg.x);
     };
+    // candidate slot k of a step [L − nl, L) ∪ [Rt, Rt + nrt)
+    auto slot = [&](uint32_t k, uint32_t cl, uint32_t cr_, uint32_t nl) { return k < nl ? cl - nl + k : cr_ + (k - nl); };
     uint32_t nl, nrt;
-    plan(kSeaSeed, nl, nrt);
-    uint32_t idx = (uint32_t)lane < nl ? L - nl + (uint32_t)lane : Rt + ((uint32_t)lane - nl);
-    bool valid = (uint32_t)lane < nl + nrt;
-    SeaEntry e = valid ? a.ent[idx] : SeaEntry{0.0, 0u, 0u};
+    plan(kSeaSeed, L, Rt, lopen, ropen, nl, nrt);
+    // per lane: step slots lane and lane + 64
+    SeaEntry e[2];
+    int32_t en[2];
+    uint32_t ix[2];
+    bool ev[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        const uint32_t k = (uint32_t)lane + 64u * u;
+        ev[u] = k < nl + nrt;
+        ix[u] = ev[u] ? slot(k, L, Rt, nl) : seg.x;
+        e[u] = a.ent[ix[u]];
+        en[u] = a.snegsd2[ix[u]];
+    }
     while (nl + nrt) {
-        bool surv = false;
-        if (valid) {
-            const double dm = (double)(SR - (int64_t)e.sd), dc = cr - e.cd;
-            surv = dm * dm / (double)NN + dc * dc <= bound + 0.5;
+        // bound test, survivors compacted into the wave's LDS lists
+        int ns = 0;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            bool surv = false;
+            if (ev[u]) {
+                const double dm = (double)(SR - (int64_t)e[u].sd), dc = cr - e[u].cd;
+                surv = dm * dm * (1.0 / NN) + dc * dc <= bound + 0.5; // 1/n² exact
+            }
+            const unsigned long long sm = __ballot(surv);
+            const int rank = ns + __popcll(sm & ((1ull << lane) - 1ull));
+            if (surv) {
+                l_idx[wv][rank] = ix[u];
+                l_pos[wv][rank] = e[u].pos;
+                l_nsd[wv][rank] = en[u];
+            }
+            ns += __popcll(sm);
         }
-        const unsigned long long sm = __ballot(surv);
-        const int rank = __popcll(sm & ((1ull << lane) - 1ull));
-        if (surv)
-            list[wv][rank] = idx;
         __builtin_amdgcn_wave_barrier();
-        const int ns = __popcll(sm);
         nevals += (uint32_t)ns;
-        // speculative prefetch of the next step (both sides assumed to stay open) and of the
-        // entries just outside the window that decide whether they do
+        // speculative prefetch of the next step (sides assumed to stay open) and of the entries
+        // just outside the window that decide whether they do
         const uint32_t L1 = L - nl, R1 = Rt + nrt;
         const uint32_t sdl = L1 > seg.x ? a.ent[L1 - 1].sd : 0u;
         const uint32_t sdr = R1 < seg.y ? a.ent[R1].sd : 0u;
         uint32_t snl, snr;
-        {
-            const uint32_t sL = L, sR = Rt;
-            L = L1;
-            Rt = R1;
-            const bool so = lopen, sro = ropen;
-            lopen = L > seg.x;
-            ropen = Rt < seg.y;
-            plan(64u, snl, snr);
-            lopen = so;
-            ropen = sro;
-            L = sL;
-            Rt = sR;
+        plan(kSeaStep, L1, R1, L1 > seg.x, R1 < seg.y, snl, snr);
+        SeaEntry ne[2];
+        int32_t nen[2];
+        uint32_t nix[2];
+        bool nev[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const uint32_t k = (uint32_t)lane + 64u * u;
+            nev[u] = k < snl + snr;
+            nix[u] = nev[u] ? slot(k, L1, R1, snl) : seg.x;
+            ne[u] = a.ent[nix[u]];
+            nen[u] = a.snegsd2[nix[u]];
         }
-        const uint32_t nidx = (uint32_t)lane < snl ? L1 - snl + (uint32_t)lane : R1 + ((uint32_t)lane - snl);
-        const bool nvalid = (uint32_t)lane < snl + snr;
-        const SeaEntry ne = nvalid ? a.ent[nidx] : SeaEntry{0.0, 0u, 0u};
 
         unsigned long long lk = kKeyNone;
         for (int g0 = 0; g0 < ns; g0 += 2 * R) { // two groups per pass: their loads overlap
@@ -256,7 +280,10 @@ __global__ void __launch_bounds__(256) sea_search(SeaArgs a)
             for (int u = 0; u < 2; ++u) {
                 const int s = g0 + u * R + i;
                 have[u] = s < ns;
-                const uint32_t si = have[u] ? list[wv][s] : seg.x;
+                const int sl = have[u] ? s : 0;
+                const uint32_t si = have[u] ? l_idx[wv][sl] : seg.x;
+                pp[u] = l_pos[wv][sl];
+                nsd2[u] = l_nsd[wv][sl];
                 const uint32_t* dp = a.spool + (size_t)si * (NN / 2) + g * W;
                 if constexpr (W % 4 == 0) {
 #pragma unroll
@@ -269,14 +296,12 @@ __global__ void __launch_bounds__(256) sea_search(SeaArgs a)
                     for (int j = 0; j < W; ++j)
                         dv[u][j] = dp[j];
                 }
-                pp[u] = a.ent[si].pos;
-                nsd2[u] = 0;
             }
 #pragma unroll
-            for (int u = 0; u < 2; ++u)
-                nsd2[u] = a.negsd2[pp[u]];
-#pragma unroll
-            for (int u = 0; u < 2; ++u)
+            for (int u = 0; u < 2; ++u) {
+                // per transform S16·8 + (T − 1 − t): the least is the candidate's miss order
+                // (least error, then the later transform); a hit takes the first t instead
+                uint32_t m = ~0u, hitt = (uint32_t)T;
 #pragma unroll
                 for (int t = 0; t < T; ++t) {
                     uint32_t X = 0;
@@ -287,14 +312,17 @@ __global__ void __launch_bounds__(256) sea_search(SeaArgs a)
                     X += (uint32_t)__shfl_xor((int)X, 1, 64);
                     if constexpr (G == 4)
                         X += (uint32_t)__shfl_xor((int)X, 2, 64);
-                    // S16 = 16Σr² − 8X + ΣD4² ≤ 64·1020² < 2^31: exact in int32
+                    // S16 = 16Σr² − 8X + ΣD4² ≤ 64·1020² < 2^27: exact in int32, ×8 fits u32
                     const int32_t s16 = 16 * sr2 - 8 * (int32_t)X - nsd2[u];
-                    const unsigned long long key = (int64_t)s16 <= a.hitH
-                                                       ? key_hit(pp[u], (uint32_t)t)
-                                                       : key_miss((uint64_t)s16, pp[u], (uint32_t)(T - 1 - t));
-                    if (have[u] && key < lk)
-                        lk = key;
+                    m = min(m, ((uint32_t)s16 << 3) | (uint32_t)(T - 1 - t));
+                    if ((int64_t)s16 <= a.hitH && hitt == (uint32_t)T)
+                        hitt = (uint32_t)t;
                 }
+                const unsigned long long key = hitt < (uint32_t)T ? key_hit(pp[u], hitt)
+                                                                  : key_miss(m >> 3, pp[u], m & 7u);
+                if (have[u] && key < lk)
+                    lk = key;
+            }
         }
         __builtin_amdgcn_wave_barrier();
 #pragma unroll
@@ -313,17 +341,26 @@ __global__ void __launch_bounds__(256) sea_search(SeaArgs a)
         Rt = R1;
         // a side closes once the mean term alone exceeds the bound (ΣD4 is monotone along it)
         const double dl = (double)(SR - (int64_t)sdl), dr = (double)((int64_t)sdr - SR);
-        lopen = L > seg.x && dl * dl / (double)NN <= bound + 0.5;
-        ropen = Rt < seg.y && dr * dr / (double)NN <= bound + 0.5;
-        plan(64u, nl, nrt);
+        lopen = L > seg.x && dl * dl * (1.0 / NN) <= bound + 0.5;
+        ropen = Rt < seg.y && dr * dr * (1.0 / NN) <= bound + 0.5;
+        plan(kSeaStep, L, Rt, lopen, ropen, nl, nrt);
         if (nl == snl && nrt == snr) { // the usual case: the prefetch was the right window
-            idx = nidx;
-            valid = nvalid;
-            e = ne;
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                e[u] = ne[u];
+                en[u] = nen[u];
+                ix[u] = nix[u];
+                ev[u] = nev[u];
+            }
         } else {
-            idx = (uint32_t)lane < nl ? L - nl + (uint32_t)lane : Rt + ((uint32_t)lane - nl);
-            valid = (uint32_t)lane < nl + nrt;
-            e = valid ? a.ent[idx] : SeaEntry{0.0, 0u, 0u};
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const uint32_t k = (uint32_t)lane + 64u * u;
+                ev[u] = k < nl + nrt;
+                ix[u] = ev[u] ? slot(k, L, Rt, nl) : seg.x;
+                e[u] = a.ent[ix[u]];
+                en[u] = a.snegsd2[ix[u]];
+            }
         }
     }
     if (lane == 0) {
