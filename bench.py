@@ -6,7 +6,7 @@ Workload (BASELINE.json configs[2]): one 4096×4096 grayscale 
 (261,121), the reference's 4 transforms, exhaustive (no classifier), rms threshold 0.
 A step = one full search of the frame's ranges already resident in HBM: domain-pool
 build, search, winner fit, fp32 fallback and — for N > 1 — the RCCL all-gather of the
-64-byte winner records.  Ranges are sharded contiguously over ranks (fixed total work:
+32-byte (domain, transform, s, o, rms) winner tuples.  Ranges are sharded contiguously over ranks (fixed total work:
 strong scaling).
 
 Run:  python bench.py [--gpus N] [--steps K] [--warmup W] [--engine valu|mfma|auto]
@@ -88,7 +88,7 @@ def main():
     import torch.distributed as dist
 
     import fractencode_amd as F
-    from fractencode_amd.distributed import RECORD_BYTES, gather_records, shard_bounds, shard_capacity
+    from fractencode_amd.distributed import TUPLE_BYTES, gather_tuples, shard_bounds, shard_capacity
     from fractencode_amd.synth import value_noise
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -122,13 +122,13 @@ def main():
     eng.set_frame(d_frame)
     eng.set_domains(doms)
     eng.set_ranges(mine)
-    mine_bytes = torch.zeros(per * RECORD_BYTES, dtype=torch.uint8, device=dev)
+    mine_bytes = torch.zeros(per * TUPLE_BYTES, dtype=torch.uint8, device=dev)
 
     def step():
         eng.run()
-        if world > 1:  # RCCL all-gather of the 64-byte winner records (same stream)
-            eng.copy_results_device(mine_bytes.data_ptr())
-            gather_records(mine_bytes, nr_total, world)
+        if world > 1:  # RCCL all-gather of the 32-byte (domain, t, s, o, rms) tuples (same stream)
+            eng.copy_tuples_device(mine_bytes.data_ptr())
+            gather_tuples(mine_bytes, nr_total, world)
 
     for _ in range(args.warmup):
         step()

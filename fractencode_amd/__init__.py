@@ -27,7 +27,11 @@ ENCODE_ITEM = np.dtype([("x", "<u4"), ("y", "<u4"), ("w", "<u4"), ("h", "<u4"),
                         ("distance", "<f8"), ("contrast", "<f8"), ("brightness", "<f8"),
                         ("transform", "<i4"), ("_pad", "<i4"),
                         ("dx", "<u4"), ("dy", "<u4"), ("sw", "<u4"), ("sh", "<u4")])
-assert GRID_ITEM.itemsize == 20 and ENCODE_ITEM.itemsize == 64
+# frac_tuple: (domain index, transform, s, o, rms) — the 32-byte record of the multi-GPU gather
+TUPLE = np.dtype([("domain", "<u4"), ("transform", "<i4"), ("contrast", "<f8"), ("brightness", "<f8"),
+                  ("distance", "<f8")])
+NO_DOMAIN = 0xFFFFFFFF
+assert GRID_ITEM.itemsize == 20 and ENCODE_ITEM.itemsize == 64 and TUPLE.itemsize == 32
 
 ENGINE_AUTO, ENGINE_VALU, ENGINE_MFMA, ENGINE_SEA = 0, 1, 2, 3
 FORM_DOT2, FORM_DIRECT, FORM_FOURIER, FORM_SEA = 0, 1, 2, 3
@@ -101,6 +105,8 @@ def lib() -> C.CDLL:
             "frac_get_stream": (vp, [vp]),
             "frac_device_results": (vp, [vp]),
             "frac_copy_results_device": (i32, [vp, vp]),
+            "frac_copy_tuples_device": (i32, [vp, vp]),
+            "frac_fetch_tuples": (i32, [vp, vp]),
             "frac_decode": (i32, [vp, vp, sz, u32, u32, i32, C.c_double, vp, C.POINTER(C.c_int),
                                   C.POINTER(C.c_double)]),
             "frac_decode_results": (i32, [vp, u32, u32, i32, C.c_double, vp, C.POINTER(C.c_int),
@@ -265,6 +271,18 @@ class Engine:
     def copy_results_device(self, dst_ptr: int) -> None:
         """Async D2D copy of the last run's results (64 B each) to a device buffer."""
         self._check(lib().frac_copy_results_device(self._ctx, C.c_void_p(dst_ptr)))
+
+    def copy_tuples_device(self, dst_ptr: int) -> None:
+        """Async pack of the last run's 32-byte (domain, transform, s, o, rms) tuples into a device buffer."""
+        self._check(lib().frac_copy_tuples_device(self._ctx, C.c_void_p(dst_ptr)))
+
+    def fetch_tuples(self) -> np.ndarray:
+        """The last run's tuples (TUPLE records) on the host."""
+        n = self._nr
+        out = np.zeros(n, dtype=TUPLE)
+        if n:
+            self._check(lib().frac_fetch_tuples(self._ctx, out.ctypes.data_as(C.c_void_p)))
+        return out
 
     def decode(self, items: np.ndarray | None, width: int, height: int, max_iter: int = -1, rms_eps: float = 1e-5,
                initial: np.ndarray | None = None):

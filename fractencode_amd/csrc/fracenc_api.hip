@@ -194,6 +194,7 @@ struct frac_ctx {
         d_sea_rord2, d_sea_bend, d_sea_spool;
     DBuf<SeaEntry> d_sea_ent;
     DBuf<int32_t> d_sea_snegsd2;
+    DBuf<frac_tuple> d_tuples; // frac_fetch_tuples staging
     DBuf<uint8_t> d_sea_tmp;
     DBuf<unsigned long long> d_sea_count; // candidates the SEA search evaluated
     uint64_t eligible_pairs = 0;          // Σ over ranges of its bucket's domain count
@@ -1114,6 +1115,7 @@ void frac_destroy(frac_ctx* c)
     c->d_sea_spool.release();
     c->d_sea_count.release();
     c->d_sea_snegsd2.release();
+    c->d_tuples.release();
     c->d_sea_ent.release();
     c->d_sea_tmp.release();
     c->d_m_entries.release();
@@ -1699,6 +1701,42 @@ int frac_decode_results(frac_ctx* c, uint32_t w, uint32_t h, int max_iter, doubl
             }
     }
     return decode_impl(c, c->d_out.ptr, c->ranges.size(), w, h, max_iter, rms_eps, plane, iterations, rms, fused);
+}
+
+int frac_copy_tuples_device(frac_ctx* c, void* d_dst)
+{
+    if (!c)
+        return FRAC_E_INVALID;
+    if (!c->ran)
+        return c->fail(FRAC_E_STATE, "no results: frac_run has not been called");
+    const uint32_t nr = (uint32_t)c->ranges.size();
+    if (nr) {
+        if (!d_dst)
+            return c->fail(FRAC_E_INVALID, "copy_tuples: NULL destination");
+        FRAC_HIP(c, hipSetDevice(c->device));
+        pack_tuples<<<(nr + 255) / 256, 256, 0, c->stream>>>(c->d_out.ptr, c->d_aux.ptr, c->d_porig.ptr, nr,
+                                                             static_cast<frac_tuple*>(d_dst));
+        FRAC_HIP(c, hipGetLastError());
+    }
+    return FRAC_OK;
+}
+
+int frac_fetch_tuples(frac_ctx* c, frac_tuple* out)
+{
+    if (!c)
+        return FRAC_E_INVALID;
+    if (!c->ran)
+        return c->fail(FRAC_E_STATE, "no results: frac_run has not been called");
+    const size_t nr = c->ranges.size();
+    if (!nr)
+        return FRAC_OK;
+    if (!out)
+        return c->fail(FRAC_E_INVALID, "fetch_tuples: NULL destination");
+    FRAC_HIP(c, c->d_tuples.ensure(nr));
+    FRAC_TRY(frac_copy_tuples_device(c, c->d_tuples.ptr));
+    FRAC_HIP(c, hipMemcpyAsync(out, c->d_tuples.ptr, nr * sizeof(frac_tuple), hipMemcpyDeviceToHost, c->stream));
+    FRAC_HIP(c, hipStreamSynchronize(c->stream));
+    return FRAC_OK;
 }
 
 int frac_copy_results_device(frac_ctx* c, void* d_dst)

@@ -492,4 +492,27 @@ __global__ void __launch_bounds__(256) fallback_fp32(FallbackArgs a)
     }
 }
 
+// ---------------------------------------------------------------------------
+// pack_tuples: 64-byte results → 32-byte (domain index, transform, s, o, rms) tuples for
+// the multi-GPU gather.  One thread per range.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) pack_tuples(const frac_encode_item* __restrict__ out,
+                                                   const RangeAux* __restrict__ aux,
+                                                   const uint32_t* __restrict__ porig, uint32_t nr,
+                                                   frac_tuple* __restrict__ dst)
+{
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= nr)
+        return;
+    const frac_encode_item o = out[r];
+    const RangeAux x = aux[r];
+    frac_tuple t;
+    t.domain = (x.flags & kAuxEmpty) ? FRAC_NO_DOMAIN : porig[x.pos];
+    t.transform = o.match.score.transform;
+    t.contrast = o.match.score.contrast;
+    t.brightness = o.match.score.brightness;
+    t.distance = o.match.score.distance;
+    dst[r] = t;
+}
+
 } // namespace fracenc

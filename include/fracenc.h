@@ -155,6 +155,23 @@ const frac_encode_item* frac_device_results(frac_ctx* ctx);
  * (ordered on the context's stream). */
 int frac_copy_results_device(frac_ctx* ctx, void* d_dst);
 
+/* The winner of one range as north_star's multi-GPU gather names it — (domain, transform,
+ * s, o, rms) — in 32 bytes instead of the 64-byte encode_item_t: the range geometry is
+ * known to every rank and the domain's origin and size follow from its index.
+ * domain = index into the list given to frac_set_domains; FRAC_NO_DOMAIN when no domain
+ * was eligible (the default record of encode/datatypes.h:8-26). */
+#define FRAC_NO_DOMAIN 0xffffffffu
+typedef struct frac_tuple {
+    uint32_t domain;
+    int32_t transform;
+    double contrast, brightness, distance;
+} frac_tuple;
+/* Asynchronous: pack the last run's nr tuples into d_dst (device memory, 32·nr bytes) on
+ * the context's stream. */
+int frac_copy_tuples_device(frac_ctx* ctx, void* d_dst);
+/* Synchronous: the last run's nr tuples into host memory. */
+int frac_fetch_tuples(frac_ctx* ctx, frac_tuple* out);
+
 /* Decoder2::decode (encode/Encoder2.hpp:67-99) on the device.  `plane` (w×h, row
  * stride w) holds the decoder's initial target (main.cpp:171-173 zero-fills it) and
  * receives the decoded image; the source starts filled with 100.  Items must not

@@ -161,6 +161,11 @@ def test_edge_cases(oracle, engine):
         e.set_frame(p)
         e.set_domains(doms)
         out, st = e.search(rg)
+        # the 32-byte gather tuples rebuild the same records, default records included
+        from fractencode_amd.distributed import records_from_tuples
+        tup = e.fetch_tuples()
+        assert (tup["domain"] == F.NO_DOMAIN).sum() == st["empty_ranges"]
+        assert records_from_tuples(tup, rg, doms).tobytes() == out.tobytes()
     want, rej, _ = oracle.estimate(p, doms, rg, use_classifier=True)
     assert_same(out, {k: want[k] for k in FIELDS}, "empty bucket")
     assert st["rejected_mappings"] == rej and st["empty_ranges"] > 0

@@ -1,5 +1,5 @@
 """N>1 path on CPU: world-size-2 `gloo` ranks shard the ranges, search their slice and
-all-gather the 64-byte records (fractencode_amd.distributed).  The per-rank search
+all-gather the 32-byte (domain, transform, s, o, rms) tuples (fractencode_amd.distributed).  The per-rank search
 here is the oracle behind the engine interface (no GPU in this container); on the
 GPU box bench.py runs the same functions over RCCL with the HIP engine."""
 import ctypes as C
@@ -25,11 +25,12 @@ def test_shard_bounds_cover_all_items_once():
 
 
 class OracleEngine:
-    """Engine-interface stand-in (CPU): set_ranges / run / copy_results_device / sync."""
+    """Engine-interface stand-in (CPU): set_ranges / run / fetch_tuples / sync."""
 
     def __init__(self, plane, doms):
         from oracle import oracle as O
         self.O, self.plane, self.doms = O, plane, doms
+        self.index = {(int(d["x"]), int(d["y"])): i for i, d in enumerate(doms)}
 
     def set_ranges(self, r):
         self.r = r
@@ -43,11 +44,14 @@ class OracleEngine:
         rec["transform"], rec["dx"], rec["dy"], rec["sw"], rec["sh"] = out["t"], out["dx"], out["dy"], out["dw"], out["dh"]
         self.rec = rec
 
-    def copy_results_device(self, ptr):
-        C.memmove(ptr, self.rec.ctypes.data, self.rec.nbytes)
-
-    def fetch(self):
-        return self.rec, {}
+    def fetch_tuples(self):
+        import fractencode_amd as F
+        t = np.zeros(len(self.rec), dtype=F.TUPLE)
+        for k in ("transform", "contrast", "brightness", "distance"):
+            t[k] = self.rec[k]
+        t["domain"] = [self.index[(int(x), int(y))] if w else F.NO_DOMAIN
+                       for x, y, w in zip(self.rec["dx"], self.rec["dy"], self.rec["sw"])]
+        return t
 
     def sync(self):
         pass
@@ -68,7 +72,7 @@ def _worker(rank, world, port, path):
     plane = rng.integers(0, 256, (64, 96), dtype=np.uint8)
     doms = F.create_uniform_grid(96, 64, 16, 8)
     rngs = F.create_uniform_grid(96, 64, 8, 8)[:93]  # ragged: not a multiple of the world size
-    full = encode_sharded(OracleEngine(plane, doms), rngs, rank, world)
+    full = encode_sharded(OracleEngine(plane, doms), rngs, doms, rank, world)
     if rank == 0:
         np.save(path, full)
     dist.barrier()
@@ -114,10 +118,11 @@ def _gpu_worker(rank, world, port, path):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     y = np.fromfile(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "lenna_y.u8"),
                     dtype=np.uint8).reshape(512, 512)
+    doms = F.create_uniform_grid(512, 512, 16, 8)
     with F.Engine(0, 4) as e:  # every rank's engine on GPU 0 (one-GPU box)
         e.set_frame(y)
-        e.set_domains(F.create_uniform_grid(512, 512, 16, 8))
-        full = encode_sharded(e, F.create_uniform_grid(512, 512, 8, 8), rank, world)
+        e.set_domains(doms)
+        full = encode_sharded(e, F.create_uniform_grid(512, 512, 8, 8), doms, rank, world)
     if rank == 0:
         np.save(path, full)
     dist.barrier()
