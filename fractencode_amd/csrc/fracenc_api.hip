@@ -451,7 +451,8 @@ int prepare(frac_ctx* c)
         // work items: groups of up to BPW blocks of one bucket × splits of its tiles, plus the
         // CSR map block → entry bases (work·BPW + wave) the resolve kernels read
         auto build_work = [&](uint32_t bpw, size_t target_wgs, std::vector<uint4>& work,
-                              std::vector<uint32_t>& blk_ptr, std::vector<uint32_t>& blk_ent) {
+                              std::vector<uint32_t>& blk_ptr, std::vector<uint32_t>& blk_ent, bool xcd_order) {
+            std::vector<uint32_t> split_of; // domain split of each work item
             size_t groups = 0;
             for (int b = 0; b < nb; ++b)
                 if (tile_count[b])
@@ -472,10 +473,62 @@ int prepare(frac_ctx* c)
                             continue;
                         const uint32_t w = (uint32_t)work.size();
                         work.push_back(make_uint4(blk_first[b] + g, nbk, t0, t1));
+                        split_of.push_back((uint32_t)sp);
                         for (uint32_t k = 0; k < nbk; ++k)
                             blk_list[blk_first[b] + g + k].push_back(w * bpw + k);
                     }
                 }
+            }
+            if (xcd_order && !work.empty()) {
+                // XCD-aware order: workgroup n runs on XCD n % 8 (dispatch round-robin), so the
+                // items of one domain split go to the same XCDs and their in-flight workgroups
+                // stream the same tiles through that XCD's L2 together
+                constexpr uint32_t kXcd = 8;
+                std::vector<std::vector<uint32_t>> q(kXcd);
+                uint32_t S = 0;
+                for (uint32_t sp : split_of)
+                    S = std::max(S, sp + 1);
+                // split s → XCDs x ≡ s (mod S) when S ≤ 8 (round-robin over them), else XCD s mod 8
+                std::vector<uint32_t> rr(S, 0);
+                for (uint32_t w = 0; w < (uint32_t)work.size(); ++w) {
+                    const uint32_t sp = split_of[w];
+                    uint32_t x = sp % kXcd;
+                    if (S <= kXcd) {
+                        const uint32_t nx = (kXcd - 1 - sp) / S + 1; // XCDs sp, sp + S, ... below 8
+                        x = sp + S * (rr[sp]++ % nx);
+                    }
+                    q[x].push_back(w);
+                }
+                std::vector<uint32_t> order;
+                order.reserve(work.size());
+                std::vector<size_t> head(kXcd, 0);
+                while (order.size() < work.size()) {
+                    bool any = false;
+                    for (uint32_t x = 0; x < kXcd; ++x)
+                        if (head[x] < q[x].size()) {
+                            order.push_back(q[x][head[x]++]);
+                            any = true;
+                        } else { // an empty queue: keep the slot's XCD busy with another split
+                            for (uint32_t y = 0; y < kXcd; ++y)
+                                if (head[y] < q[y].size()) {
+                                    order.push_back(q[y][head[y]++]);
+                                    any = true;
+                                    break;
+                                }
+                        }
+                    if (!any)
+                        break;
+                }
+                std::vector<uint32_t> inv(work.size());
+                std::vector<uint4> nw(work.size());
+                for (uint32_t n = 0; n < (uint32_t)order.size(); ++n) {
+                    nw[n] = work[order[n]];
+                    inv[order[n]] = n;
+                }
+                work.swap(nw);
+                for (auto& lst : blk_list)
+                    for (uint32_t& e : lst)
+                        e = inv[e / bpw] * bpw + e % bpw;
             }
             blk_ptr.assign(c->nblocks + 1, 0);
             blk_ent.clear();
@@ -485,12 +538,14 @@ int prepare(frac_ctx* c)
             }
             blk_ptr[c->nblocks] = (uint32_t)blk_ent.size();
         };
-        build_work(4, 8192, c->m_work, c->m_blk_ptr, c->m_blk_ent);
+        build_work(4, 8192, c->m_work, c->m_blk_ptr, c->m_blk_ent, false);
         if (n == 8 && c->p.transforms == 4) {
             // FRAC_DFT_WGS (tuning knob): target workgroup count of the Fourier search
             const char* tw = getenv("FRAC_DFT_WGS");
             const size_t wgs = tw ? (size_t)std::max(1, atoi(tw)) : 8192 / kDftBlocksPerWG * 4;
-            build_work(kDftBlocksPerWG, wgs, c->m8_work, c->m8_blk_ptr, c->m8_blk_ent);
+            // FRAC_XCD_ORDER (tuning knob): 0 = work items in (block group, split) order
+            const char* xo = getenv("FRAC_XCD_ORDER");
+            build_work(kDftBlocksPerWG, wgs, c->m8_work, c->m8_blk_ptr, c->m8_blk_ent, xo ? atoi(xo) != 0 : true);
         }
         else {
             c->m8_work.clear();
