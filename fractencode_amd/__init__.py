@@ -307,12 +307,15 @@ class Engine:
         qp = FracQuadtreeParams(max_size, min_size, split_distance)
         n = C.c_size_t(0)
         st = FracStats()
-        # one pass with a worst-case capacity: every range at min_size
+        # one pass with a worst-case capacity (every range at min_size), in a buffer kept across
+        # calls: a fresh one costs a page fault per 4 KiB on first touch
         W, H = self._frame_wh
-        cap = (W // min_size) * (H // min_size)
-        out = np.zeros(max(cap, 1), dtype=ENCODE_ITEM)
-        self._check(lib().frac_encode_quadtree(self._ctx, C.byref(qp), out.ctypes.data, cap, C.byref(n), C.byref(st)))
-        return out[: n.value].copy(), st.as_dict()
+        cap = max((W // min_size) * (H // min_size), 1)
+        buf = getattr(self, "_qt_buf", None)
+        if buf is None or len(buf) < cap:
+            buf = self._qt_buf = np.empty(cap, dtype=ENCODE_ITEM)
+        self._check(lib().frac_encode_quadtree(self._ctx, C.byref(qp), buf.ctypes.data, cap, C.byref(n), C.byref(st)))
+        return buf[: n.value].copy(), st.as_dict()
 
     def classify(self, items: np.ndarray, target_plane: bool = False) -> np.ndarray:
         """BrightnessBlocksClassifier2 categories of `items` computed on the device plane set by

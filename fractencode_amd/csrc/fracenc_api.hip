@@ -7,6 +7,8 @@
 //   rejected-mapping count encode/TransformEstimator2.hpp:43-45,59 (derived from the winner)
 //   search order / ties    encode/TransformEstimator2.hpp:29-48
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -195,6 +197,7 @@ struct frac_ctx {
     DBuf<SeaEntry> d_sea_ent;
     DBuf<int32_t> d_sea_snegsd2;
     DBuf<frac_tuple> d_tuples; // frac_fetch_tuples staging
+    std::vector<frac_encode_item> qt_res; // quadtree: one level's results (kept: no page faults per call)
     DBuf<uint8_t> d_sea_tmp;
     DBuf<unsigned long long> d_sea_count; // candidates the SEA search evaluated
     uint64_t eligible_pairs = 0;          // Σ over ranges of its bucket's domain count
@@ -252,6 +255,27 @@ int check_params(const frac_params* p, std::string& msg)
     return FRAC_OK;
 }
 
+// FRAC_TRACE=1: host wall-clock of the preparation and quadtree phases on stderr (tuning aid)
+struct HostTrace {
+    bool on;
+    const char* what;
+    std::chrono::steady_clock::time_point t0, t;
+    explicit HostTrace(const char* w) : on(getenv("FRAC_TRACE") != nullptr), what(w)
+    {
+        t0 = t = std::chrono::steady_clock::now();
+    }
+    void mark(const char* phase)
+    {
+        if (!on)
+            return;
+        const auto now = std::chrono::steady_clock::now();
+        fprintf(stderr, "[frac %s] %-22s %8.3f ms (total %8.3f)\n", what, phase,
+                std::chrono::duration<double, std::milli>(now - t).count(),
+                std::chrono::duration<double, std::milli>(now - t0).count());
+        t = now;
+    }
+};
+
 // Categories of items[list[k]] on the device plane (classify_items); synchronous.
 int classify_on_device(frac_ctx* c, const std::vector<frac_grid_item>& items, const std::vector<uint32_t>& list,
                        const uint8_t* dplane, uint32_t dstride, std::vector<int32_t>& out)
@@ -259,6 +283,7 @@ int classify_on_device(frac_ctx* c, const std::vector<frac_grid_item>& items, co
     out.assign(list.size(), -1);
     if (list.empty())
         return FRAC_OK;
+    HostTrace tr("classify");
     FRAC_HIP(c, c->d_cls_items.ensure(items.size()));
     FRAC_HIP(c, c->d_cls_list.ensure(list.size()));
     FRAC_HIP(c, c->d_cls_out.ensure(list.size()));
@@ -273,11 +298,14 @@ int classify_on_device(frac_ctx* c, const std::vector<frac_grid_item>& items, co
     a.list = c->d_cls_list.ptr;
     a.n = (uint32_t)list.size();
     a.out = c->d_cls_out.ptr;
+    tr.mark("alloc + H2D");
     classify_items<<<(unsigned)((list.size() + 3) / 4), 256, 0, c->stream>>>(a);
     FRAC_HIP(c, hipGetLastError());
+    tr.mark("launch");
     FRAC_HIP(c, hipMemcpyAsync(out.data(), c->d_cls_out.ptr, list.size() * sizeof(int32_t), hipMemcpyDeviceToHost,
                                c->stream));
     FRAC_HIP(c, hipStreamSynchronize(c->stream));
+    tr.mark("D2H + sync");
     return FRAC_OK;
 }
 
@@ -292,6 +320,7 @@ int upload_plane(frac_ctx* c, const HostPlane& hp, DBuf<uint8_t>& d, uint32_t& d
 
 int prepare(frac_ctx* c)
 {
+    HostTrace tr("prepare");
     if (!c->planes_set || !c->doms_set || !c->ranges_set)
         return c->fail(FRAC_E_STATE, "planes, domains and ranges must be set before frac_run");
     const uint32_t T = c->p.transforms;
@@ -318,6 +347,7 @@ int prepare(frac_ctx* c)
     c->G = n == 16 ? 1u : (n <= 4 ? T : 4u);
     c->NG = T / c->G;
 
+    tr.mark("validate");
     // buckets: category + 1 (0 = category −1) with the classifier, a single bucket without
     const int nb = c->p.use_classifier ? 7 : 1;
     std::vector<int32_t> dbk(c->doms.size(), 0);
@@ -351,17 +381,25 @@ int prepare(frac_ctx* c)
             if (c->range_bucket[i] < 0 || c->range_bucket[i] >= nb)
                 return c->fail(FRAC_E_INVALID, "range category outside -1..5");
     }
-    c->bucket_begin.assign(nb, 0);
-    c->bucket_end.assign(nb, 0);
-    c->porig.clear();
-    c->porig.reserve(c->doms.size());
-    for (int b = 0; b < nb; ++b) {
-        c->bucket_begin[b] = (uint32_t)c->porig.size();
-        for (size_t i = 0; i < c->doms.size(); ++i)
-            if (dbk[i] == b)
-                c->porig.push_back((uint32_t)i);
-        c->bucket_end[b] = (uint32_t)c->porig.size();
-    }
+    tr.mark("classify");
+    // stable counting sort of item indices by bucket: order[beg[b] .. beg[b + 1]) = bucket b
+    auto bucket_order = [nb](const std::vector<int32_t>& key, std::vector<uint32_t>& order,
+                             std::vector<uint32_t>& beg) {
+        beg.assign(nb + 1, 0);
+        for (int32_t k : key)
+            ++beg[k + 1];
+        for (int b = 0; b < nb; ++b)
+            beg[b + 1] += beg[b];
+        order.resize(key.size());
+        std::vector<uint32_t> pos(beg.begin(), beg.end() - 1);
+        for (size_t i = 0; i < key.size(); ++i)
+            order[pos[key[i]]++] = (uint32_t)i;
+    };
+    std::vector<uint32_t> dbeg, rord, rbeg;
+    bucket_order(dbk, c->porig, dbeg);
+    bucket_order(c->range_bucket, rord, rbeg);
+    c->bucket_begin.assign(dbeg.begin(), dbeg.end() - 1);
+    c->bucket_end.assign(dbeg.begin() + 1, dbeg.end());
     c->rbucket.resize(c->ranges.size());
     for (size_t i = 0; i < c->ranges.size(); ++i) {
         const int b = c->range_bucket[i];
@@ -373,9 +411,8 @@ int prepare(frac_ctx* c)
     std::vector<std::pair<uint32_t, int>> blocks; // (slot base, bucket)
     for (int b = 0; b < nb; ++b) {
         const uint32_t base = (uint32_t)c->slot_range.size();
-        for (size_t i = 0; i < c->ranges.size(); ++i)
-            if (c->range_bucket[i] == b)
-                c->slot_range.push_back((int32_t)i);
+        for (uint32_t k = rbeg[b]; k < rbeg[b + 1]; ++k)
+            c->slot_range.push_back((int32_t)rord[k]);
         const uint32_t cnt = (uint32_t)c->slot_range.size() - base;
         if (cnt == 0)
             continue;
@@ -406,6 +443,7 @@ int prepare(frac_ctx* c)
                     c->work.push_back(make_uint4(bl.first, pb, pe, g));
             }
     }
+    tr.mark("buckets + valu work");
     c->eligible_pairs = 0;
     for (size_t i = 0; i < c->ranges.size(); ++i)
         c->eligible_pairs += c->rbucket[i].y - c->rbucket[i].x;
@@ -427,11 +465,11 @@ int prepare(frac_ctx* c)
         std::vector<uint32_t> blk_first(nb, 0), blk_count(nb, 0);
         for (int b = 0; b < nb; ++b) {
             blk_first[b] = (uint32_t)(c->m_slot_range.size() / 32);
-            for (size_t i = 0; i < c->ranges.size(); ++i)
-                if (c->range_bucket[i] == b) {
-                    c->m_range_slot[i] = (uint32_t)c->m_slot_range.size();
-                    c->m_slot_range.push_back((int32_t)i);
-                }
+            for (uint32_t k = rbeg[b]; k < rbeg[b + 1]; ++k) {
+                const uint32_t i = rord[k];
+                c->m_range_slot[i] = (uint32_t)c->m_slot_range.size();
+                c->m_slot_range.push_back((int32_t)i);
+            }
             while (c->m_slot_range.size() % 32)
                 c->m_slot_range.push_back(-1);
             blk_count[b] = (uint32_t)(c->m_slot_range.size() / 32) - blk_first[b];
@@ -554,6 +592,7 @@ int prepare(frac_ctx* c)
         }
     }
 
+    tr.mark("engine work");
     const size_t nr = c->ranges.size(), P = c->porig.size();
     FRAC_HIP(c, c->d_doms.ensure(c->doms.size()));
     FRAC_HIP(c, c->d_ranges.ensure(nr));
@@ -640,6 +679,7 @@ int prepare(frac_ctx* c)
     }
     c->h_aux.resize(nr);
     c->dirty = false;
+    tr.mark("uploads");
     return FRAC_OK;
 }
 
@@ -1429,15 +1469,21 @@ int frac_encode_quadtree(frac_ctx* c, const frac_quadtree_params* qp, frac_encod
     };
     std::vector<frac_grid_item> pending = grid(qp->max_size, qp->max_size);
     std::vector<frac_encode_item> emitted;
+    emitted.reserve((size_t)(W / qp->min_size) * (H / qp->min_size));
     frac_stats total{};
+    HostTrace tr("quadtree");
     for (uint32_t n = qp->max_size; !pending.empty() && n >= qp->min_size; n /= 2) {
         const std::vector<frac_grid_item> doms = grid(2 * n, n);
         FRAC_TRY(frac_set_domains(c, doms.data(), doms.size()));
         FRAC_TRY(frac_set_ranges(c, pending.data(), pending.size()));
+        tr.mark("grids");
         FRAC_TRY(frac_run(c));
-        std::vector<frac_encode_item> res(pending.size());
+        tr.mark("run (enqueue)");
+        c->qt_res.resize(pending.size());
+        std::vector<frac_encode_item>& res = c->qt_res;
         frac_stats st{};
         FRAC_TRY(frac_fetch(c, res.data(), &st));
+        tr.mark("fetch (sync)");
         total.rejected_mappings += st.rejected_mappings;
         total.total_mappings += st.total_mappings;
         total.hit_ranges += st.hit_ranges;
@@ -1465,6 +1511,7 @@ int frac_encode_quadtree(frac_ctx* c, const frac_quadtree_params* qp, frac_encod
             }
         }
         pending.swap(next);
+        tr.mark("split");
     }
     *n_out = emitted.size();
     if (out)
@@ -1601,7 +1648,8 @@ static int decode_fused_impl(frac_ctx* c, const frac_encode_item* d_items, size_
     FRAC_HIP(c, c->d_dec_src.ensure(bytes));
     FRAC_HIP(c, c->d_dec_tgt.ensure(bytes));
     const uint32_t nblk = (uint32_t)((n + 3) / 4);
-    FRAC_HIP(c, c->d_dec_part.ensure(std::max<uint32_t>(nblk, 1)));
+    FRAC_HIP(c, c->d_dec_part.ensure(kDecodeSlots));
+    FRAC_HIP(c, hipMemsetAsync(c->d_dec_part.ptr, 0, kDecodeSlots * sizeof(unsigned long long), c->stream));
     FRAC_HIP(c, c->d_dec_state.ensure(1));
     if (!c->h_dec_state)
         FRAC_HIP(c, hipHostMalloc(reinterpret_cast<void**>(&c->h_dec_state), sizeof(DecodeState)));
@@ -1622,8 +1670,8 @@ static int decode_fused_impl(frac_ctx* c, const frac_encode_item* d_items, size_
             a.src = buf[enq & 1];
             a.tgt = buf[(enq + 1) & 1];
             decode_fused<<<nblk, 256, 0, c->stream>>>(a, c->d_dec_state.ptr, c->d_dec_part.ptr);
-            decode_check<<<1, 256, 0, c->stream>>>(c->d_dec_part.ptr, nblk, (uint64_t)w * h, eps, enq, iters - 1,
-                                                   c->d_dec_state.ptr);
+            decode_check<<<1, kDecodeSlots, 0, c->stream>>>(c->d_dec_part.ptr, (uint64_t)w * h, eps, enq, iters - 1,
+                                                            c->d_dec_state.ptr);
         }
         FRAC_HIP(c, hipMemcpyAsync(c->h_dec_state, c->d_dec_state.ptr, sizeof(DecodeState), hipMemcpyDeviceToHost,
                                    c->stream));

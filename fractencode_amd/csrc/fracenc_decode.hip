@@ -92,6 +92,8 @@ __global__ void __launch_bounds__(256) decode_rms(const uint8_t* __restrict__ sr
 // the host only checks a flag every few iterations.  After convergence the remaining
 // enqueued iterations exit at their first instruction.
 // ---------------------------------------------------------------------------
+constexpr uint32_t kDecodeSlots = 256; // partial-sum slots between decode_fused and decode_check
+
 struct DecodeState {
     int32_t done;       // 1 once rms < eps
     int32_t iterations; // Decoder2's returned count
@@ -111,9 +113,11 @@ __global__ void __launch_bounds__(256) decode_fused(DecodeArgs a, const DecodeSt
         const uint32_t sw = e.match.sw, sh = e.match.sh;
         const double s = e.match.score.contrast, o = e.match.score.brightness;
         const int t = e.match.score.transform;
+        const bool pow2 = (e.w & (e.w - 1)) == 0, ratio2 = sw == 2 * e.w && sh == 2 * e.h;
+        const uint32_t lw = e.w ? (uint32_t)__builtin_ctz(e.w) : 0u; // log2(e.w) when pow2
         for (uint32_t q = lane; q < e.w * e.h; q += 64) {
-            const uint32_t x = q % e.w, y = q / e.w;
-            const uint32_t sx = (x * sw) / e.w, sy = (y * sh) / e.h;
+            const uint32_t x = pow2 ? q & (e.w - 1) : q % e.w, y = pow2 ? q >> lw : q / e.w;
+            const uint32_t sx = ratio2 ? 2 * x : (x * sw) / e.w, sy = ratio2 ? 2 * y : (y * sh) / e.h;
             const double smp = (double)sample_sum_dev(a.src, a.stride, e.match.x, e.match.y, sw, sh, sx, sy, t) / 4.0;
             const double v = __fma_rn(s, smp, o);
             const uint8_t nv = v < 0.0 ? 0 : v > 255 ? 255 : (uint8_t)v;
@@ -130,20 +134,20 @@ __global__ void __launch_bounds__(256) decode_fused(DecodeArgs a, const DecodeSt
     if (lane == 0)
         part[threadIdx.x >> 6] = acc;
     __syncthreads();
-    if (threadIdx.x == 0)
-        partial[blockIdx.x] = part[0] + part[1] + part[2] + part[3];
+    if (threadIdx.x == 0) // 256 accumulation slots: one load per thread in decode_check
+        atomicAdd(&partial[blockIdx.x & (kDecodeSlots - 1)], part[0] + part[1] + part[2] + part[3]);
 }
 
-// one block: Σ partials → rms of step `step` exactly as the reference (int32 sum / area)
-__global__ void __launch_bounds__(256) decode_check(const unsigned long long* __restrict__ partial, uint32_t nparts,
-                                                    uint64_t area, double eps, int32_t step, int32_t last_step,
-                                                    DecodeState* __restrict__ st)
+// one block: Σ of the kDecodeSlots partial slots (re-zeroed for the next step) → rms of step
+// `step` exactly as the reference (int32 sum / area)
+__global__ void __launch_bounds__(kDecodeSlots) decode_check(unsigned long long* __restrict__ partial,
+                                                             uint64_t area, double eps, int32_t step,
+                                                             int32_t last_step, DecodeState* __restrict__ st)
 {
     if (st->done)
         return;
-    unsigned long long acc = 0;
-    for (uint32_t i = threadIdx.x; i < nparts; i += 256)
-        acc += partial[i];
+    unsigned long long acc = partial[threadIdx.x];
+    partial[threadIdx.x] = 0;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1)
         acc += __shfl_xor(acc, o, 64);

@@ -460,43 +460,55 @@ __global__ void __launch_bounds__(256) resolve_mfma(MfmaResolveArgs a)
     // hits: the sentinel 0 (kernel run with H > 0), or a best error that meets H = 0
     const bool hit = a.hitH >= 0 && (vmin == 0 || target <= a.hitH);
     unsigned long long bestk = kKeyNone;
-    for (uint32_t j = 0; j < nent; ++j) { // wave-uniform loop over entries
-        const uint32_t e = e0 + j / (2u * a.T), t = (j >> 1) % a.T, h = j & 1u;
-        const uint2 en = a.entries[((size_t)a.blk_ent[e] * a.T + t) * 64 + col + 32 * h];
-        if (en.x != vmin)
-            continue;
-        const int row = (i & 3) + 8 * (i >> 2) + 4 * (int)h;
-        const Aff af = lut((int)t);
-        // the entry names the first tile of the chunk that attained the minimum: scan the
-        // chunk's tiles in order; the first matching row is the earliest domain
-        for (uint32_t tile = en.y; tile < min(en.y + (uint32_t)kTilesPerStage, a.ntiles); ++tile) {
-            const int p = a.tile_pos[tile * 32 + row];
-            int64_t X = 0;
-            if (p >= 0) {
-                const uint32_t* dp = a.pool + (size_t)p * (NN / 2);
+    // only the entries holding the minimum are re-evaluated: the lanes test 64 entries at a
+    // time and the wave walks the ballot of matches (the cost does not grow with the splits)
+    for (uint32_t c0 = 0; c0 < nent; c0 += 64) {
+        const uint32_t jl = c0 + (uint32_t)lane;
+        uint2 enl = make_uint2(0xffffffffu, 0u);
+        if (jl < nent) {
+            const uint32_t e = e0 + jl / (2u * a.T), t = (jl >> 1) % a.T, h = jl & 1u;
+            enl = a.entries[((size_t)a.blk_ent[e] * a.T + t) * 64 + col + 32 * h];
+        }
+        unsigned long long match = __ballot(jl < nent && enl.x == vmin);
+        while (match) {
+            const int src = __ffsll((long long)match) - 1;
+            match &= match - 1;
+            const uint32_t j = c0 + (uint32_t)src;
+            const uint32_t t = (j >> 1) % a.T, h = j & 1u;
+            const uint2 en = make_uint2(vmin, (uint32_t)__shfl((int)enl.y, src, 64));
+            const int row = (i & 3) + 8 * (i >> 2) + 4 * (int)h;
+            const Aff af = lut((int)t);
+            // the entry names the first tile of the chunk that attained the minimum: scan the
+            // chunk's tiles in order; the first matching row is the earliest domain
+            for (uint32_t tile = en.y; tile < min(en.y + (uint32_t)kTilesPerStage, a.ntiles); ++tile) {
+                const int p = a.tile_pos[tile * 32 + row];
+                int64_t X = 0;
+                if (p >= 0) {
+                    const uint32_t* dp = a.pool + (size_t)p * (NN / 2);
 #pragma unroll
-                for (int u = 0; u < PG; ++u) {
-                    const int q = g * PG + u;
-                    if (q < NN) {
-                        const int f = fwd_rt(af, N, q);
-                        const uint32_t w = dp[f >> 1];
-                        X += (int64_t)px[u] * (int64_t)((f & 1) ? (w >> 16) : (w & 0xffffu));
+                    for (int u = 0; u < PG; ++u) {
+                        const int q = g * PG + u;
+                        if (q < NN) {
+                            const int f = fwd_rt(af, N, q);
+                            const uint32_t w = dp[f >> 1];
+                            X += (int64_t)px[u] * (int64_t)((f & 1) ? (w >> 16) : (w & 0xffffu));
+                        }
                     }
                 }
-            }
-            X += __shfl_xor(X, 1, 64);
-            X += __shfl_xor(X, 2, 64);
-            const int64_t s16 = p >= 0 ? 16 * sr2 - 8 * X - (int64_t)a.negsd2[p] : 0;
-            const bool ok = p >= 0 && g == 0 && (hit ? (s16 <= a.hitH) : (s16 == target));
-            const unsigned long long mask = __ballot(ok);
-            if (mask) {
-                const int first = __ffsll((long long)mask) - 1; // lowest lane = lowest row of the half
-                const int64_t s16f = __shfl(s16, first, 64);
-                const int pf = __shfl(p, first, 64);
-                const unsigned long long k =
-                    hit ? key_hit((uint32_t)pf, t) : key_miss((uint64_t)s16f, (uint32_t)pf, a.T - 1 - t);
-                bestk = k < bestk ? k : bestk;
-                break;
+                X += __shfl_xor(X, 1, 64);
+                X += __shfl_xor(X, 2, 64);
+                const int64_t s16 = p >= 0 ? 16 * sr2 - 8 * X - (int64_t)a.negsd2[p] : 0;
+                const bool ok = p >= 0 && g == 0 && (hit ? (s16 <= a.hitH) : (s16 == target));
+                const unsigned long long mask = __ballot(ok);
+                if (mask) {
+                    const int first = __ffsll((long long)mask) - 1; // lowest lane = lowest row of the half
+                    const int64_t s16f = __shfl(s16, first, 64);
+                    const int pf = __shfl(p, first, 64);
+                    const unsigned long long k =
+                        hit ? key_hit((uint32_t)pf, t) : key_miss((uint64_t)s16f, (uint32_t)pf, a.T - 1 - t);
+                    bestk = k < bestk ? k : bestk;
+                    break;
+                }
             }
         }
     }

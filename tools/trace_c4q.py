@@ -1,0 +1,18 @@
+#!/usr/bin/env python3
+"""C4 quadtree encode with FRAC_TRACE=1 (host phase timings on stderr)."""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import fractencode_amd as F  # noqa: E402
+from fractencode_amd.synth import value_noise  # noqa: E402
+
+frame = value_noise(4096, 4096, 1234)[:2048, :2048].copy()
+split = float(sys.argv[1]) if len(sys.argv) > 1 else 0.05
+with F.Engine(0, 4, True, timing=True) as e:
+    e.set_frame(frame)
+    e.encode_quadtree(16, 4, split)
+    os.environ["FRAC_TRACE"] = "1"
+    for _ in range(2):
+        items, st = e.encode_quadtree(16, 4, split)
+    print("items", len(items), "ms_search", st["ms_search"], "ms_device", st["ms_device"], file=sys.stderr)
