@@ -106,6 +106,7 @@ def lib() -> C.CDLL:
             "frac_device_results": (vp, [vp]),
             "frac_copy_results_device": (i32, [vp, vp]),
             "frac_copy_tuples_device": (i32, [vp, vp]),
+            "frac_pack_frc1": (i32, [vp, u32, u32, vp, sz, C.POINTER(C.c_size_t)]),
             "frac_fetch_tuples": (i32, [vp, vp]),
             "frac_decode": (i32, [vp, vp, sz, u32, u32, i32, C.c_double, vp, C.POINTER(C.c_int),
                                   C.POINTER(C.c_double)]),
@@ -275,6 +276,16 @@ class Engine:
     def copy_tuples_device(self, dst_ptr: int) -> None:
         """Async pack of the last run's 32-byte (domain, transform, s, o, rms) tuples into a device buffer."""
         self._check(lib().frac_copy_tuples_device(self._ctx, C.c_void_p(dst_ptr)))
+
+    def pack_frc1(self, contrast_bits: int = 5, brightness_bits: int = 7) -> bytes:
+        """The last run's results as an FRC1 stream (codec.py layout), quantized and packed on the
+        device (frac_pack_frc1)."""
+        n = C.c_size_t(0)
+        self._check(lib().frac_pack_frc1(self._ctx, contrast_bits, brightness_bits, None, 0, C.byref(n)))
+        buf = np.empty(n.value, dtype=np.uint8)
+        self._check(lib().frac_pack_frc1(self._ctx, contrast_bits, brightness_bits, buf.ctypes.data_as(C.c_void_p),
+                                         n.value, C.byref(n)))
+        return buf.tobytes()
 
     def fetch_tuples(self) -> np.ndarray:
         """The last run's tuples (TUPLE records) on the host."""

@@ -23,6 +23,7 @@
 #include "fracenc_color.hip"
 #include "fracenc_classify.hip"
 #include "fracenc_sea.hip"
+#include "fracenc_stream.hip"
 
 using namespace fracenc;
 
@@ -197,6 +198,9 @@ struct frac_ctx {
     DBuf<SeaEntry> d_sea_ent;
     DBuf<int32_t> d_sea_snegsd2;
     DBuf<frac_tuple> d_tuples; // frac_fetch_tuples staging
+    DBuf<Frc1MinMax> d_frc_mm;             // frac_pack_frc1
+    DBuf<unsigned long long> d_frc_rec;
+    DBuf<uint32_t> d_frc_words;
     std::vector<frac_encode_item> qt_res; // quadtree: one level's results (kept: no page faults per call)
     DBuf<uint8_t> d_sea_tmp;
     DBuf<unsigned long long> d_sea_count; // candidates the SEA search evaluated
@@ -1211,6 +1215,9 @@ void frac_destroy(frac_ctx* c)
     c->d_sea_count.release();
     c->d_sea_snegsd2.release();
     c->d_tuples.release();
+    c->d_frc_mm.release();
+    c->d_frc_rec.release();
+    c->d_frc_words.release();
     c->d_sea_ent.release();
     c->d_sea_tmp.release();
     c->d_m_entries.release();
@@ -1821,6 +1828,104 @@ int frac_copy_tuples_device(frac_ctx* c, void* d_dst)
                                                              static_cast<frac_tuple*>(d_dst));
         FRAC_HIP(c, hipGetLastError());
     }
+    return FRAC_OK;
+}
+
+int frac_pack_frc1(frac_ctx* c, uint32_t cbits, uint32_t bbits, uint8_t* out, size_t cap, size_t* n_out)
+{
+    if (!c)
+        return FRAC_E_INVALID;
+    if (!n_out)
+        return c->fail(FRAC_E_INVALID, "pack_frc1: n_out is NULL");
+    if (!c->ran)
+        return c->fail(FRAC_E_STATE, "pack_frc1: frac_run has not been called");
+    if (cbits < 2 || cbits > 16 || bbits < 2 || bbits > 16)
+        return c->fail(FRAC_E_INVALID, "pack_frc1: contrast/brightness bits must be in [2, 16]");
+    const uint32_t W = c->tgt.w, H = c->tgt.h, n = (uint32_t)c->n;
+    if (c->src.w != W || c->src.h != H)
+        return c->fail(FRAC_E_INVALID, "pack_frc1: source and target planes must have one size");
+    // the stream's implicit geometry: createUniformGrid ranges (row-major) and domains
+    auto same_grid = [&](const std::vector<frac_grid_item>& g, uint32_t size, uint32_t off) {
+        const size_t cnt = frac_uniform_grid(W, H, size, off, nullptr, 0);
+        if (cnt != g.size())
+            return false;
+        std::vector<frac_grid_item> u(cnt);
+        if (cnt)
+            frac_uniform_grid(W, H, size, off, u.data(), cnt);
+        for (size_t i = 0; i < cnt; ++i)
+            if (u[i].x != g[i].x || u[i].y != g[i].y || u[i].w != g[i].w || u[i].h != g[i].h)
+                return false;
+        return true;
+    };
+    if (!same_grid(c->ranges, n, n))
+        return c->fail(FRAC_E_INVALID, "pack_frc1: ranges are not the row-major range grid");
+    if (!same_grid(c->doms, 2 * n, n))
+        return c->fail(FRAC_E_INVALID, "pack_frc1: domains are not the domain lattice (size 2n, stride n)");
+    const uint32_t nr = (uint32_t)c->ranges.size(), nd = (uint32_t)c->doms.size(), T = c->p.transforms;
+    auto bitlen = [](uint64_t v) { uint32_t b = 0; while (v) { ++b; v >>= 1; } return b; };
+    const uint32_t ib = std::max(1u, bitlen(nd)), tb = std::max(1u, bitlen(T - 1));
+    const uint32_t width = ib + tb + cbits + bbits;
+    if (width > 64)
+        return c->fail(FRAC_E_INVALID, "pack_frc1: record wider than 64 bits");
+    const uint64_t body = ((uint64_t)nr * width + 7) / 8, nwords = ((uint64_t)nr * width + 31) / 32;
+    *n_out = FRAC_FRC1_HEADER_BYTES + body;
+    if (!out)
+        return FRAC_OK;
+    FRAC_HIP(c, hipSetDevice(c->device));
+    Frc1MinMax mm{~0ull, 0ull, ~0ull, 0ull};
+    std::vector<uint32_t> words(nwords);
+    if (nr) {
+        FRAC_HIP(c, c->d_frc_mm.ensure(1));
+        FRAC_HIP(c, c->d_frc_rec.ensure(nr));
+        FRAC_HIP(c, c->d_frc_words.ensure(nwords));
+        FRAC_HIP(c, hipMemsetAsync(c->d_frc_mm.ptr, 0xff, sizeof(unsigned long long), c->stream));
+        FRAC_HIP(c, hipMemsetAsync(&c->d_frc_mm.ptr->cmax, 0, sizeof(unsigned long long), c->stream));
+        FRAC_HIP(c, hipMemsetAsync(&c->d_frc_mm.ptr->bmin, 0xff, sizeof(unsigned long long), c->stream));
+        FRAC_HIP(c, hipMemsetAsync(&c->d_frc_mm.ptr->bmax, 0, sizeof(unsigned long long), c->stream));
+        frc1_minmax<<<std::min<uint32_t>(1024, (nr + 255) / 256), 256, 0, c->stream>>>(c->d_out.ptr, nr,
+                                                                                          c->d_frc_mm.ptr);
+        Frc1Args a;
+        a.out = c->d_out.ptr;
+        a.n = nr;
+        a.dstride = n;
+        a.dcols = (uint32_t)((W - 2 * n) / n + 1);
+        a.ndomains = nd;
+        a.index_bits = ib;
+        a.t_bits = tb;
+        a.c_bits = cbits;
+        a.b_bits = bbits;
+        a.mm = c->d_frc_mm.ptr;
+        a.rec = c->d_frc_rec.ptr;
+        frc1_records<<<(nr + 255) / 256, 256, 0, c->stream>>>(a);
+        frc1_words<<<(unsigned)((nwords + 255) / 256), 256, 0, c->stream>>>(c->d_frc_rec.ptr, nr, width, nwords,
+                                                                             c->d_frc_words.ptr);
+        FRAC_HIP(c, hipGetLastError());
+        FRAC_HIP(c, hipMemcpyAsync(&mm, c->d_frc_mm.ptr, sizeof(mm), hipMemcpyDeviceToHost, c->stream));
+        FRAC_HIP(c, hipMemcpyAsync(words.data(), c->d_frc_words.ptr, nwords * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                                   c->stream));
+        FRAC_HIP(c, hipStreamSynchronize(c->stream));
+    }
+    // header "<4sHHIIIIIBBBBIIdddd" (fractencode_amd/codec.py)
+    uint8_t hdr[FRAC_FRC1_HEADER_BYTES] = {};
+    size_t o = 0;
+    auto put = [&](const void* v, size_t k) { std::memcpy(hdr + o, v, k); o += k; };
+    const uint16_t version = 1, flags = c->p.use_classifier ? 1 : 0;
+    const uint32_t u32s[5] = {W, H, n, 2 * n, n};
+    const uint8_t u8s[4] = {(uint8_t)T, (uint8_t)cbits, (uint8_t)bbits, (uint8_t)ib};
+    const uint32_t counts[2] = {nr, nd};
+    const double mm_d[4] = {nr ? dkey_inv(mm.cmin) : 0.0, nr ? dkey_inv(mm.cmax) : 0.0, nr ? dkey_inv(mm.bmin) : 0.0,
+                            nr ? dkey_inv(mm.bmax) : 0.0};
+    put("FRC1", 4);
+    put(&version, 2);
+    put(&flags, 2);
+    put(u32s, sizeof(u32s));
+    put(u8s, sizeof(u8s));
+    put(counts, sizeof(counts));
+    put(mm_d, sizeof(mm_d));
+    const size_t total = FRAC_FRC1_HEADER_BYTES + body;
+    std::memcpy(out, hdr, std::min<size_t>(cap, FRAC_FRC1_HEADER_BYTES));
+    if (cap > FRAC_FRC1_HEADER_BYTES)
+        std::memcpy(out + FRAC_FRC1_HEADER_BYTES, words.data(), std::min<size_t>(cap, total) - FRAC_FRC1_HEADER_BYTES);
     return FRAC_OK;
 }
 

@@ -221,6 +221,22 @@ int frac_rgb_to_yuv_device(frac_ctx* ctx, const void* d_rgb, uint32_t w, uint32_
 int frac_rgb_to_yuv(frac_ctx* ctx, const uint8_t* rgb, uint32_t w, uint32_t h, uint32_t rgb_stride, uint8_t* y,
                     uint8_t* u, uint8_t* v);
 
+/* ---- FRC1 quantized stream, packed on the device --------------------------
+ * The reference has no file format; encode_data_statistics (main.cpp:106-140) builds
+ * Frac::Quantizerd over the frame's (contrast, brightness) range with 5 / 7 bits
+ * (main.cpp:120-121).  FRC1 (fractencode_amd/codec.py documents the layout) stores per
+ * range (domain index, transform, q_contrast, q_brightness) bit-packed after a 72-byte
+ * header.  This packs the last run's results into it: min/max reductions, Quantizer codes
+ * (encode/Quantizer.hpp:7-45, FP64 as the reference) and the bit packing all run on the
+ * device; only the finished stream is copied out.  Requires the ranges to be the
+ * createUniformGrid(range_size, range_size) lattice in row-major order and the domains the
+ * createUniformGrid(2·range_size, range_size) lattice (the CLI's grids, main.cpp:147-152).
+ * contrast_bits, brightness_bits in [2, 16].  *n_out = stream size; writes min(cap, size)
+ * bytes (out may be NULL to query the size). */
+#define FRAC_FRC1_HEADER_BYTES 72
+int frac_pack_frc1(frac_ctx* ctx, uint32_t contrast_bits, uint32_t brightness_bits, uint8_t* out, size_t cap,
+                   size_t* n_out);
+
 /* ---- host helpers (no device needed) ------------------------------------ */
 /* createUniformGrid (image/partition2.hpp:109-135): returns the item count and
  * writes min(count, cap) items (categories -1). */

@@ -179,9 +179,16 @@ def main():
                 t0 = time.perf_counter()
                 buf = codec.pack_stream(out, 4096, 4096, 8)
                 sec = time.perf_counter() - t0
+                e.pack_frc1()
+                t0 = time.perf_counter()
+                for _ in range(args.steps):
+                    dbuf = e.pack_frc1()
+                dsec = (time.perf_counter() - t0) / args.steps
+                assert dbuf == buf
                 print(json.dumps({"path": "stream", "ranges": len(out), "bytes": len(buf),
                                   "bits_per_range": round(8 * (len(buf) - codec.HEADER.size) / len(out), 3),
-                                  "pack_ms_host": round(sec * 1e3, 2)}), flush=True)
+                                  "pack_ms_host": round(sec * 1e3, 2),
+                                  "pack_ms_device_incl_d2h": round(dsec * 1e3, 3)}), flush=True)
 
 
 if __name__ == "__main__":
