@@ -455,13 +455,12 @@ int prepare(frac_ctx* c)
     c->all_fallback = c->hitH >= kExactLimit;
 
     // engine: the MFMA encoding is exact for n <= 8 (|Σ(r−128)(D4−510)| < 2^22)
-    if (c->p.engine == FRAC_ENGINE_MFMA && n > 8)
-        return c->fail(FRAC_E_INVALID, "the MFMA engine supports range sizes 2, 4 and 8");
     if (c->p.engine == FRAC_ENGINE_SEA && n > 8)
         return c->fail(FRAC_E_INVALID, "the SEA engine supports range sizes 2, 4 and 8");
-    c->engine = (c->p.engine == FRAC_ENGINE_VALU || n > 8) ? FRAC_ENGINE_VALU
-                : c->p.engine == FRAC_ENGINE_SEA       ? FRAC_ENGINE_SEA
-                                                       : FRAC_ENGINE_MFMA;
+    // MFMA: exact for every supported n (n = 16 through search_mfma16's integer epilogue)
+    c->engine = c->p.engine == FRAC_ENGINE_VALU  ? FRAC_ENGINE_VALU
+                : c->p.engine == FRAC_ENGINE_SEA ? FRAC_ENGINE_SEA
+                                                 : FRAC_ENGINE_MFMA;
     if (c->engine == FRAC_ENGINE_MFMA) {
         // range blocks of 32 slots per bucket; domain tiles of 32 pool positions per bucket
         c->m_slot_range.clear();
@@ -580,7 +579,10 @@ int prepare(frac_ctx* c)
             }
             blk_ptr[c->nblocks] = (uint32_t)blk_ent.size();
         };
-        build_work(4, 8192, c->m_work, c->m_blk_ptr, c->m_blk_ent, false);
+        if (n == 16) // search_mfma16: one range block per workgroup (T waves)
+            build_work(1, 4096, c->m_work, c->m_blk_ptr, c->m_blk_ent, false);
+        else
+            build_work(4, 8192, c->m_work, c->m_blk_ptr, c->m_blk_ent, false);
         if (n == 8 && c->p.transforms == 4) {
             // FRAC_DFT_WGS (tuning knob): target workgroup count of the Fourier search
             const char* tw = getenv("FRAC_DFT_WGS");
@@ -913,7 +915,21 @@ int launch_mfma(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride)
         a.nwork = (uint32_t)c->m_work.size();
         a.hitH = (uint32_t)std::max<int64_t>(c->hitH, 0);
         a.entries = c->d_m_entries.ptr;
-        if (T == 8)
+        if constexpr (N == 16) { // one range block × its T transforms per workgroup
+            const unsigned nwg = (unsigned)c->m_work.size();
+            const bool hits = c->hitH > 0;
+            if (T == 8) {
+                if (hits)
+                    search_mfma16<8, true><<<nwg, 512, 0, c->stream>>>(a);
+                else
+                    search_mfma16<8, false><<<nwg, 512, 0, c->stream>>>(a);
+            } else {
+                if (hits)
+                    search_mfma16<4, true><<<nwg, 256, 0, c->stream>>>(a);
+                else
+                    search_mfma16<4, false><<<nwg, 256, 0, c->stream>>>(a);
+            }
+        } else if (T == 8)
             launch_search_mfma<N, 8>(c, a);
         else
             launch_search_mfma<N, 4>(c, a);
@@ -1020,9 +1036,9 @@ int launch_all(frac_ctx* c)
         pool_build<N><<<(P + 3) / 4, 256, 0, c->stream>>>(dsrc, c->d_sstride, c->d_doms.ptr, c->d_porig.ptr, P,
                                                           c->d_pool.ptr, c->d_negsd2.ptr);
     const bool use_sea = c->engine == FRAC_ENGINE_SEA && !c->all_fallback;
+    if (use_mfma)
+        FRAC_TRY(launch_mfma<N>(c, dtgt, tstride));
     if constexpr (N <= 8) {
-        if (use_mfma)
-            FRAC_TRY(launch_mfma<N>(c, dtgt, tstride));
         if (use_sea)
             FRAC_TRY(launch_sea<N>(c, dtgt, tstride, timing));
     }

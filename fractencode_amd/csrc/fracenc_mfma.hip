@@ -35,11 +35,14 @@ struct MfmaGeom {
 };
 
 // c_r: v − c_r = S16 for a range with pixel sum Σr and square sum Σr²
-// v = 2^25 − 8Z + ΣD4² − 1024ΣD4  and  −8Z = −8X + 4080Σr + 1024ΣD4 − 8·NN·65280
-//   ⇒ v = S16 − 16Σr² + 4080Σr + 2^25 − 8·NN·65280
+// v = V0 − 8Z + ΣD4² − 1024ΣD4  and  −8Z = −8X + 4080Σr + 1024ΣD4 − 8·NN·65280
+//   ⇒ v = S16 − 16Σr² + 4080Σr + V0 − 8·NN·65280
+// V0 = 2^25 for n ≤ 8 (the offset-binary epilogue); 2^28 for n = 16, where |8Z| < 2^27 and
+// ΣD4(D4 − 1024) ≥ −2^26 would take v below zero with 2^25 (search_mfma16)
+constexpr int64_t mfma_v0(int NN) { return NN > 64 ? (1ll << 28) : (1ll << 25); }
 __host__ __device__ inline uint32_t mfma_range_const(int NN, int64_t sr, int64_t sr2)
 {
-    return (uint32_t)(int64_t)(-16 * sr2 + 4080 * sr + (1ll << 25) - 8ll * NN * 65280);
+    return (uint32_t)(int64_t)(-16 * sr2 + 4080 * sr + mfma_v0(NN) - 8ll * NN * 65280);
 }
 
 // ---------------------------------------------------------------------------
@@ -87,7 +90,9 @@ __global__ void __launch_bounds__(256) mfma_domain_prep(MfmaDomainPrepArgs a)
     }
     if (p >= 0)
         sd2 = -a.negsd2[p];
-    const uint32_t e = p >= 0 ? (uint32_t)(sd2 - 1024 * sumd) - 0x58000000u : kMfmaPadConst;
+    // n ≤ 8: v = (bits(acc) << 3) + e with bits(acc) = 0x4B400000 − Z;  n = 16: v = (int(acc) << 3) + e
+    const uint32_t e = p >= 0 ? (uint32_t)(sd2 - 1024 * sumd) + (N == 16 ? (1u << 28) : (uint32_t)-0x58000000)
+                              : kMfmaPadConst;
     // row = (i&3) + 8(i>>2) + 4h  ⇔  h = (row>>2)&1, i = (row&3) + 4(row>>3)
     const uint32_t h = (row >> 2) & 1u, i = (row & 3u) + 4u * (row >> 3);
     a.dconst[(size_t)tile * 32 + h * 16 + i] = e;
@@ -385,6 +390,89 @@ __global__ void __launch_bounds__(256) search_mfma(MfmaSearchArgs a)
         for (int t = 0; t < T; ++t)
             a.entries[((size_t)(blockIdx.x * 4u + wv) * T + t) * 64 + lane] = make_uint2(best[t], btile[t]);
     }
+}
+
+// ---------------------------------------------------------------------------
+// search_mfma16<T, HITS>: the direct form for n = 16 (K = 256: 16 MFMAs per transform and
+// tile pair).  |Z| ≤ 256·128·510 < 2^24, so the fp32 accumulation from 0 is exact, but the
+// offset-binary epilogue of n ≤ 8 needs |Z| < 2^22: here acc = −Z is converted to an
+// integer and v = (int(acc) << 3) + e (e carries V0 = 2^28, mfma_range_const).  The B
+// fragments of one transform take 64 VGPRs, so a workgroup is T waves = one range block ×
+// its T transforms sharing the LDS stages (2 tiles of 16 KiB + row constants, double
+// buffered).  Entries keep search_mfma's layout with one block per work item
+// ((work·1 + 0)·T + t), so resolve_mfma reads them unchanged.
+// ---------------------------------------------------------------------------
+constexpr int kTilesPerStage16 = 2;
+
+template <int T, bool HITS>
+__global__ void __launch_bounds__(64 * T) search_mfma16(MfmaSearchArgs a)
+{
+    constexpr int KS = MfmaGeom<16>::KS; // 16
+    constexpr int STAGE = kTilesPerStage16 * KS * 64 + kTilesPerStage16 * 8;
+    __shared__ uint4 lds0[STAGE];
+    __shared__ uint4 lds1[STAGE];
+    const uint4 wk = a.work[blockIdx.x];
+    const uint32_t t = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    const uint32_t blk = wk.x;
+    half8_t bf[KS];
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
+        bf[s] = __builtin_bit_cast(half8_t, a.rfrags[((size_t)(blk * T + t) * KS + s) * 64 + lane]);
+    uint32_t hl = 0;
+    if constexpr (HITS)
+        hl = a.hitH + a.rconst[blk * 32 + (lane & 31u)];
+    const floatx16_t zero = {};
+    uint32_t best = 0xffffffffu, btile = 0;
+    const uint32_t h = lane >> 5;
+    auto compute = [&](const uint4* la, uint32_t nt, uint32_t tb) {
+        const uint4* lc = la + nt * KS * 64u;
+        uint32_t cm = 0xffffffffu;
+        for (uint32_t q = 0; q < nt; ++q) {
+            floatx16_t acc = zero;
+#pragma unroll
+            for (int s = 0; s < KS; ++s)
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(half8_t, la[(q * KS + s) * 64 + lane]),
+                                                           bf[s], acc, 0, 0, 0);
+            uint32_t e[16];
+#pragma unroll
+            for (int c4 = 0; c4 < 4; ++c4) {
+                const uint4 v = lc[q * 8 + h * 4 + c4];
+                e[4 * c4 + 0] = v.x;
+                e[4 * c4 + 1] = v.y;
+                e[4 * c4 + 2] = v.z;
+                e[4 * c4 + 3] = v.w;
+            }
+#pragma unroll
+            for (int i = 0; i < 16; ++i)
+                cm = min(cm, ((uint32_t)(int32_t)acc[i] << 3) + e[i]); // acc: exact integer, |acc| < 2^24
+        }
+        if constexpr (HITS)
+            cm = cm <= hl ? 0u : cm; // any hit in the chunk: the first-hit chunk wins
+        if (cm < best) {
+            best = cm;
+            btile = tb;
+        }
+    };
+    const uint32_t nstage = (wk.w - wk.z + kTilesPerStage16 - 1) / kTilesPerStage16;
+    auto stage_nt = [&](uint32_t st) { return min((uint32_t)kTilesPerStage16, wk.w - (wk.z + st * kTilesPerStage16)); };
+    // chunks of kTilesPerStage (4) tiles for resolve_mfma: two stages per chunk, both
+    // reported under the chunk's first tile
+    if (nstage)
+        stage_tiles<KS, 64 * T>(lds0, a.dtiles, a.dconst, wk.z, stage_nt(0));
+    for (uint32_t st = 0; st < nstage; st += 2) {
+        const uint32_t tb = wk.z + st * kTilesPerStage16;
+        __syncthreads();
+        if (st + 1 < nstage)
+            stage_tiles<KS, 64 * T>(lds1, a.dtiles, a.dconst, tb + kTilesPerStage16, stage_nt(st + 1));
+        compute(lds0, stage_nt(st), tb);
+        if (st + 1 < nstage) {
+            __syncthreads();
+            if (st + 2 < nstage)
+                stage_tiles<KS, 64 * T>(lds0, a.dtiles, a.dconst, tb + 2 * kTilesPerStage16, stage_nt(st + 2));
+            compute(lds1, stage_nt(st + 1), tb);
+        }
+    }
+    a.entries[((size_t)blockIdx.x * T + t) * 64 + lane] = make_uint2(best, btile);
 }
 
 // ---------------------------------------------------------------------------

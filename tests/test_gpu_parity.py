@@ -23,8 +23,8 @@ def as_oracle_fields(out):
 
 
 def run_engine(p, meta, engine, tgt=None, ranges_idx=None):
-    if engine in (F.ENGINE_MFMA, F.ENGINE_SEA) and meta["tgt"] > 8:
-        pytest.skip("the MFMA and SEA engines cover n <= 8 (n = 16 runs on the VALU engine)")
+    if engine == F.ENGINE_SEA and meta["tgt"] > 8:
+        pytest.skip("the SEA engine covers n <= 8")
     H, W = p.shape
     doms = F.create_uniform_grid(W, H, meta["src"], meta["src"] // 2)
     rngs = F.create_uniform_grid(W, H, meta["tgt"], meta["tgt"])
@@ -82,6 +82,8 @@ CASES = [
     (32, 32, 2, 8, True, 0.0, -1.0, "flat"),
     (96, 96, 16, 4, False, 0.0, -1.0, "noise"),
     (128, 96, 16, 8, True, 30.0, -1.0, "uniform"),
+    (64, 64, 16, 8, False, 0.0, -1.0, "flat"),     # n = 16 ties (MFMA integer epilogue)
+    (96, 64, 16, 4, True, 0.0, 0.5, "noise"),
     (64, 64, 8, 4, False, 1e9, -1.0, "noise"),   # every candidate hits: all-fallback mode
     (64, 64, 8, 8, False, 5000.0, -1.0, "uniform"),
 ]
@@ -221,10 +223,9 @@ def test_full_4096_frame(engine):
     assert (out["sw"] == 16).all()
 
 
-@pytest.mark.parametrize("engine", [F.ENGINE_MFMA, F.ENGINE_SEA])
-def test_mfma_and_sea_reject_n16(engine):
+def test_sea_rejects_n16():
     p = np.zeros((64, 64), np.uint8)
-    with F.Engine(0, 4, engine=engine) as e:
+    with F.Engine(0, 4, engine=F.ENGINE_SEA) as e:
         e.set_frame(p)
         e.set_domains(F.create_uniform_grid(64, 64, 32, 16))
         with pytest.raises(F.FracError):
