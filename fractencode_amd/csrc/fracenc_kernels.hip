@@ -317,8 +317,9 @@ __global__ void __launch_bounds__(256) fit_winner(FitArgs a)
     const frac_grid_item d = a.doms[a.porig[p]];
     const uint32_t* dp = a.pool + (size_t)p * (NN / 2);
 
-    long long sA = 0, sA2 = 0, sD = 0, sD2 = 0;
-    long long X[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    // every sum fits int32 for n ≤ 16 (ΣD4² ≤ 256·1020² < 2^31, X ≤ 256·255·1020 < 2^27)
+    int sA = 0, sA2 = 0, sD = 0, sD2 = 0;
+    int X[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     for (int q = lane; q < NN; q += 64) {
         const int rv = a.tgt[(size_t)(rg.y + q / N) * a.tstride + rg.x + (q % N)];
         const uint32_t dw = dp[q >> 1];
@@ -334,24 +335,25 @@ __global__ void __launch_bounds__(256) fit_winner(FitArgs a)
                 const int f = fwd_index<N>(t, q);
                 const uint32_t fw = dp[f >> 1];
                 const int fv = (f & 1) ? (int)(fw >> 16) : (int)(fw & 0xffffu);
-                X[t] += (long long)rv * fv;
+                X[t] += rv * fv;
             }
         }
     }
-    sA = wave_sum_ll(sA);
-    sA2 = wave_sum_ll(sA2);
-    sD = wave_sum_ll(sD);
-    sD2 = wave_sum_ll(sD2);
+    sA = wave_sum_i(sA);
+    sA2 = wave_sum_i(sA2);
+    sD = wave_sum_i(sD);
+    sD2 = wave_sum_i(sD2);
 #pragma unroll
     for (int t = 0; t < 8; ++t)
-        X[t] = wave_sum_ll(X[t]);
+        if (t < (int)a.T) // wave-uniform
+            X[t] = wave_sum_i(X[t]);
     if (lane != 0)
         return;
     long long S16[8];
     long long minS = LLONG_MAX;
     int tsel = -1;
     for (int t = 0; t < (int)a.T; ++t) {
-        S16[t] = 16 * sA2 - 8 * X[t] + sD2;
+        S16[t] = 16 * (long long)sA2 - 8 * (long long)X[t] + sD2;
         if (S16[t] < minS)
             minS = S16[t];
     }
