@@ -74,6 +74,20 @@ class ColorEncoder:
         """[(encode items, stats)] for Y, U, V."""
         return [e.fetch() for e in self.engines]
 
+    def encode_sharded(self, rank: int, world: int, device=None, group=None):
+        """C5 over several GPUs (BASELINE configs[4]): after load(), every rank searches its
+        contiguous shard of each plane's ranges and the (domain, transform, s, o, rms) tuples are
+        all-gathered (fractencode_amd.distributed); returns the full Y, U, V encode_item_t arrays
+        on every rank.  `device` = a CUDA device for nccl, None for gloo (host tuples)."""
+        from .distributed import encode_sharded
+
+        out = []
+        for e, rngs, p in zip(self.engines, self.ranges, self.planes):
+            H, W = p.shape
+            doms = create_uniform_grid(W, H, self.domain_size, self.domain_size // 2)
+            out.append(encode_sharded(e, rngs, doms, rank, world, device=device, group=group))
+        return out
+
     def host_planes(self):
         return [p.cpu().numpy() for p in self.planes]
 
