@@ -1,0 +1,26 @@
+#!/usr/bin/env python3
+"""C2 (Lenna 512², 8×8 ranges, 16×16 domains, all 8 transforms): per-run device ms
+(library HIP events) for the MFMA engine; run under rocprofv3 for the kernel breakdown."""
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import fractencode_amd as F  # noqa: E402
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+p = np.fromfile(os.path.join(ROOT, "tests", "golden", "lenna_y.u8"), np.uint8).reshape(512, 512)
+for T in (8, 4):
+    with F.Engine(0, T, False, 0.0, -1.0, F.ENGINE_AUTO, timing=True) as e:
+        e.set_frame(p)
+        e.set_domains(F.create_uniform_grid(512, 512, 16, 8))
+        e.set_ranges(F.create_uniform_grid(512, 512, 8, 8))
+        ms = []
+        for _ in range(20):
+            e.run()
+            _, st = e.fetch()
+            ms.append((st["ms_device"], st["ms_prep"], st["ms_search"], st["ms_finish"]))
+        a = np.median(np.array(ms[2:]), axis=0)
+        print(f"T={T}: device {a[0]:.3f} ms (prep {a[1]:.3f}, search {a[2]:.3f}, finish {a[3]:.3f}), "
+              f"{4096 / a[0] * 1e3 / 1e6:.2f} M range-blocks/s", flush=True)
