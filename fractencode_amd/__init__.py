@@ -34,8 +34,9 @@ NO_DOMAIN = 0xFFFFFFFF
 assert GRID_ITEM.itemsize == 20 and ENCODE_ITEM.itemsize == 64 and TUPLE.itemsize == 32
 
 ENGINE_AUTO, ENGINE_VALU, ENGINE_MFMA, ENGINE_SEA = 0, 1, 2, 3
-FORM_DOT2, FORM_DIRECT, FORM_FOURIER, FORM_SEA = 0, 1, 2, 3
-FORM_NAMES = {FORM_DOT2: "dot2", FORM_DIRECT: "direct", FORM_FOURIER: "fourier", FORM_SEA: "sea"}
+FORM_DOT2, FORM_DIRECT, FORM_FOURIER, FORM_SEA, FORM_SEA_MFMA = 0, 1, 2, 3, 4
+FORM_NAMES = {FORM_DOT2: "dot2", FORM_DIRECT: "direct", FORM_FOURIER: "fourier", FORM_SEA: "sea",
+              FORM_SEA_MFMA: "sea_mfma"}
 FLAG_TIMING = 1
 
 # Frac::TransformType (image/transform.h:16-25)

@@ -24,6 +24,7 @@
 #include "fracenc_classify.hip"
 #include "fracenc_sea.hip"
 #include "fracenc_stream.hip"
+#include "fracenc_tp.hip"
 
 using namespace fracenc;
 
@@ -198,6 +199,17 @@ struct frac_ctx {
     DBuf<SeaEntry> d_sea_ent;
     DBuf<int32_t> d_sea_snegsd2;
     DBuf<frac_tuple> d_tuples; // frac_fetch_tuples staging
+    // SEA engine, tiled form (fracenc_tp.hip)
+    bool tp = false;
+    TpBuckets tp_bk{};
+    std::vector<uint4> tp_groups, h_tp_work;
+    std::vector<uint2> tp_blk_group;
+    DBuf<uint4> d_tp_groups;
+    DBuf<uint2> d_tp_blk_group, d_tp_tile_sd, d_tp_blk_sr;
+    DBuf<uint32_t> d_tp_blk_u, d_tp_nch, d_tp_choff, d_tp_blkcnt, d_tp_tot;
+    DBuf<int32_t> d_tp_rbk;
+    DBuf<uint8_t> d_tp_tmp;
+    size_t tp_tmp_bytes = 0;
     DBuf<Frc1MinMax> d_frc_mm;             // frac_pack_frc1
     DBuf<unsigned long long> d_frc_rec;
     DBuf<uint32_t> d_frc_words;
@@ -461,6 +473,46 @@ int prepare(frac_ctx* c)
     c->engine = c->p.engine == FRAC_ENGINE_VALU  ? FRAC_ENGINE_VALU
                 : c->p.engine == FRAC_ENGINE_SEA ? FRAC_ENGINE_SEA
                                                  : FRAC_ENGINE_MFMA;
+    // SEA, n = 8, T = 4: the tiled form (FRAC_SEA_TILED=0 keeps the per-range form, A/B knob)
+    {
+        const char* st = getenv("FRAC_SEA_TILED");
+        c->tp = c->engine == FRAC_ENGINE_SEA && n == 8 && T == 4 && (st ? atoi(st) != 0 : true);
+    }
+    if (c->tp) {
+        if (nb > kTpMaxBuckets)
+            return c->fail(FRAC_E_INVALID, "SEA: too many classifier buckets");
+        TpBuckets& bk = c->tp_bk;
+        bk = TpBuckets{};
+        bk.nb = (uint32_t)nb;
+        uint32_t nt = 0, nbk = 0;
+        for (int b = 0; b < nb; ++b) {
+            bk.dom_begin[b] = c->bucket_begin[b];
+            bk.dom_count[b] = c->bucket_end[b] - c->bucket_begin[b];
+            bk.tile_first[b] = nt;
+            bk.tile_count[b] = (bk.dom_count[b] + 31) / 32;
+            nt += bk.tile_count[b];
+            bk.rng_begin[b] = rbeg[b];
+            bk.rng_count[b] = rbeg[b + 1] - rbeg[b];
+            bk.blk_first[b] = nbk;
+            bk.blk_count[b] = (bk.rng_count[b] + 31) / 32;
+            nbk += bk.blk_count[b];
+        }
+        c->ntiles = nt;
+        c->nblocks = nbk;
+        c->tp_groups.clear();
+        c->tp_blk_group.assign(nbk, make_uint2(0xffffffffu, 0u));
+        for (int b = 0; b < nb; ++b) {
+            if (!bk.tile_count[b])
+                continue; // no domain: the bucket's ranges keep the default record
+            for (uint32_t g0 = 0; g0 < bk.blk_count[b]; g0 += kDftBlocksPerWG) {
+                const uint32_t gi = (uint32_t)c->tp_groups.size();
+                const uint32_t nbl = std::min(kDftBlocksPerWG, bk.blk_count[b] - g0);
+                c->tp_groups.push_back(make_uint4(bk.blk_first[b] + g0, nbl, bk.tile_first[b], bk.tile_count[b]));
+                for (uint32_t k = 0; k < nbl; ++k)
+                    c->tp_blk_group[bk.blk_first[b] + g0 + k] = make_uint2(gi, k);
+            }
+        }
+    }
     if (c->engine == FRAC_ENGINE_MFMA) {
         // range blocks of 32 slots per bucket; domain tiles of 32 pool positions per bucket
         c->m_slot_range.clear();
@@ -652,8 +704,46 @@ int prepare(frac_ctx* c)
         FRAC_HIP(c, hipcub::DeviceRadixSort::SortPairs(nullptr, t2, c->d_sea_rkey.ptr, c->d_sea_rkey2.ptr,
                                                         c->d_sea_rord.ptr, c->d_sea_rord2.ptr, (int)nr, 0, 17,
                                                         c->stream));
-        c->sea_tmp_bytes = std::max<size_t>(std::max(t1, t2), 1);
+        size_t t3 = 0;
+        FRAC_HIP(c, hipcub::DeviceRadixSort::SortPairs(nullptr, t3, c->d_sea_rkey.ptr, c->d_sea_rkey2.ptr,
+                                                        c->d_sea_rord.ptr, c->d_sea_rord2.ptr, (int)nr, 0, 20,
+                                                        c->stream));
+        c->sea_tmp_bytes = std::max<size_t>(std::max(std::max(t1, t2), t3), 1);
         FRAC_HIP(c, c->d_sea_tmp.ensure(c->sea_tmp_bytes));
+    }
+    if (c->tp) {
+        const size_t ng = c->tp_groups.size(), nbk = c->nblocks, nt = c->ntiles;
+        FRAC_HIP(c, c->d_m_slot_range.ensure(std::max<size_t>(nbk * 32, 1)));
+        FRAC_HIP(c, c->d_m_range_slot.ensure(std::max<size_t>(nr, 1)));
+        FRAC_HIP(c, c->d_m_tile_pos.ensure(std::max<size_t>(nt * 32, 1)));
+        FRAC_HIP(c, c->d_m_dtiles.ensure(std::max<size_t>(nt * 4 * 64, 1)));
+        FRAC_HIP(c, c->d_m_dconst.ensure(std::max<size_t>(nt * 32, 1)));
+        FRAC_HIP(c, c->d_m_rfrags.ensure(std::max<size_t>(nbk * 7 * 64, 1)));
+        FRAC_HIP(c, c->d_m_rconst.ensure(std::max<size_t>(nbk * 32, 1)));
+        FRAC_HIP(c, c->d_dft_tguard.ensure(std::max<size_t>(nt, 1)));
+        FRAC_HIP(c, c->d_dft_rguard.ensure(std::max<size_t>(nbk, 1)));
+        FRAC_HIP(c, c->d_m8_work.ensure(std::max<size_t>(ng, 1)));
+        FRAC_HIP(c, c->d_m8_blk_ptr.ensure(nbk + 1));
+        FRAC_HIP(c, c->d_tp_groups.ensure(std::max<size_t>(ng, 1)));
+        FRAC_HIP(c, c->d_tp_blk_group.ensure(std::max<size_t>(nbk, 1)));
+        FRAC_HIP(c, c->d_tp_tile_sd.ensure(std::max<size_t>(nt, 1)));
+        FRAC_HIP(c, c->d_tp_blk_sr.ensure(std::max<size_t>(nbk, 1)));
+        FRAC_HIP(c, c->d_tp_blk_u.ensure(std::max<size_t>(nbk, 1)));
+        FRAC_HIP(c, c->d_tp_nch.ensure(ng + 1));
+        FRAC_HIP(c, c->d_tp_choff.ensure(ng + 1));
+        FRAC_HIP(c, c->d_tp_blkcnt.ensure(nbk + 1));
+        FRAC_HIP(c, c->d_tp_tot.ensure(2));
+        FRAC_HIP(c, c->d_tp_rbk.ensure(std::max<size_t>(nr, 1)));
+        FRAC_TRY(up(c->d_tp_groups.ptr, c->tp_groups.data(), ng * sizeof(uint4)));
+        FRAC_TRY(up(c->d_tp_blk_group.ptr, c->tp_blk_group.data(), nbk * sizeof(uint2)));
+        FRAC_TRY(up(c->d_tp_rbk.ptr, c->range_bucket.data(), nr * sizeof(int32_t)));
+        size_t s1 = 0, s2 = 0;
+        FRAC_HIP(c, hipcub::DeviceScan::ExclusiveSum(nullptr, s1, c->d_tp_nch.ptr, c->d_tp_choff.ptr, (int)(ng + 1),
+                                                     c->stream));
+        FRAC_HIP(c, hipcub::DeviceScan::ExclusiveSum(nullptr, s2, c->d_tp_blkcnt.ptr, c->d_m8_blk_ptr.ptr,
+                                                     (int)(nbk + 1), c->stream));
+        c->tp_tmp_bytes = std::max<size_t>(std::max(s1, s2), 1);
+        FRAC_HIP(c, c->d_tp_tmp.ensure(c->tp_tmp_bytes));
     }
     if (c->engine == FRAC_ENGINE_MFMA) {
         const int KS = (n * n + 15) / 16;
@@ -863,7 +953,7 @@ inline int launch_dft(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride)
         v.T = 4;
         v.hitH = c->hitH;
         v.best_key = c->d_best_key.ptr;
-        resolve_dft<<<(nr + 3) / 4, 256, 0, c->stream>>>(v);
+        resolve_dft<false><<<(nr + 3) / 4, 256, 0, c->stream>>>(v);
     }
     return FRAC_OK;
 }
@@ -959,11 +1049,176 @@ int launch_mfma(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride)
     return FRAC_OK;
 }
 
+// SEA engine, tiled form (fracenc_tp.hip): sorted tiles and blocks, per-range seed bounds,
+// per-group windows, the Fourier search over the windows with per-chunk entries, resolve_dft.
+// One host synchronisation sizes the entry arrays (their count depends on the windows).
+int launch_tp(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool timing)
+{
+    const uint32_t nr = (uint32_t)c->ranges.size(), P = (uint32_t)c->porig.size();
+    const uint32_t nt = c->ntiles, nbk = c->nblocks, ng = (uint32_t)c->tp_groups.size();
+    c->form_ran = FRAC_FORM_SEA_MFMA;
+    c->flops_ran = 0;
+    c->evaluated_ran = 0;
+    if (P) {
+        sea_domain_keys<8><<<(P + 255) / 256, 256, 0, c->stream>>>(c->d_pool.ptr, P, c->d_sea_bend.ptr,
+                                                                   (uint32_t)c->bucket_end.size(), c->d_sea_dkey.ptr,
+                                                                   c->d_sea_dpos.ptr);
+        size_t tb = c->sea_tmp_bytes;
+        FRAC_HIP(c, hipcub::DeviceRadixSort::SortPairs(c->d_sea_tmp.ptr, tb, c->d_sea_dkey.ptr, c->d_sea_dkey2.ptr,
+                                                        c->d_sea_dpos.ptr, c->d_sea_dpos2.ptr, (int)P, 0, 20,
+                                                        c->stream));
+    }
+    if (nt) {
+        tp_build_tiles<<<(nt * 32 + 255) / 256, 256, 0, c->stream>>>(c->tp_bk, c->d_sea_dkey2.ptr, c->d_sea_dpos2.ptr,
+                                                                     nt, c->d_m_tile_pos.ptr, c->d_tp_tile_sd.ptr);
+        FRAC_HIP(c, hipMemsetAsync(c->d_dft_tguard.ptr, 0, nt * sizeof(uint2), c->stream));
+        MfmaDomainPrepArgs d;
+        d.pool = c->d_pool.ptr;
+        d.negsd2 = c->d_negsd2.ptr;
+        d.tile_pos = c->d_m_tile_pos.ptr;
+        d.ntiles = nt;
+        d.dtiles = c->d_m_dtiles.ptr;
+        d.dconst = c->d_m_dconst.ptr;
+        DftDomainBuildArgs b;
+        b.src = c->d_src.ptr;
+        b.sstride = c->d_sstride;
+        b.doms = c->d_doms.ptr;
+        b.porig = c->d_porig.ptr;
+        b.pool = c->d_pool.ptr;
+        b.negsd2 = c->d_negsd2.ptr;
+        dft_domain_build<<<(nt * 32 + 255) / 256, 256, 0, c->stream>>>(d, b, c->d_dft_tguard.ptr);
+    }
+    if (nr) {
+        tp_range_keys<<<(nr + 255) / 256, 256, 0, c->stream>>>(dtgt, tstride, c->d_ranges.ptr, c->d_tp_rbk.ptr, nr,
+                                                               c->d_sea_rkey.ptr, c->d_sea_rord.ptr);
+        size_t tb = c->sea_tmp_bytes;
+        FRAC_HIP(c, hipcub::DeviceRadixSort::SortPairs(c->d_sea_tmp.ptr, tb, c->d_sea_rkey.ptr, c->d_sea_rkey2.ptr,
+                                                        c->d_sea_rord.ptr, c->d_sea_rord2.ptr, (int)nr, 0, 20,
+                                                        c->stream));
+    }
+    if (nbk) {
+        tp_build_slots<<<(nbk * 32 + 255) / 256, 256, 0, c->stream>>>(c->tp_bk, c->d_sea_rkey2.ptr, c->d_sea_rord2.ptr,
+                                                                      nbk, c->d_m_slot_range.ptr,
+                                                                      c->d_m_range_slot.ptr, c->d_tp_blk_sr.ptr,
+                                                                      c->d_tp_blk_u.ptr);
+        FRAC_HIP(c, hipMemsetAsync(c->d_dft_rguard.ptr, 0, nbk * sizeof(uint32_t), c->stream));
+        MfmaRangePrepArgs r;
+        r.tgt = dtgt;
+        r.tstride = tstride;
+        r.ranges = c->d_ranges.ptr;
+        r.slot_range = c->d_m_slot_range.ptr;
+        r.nblocks = nbk;
+        r.T = 4;
+        r.rfrags = c->d_m_rfrags.ptr;
+        r.rconst = c->d_m_rconst.ptr;
+        dft_range_prep<<<(nbk * 32 + 255) / 256, 256, 0, c->stream>>>(r, c->d_dft_rguard.ptr);
+    }
+    if (timing)
+        FRAC_HIP(c, hipEventRecord(c->ev[1], c->stream));
+    if (!nr || !ng) // no ranges, or no domain in any range's bucket: every record is the default
+        return FRAC_OK;
+    TpSeedArgs s;
+    s.tgt = dtgt;
+    s.tstride = tstride;
+    s.ranges = c->d_ranges.ptr;
+    s.range_slot = c->d_m_range_slot.ptr;
+    s.rbucket_idx = c->d_tp_rbk.ptr;
+    s.bk = c->tp_bk;
+    s.tile_sd = c->d_tp_tile_sd.ptr;
+    s.tile_pos = c->d_m_tile_pos.ptr;
+    s.pool = c->d_pool.ptr;
+    s.negsd2 = c->d_negsd2.ptr;
+    s.nr = nr;
+    s.blk_u = c->d_tp_blk_u.ptr;
+    tp_seed<<<(nr + 3) / 4, 256, 0, c->stream>>>(s);
+    TpWindowArgs w;
+    w.groups = c->d_tp_groups.ptr;
+    w.ngroups = ng;
+    w.blk_sr = c->d_tp_blk_sr.ptr;
+    w.blk_u = c->d_tp_blk_u.ptr;
+    w.tile_sd = c->d_tp_tile_sd.ptr;
+    w.hitH = c->hitH;
+    w.work = c->d_m8_work.ptr;
+    w.nchunks = c->d_tp_nch.ptr;
+    FRAC_HIP(c, hipMemsetAsync(c->d_tp_nch.ptr + ng, 0, sizeof(uint32_t), c->stream));
+    tp_windows<<<(ng + 255) / 256, 256, 0, c->stream>>>(w);
+    size_t tb = c->tp_tmp_bytes;
+    FRAC_HIP(c, hipcub::DeviceScan::ExclusiveSum(c->d_tp_tmp.ptr, tb, c->d_tp_nch.ptr, c->d_tp_choff.ptr, (int)(ng + 1),
+                                                 c->stream));
+    FRAC_HIP(c, hipMemsetAsync(c->d_tp_blkcnt.ptr + nbk, 0, sizeof(uint32_t), c->stream));
+    tp_block_counts<<<(nbk + 255) / 256, 256, 0, c->stream>>>(c->d_tp_blk_group.ptr, c->d_tp_nch.ptr, nbk,
+                                                              c->d_tp_blkcnt.ptr);
+    tb = c->tp_tmp_bytes;
+    FRAC_HIP(c, hipcub::DeviceScan::ExclusiveSum(c->d_tp_tmp.ptr, tb, c->d_tp_blkcnt.ptr, c->d_m8_blk_ptr.ptr,
+                                                 (int)(nbk + 1), c->stream));
+    // sizes of the entry arrays: total chunks and total block → entry links
+    uint32_t tot[2] = {0, 0};
+    c->h_tp_work.resize(ng);
+    FRAC_HIP(c, hipMemcpyAsync(&tot[0], c->d_tp_choff.ptr + ng, sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
+    FRAC_HIP(c, hipMemcpyAsync(&tot[1], c->d_m8_blk_ptr.ptr + nbk, sizeof(uint32_t), hipMemcpyDeviceToHost,
+                               c->stream));
+    FRAC_HIP(c, hipMemcpyAsync(c->h_tp_work.data(), c->d_m8_work.ptr, ng * sizeof(uint4), hipMemcpyDeviceToHost,
+                               c->stream));
+    FRAC_HIP(c, hipStreamSynchronize(c->stream));
+    FRAC_HIP(c, c->d_m_entries.ensure(std::max<size_t>((size_t)tot[0] * kDftBlocksPerWG * 64, 1)));
+    FRAC_HIP(c, c->d_m8_blk_ent.ensure(std::max<size_t>(tot[1], 1)));
+    tp_fill_entries<<<(nbk + 255) / 256, 256, 0, c->stream>>>(c->d_tp_blk_group.ptr, c->d_tp_choff.ptr,
+                                                              c->d_m8_blk_ptr.ptr, nbk, c->d_m8_blk_ent.ptr);
+    for (const uint4& wk : c->h_tp_work) { // issued matrix work and evaluated (slot, domain row) pairs
+        c->flops_ran += (uint64_t)wk.y * (wk.w - wk.z) * 8ull * 32768ull;
+        c->evaluated_ran += (uint64_t)wk.y * 32ull * (wk.w - wk.z) * 32ull;
+    }
+    MfmaSearchArgs a;
+    a.dtiles = c->d_m_dtiles.ptr;
+    a.dconst = reinterpret_cast<const uint4*>(c->d_m_dconst.ptr);
+    a.rfrags = c->d_m_rfrags.ptr;
+    a.rconst = c->d_m_rconst.ptr;
+    a.work = c->d_m8_work.ptr;
+    a.nwork = ng;
+    a.hitH = (uint32_t)std::max<int64_t>(c->hitH, 0);
+    a.entries = c->d_m_entries.ptr;
+    DftArgs da;
+    da.m = a;
+    da.rguard = c->d_dft_rguard.ptr;
+    da.tguard = c->d_dft_tguard.ptr;
+    da.choff = c->d_tp_choff.ptr;
+    constexpr uint32_t W8 = kDftBlocksPerWG;
+    if (c->hitH > 0)
+        search_dft<true, 1, W8, 4, true><<<ng, 64 * W8, 0, c->stream>>>(da);
+    else
+        search_dft<false, 1, W8, 4, true><<<ng, 64 * W8, 0, c->stream>>>(da);
+    if (timing)
+        FRAC_HIP(c, hipEventRecord(c->ev[2], c->stream));
+    MfmaResolveArgs v;
+    v.tgt = dtgt;
+    v.tstride = tstride;
+    v.ranges = c->d_ranges.ptr;
+    v.range_slot = c->d_m_range_slot.ptr;
+    v.blk_ptr = c->d_m8_blk_ptr.ptr;
+    v.blk_ent = c->d_m8_blk_ent.ptr;
+    v.entries = c->d_m_entries.ptr;
+    v.rconst = c->d_m_rconst.ptr;
+    v.tile_pos = c->d_m_tile_pos.ptr;
+    v.ntiles = nt;
+    v.pool = c->d_pool.ptr;
+    v.negsd2 = c->d_negsd2.ptr;
+    v.nr = nr;
+    v.T = 4;
+    v.hitH = c->hitH;
+    v.best_key = c->d_best_key.ptr;
+    resolve_dft<true><<<(nr + 3) / 4, 256, 0, c->stream>>>(v);
+    return FRAC_OK;
+}
+
 // SEA engine (fracenc_sea.hip): domain keys → radix sort (bucket, ΣD4) → sorted entries;
 // range keys → radix sort by ΣR; then one wave per range writes best_key.
 template <int N>
 int launch_sea(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool timing)
 {
+    if constexpr (N == 8) {
+        if (c->tp)
+            return launch_tp(c, dtgt, tstride, timing);
+    }
     const uint32_t nr = (uint32_t)c->ranges.size(), P = (uint32_t)c->porig.size();
     if (P) {
         sea_domain_keys<N><<<(P + 255) / 256, 256, 0, c->stream>>>(c->d_pool.ptr, P, c->d_sea_bend.ptr,
@@ -1127,7 +1382,8 @@ int launch_all(frac_ctx* c)
         FRAC_HIP(c, hipEventRecord(c->ev[3], c->stream));
     FRAC_HIP(c, hipGetLastError());
     c->engine_ran = use_mfma ? FRAC_ENGINE_MFMA : use_sea ? FRAC_ENGINE_SEA : FRAC_ENGINE_VALU;
-    c->evaluated_ran = c->all_fallback ? 0 : c->eligible_pairs; // SEA: read back at fetch
+    if (!(use_sea && c->tp)) // the tiled form counted its evaluated pairs in launch_tp
+        c->evaluated_ran = c->all_fallback ? 0 : c->eligible_pairs; // SEA: read back at fetch
     if (use_valu) {
         c->form_ran = FRAC_FORM_DOT2;
         c->flops_ran = 0;
@@ -1231,6 +1487,17 @@ void frac_destroy(frac_ctx* c)
     c->d_sea_count.release();
     c->d_sea_snegsd2.release();
     c->d_tuples.release();
+    c->d_tp_groups.release();
+    c->d_tp_blk_group.release();
+    c->d_tp_tile_sd.release();
+    c->d_tp_blk_sr.release();
+    c->d_tp_blk_u.release();
+    c->d_tp_nch.release();
+    c->d_tp_choff.release();
+    c->d_tp_blkcnt.release();
+    c->d_tp_tot.release();
+    c->d_tp_rbk.release();
+    c->d_tp_tmp.release();
     c->d_frc_mm.release();
     c->d_frc_rec.release();
     c->d_frc_words.release();
@@ -1400,7 +1667,7 @@ int frac_fetch(frac_ctx* c, frac_encode_item* out, frac_stats* stats)
         FRAC_HIP(c, hipMemcpyAsync(c->h_aux.data(), c->d_aux.ptr, nr * sizeof(RangeAux), hipMemcpyDeviceToHost,
                                    c->stream));
     unsigned long long sea_count = 0;
-    const bool sea_ran = c->engine_ran == FRAC_ENGINE_SEA;
+    const bool sea_ran = c->engine_ran == FRAC_ENGINE_SEA && c->form_ran == FRAC_FORM_SEA;
     if (sea_ran)
         FRAC_HIP(c, hipMemcpyAsync(&sea_count, c->d_sea_count.ptr, sizeof(sea_count), hipMemcpyDeviceToHost,
                                    c->stream));

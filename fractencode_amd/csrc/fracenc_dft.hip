@@ -105,6 +105,7 @@ struct DftArgs {
     MfmaSearchArgs m;
     uint32_t* rguard;     // [nblocks]  max over the block's ranges of R1 = Σ_o(|s_a| + |u_a|)
     uint2* tguard;        // [ntiles]   {max 4·D∞, max Σb²} over the tile's valid rows
+    const uint32_t* choff; // CHUNKED: [work] first chunk entry of the work item (fracenc_tp.hip)
 };
 
 // ---------------------------------------------------------------------------
@@ -406,7 +407,10 @@ __device__ inline float dft_compute_stage(const uint4* __restrict__ la, uint32_t
 
 constexpr uint32_t kDftBlocksPerWG = 8; // waves (range blocks) sharing one LDS domain stage
 
-template <bool HITS, int VAR, uint32_t WAVES = 4, uint32_t TPS = kTilesPerStage>
+// CHUNKED (the SEA engine's tiled form, fracenc_tp.hip): tiles are in ΣD4 order, not domain
+// order, so instead of the first chunk attaining each lane's maximum every chunk's maximum is
+// written, entry ((choff[work] + chunk)·WAVES + wave)·64 + lane, and resolve_dft keeps all ties.
+template <bool HITS, int VAR, uint32_t WAVES = 4, uint32_t TPS = kTilesPerStage, bool CHUNKED = false>
 __global__ void __launch_bounds__(64 * WAVES) search_dft(DftArgs d)
 {
     const MfmaSearchArgs& a = d.m;
@@ -434,6 +438,13 @@ __global__ void __launch_bounds__(64 * WAVES) search_dft(DftArgs d)
     auto finish_stage = [&](float cm, uint32_t tb) {
         if constexpr (HITS)
             cm = cm >= hl ? __builtin_inff() : cm; // any hit in the chunk: the first-hit chunk wins
+        if constexpr (CHUNKED) {
+            static_assert(TPS == 4, "chunk entries assume 4-tile stages");
+            if (active)
+                a.entries[((size_t)(d.choff[blockIdx.x] + (tb - wk.z) / 4u) * WAVES + wv) * 64 + lane] =
+                    make_uint2(__float_as_uint(cm), tb);
+            return;
+        }
         if (cm > best) {
             best = cm;
             btile = tb;
@@ -469,7 +480,7 @@ __global__ void __launch_bounds__(64 * WAVES) search_dft(DftArgs d)
                     dft_compute_stage<VAR>(lds1, stage_nt(st + 1), lane, bf, tb, d.tguard, r1, c0, c0 + 4), tb + c0);
         }
     }
-    if (active)
+    if (active && !CHUNKED)
         a.entries[(size_t)(blockIdx.x * WAVES + wv) * 64 + lane] = make_uint2(__float_as_uint(best), btile);
 }
 
@@ -481,6 +492,9 @@ __global__ void __launch_bounds__(64 * WAVES) search_dft(DftArgs d)
 // keeping the least selection key (first hit in (domain, transform) order, else least
 // error with ties to the earliest domain, then the later transform).
 // ---------------------------------------------------------------------------
+// SORTED (tiles in ΣD4 order, fracenc_tp.hip): rows and tiles are not in domain order, so the
+// least key over every matching row of every tile of the chunk is taken (no first-row shortcut).
+template <bool SORTED = false>
 __global__ void __launch_bounds__(256) resolve_dft(MfmaResolveArgs a)
 {
     constexpr int N = 8, NN = 64, PG = 16, T = 4;
@@ -576,18 +590,31 @@ __global__ void __launch_bounds__(256) resolve_dft(MfmaResolveArgs a)
                     // S16 = 16Σr² − 8X + ΣD4² ≤ 64·1020² < 2^31: exact in int32
                     const int64_t s16 = p >= 0 ? (int64_t)(16 * sr2 - 8 * (int32_t)X - nsd2) : 0;
                     const bool ok = p >= 0 && g == 0 && (hit ? (s16 <= a.hitH) : (s16 == target));
-                    const unsigned long long mask = __ballot(ok);
-                    if (mask) {
-                        const int first = __ffsll((long long)mask) - 1;
-                        const int pf = __shfl(p, first, 64);
-                        const unsigned long long k =
-                            hit ? key_hit((uint32_t)pf, t) : key_miss((uint64_t)target, (uint32_t)pf, T - 1 - t);
+                    if constexpr (SORTED) {
+                        unsigned long long k =
+                            ok ? (hit ? key_hit((uint32_t)p, t) : key_miss((uint64_t)target, (uint32_t)p, T - 1 - t))
+                               : kKeyNone;
+#pragma unroll
+                        for (int o = 32; o > 0; o >>= 1) {
+                            const unsigned long long ok2 = __shfl_xor(k, o, 64);
+                            k = ok2 < k ? ok2 : k;
+                        }
                         tk = k < tk ? k : tk;
+                    } else {
+                        const unsigned long long mask = __ballot(ok);
+                        if (mask) {
+                            const int first = __ffsll((long long)mask) - 1;
+                            const int pf = __shfl(p, first, 64);
+                            const unsigned long long k = hit ? key_hit((uint32_t)pf, t)
+                                                             : key_miss((uint64_t)target, (uint32_t)pf, T - 1 - t);
+                            tk = k < tk ? k : tk;
+                        }
                     }
                 }
                 if (tk != kKeyNone) {
                     bestk = tk < bestk ? tk : bestk;
-                    break;
+                    if constexpr (!SORTED)
+                        break;
                 }
             }
         }

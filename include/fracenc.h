@@ -111,6 +111,7 @@ typedef struct frac_stats {
 #define FRAC_FORM_DIRECT 1  /* MFMA engine: one f16 GEMM per transform (n²·T MACs per pair)        */
 #define FRAC_FORM_FOURIER 2 /* MFMA engine, n = 8, T = 4: rotation-group Fourier form (96 MACs)    */
 #define FRAC_FORM_SEA 3     /* SEA engine: bound-pruned exact evaluation (v_dot2)                */
+#define FRAC_FORM_SEA_MFMA 4 /* SEA engine, n = 8, T = 4: the bound per tile pair, Fourier MFMA search */
 
 typedef struct frac_ctx frac_ctx;
 
