@@ -203,10 +203,11 @@ struct frac_ctx {
     bool tp = false;
     TpBuckets tp_bk{};
     std::vector<uint4> tp_groups, h_tp_work;
+    std::vector<uint32_t> tp_iota;
     std::vector<uint2> tp_blk_group;
     DBuf<uint4> d_tp_groups;
     DBuf<uint2> d_tp_blk_group, d_tp_tile_sd, d_tp_blk_sr;
-    DBuf<uint32_t> d_tp_blk_u, d_tp_nch, d_tp_choff, d_tp_blkcnt, d_tp_tot;
+    DBuf<uint32_t> d_tp_blk_u, d_tp_nch, d_tp_choff, d_tp_blkcnt, d_tp_tot, d_tp_iota;
     DBuf<int32_t> d_tp_rbk;
     DBuf<uint8_t> d_tp_tmp;
     size_t tp_tmp_bytes = 0;
@@ -737,6 +738,11 @@ int prepare(frac_ctx* c)
         FRAC_TRY(up(c->d_tp_groups.ptr, c->tp_groups.data(), ng * sizeof(uint4)));
         FRAC_TRY(up(c->d_tp_blk_group.ptr, c->tp_blk_group.data(), nbk * sizeof(uint2)));
         FRAC_TRY(up(c->d_tp_rbk.ptr, c->range_bucket.data(), nr * sizeof(int32_t)));
+        c->tp_iota.resize(ng);
+        for (size_t g = 0; g < ng; ++g)
+            c->tp_iota[g] = (uint32_t)g;
+        FRAC_HIP(c, c->d_tp_iota.ensure(std::max<size_t>(ng, 1)));
+        FRAC_TRY(up(c->d_tp_iota.ptr, c->tp_iota.data(), ng * sizeof(uint32_t)));
         size_t s1 = 0, s2 = 0;
         FRAC_HIP(c, hipcub::DeviceScan::ExclusiveSum(nullptr, s1, c->d_tp_nch.ptr, c->d_tp_choff.ptr, (int)(ng + 1),
                                                      c->stream));
@@ -1117,20 +1123,30 @@ int launch_tp(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool timing)
         FRAC_HIP(c, hipEventRecord(c->ev[1], c->stream));
     if (!nr || !ng) // no ranges, or no domain in any range's bucket: every record is the default
         return FRAC_OK;
-    TpSeedArgs s;
-    s.tgt = dtgt;
-    s.tstride = tstride;
-    s.ranges = c->d_ranges.ptr;
-    s.range_slot = c->d_m_range_slot.ptr;
-    s.rbucket_idx = c->d_tp_rbk.ptr;
-    s.bk = c->tp_bk;
-    s.tile_sd = c->d_tp_tile_sd.ptr;
-    s.tile_pos = c->d_m_tile_pos.ptr;
-    s.pool = c->d_pool.ptr;
-    s.negsd2 = c->d_negsd2.ptr;
-    s.nr = nr;
-    s.blk_u = c->d_tp_blk_u.ptr;
-    tp_seed<<<(nr + 3) / 4, 256, 0, c->stream>>>(s);
+    constexpr uint32_t W8 = kDftBlocksPerWG;
+    MfmaSearchArgs a;
+    a.dtiles = c->d_m_dtiles.ptr;
+    a.dconst = reinterpret_cast<const uint4*>(c->d_m_dconst.ptr);
+    a.rfrags = c->d_m_rfrags.ptr;
+    a.rconst = c->d_m_rconst.ptr;
+    a.work = c->d_m8_work.ptr;
+    a.nwork = ng;
+    a.hitH = (uint32_t)std::max<int64_t>(c->hitH, 0);
+    a.entries = c->d_m_entries.ptr;
+    DftArgs da;
+    da.m = a;
+    da.rguard = c->d_dft_rguard.ptr;
+    da.tguard = c->d_dft_tguard.ptr;
+    // seed: the Fourier search over one tile per group, one chunk entry per wave (choff = group)
+    tp_seed_work<<<(ng + 255) / 256, 256, 0, c->stream>>>(c->d_tp_groups.ptr, ng, c->d_tp_blk_sr.ptr,
+                                                          c->d_tp_tile_sd.ptr, c->d_m8_work.ptr);
+    FRAC_HIP(c, c->d_m_entries.ensure((size_t)ng * W8 * 64));
+    da.m.entries = c->d_m_entries.ptr;
+    da.choff = c->d_tp_iota.ptr;
+    search_dft<false, 1, W8, 4, true><<<ng, 64 * W8, 0, c->stream>>>(da);
+    tp_seed_reduce<<<(nbk * 32 + 255) / 256, 256, 0, c->stream>>>(c->d_tp_blk_group.ptr, c->d_m_entries.ptr,
+                                                                   c->d_m_slot_range.ptr, c->d_m_rconst.ptr, nbk,
+                                                                   c->d_tp_blk_u.ptr);
     TpWindowArgs w;
     w.groups = c->d_tp_groups.ptr;
     w.ngroups = ng;
@@ -1168,21 +1184,8 @@ int launch_tp(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool timing)
         c->flops_ran += (uint64_t)wk.y * (wk.w - wk.z) * 8ull * 32768ull;
         c->evaluated_ran += (uint64_t)wk.y * 32ull * (wk.w - wk.z) * 32ull;
     }
-    MfmaSearchArgs a;
-    a.dtiles = c->d_m_dtiles.ptr;
-    a.dconst = reinterpret_cast<const uint4*>(c->d_m_dconst.ptr);
-    a.rfrags = c->d_m_rfrags.ptr;
-    a.rconst = c->d_m_rconst.ptr;
-    a.work = c->d_m8_work.ptr;
-    a.nwork = ng;
-    a.hitH = (uint32_t)std::max<int64_t>(c->hitH, 0);
-    a.entries = c->d_m_entries.ptr;
-    DftArgs da;
-    da.m = a;
-    da.rguard = c->d_dft_rguard.ptr;
-    da.tguard = c->d_dft_tguard.ptr;
+    da.m.entries = c->d_m_entries.ptr;
     da.choff = c->d_tp_choff.ptr;
-    constexpr uint32_t W8 = kDftBlocksPerWG;
     if (c->hitH > 0)
         search_dft<true, 1, W8, 4, true><<<ng, 64 * W8, 0, c->stream>>>(da);
     else
@@ -1496,6 +1499,7 @@ void frac_destroy(frac_ctx* c)
     c->d_tp_choff.release();
     c->d_tp_blkcnt.release();
     c->d_tp_tot.release();
+    c->d_tp_iota.release();
     c->d_tp_rbk.release();
     c->d_tp_tmp.release();
     c->d_frc_mm.release();

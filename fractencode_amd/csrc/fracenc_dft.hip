@@ -591,14 +591,10 @@ __global__ void __launch_bounds__(256) resolve_dft(MfmaResolveArgs a)
                     const int64_t s16 = p >= 0 ? (int64_t)(16 * sr2 - 8 * (int32_t)X - nsd2) : 0;
                     const bool ok = p >= 0 && g == 0 && (hit ? (s16 <= a.hitH) : (s16 == target));
                     if constexpr (SORTED) {
-                        unsigned long long k =
+                        // lane-local least key; one wave reduction per range at the end
+                        const unsigned long long k =
                             ok ? (hit ? key_hit((uint32_t)p, t) : key_miss((uint64_t)target, (uint32_t)p, T - 1 - t))
                                : kKeyNone;
-#pragma unroll
-                        for (int o = 32; o > 0; o >>= 1) {
-                            const unsigned long long ok2 = __shfl_xor(k, o, 64);
-                            k = ok2 < k ? ok2 : k;
-                        }
                         tk = k < tk ? k : tk;
                     } else {
                         const unsigned long long mask = __ballot(ok);
@@ -617,6 +613,13 @@ __global__ void __launch_bounds__(256) resolve_dft(MfmaResolveArgs a)
                         break;
                 }
             }
+        }
+    }
+    if constexpr (SORTED) {
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            const unsigned long long ok2 = __shfl_xor(bestk, o, 64);
+            bestk = ok2 < bestk ? ok2 : bestk;
         }
     }
     if (lane == 0)

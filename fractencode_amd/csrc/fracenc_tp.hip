@@ -5,8 +5,9 @@
 //   * domains of each classifier bucket sorted by ΣD4 into 32-domain tiles (tile_pos), each
 //     tile with its [min, max] ΣD4; ranges of each bucket sorted by ΣR into 32-range blocks,
 //     groups of 8 blocks per workgroup as in the exhaustive search;
-//   * tp_seed: per range the exact least error U_r over the tile nearest its ΣR (any real
-//     candidate's error bounds the range's minimum from above);
+//   * seed: the Fourier search over one tile per group (the tile nearest its middle block's
+//     ΣR), tp_seed_reduce turning each range's maximum into U_r, the least exact error over
+//     that tile (any real candidate's error bounds the range's minimum from above);
 //   * tp_windows: per group the tiles whose ΣD4 interval meets [min ΣR − D, max ΣR + D],
 //     D² = n²·(max(U, H) + 1/2) over the group's ranges: outside it (ΣR − ΣD)²/n² alone
 //     exceeds the bound, so no candidate there can win, tie or hit (fracenc_sea.hip);
@@ -98,100 +99,49 @@ __global__ void __launch_bounds__(256) tp_build_slots(TpBuckets bk, const uint32
     }
 }
 
-// per range: least exact error over the 32 domains of the tile nearest its ΣR → atomicMax
-// into its block's bound (lanes: 16 rows × 4 pixel slices, two rounds, as resolve_dft)
-struct TpSeedArgs {
-    const uint8_t* tgt;
-    uint32_t tstride;
-    const frac_grid_item* ranges;
-    const uint32_t* range_slot;
-    const int32_t* rbucket_idx;
-    TpBuckets bk;
-    const uint2* tile_sd;
-    const int32_t* tile_pos;
-    const uint32_t* pool;
-    const int32_t* negsd2;
-    uint32_t nr;
-    uint32_t* blk_u;
-};
-
-__global__ void __launch_bounds__(256) tp_seed(TpSeedArgs a)
+// seed work: per group the one tile of its bucket nearest the ΣR of its middle block
+__global__ void __launch_bounds__(256) tp_seed_work(const uint4* __restrict__ groups, uint32_t ngroups,
+                                                    const uint2* __restrict__ blk_sr, const uint2* __restrict__ tile_sd,
+                                                    uint4* __restrict__ work)
 {
-    constexpr int N = 8, NN = 64, PG = 16, T = 4;
-    const uint32_t r = blockIdx.x * 4u + (threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    if (r >= a.nr)
+    const uint32_t gi = blockIdx.x * blockDim.x + threadIdx.x;
+    if (gi >= ngroups)
         return;
-    const int b = a.rbucket_idx[r];
-    const uint32_t t0 = a.bk.tile_first[b], tn = a.bk.tile_count[b];
-    if (tn == 0)
-        return; // no domain in the bucket: the search has nothing to bound
-    const frac_grid_item rg = a.ranges[r];
-    const int rv = (int)a.tgt[(size_t)(rg.y + lane / N) * a.tstride + rg.x + (lane % N)];
-    int sr = rv, sr2 = rv * rv;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        sr += __shfl_xor(sr, o, 64);
-        sr2 += __shfl_xor(sr2, o, 64);
-    }
-    const uint32_t SR = 4u * (uint32_t)sr;
-    // the first tile of the bucket whose max ΣD4 reaches ΣR (else the last)
-    uint32_t lo = 0, hi = tn - 1;
+    const uint4 gr = groups[gi];
+    const uint2 s = blk_sr[gr.x + gr.y / 2];
+    const uint32_t SR = (s.x + s.y) / 2;
+    uint32_t lo = 0, hi = gr.w - 1; // first tile whose max ΣD4 reaches SR (else the last)
     while (lo < hi) {
-        const uint32_t mid = (lo + hi) / 2;
-        if (a.tile_sd[t0 + mid].y < SR)
-            lo = mid + 1;
+        const uint32_t m = (lo + hi) / 2;
+        if (tile_sd[gr.z + m].y < SR)
+            lo = m + 1;
         else
-            hi = mid;
+            hi = m;
     }
-    const uint32_t tile = t0 + lo;
-    const int i = lane >> 2, g = lane & 3;
-    uint32_t pk[T][PG / 2];
-#pragma unroll
-    for (int t = 0; t < T; ++t)
-#pragma unroll
-        for (int j = 0; j < PG / 2; ++j) {
-            const int k = g * PG + 2 * j;
-            const uint32_t l = (uint32_t)__shfl(rv, inv_index<N>(t, k), 64);
-            const uint32_t h = (uint32_t)__shfl(rv, inv_index<N>(t, k + 1), 64);
-            pk[t][j] = l | (h << 16);
-        }
-    int64_t best = INT64_MAX;
-#pragma unroll
-    for (int half = 0; half < 2; ++half) {
-        const int p = a.tile_pos[tile * 32 + 16 * half + i];
-        uint32_t dv[PG / 2] = {};
-        if (p >= 0) {
-            const uint4* dp = reinterpret_cast<const uint4*>(a.pool + (size_t)p * (NN / 2) + g * (PG / 2));
-            const uint4 d0 = dp[0], d1 = dp[1];
-            dv[0] = d0.x, dv[1] = d0.y, dv[2] = d0.z, dv[3] = d0.w;
-            dv[4] = d1.x, dv[5] = d1.y, dv[6] = d1.z, dv[7] = d1.w;
-        }
-        const int nsd2 = p >= 0 ? a.negsd2[p] : 0;
-#pragma unroll
-        for (int t = 0; t < T; ++t) {
-            uint32_t X = 0;
-#pragma unroll
-            for (int q = 0; q < PG / 2; ++q)
-                X = __builtin_amdgcn_udot2(__builtin_bit_cast(ushort2_t, pk[t][q]),
-                                           __builtin_bit_cast(ushort2_t, dv[q]), X, false);
-            X += (uint32_t)__shfl_xor((int)X, 1, 64);
-            X += (uint32_t)__shfl_xor((int)X, 2, 64);
-            const int64_t s16 = (int64_t)(16 * sr2 - 8 * (int32_t)X - nsd2);
-            if (p >= 0 && s16 < best)
-                best = s16;
-        }
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const int64_t ob = __shfl_xor(best, o, 64);
-        best = ob < best ? ob : best;
-    }
-    if (lane == 0) {
-        // no valid row cannot happen (the tile holds ≥ 1 domain); S16 < 2^27 fits u32
-        const uint32_t u = best == INT64_MAX ? 0xffffffffu : (uint32_t)best;
-        atomicMax(&a.blk_u[a.range_slot[r] >> 5], u);
-    }
+    work[gi] = make_uint4(gr.x, gr.y, gr.z + lo, gr.z + lo + 1);
+}
+
+// per range slot: the seed search's maximum y over the seed tile → U = 16Σa² − y, the least
+// exact error over that tile (exact regime; else no bound), atomicMax into the block's bound
+__global__ void __launch_bounds__(256) tp_seed_reduce(const uint2* __restrict__ blk_group,
+                                                      const uint2* __restrict__ entries,
+                                                      const int32_t* __restrict__ slot_range,
+                                                      const uint32_t* __restrict__ rconst, uint32_t nblocks,
+                                                      uint32_t* __restrict__ blk_u)
+{
+    const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid >= nblocks * 32u)
+        return;
+    const uint32_t b = gid >> 5, col = gid & 31u;
+    const uint2 gw = blk_group[b];
+    if (gw.x == 0xffffffffu || slot_range[gid] < 0)
+        return;
+    const size_t e = ((size_t)gw.x * 8u + gw.y) * 64u + col;
+    const float y = fmaxf(__uint_as_float(entries[e].x), __uint_as_float(entries[e + 32].x));
+    const int64_t sa16 = (int64_t)rconst[gid];
+    // y = 16Σa² − min S16 is exact while min S16 < 2^24 (fracenc_dft.hip)
+    const uint32_t u = y > (float)(sa16 - kExactLimit) ? (uint32_t)(sa16 - (int64_t)y) : 0xffffffffu;
+    atomicMax(&blk_u[b], u);
 }
 
 // per group of ≤ 8 blocks: the tile window and its chunk count
