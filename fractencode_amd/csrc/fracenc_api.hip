@@ -32,6 +32,18 @@ namespace {
 
 thread_local std::string g_last_error;
 
+// (key, value) radix sort of u32 pairs on the low `bits` key bits. rocPRIM's default picks a
+// block-sort + merge-sort path below 2^20 items: 17 launches for the 2^18 keys of a C3 frame,
+// whose launch gaps cost more than the sort. Merge-sort limit 0 selects Onesweep (histogram +
+// one pass per 8-bit digit).
+using OnesweepConfig =
+    rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config, rocprim::default_config, 0>;
+hipError_t sort_pairs_u32(void* tmp, size_t& bytes, const uint32_t* kin, uint32_t* kout, const uint32_t* vin,
+                          uint32_t* vout, uint32_t n, uint32_t bits, hipStream_t s)
+{
+    return rocprim::radix_sort_pairs<OnesweepConfig>(tmp, bytes, kin, kout, vin, vout, n, 0u, bits, s);
+}
+
 template <class T>
 struct DBuf {
     T* ptr = nullptr;
@@ -498,6 +510,8 @@ int prepare(frac_ctx* c)
             bk.blk_count[b] = (bk.rng_count[b] + 31) / 32;
             nbk += bk.blk_count[b];
         }
+        if (nt >= (1u << 28)) // chunk entries hold the tile in 28 bits (search_dft CHUNKED)
+            return c->fail(FRAC_E_INVALID, "SEA: too many domain tiles");
         c->ntiles = nt;
         c->nblocks = nbk;
         c->tp_groups.clear();
@@ -699,16 +713,13 @@ int prepare(frac_ctx* c)
         FRAC_HIP(c, c->d_sea_count.ensure(1));
         FRAC_TRY(up(c->d_sea_bend.ptr, c->bucket_end.data(), c->bucket_end.size() * sizeof(uint32_t)));
         size_t t1 = 0, t2 = 0;
-        FRAC_HIP(c, hipcub::DeviceRadixSort::SortPairs(nullptr, t1, c->d_sea_dkey.ptr, c->d_sea_dkey2.ptr,
-                                                        c->d_sea_dpos.ptr, c->d_sea_dpos2.ptr, (int)P, 0, 20,
-                                                        c->stream));
-        FRAC_HIP(c, hipcub::DeviceRadixSort::SortPairs(nullptr, t2, c->d_sea_rkey.ptr, c->d_sea_rkey2.ptr,
-                                                        c->d_sea_rord.ptr, c->d_sea_rord2.ptr, (int)nr, 0, 17,
-                                                        c->stream));
+        FRAC_HIP(c, sort_pairs_u32(nullptr, t1, c->d_sea_dkey.ptr, c->d_sea_dkey2.ptr, c->d_sea_dpos.ptr,
+                                   c->d_sea_dpos2.ptr, P, 20, c->stream));
+        FRAC_HIP(c, sort_pairs_u32(nullptr, t2, c->d_sea_rkey.ptr, c->d_sea_rkey2.ptr, c->d_sea_rord.ptr,
+                                   c->d_sea_rord2.ptr, nr, 17, c->stream));
         size_t t3 = 0;
-        FRAC_HIP(c, hipcub::DeviceRadixSort::SortPairs(nullptr, t3, c->d_sea_rkey.ptr, c->d_sea_rkey2.ptr,
-                                                        c->d_sea_rord.ptr, c->d_sea_rord2.ptr, (int)nr, 0, 20,
-                                                        c->stream));
+        FRAC_HIP(c, sort_pairs_u32(nullptr, t3, c->d_sea_rkey.ptr, c->d_sea_rkey2.ptr, c->d_sea_rord.ptr,
+                                   c->d_sea_rord2.ptr, nr, 20, c->stream));
         c->sea_tmp_bytes = std::max<size_t>(std::max(std::max(t1, t2), t3), 1);
         FRAC_HIP(c, c->d_sea_tmp.ensure(c->sea_tmp_bytes));
     }
@@ -1070,9 +1081,8 @@ int launch_tp(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool timing)
                                                                    (uint32_t)c->bucket_end.size(), c->d_sea_dkey.ptr,
                                                                    c->d_sea_dpos.ptr);
         size_t tb = c->sea_tmp_bytes;
-        FRAC_HIP(c, hipcub::DeviceRadixSort::SortPairs(c->d_sea_tmp.ptr, tb, c->d_sea_dkey.ptr, c->d_sea_dkey2.ptr,
-                                                        c->d_sea_dpos.ptr, c->d_sea_dpos2.ptr, (int)P, 0, 20,
-                                                        c->stream));
+        FRAC_HIP(c, sort_pairs_u32(c->d_sea_tmp.ptr, tb, c->d_sea_dkey.ptr, c->d_sea_dkey2.ptr, c->d_sea_dpos.ptr,
+                                   c->d_sea_dpos2.ptr, P, 20, c->stream));
     }
     if (nt) {
         tp_build_tiles<<<(nt * 32 + 255) / 256, 256, 0, c->stream>>>(c->tp_bk, c->d_sea_dkey2.ptr, c->d_sea_dpos2.ptr,
@@ -1098,9 +1108,8 @@ int launch_tp(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool timing)
         tp_range_keys<<<(nr + 255) / 256, 256, 0, c->stream>>>(dtgt, tstride, c->d_ranges.ptr, c->d_tp_rbk.ptr, nr,
                                                                c->d_sea_rkey.ptr, c->d_sea_rord.ptr);
         size_t tb = c->sea_tmp_bytes;
-        FRAC_HIP(c, hipcub::DeviceRadixSort::SortPairs(c->d_sea_tmp.ptr, tb, c->d_sea_rkey.ptr, c->d_sea_rkey2.ptr,
-                                                        c->d_sea_rord.ptr, c->d_sea_rord2.ptr, (int)nr, 0, 20,
-                                                        c->stream));
+        FRAC_HIP(c, sort_pairs_u32(c->d_sea_tmp.ptr, tb, c->d_sea_rkey.ptr, c->d_sea_rkey2.ptr, c->d_sea_rord.ptr,
+                                   c->d_sea_rord2.ptr, nr, 20, c->stream));
     }
     if (nbk) {
         tp_build_slots<<<(nbk * 32 + 255) / 256, 256, 0, c->stream>>>(c->tp_bk, c->d_sea_rkey2.ptr, c->d_sea_rord2.ptr,
@@ -1228,9 +1237,8 @@ int launch_sea(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool timing)
                                                                    (uint32_t)c->bucket_end.size(), c->d_sea_dkey.ptr,
                                                                    c->d_sea_dpos.ptr);
         size_t tb = c->sea_tmp_bytes;
-        FRAC_HIP(c, hipcub::DeviceRadixSort::SortPairs(c->d_sea_tmp.ptr, tb, c->d_sea_dkey.ptr, c->d_sea_dkey2.ptr,
-                                                        c->d_sea_dpos.ptr, c->d_sea_dpos2.ptr, (int)P, 0, 20,
-                                                        c->stream));
+        FRAC_HIP(c, sort_pairs_u32(c->d_sea_tmp.ptr, tb, c->d_sea_dkey.ptr, c->d_sea_dkey2.ptr, c->d_sea_dpos.ptr,
+                                   c->d_sea_dpos2.ptr, P, 20, c->stream));
         const uint32_t pieces = (N * N / 2 + 3) / 4;
         sea_domain_entries<N><<<(P * pieces + 255) / 256, 256, 0, c->stream>>>(
             c->d_sea_dkey2.ptr, c->d_sea_dpos2.ptr, c->d_negsd2.ptr, c->d_pool.ptr, P, c->d_sea_ent.ptr,
@@ -1240,9 +1248,8 @@ int launch_sea(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool timing)
         sea_range_keys<N><<<(nr + 255) / 256, 256, 0, c->stream>>>(dtgt, tstride, c->d_ranges.ptr, nr,
                                                                     c->d_sea_rkey.ptr, c->d_sea_rord.ptr);
         size_t tb = c->sea_tmp_bytes;
-        FRAC_HIP(c, hipcub::DeviceRadixSort::SortPairs(c->d_sea_tmp.ptr, tb, c->d_sea_rkey.ptr, c->d_sea_rkey2.ptr,
-                                                        c->d_sea_rord.ptr, c->d_sea_rord2.ptr, (int)nr, 0, 17,
-                                                        c->stream));
+        FRAC_HIP(c, sort_pairs_u32(c->d_sea_tmp.ptr, tb, c->d_sea_rkey.ptr, c->d_sea_rkey2.ptr, c->d_sea_rord.ptr,
+                                   c->d_sea_rord2.ptr, nr, 17, c->stream));
     }
     if (timing)
         FRAC_HIP(c, hipEventRecord(c->ev[1], c->stream));
@@ -1361,7 +1368,7 @@ int launch_all(frac_ctx* c)
         f.aux = c->d_aux.ptr;
         f.fb_count = c->d_fb_count.ptr;
         f.fb_list = c->d_fb_list.ptr;
-        fit_winner<N><<<(nr + 3) / 4, 256, 0, c->stream>>>(f);
+        fit_winner<N><<<(nr + 4 * (64 / fit_lanes<N>()) - 1) / (4 * (64 / fit_lanes<N>())), 256, 0, c->stream>>>(f);
     }
     if (nr) {
         FallbackArgs b;

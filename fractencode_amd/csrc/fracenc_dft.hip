@@ -363,11 +363,13 @@ __device__ inline float dft_tile_max(const half8_t (&af)[4], const half8_t (&bf)
     return __builtin_fmaxf(m0, m1);
 }
 
-template <int VAR>
+// MASK (CHUNKED search): masks[0] gets the chunk tiles attaining the lane's maximum, masks[1]
+// (HITS) the tiles holding a hit (y ≥ hl), bit k for tile q0 + k
+template <int VAR, bool MASK = false, bool HITS = false>
 __device__ inline float dft_compute_stage(const uint4* __restrict__ la, uint32_t nt, uint32_t lane,
                                           const half8_t (&bf)[kDftRangeFrags], uint32_t tb,
                                           const uint2* __restrict__ tguard, uint32_t r1, uint32_t q0 = 0,
-                                          uint32_t q1 = ~0u)
+                                          uint32_t q1 = ~0u, uint32_t* masks = nullptr, float hl = 0.0f)
 {
     const uint4* lc = la + nt * 4u * 64u;
     const uint32_t h = lane >> 5;
@@ -400,7 +402,16 @@ __device__ inline float dft_compute_stage(const uint4* __restrict__ la, uint32_t
         }
         // wave-uniform guard: every partial sum of 4U − Σb² stays within 2^24
         const bool fast = (gfast >> (q - q0)) & 1u;
-        cm = dft_tile_max<VAR>(af, bf, ny, fast, cm);
+        if constexpr (MASK) {
+            const float tm = dft_tile_max<VAR>(af, bf, ny, fast, -__builtin_inff());
+            const uint32_t bit = 1u << (q - q0);
+            masks[0] = tm > cm ? bit : (tm == cm ? masks[0] | bit : masks[0]);
+            if constexpr (HITS)
+                masks[1] |= tm >= hl ? bit : 0u;
+            cm = __builtin_fmaxf(cm, tm);
+        } else {
+            cm = dft_tile_max<VAR>(af, bf, ny, fast, cm);
+        }
     }
     return cm;
 }
@@ -435,16 +446,27 @@ __global__ void __launch_bounds__(64 * WAVES) search_dft(DftArgs d)
 
     float best = -__builtin_inff();
     uint32_t btile = 0;
+    uint32_t masks[2] = {0u, 0u};
     auto finish_stage = [&](float cm, uint32_t tb) {
-        if constexpr (HITS)
-            cm = cm >= hl ? __builtin_inff() : cm; // any hit in the chunk: the first-hit chunk wins
         if constexpr (CHUNKED) {
             static_assert(TPS == 4, "chunk entries assume 4-tile stages");
+            // the entry carries the chunk's tile mask in bits 28..31 of its tile (resolve_dft<true>
+            // evaluates only those tiles): the hit tiles when the chunk holds a hit, else the
+            // tiles attaining the maximum
+            uint32_t msk = masks[0];
+            if constexpr (HITS)
+                if (cm >= hl) {
+                    cm = __builtin_inff();
+                    msk = masks[1];
+                }
             if (active)
                 a.entries[((size_t)(d.choff[blockIdx.x] + (tb - wk.z) / 4u) * WAVES + wv) * 64 + lane] =
-                    make_uint2(__float_as_uint(cm), tb);
+                    make_uint2(__float_as_uint(cm), tb | (msk << 28));
+            masks[0] = masks[1] = 0u;
             return;
         }
+        if constexpr (HITS)
+            cm = cm >= hl ? __builtin_inff() : cm; // any hit in the chunk: the first-hit chunk wins
         if (cm > best) {
             best = cm;
             btile = tb;
@@ -466,7 +488,8 @@ __global__ void __launch_bounds__(64 * WAVES) search_dft(DftArgs d)
             if (st + 1 < nstage && (!SKIPDMA || st == 0))
                 stage_tiles<KS, 64 * WAVES>(lds1, a.dtiles, a.dconst, tb + kTilesPerStage, stage_nt(st + 1));
             for (uint32_t c0 = 0; c0 < stage_nt(st); c0 += 4)
-                finish_stage(dft_compute_stage<VAR>(lds0, stage_nt(st), lane, bf, tb, d.tguard, r1, c0, c0 + 4),
+                finish_stage(dft_compute_stage<VAR, CHUNKED, HITS>(lds0, stage_nt(st), lane, bf, tb, d.tguard, r1, c0,
+                                                                   c0 + 4, masks, hl),
                              tb + c0);
         }
         if (st + 1 < nstage) {
@@ -476,8 +499,9 @@ __global__ void __launch_bounds__(64 * WAVES) search_dft(DftArgs d)
             if (st + 2 < nstage && !SKIPDMA)
                 stage_tiles<KS, 64 * WAVES>(lds0, a.dtiles, a.dconst, tb + kTilesPerStage, stage_nt(st + 2));
             for (uint32_t c0 = 0; c0 < stage_nt(st + 1); c0 += 4)
-                finish_stage(
-                    dft_compute_stage<VAR>(lds1, stage_nt(st + 1), lane, bf, tb, d.tguard, r1, c0, c0 + 4), tb + c0);
+                finish_stage(dft_compute_stage<VAR, CHUNKED, HITS>(lds1, stage_nt(st + 1), lane, bf, tb, d.tguard, r1,
+                                                                   c0, c0 + 4, masks, hl),
+                             tb + c0);
         }
     }
     if (active && !CHUNKED)
@@ -554,7 +578,11 @@ __global__ void __launch_bounds__(256) resolve_dft(MfmaResolveArgs a)
             const int src = __ffsll((long long)match) - 1;
             match &= match - 1;
             const uint32_t j = c0 + (uint32_t)src;
-            const uint2 en = make_uint2(vbits, (uint32_t)__shfl((int)enl.y, src, 64));
+            uint2 en = make_uint2(vbits, (uint32_t)__shfl((int)enl.y, src, 64));
+            // SORTED entries carry the chunk's tile mask in bits 28..31 (search_dft CHUNKED)
+            const uint32_t tmask = SORTED ? (en.y >> 28) : 0xfu;
+            if constexpr (SORTED)
+                en.y &= 0x0fffffffu;
             const int row = (i & 3) + 8 * (i >> 2) + 4 * (int)(j & 1);
             if (!exact) {
                 // fp32 fallback regime: every candidate has S16 ≥ 2^24; any valid domain of the
@@ -568,6 +596,8 @@ __global__ void __launch_bounds__(256) resolve_dft(MfmaResolveArgs a)
                 continue;
             }
             for (uint32_t tile = en.y; tile < min(en.y + (uint32_t)kTilesPerStage, a.ntiles); ++tile) {
+                if (!((tmask >> (tile - en.y)) & 1u))
+                    continue;
                 const int p = a.tile_pos[tile * 32 + row];
                 uint32_t dv[PG / 2] = {};
                 if (p >= 0) {

@@ -225,8 +225,8 @@ __global__ void __launch_bounds__(256) search_valu(SearchArgs a)
 }
 
 // ---------------------------------------------------------------------------
-// fit_winner<N>: one wave per range.  Re-derives the winner's transform from the
-// integer errors of its domain, then TransformMatcher::match_generic's fit
+// fit_winner<N>: one lane group per range (fit_lanes: 16 lanes × 4 pixels at n = 8).
+// Re-derives the winner's transform from the integer errors of its domain, then TransformMatcher::match_generic's fit
 // (encode/transformmatcher.h:89-108).  All of ΣA, ΣA², ΣB = ΣD4/4, ΣAB = X/4
 // are exact in FP64, so s is bit-exact in any summation order; o uses the
 // reference's FMA-contracted form.  Distance = (S16/16)/(domain area), the
@@ -293,18 +293,36 @@ __device__ inline void write_default(frac_encode_item& o, const frac_grid_item& 
     o.match.sh = 0;
 }
 
+// lane groups of L: ranges per wave = 64 / L, 4 pixels per lane (n = 2: one lane per range)
+template <int N>
+constexpr int fit_lanes()
+{
+    return N * N >= 256 ? 64 : (N * N / 4 > 0 ? N * N / 4 : 1);
+}
+
+template <int L>
+__device__ inline int group_sum_i(int v)
+{
+#pragma unroll
+    for (int o = L / 2; o > 0; o >>= 1)
+        v += __shfl_xor(v, o, 64);
+    return v;
+}
+
 template <int N>
 __global__ void __launch_bounds__(256) fit_winner(FitArgs a)
 {
-    constexpr int NN = N * N;
-    const uint32_t r = blockIdx.x * 4u + (threadIdx.x >> 6);
+    constexpr int NN = N * N, L = fit_lanes<N>(), PPL = NN / L, RPW = 64 / L;
     const int lane = threadIdx.x & 63;
+    const uint32_t r = (blockIdx.x * 4u + (threadIdx.x >> 6)) * RPW + (uint32_t)(lane / L);
+    const int sub = lane % L;
+    // whole lane groups leave together below, so the group sums only read live lanes
     if (r >= a.nr)
         return;
     const frac_grid_item rg = a.ranges[r];
     const unsigned long long key = a.best_key[r];
     if (key == kKeyNone) {
-        if (lane == 0) {
+        if (sub == 0) {
             write_default(a.out[r], rg);
             a.aux[r] = RangeAux{0u, (uint32_t)kAuxEmpty};
         }
@@ -320,7 +338,9 @@ __global__ void __launch_bounds__(256) fit_winner(FitArgs a)
     // every sum fits int32 for n ≤ 16 (ΣD4² ≤ 256·1020² < 2^31, X ≤ 256·255·1020 < 2^27)
     int sA = 0, sA2 = 0, sD = 0, sD2 = 0;
     int X[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (int q = lane; q < NN; q += 64) {
+#pragma unroll
+    for (int k = 0; k < PPL; ++k) {
+        const int q = sub * PPL + k;
         const int rv = a.tgt[(size_t)(rg.y + q / N) * a.tstride + rg.x + (q % N)];
         const uint32_t dw = dp[q >> 1];
         const int dv = (q & 1) ? (int)(dw >> 16) : (int)(dw & 0xffffu);
@@ -339,15 +359,15 @@ __global__ void __launch_bounds__(256) fit_winner(FitArgs a)
             }
         }
     }
-    sA = wave_sum_i(sA);
-    sA2 = wave_sum_i(sA2);
-    sD = wave_sum_i(sD);
-    sD2 = wave_sum_i(sD2);
+    sA = group_sum_i<L>(sA);
+    sA2 = group_sum_i<L>(sA2);
+    sD = group_sum_i<L>(sD);
+    sD2 = group_sum_i<L>(sD2);
 #pragma unroll
     for (int t = 0; t < 8; ++t)
         if (t < (int)a.T) // wave-uniform
-            X[t] = wave_sum_i(X[t]);
-    if (lane != 0)
+            X[t] = group_sum_i<L>(X[t]);
+    if (sub != 0)
         return;
     long long S16[8];
     long long minS = LLONG_MAX;
