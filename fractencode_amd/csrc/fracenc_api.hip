@@ -201,6 +201,8 @@ struct frac_ctx {
     DBuf<DecodeState> d_dec_state;
     DecodeState* h_dec_state = nullptr;
     DBuf<uint2> d_dft_tguard;
+    DBuf<uint32_t> d_dft_tpool; // pool rows in tile order (resolve_dft)
+    DBuf<uint32_t> d_dft_rorb;  // range pixel pairs in orbit order, per slot (resolve_dft)
     DBuf<frac_grid_item> d_cls_items;
     DBuf<uint32_t> d_cls_list;
     DBuf<int32_t> d_cls_out;
@@ -214,12 +216,13 @@ struct frac_ctx {
     // SEA engine, tiled form (fracenc_tp.hip)
     bool tp = false;
     TpBuckets tp_bk{};
-    std::vector<uint4> tp_groups, h_tp_work;
+    std::vector<uint4> tp_groups;
+    uint32_t tp_key_bits = 16; // (bucket << 16 | Σ) sort keys: 16 + ⌈log2 nb⌉ bits
     std::vector<uint32_t> tp_iota;
     std::vector<uint2> tp_blk_group;
     DBuf<uint4> d_tp_groups;
     DBuf<uint2> d_tp_blk_group, d_tp_tile_sd, d_tp_blk_sr;
-    DBuf<uint32_t> d_tp_blk_u, d_tp_nch, d_tp_choff, d_tp_blkcnt, d_tp_tot, d_tp_iota;
+    DBuf<uint32_t> d_tp_blk_u, d_tp_nch, d_tp_choff, d_tp_blkcnt, d_tp_tot, d_tp_iota, d_tp_pairs;
     DBuf<int32_t> d_tp_rbk;
     DBuf<uint8_t> d_tp_tmp;
     size_t tp_tmp_bytes = 0;
@@ -514,6 +517,9 @@ int prepare(frac_ctx* c)
             return c->fail(FRAC_E_INVALID, "SEA: too many domain tiles");
         c->ntiles = nt;
         c->nblocks = nbk;
+        c->tp_key_bits = 16;
+        while ((1u << (c->tp_key_bits - 16)) < (uint32_t)nb)
+            ++c->tp_key_bits;
         c->tp_groups.clear();
         c->tp_blk_group.assign(nbk, make_uint2(0xffffffffu, 0u));
         for (int b = 0; b < nb; ++b) {
@@ -733,6 +739,7 @@ int prepare(frac_ctx* c)
         FRAC_HIP(c, c->d_m_rfrags.ensure(std::max<size_t>(nbk * 7 * 64, 1)));
         FRAC_HIP(c, c->d_m_rconst.ensure(std::max<size_t>(nbk * 32, 1)));
         FRAC_HIP(c, c->d_dft_tguard.ensure(std::max<size_t>(nt, 1)));
+        FRAC_HIP(c, c->d_dft_tpool.ensure(std::max<size_t>(nt * 32 * 32, 1)));
         FRAC_HIP(c, c->d_dft_rguard.ensure(std::max<size_t>(nbk, 1)));
         FRAC_HIP(c, c->d_m8_work.ensure(std::max<size_t>(ng, 1)));
         FRAC_HIP(c, c->d_m8_blk_ptr.ensure(nbk + 1));
@@ -744,7 +751,8 @@ int prepare(frac_ctx* c)
         FRAC_HIP(c, c->d_tp_nch.ensure(ng + 1));
         FRAC_HIP(c, c->d_tp_choff.ensure(ng + 1));
         FRAC_HIP(c, c->d_tp_blkcnt.ensure(nbk + 1));
-        FRAC_HIP(c, c->d_tp_tot.ensure(2));
+        FRAC_HIP(c, c->d_tp_tot.ensure(4));
+        FRAC_HIP(c, c->d_tp_pairs.ensure(std::max<size_t>(ng, 1)));
         FRAC_HIP(c, c->d_tp_rbk.ensure(std::max<size_t>(nr, 1)));
         FRAC_TRY(up(c->d_tp_groups.ptr, c->tp_groups.data(), ng * sizeof(uint4)));
         FRAC_TRY(up(c->d_tp_blk_group.ptr, c->tp_blk_group.data(), nbk * sizeof(uint2)));
@@ -856,9 +864,8 @@ inline int launch_dft(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride)
     d.dtiles = c->d_m_dtiles.ptr;
     d.dconst = c->d_m_dconst.ptr;
     FRAC_HIP(c, c->d_dft_tguard.ensure(std::max<size_t>(c->ntiles, 1)));
+    FRAC_HIP(c, c->d_dft_tpool.ensure(std::max<size_t>((size_t)c->ntiles * 32 * 32, 1)));
     FRAC_HIP(c, c->d_dft_rguard.ensure(std::max<size_t>(c->nblocks, 1)));
-    FRAC_HIP(c, hipMemsetAsync(c->d_dft_tguard.ptr, 0, c->ntiles * sizeof(uint2), c->stream));
-    FRAC_HIP(c, hipMemsetAsync(c->d_dft_rguard.ptr, 0, c->nblocks * sizeof(uint32_t), c->stream));
     DftDomainBuildArgs b;
     b.src = c->d_src.ptr;
     b.sstride = c->d_sstride;
@@ -866,6 +873,7 @@ inline int launch_dft(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride)
     b.porig = c->d_porig.ptr;
     b.pool = c->d_pool.ptr;
     b.negsd2 = c->d_negsd2.ptr;
+    b.tpool = c->d_dft_tpool.ptr;
     if (c->ntiles)
         dft_domain_build<<<(c->ntiles * 32 + 255) / 256, 256, 0, c->stream>>>(d, b, c->d_dft_tguard.ptr);
     MfmaRangePrepArgs r;
@@ -877,6 +885,8 @@ inline int launch_dft(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride)
     r.T = 4;
     r.rfrags = c->d_m_rfrags.ptr;
     r.rconst = c->d_m_rconst.ptr;
+    FRAC_HIP(c, c->d_dft_rorb.ensure(std::max<size_t>((size_t)r.nblocks * 32 * 32, 1)));
+    r.rorb = c->d_dft_rorb.ptr;
     if (c->nblocks)
         dft_range_prep<<<(c->nblocks * 32 + 255) / 256, 256, 0, c->stream>>>(r, c->d_dft_rguard.ptr);
     if (c->p.flags & FRAC_FLAG_TIMING)
@@ -970,7 +980,11 @@ inline int launch_dft(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride)
         v.T = 4;
         v.hitH = c->hitH;
         v.best_key = c->d_best_key.ptr;
-        resolve_dft<false><<<(nr + 3) / 4, 256, 0, c->stream>>>(v);
+        v.slot_range = c->d_m_slot_range.ptr;
+        v.nslots = c->nblocks * 32u;
+        v.tpool = c->d_dft_tpool.ptr;
+        v.rorb = c->d_dft_rorb.ptr;
+        resolve_dft<false><<<std::max(1u, (v.nslots + 3) / 4), 256, 0, c->stream>>>(v);
     }
     return FRAC_OK;
 }
@@ -1077,17 +1091,17 @@ int launch_tp(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool timing)
     c->flops_ran = 0;
     c->evaluated_ran = 0;
     if (P) {
-        sea_domain_keys<8><<<(P + 255) / 256, 256, 0, c->stream>>>(c->d_pool.ptr, P, c->d_sea_bend.ptr,
-                                                                   (uint32_t)c->bucket_end.size(), c->d_sea_dkey.ptr,
-                                                                   c->d_sea_dpos.ptr);
+        tp_domain_keys<<<(P + 255) / 256, 256, 0, c->stream>>>(c->d_src.ptr, c->d_sstride, c->d_doms.ptr,
+                                                               c->d_porig.ptr, P, c->d_sea_bend.ptr,
+                                                               (uint32_t)c->bucket_end.size(), c->d_sea_dkey.ptr,
+                                                               c->d_sea_dpos.ptr);
         size_t tb = c->sea_tmp_bytes;
         FRAC_HIP(c, sort_pairs_u32(c->d_sea_tmp.ptr, tb, c->d_sea_dkey.ptr, c->d_sea_dkey2.ptr, c->d_sea_dpos.ptr,
-                                   c->d_sea_dpos2.ptr, P, 20, c->stream));
+                                   c->d_sea_dpos2.ptr, P, c->tp_key_bits, c->stream));
     }
     if (nt) {
         tp_build_tiles<<<(nt * 32 + 255) / 256, 256, 0, c->stream>>>(c->tp_bk, c->d_sea_dkey2.ptr, c->d_sea_dpos2.ptr,
                                                                      nt, c->d_m_tile_pos.ptr, c->d_tp_tile_sd.ptr);
-        FRAC_HIP(c, hipMemsetAsync(c->d_dft_tguard.ptr, 0, nt * sizeof(uint2), c->stream));
         MfmaDomainPrepArgs d;
         d.pool = c->d_pool.ptr;
         d.negsd2 = c->d_negsd2.ptr;
@@ -1102,6 +1116,7 @@ int launch_tp(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool timing)
         b.porig = c->d_porig.ptr;
         b.pool = c->d_pool.ptr;
         b.negsd2 = c->d_negsd2.ptr;
+        b.tpool = c->d_dft_tpool.ptr;
         dft_domain_build<<<(nt * 32 + 255) / 256, 256, 0, c->stream>>>(d, b, c->d_dft_tguard.ptr);
     }
     if (nr) {
@@ -1109,14 +1124,13 @@ int launch_tp(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool timing)
                                                                c->d_sea_rkey.ptr, c->d_sea_rord.ptr);
         size_t tb = c->sea_tmp_bytes;
         FRAC_HIP(c, sort_pairs_u32(c->d_sea_tmp.ptr, tb, c->d_sea_rkey.ptr, c->d_sea_rkey2.ptr, c->d_sea_rord.ptr,
-                                   c->d_sea_rord2.ptr, nr, 20, c->stream));
+                                   c->d_sea_rord2.ptr, nr, c->tp_key_bits, c->stream));
     }
     if (nbk) {
         tp_build_slots<<<(nbk * 32 + 255) / 256, 256, 0, c->stream>>>(c->tp_bk, c->d_sea_rkey2.ptr, c->d_sea_rord2.ptr,
                                                                       nbk, c->d_m_slot_range.ptr,
                                                                       c->d_m_range_slot.ptr, c->d_tp_blk_sr.ptr,
                                                                       c->d_tp_blk_u.ptr);
-        FRAC_HIP(c, hipMemsetAsync(c->d_dft_rguard.ptr, 0, nbk * sizeof(uint32_t), c->stream));
         MfmaRangePrepArgs r;
         r.tgt = dtgt;
         r.tstride = tstride;
@@ -1126,6 +1140,8 @@ int launch_tp(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool timing)
         r.T = 4;
         r.rfrags = c->d_m_rfrags.ptr;
         r.rconst = c->d_m_rconst.ptr;
+        FRAC_HIP(c, c->d_dft_rorb.ensure(std::max<size_t>((size_t)r.nblocks * 32 * 32, 1)));
+        r.rorb = c->d_dft_rorb.ptr;
         dft_range_prep<<<(nbk * 32 + 255) / 256, 256, 0, c->stream>>>(r, c->d_dft_rguard.ptr);
     }
     if (timing)
@@ -1165,6 +1181,7 @@ int launch_tp(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool timing)
     w.hitH = c->hitH;
     w.work = c->d_m8_work.ptr;
     w.nchunks = c->d_tp_nch.ptr;
+    w.pairs = c->d_tp_pairs.ptr;
     FRAC_HIP(c, hipMemsetAsync(c->d_tp_nch.ptr + ng, 0, sizeof(uint32_t), c->stream));
     tp_windows<<<(ng + 255) / 256, 256, 0, c->stream>>>(w);
     size_t tb = c->tp_tmp_bytes;
@@ -1176,23 +1193,20 @@ int launch_tp(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool timing)
     tb = c->tp_tmp_bytes;
     FRAC_HIP(c, hipcub::DeviceScan::ExclusiveSum(c->d_tp_tmp.ptr, tb, c->d_tp_blkcnt.ptr, c->d_m8_blk_ptr.ptr,
                                                  (int)(nbk + 1), c->stream));
-    // sizes of the entry arrays: total chunks and total block → entry links
-    uint32_t tot[2] = {0, 0};
-    c->h_tp_work.resize(ng);
-    FRAC_HIP(c, hipMemcpyAsync(&tot[0], c->d_tp_choff.ptr + ng, sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
-    FRAC_HIP(c, hipMemcpyAsync(&tot[1], c->d_m8_blk_ptr.ptr + nbk, sizeof(uint32_t), hipMemcpyDeviceToHost,
-                               c->stream));
-    FRAC_HIP(c, hipMemcpyAsync(c->h_tp_work.data(), c->d_m8_work.ptr, ng * sizeof(uint4), hipMemcpyDeviceToHost,
-                               c->stream));
+    // sizes of the entry arrays (total chunks, block → entry links) and the searched pairs: one copy
+    tp_totals<<<1, 256, 0, c->stream>>>(c->d_tp_choff.ptr, ng, c->d_m8_blk_ptr.ptr, nbk, c->d_tp_pairs.ptr,
+                                        c->d_tp_tot.ptr);
+    uint32_t tot[4] = {0, 0, 0, 0};
+    FRAC_HIP(c, hipMemcpyAsync(tot, c->d_tp_tot.ptr, sizeof(tot), hipMemcpyDeviceToHost, c->stream));
     FRAC_HIP(c, hipStreamSynchronize(c->stream));
     FRAC_HIP(c, c->d_m_entries.ensure(std::max<size_t>((size_t)tot[0] * kDftBlocksPerWG * 64, 1)));
     FRAC_HIP(c, c->d_m8_blk_ent.ensure(std::max<size_t>(tot[1], 1)));
     tp_fill_entries<<<(nbk + 255) / 256, 256, 0, c->stream>>>(c->d_tp_blk_group.ptr, c->d_tp_choff.ptr,
                                                               c->d_m8_blk_ptr.ptr, nbk, c->d_m8_blk_ent.ptr);
-    for (const uint4& wk : c->h_tp_work) { // issued matrix work and evaluated (slot, domain row) pairs
-        c->flops_ran += (uint64_t)wk.y * (wk.w - wk.z) * 8ull * 32768ull;
-        c->evaluated_ran += (uint64_t)wk.y * 32ull * (wk.w - wk.z) * 32ull;
-    }
+    // issued matrix work (8 MFMA 32×32×16 per block × tile) and evaluated (slot, domain row) pairs
+    const uint64_t pairs = (uint64_t)tot[2] | ((uint64_t)tot[3] << 32);
+    c->flops_ran = pairs * 8ull * 32768ull;
+    c->evaluated_ran = pairs * 32ull * 32ull;
     da.m.entries = c->d_m_entries.ptr;
     da.choff = c->d_tp_choff.ptr;
     if (c->hitH > 0)
@@ -1218,7 +1232,11 @@ int launch_tp(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool timing)
     v.T = 4;
     v.hitH = c->hitH;
     v.best_key = c->d_best_key.ptr;
-    resolve_dft<true><<<(nr + 3) / 4, 256, 0, c->stream>>>(v);
+    v.slot_range = c->d_m_slot_range.ptr;
+    v.nslots = c->nblocks * 32u;
+    v.tpool = c->d_dft_tpool.ptr;
+    v.rorb = c->d_dft_rorb.ptr;
+    resolve_dft<true><<<std::max(1u, (v.nslots + 3) / 4), 256, 0, c->stream>>>(v);
     return FRAC_OK;
 }
 
@@ -1295,8 +1313,10 @@ int launch_all(frac_ctx* c)
     // with the stream)
     FRAC_HIP(c, hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(c->d_fb_count.ptr), (int)fbc, 1, c->stream));
     const bool use_mfma = c->engine == FRAC_ENGINE_MFMA && !c->all_fallback;
-    // the Fourier path builds the pool in its fused domain pass (dft_domain_build)
-    const bool fused_pool = N == 8 && use_mfma && c->p.transforms == 4 && mfma_dft_enabled();
+    // the Fourier path and the SEA engine's tiled form build the pool in their fused domain pass
+    // (dft_domain_build)
+    const bool fused_pool = N == 8 && ((use_mfma && c->p.transforms == 4 && mfma_dft_enabled()) ||
+                                       (c->engine == FRAC_ENGINE_SEA && !c->all_fallback && c->tp));
     if (P && !fused_pool)
         pool_build<N><<<(P + 3) / 4, 256, 0, c->stream>>>(dsrc, c->d_sstride, c->d_doms.ptr, c->d_porig.ptr, P,
                                                           c->d_pool.ptr, c->d_negsd2.ptr);
@@ -1368,7 +1388,8 @@ int launch_all(frac_ctx* c)
         f.aux = c->d_aux.ptr;
         f.fb_count = c->d_fb_count.ptr;
         f.fb_list = c->d_fb_list.ptr;
-        fit_winner<N><<<(nr + 4 * (64 / fit_lanes<N>()) - 1) / (4 * (64 / fit_lanes<N>())), 256, 0, c->stream>>>(f);
+        fit_winner<N><<<std::max(1u, (nr + 4 * (64 / fit_lanes<N>()) - 1) / (4 * (64 / fit_lanes<N>()))), 256, 0,
+                        c->stream>>>(f);
     }
     if (nr) {
         FallbackArgs b;
@@ -1506,6 +1527,7 @@ void frac_destroy(frac_ctx* c)
     c->d_tp_choff.release();
     c->d_tp_blkcnt.release();
     c->d_tp_tot.release();
+    c->d_tp_pairs.release();
     c->d_tp_iota.release();
     c->d_tp_rbk.release();
     c->d_tp_tmp.release();
@@ -1522,6 +1544,8 @@ void frac_destroy(frac_ctx* c)
     if (c->h_dec_state)
         (void)hipHostFree(c->h_dec_state);
     c->d_dft_tguard.release();
+    c->d_dft_tpool.release();
+    c->d_dft_rorb.release();
     c->d_cls_items.release();
     c->d_cls_list.release();
     c->d_cls_out.release();

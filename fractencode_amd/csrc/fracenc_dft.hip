@@ -114,10 +114,11 @@ struct DftArgs {
 // (SamplerBilinear's integer sum, image/sampler.h:21-38, as pool_build), two cells per
 // 32-bit word — (w & 0x00ff00ff) + ((w >> 8) & 0x00ff00ff) over the word of both rows is
 // the packed u16 pair the pool stores — and the same registers feed the tile fragments.
-// Outputs: the pool and −ΣD4² (read by resolve_dft, fit_winner and fallback_fp32); per
-// 32-domain tile the A fragments of the four K-steps [s_b | u_b | γ | δ] (lane l: row l&31,
-// orbit 8(l>>5) + j), −Σb² per row in the [2][16] lane-half layout of the epilogue, and the
-// tile's fast-path guard terms.  Every pool position sits in exactly one tile row.
+// Outputs: the pool and −ΣD4² (read by fit_winner and fallback_fp32), the pool rows again in
+// tile order (resolve_dft); per 32-domain tile the A fragments of the four K-steps
+// [s_b | u_b | γ | δ] (lane l: row l&31, orbit 8(l>>5) + j), −Σb² per row in the [2][16]
+// lane-half layout of the epilogue, and the tile's fast-path guard terms.  Every pool
+// position sits in exactly one tile row.
 // ---------------------------------------------------------------------------
 struct DftDomainBuildArgs {
     const uint8_t* src;
@@ -126,6 +127,7 @@ struct DftDomainBuildArgs {
     const uint32_t* porig;      // pool position → domain index
     uint32_t* pool;             // [P][32] packed u16 pairs of D4
     int32_t* negsd2;            // [P]
+    uint32_t* tpool;            // [ntiles*32][32] the same rows in tile order, orbit order (resolve_dft)
 };
 
 __device__ inline uint32_t pair_sums(uint32_t w0, uint32_t w1)
@@ -179,6 +181,19 @@ __global__ void __launch_bounds__(256) dft_domain_build(MfmaDomainPrepArgs a, Df
 #pragma unroll
         for (int k = 0; k < NN / 8; ++k)
             pw[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
+        // the tile-order copy for resolve_dft, orbit o as (D_{o,0} | D_{o,1} << 16), (D_{o,2} | D_{o,3} << 16)
+        auto cell = [&](int q) { return (w[q >> 1] >> (16 * (q & 1))) & 0xffffu; };
+        uint4* tw = reinterpret_cast<uint4*>(s.tpool + (size_t)gid * (NN / 2));
+#pragma unroll
+        for (int v = 0; v < NN / 8; ++v) {
+            uint32_t d[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int o = 2 * v + (e >> 1), k = 2 * (e & 1);
+                d[e] = cell(kOrb8.p[o][k]) | (cell(kOrb8.p[o][k + 1]) << 16);
+            }
+            tw[v] = make_uint4(d[0], d[1], d[2], d[3]);
+        }
         s.negsd2[p] = -sq;
     } else {
 #pragma unroll
@@ -220,10 +235,16 @@ __global__ void __launch_bounds__(256) dft_domain_build(MfmaDomainPrepArgs a, Df
     const float ny = p >= 0 ? -(float)sb2 : kDftPadY;
     const uint32_t h = (row >> 2) & 1u, i = (row & 3u) + 4u * (row >> 3);
     a.dconst[(size_t)tile * 32 + h * 16 + i] = __float_as_uint(ny);
-    if (p >= 0) {
-        atomicMax(&tguard[tile].x, (uint32_t)(4 * dinf));
-        atomicMax(&tguard[tile].y, (uint32_t)sb2);
+    // the tile's guard terms over its valid rows: a 32-lane maximum (whole tiles leave together
+    // above), one writer per tile
+    uint32_t gx = p >= 0 ? (uint32_t)(4 * dinf) : 0u, gy = p >= 0 ? (uint32_t)sb2 : 0u;
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) {
+        gx = max(gx, (uint32_t)__shfl_xor((int)gx, o, 64));
+        gy = max(gy, (uint32_t)__shfl_xor((int)gy, o, 64));
     }
+    if (row == 0)
+        tguard[tile] = make_uint2(gx, gy);
 }
 
 // ---------------------------------------------------------------------------
@@ -245,11 +266,24 @@ __global__ void __launch_bounds__(256) dft_range_prep(MfmaRangePrepArgs a, uint3
     int sa2 = 0;
     if (ri >= 0) {
         const frac_grid_item rg = a.ranges[ri];
+        const uint8_t* base = a.tgt + (size_t)rg.y * a.tstride + rg.x;
+        if ((((uintptr_t)base | a.tstride) & 7u) == 0) {
+            // one 8-byte load per row (range origins on the 8-pixel grid)
 #pragma unroll
-        for (int q = 0; q < NN; ++q) {
-            av[q] = (int)a.tgt[(size_t)(rg.y + q / N) * a.tstride + rg.x + (q % N)] - 128;
-            sa2 += av[q] * av[q];
+            for (int y = 0; y < N; ++y) {
+                const uint2 w = *reinterpret_cast<const uint2*>(base + (size_t)y * a.tstride);
+#pragma unroll
+                for (int x = 0; x < N; ++x)
+                    av[y * N + x] = (int)(((x < 4 ? w.x : w.y) >> (8 * (x & 3))) & 0xffu) - 128;
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < NN; ++q)
+                av[q] = (int)base[(size_t)(q / N) * a.tstride + (q % N)] - 128;
         }
+#pragma unroll
+        for (int q = 0; q < NN; ++q)
+            sa2 += av[q] * av[q];
     } else {
 #pragma unroll
         for (int q = 0; q < NN; ++q)
@@ -281,7 +315,27 @@ __global__ void __launch_bounds__(256) dft_range_prep(MfmaRangePrepArgs a, uint3
             a.rfrags[((size_t)b * kDftRangeFrags + f) * 64 + col + 32 * h] = __builtin_bit_cast(uint4, v8);
         }
     a.rconst[gid] = ri >= 0 ? (uint32_t)(16 * sa2) : 0u; // 16Σa² ≤ 2^24
-    atomicMax(&rguard[b], (uint32_t)r1);
+    if (a.rorb) {
+        // raw pixels r = a + 128, orbit o as the pairs (r_{o,0} | r_{o,1} << 16), (r_{o,2} | r_{o,3} << 16)
+        uint4* ro = reinterpret_cast<uint4*>(a.rorb + (size_t)gid * 32);
+#pragma unroll
+        for (int v = 0; v < 8; ++v) {
+            uint32_t d[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int o = 2 * v + (e >> 1), k = 2 * (e & 1);
+                d[e] = (uint32_t)(av[kOrb8.p[o][k]] + 128) | ((uint32_t)(av[kOrb8.p[o][k + 1]] + 128) << 16);
+            }
+            ro[v] = make_uint4(d[0], d[1], d[2], d[3]);
+        }
+    }
+    // the block's guard: a 32-lane maximum (whole blocks leave together above), one writer
+    uint32_t g1 = (uint32_t)r1;
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1)
+        g1 = max(g1, (uint32_t)__shfl_xor((int)g1, o, 64));
+    if (col == 0)
+        rguard[b] = g1;
 }
 
 // ---------------------------------------------------------------------------
@@ -518,22 +572,44 @@ __global__ void __launch_bounds__(64 * WAVES) search_dft(DftArgs d)
 // ---------------------------------------------------------------------------
 // SORTED (tiles in ΣD4 order, fracenc_tp.hip): rows and tiles are not in domain order, so the
 // least key over every matching row of every tile of the chunk is taken (no first-row shortcut).
-template <bool SORTED = false>
-__global__ void __launch_bounds__(256) resolve_dft(MfmaResolveArgs a)
+template <bool SORTED>
+__device__ inline void resolve_dft_slot(const MfmaResolveArgs& a, uint32_t slot, int lane)
 {
-    constexpr int N = 8, NN = 64, PG = 16, T = 4;
-    const uint32_t r = blockIdx.x * 4u + (threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    if (r >= a.nr)
+    constexpr int PG = 16, T = 4;
+    const int ri = a.slot_range[slot];
+    if (ri < 0)
         return;
-    const uint32_t slot = a.range_slot[r];
+    const uint32_t r = (uint32_t)ri;
     const uint32_t blk = slot >> 5, col = slot & 31u;
+    const int i = lane >> 2, g = lane & 3;
+    // lane (i, g) holds orbits 4g..4g+3 of the range as pixel pairs (dft_range_prep) and meets
+    // the same orbits of a domain row (tile-order pool, dft_domain_build). With fwd(t) = g^t,
+    //   X_t = Σ_q r(q)·D4(fwd_t q) = Σ_{o,k} r_{o,k}·D_{o,k+t}:
+    // t = 0 pairs (A, B) = (D0|D1, D2|D3), t = 2 the swapped pairs (B, A), t = 1 the rotated
+    // pairs (D1|D2, D3|D0) = (alignbit(B, A, 16), alignbit(A, B, 16)) and t = 3 those swapped —
+    // two v_alignbit per orbit for all four transforms.
+    const uint4* rp4 = reinterpret_cast<const uint4*>(a.rorb + (size_t)slot * 32 + g * (PG / 2));
+    const uint4 r0 = rp4[0], r1 = rp4[1];
+    const uint32_t rp[PG / 2] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
+    uint32_t sr2u = 0;
+#pragma unroll
+    for (int q = 0; q < PG / 2; ++q)
+        sr2u = __builtin_amdgcn_udot2(__builtin_bit_cast(ushort2_t, rp[q]), __builtin_bit_cast(ushort2_t, rp[q]), sr2u,
+                                      false);
+    sr2u += (uint32_t)__shfl_xor((int)sr2u, 1, 64);
+    sr2u += (uint32_t)__shfl_xor((int)sr2u, 2, 64);
+    const int sr2 = (int)sr2u; // Σr² ≤ 64·255²
     const uint32_t e0 = a.blk_ptr[blk], e1 = a.blk_ptr[blk + 1];
     const uint32_t nent = (e1 - e0) * 2u;
+    // the first 64 entries stay in registers for the ballot walk below
+    uint2 en0 = make_uint2(0u, 0u);
     float vmax = -__builtin_inff();
-    for (uint32_t j = lane; j < nent; j += 64)
-        vmax = __builtin_fmaxf(vmax,
-                               __uint_as_float(a.entries[(size_t)a.blk_ent[e0 + j / 2] * 64 + col + 32 * (j & 1)].x));
+    for (uint32_t j = lane; j < nent; j += 64) {
+        const uint2 v = a.entries[(size_t)a.blk_ent[e0 + j / 2] * 64 + col + 32 * (j & 1)];
+        if (j < 64)
+            en0 = v;
+        vmax = __builtin_fmaxf(vmax, __uint_as_float(v.x));
+    }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1)
         vmax = __builtin_fmaxf(vmax, __shfl_xor(vmax, o, 64));
@@ -544,26 +620,6 @@ __global__ void __launch_bounds__(256) resolve_dft(MfmaResolveArgs a)
     const bool exact = sentinel || vmax > (float)(sa16 - kExactLimit);
     const int64_t target = exact && !sentinel ? sa16 - (int64_t)vmax : -1;
     const bool hit = a.hitH >= 0 && (sentinel || (target >= 0 && target <= a.hitH));
-    const frac_grid_item rg = a.ranges[r];
-    const int i = lane >> 2, g = lane & 3;
-    // the range's pixel q on lane q; lane (i, g) then holds, per transform, the inverse-
-    // permuted pixels of decimated cells k ∈ [16g, 16g + 16) as packed u16 pairs, so that
-    // X_t = Σ_k r[inv_t(k)]·D4[k] is 8 v_dot2_u32_u16 against two dwordx4 of the pool
-    const int rv = (int)a.tgt[(size_t)(rg.y + lane / N) * a.tstride + rg.x + (lane % N)];
-    int sr2 = rv * rv;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1)
-        sr2 += __shfl_xor(sr2, o, 64);
-    uint32_t pk[T][PG / 2];
-#pragma unroll
-    for (int t = 0; t < T; ++t)
-#pragma unroll
-        for (int j = 0; j < PG / 2; ++j) {
-            const int k = g * PG + 2 * j;
-            const uint32_t lo = (uint32_t)__shfl(rv, inv_index<N>(t, k), 64);
-            const uint32_t hi = (uint32_t)__shfl(rv, inv_index<N>(t, k + 1), 64);
-            pk[t][j] = lo | (hi << 16);
-        }
     unsigned long long bestk = kKeyNone;
     const uint32_t vbits = __float_as_uint(vmax);
     // only the entries holding the maximum are re-evaluated (usually one): the lanes test 64
@@ -571,8 +627,9 @@ __global__ void __launch_bounds__(256) resolve_dft(MfmaResolveArgs a)
     // with the number of domain splits (many splits per block when ranges are sharded)
     for (uint32_t c0 = 0; c0 < nent; c0 += 64) {
         const uint32_t jl = c0 + (uint32_t)lane;
-        const uint2 enl = jl < nent ? a.entries[(size_t)a.blk_ent[e0 + jl / 2] * 64 + col + 32 * (jl & 1)]
-                                    : make_uint2(0u, 0u);
+        const uint2 enl = jl >= nent ? make_uint2(0u, 0u)
+                          : c0 == 0  ? en0
+                                     : a.entries[(size_t)a.blk_ent[e0 + jl / 2] * 64 + col + 32 * (jl & 1)];
         unsigned long long match = __ballot(jl < nent && enl.x == vbits);
         while (match) {
             const int src = __ffsll((long long)match) - 1;
@@ -598,23 +655,37 @@ __global__ void __launch_bounds__(256) resolve_dft(MfmaResolveArgs a)
             for (uint32_t tile = en.y; tile < min(en.y + (uint32_t)kTilesPerStage, a.ntiles); ++tile) {
                 if (!((tmask >> (tile - en.y)) & 1u))
                     continue;
+                // the row's pool position (for the key) and its D4 from the tile-order copy are
+                // independent loads; ΣD4² is summed here rather than loaded through the position
                 const int p = a.tile_pos[tile * 32 + row];
-                uint32_t dv[PG / 2] = {};
-                if (p >= 0) {
-                    const uint4* dp = reinterpret_cast<const uint4*>(a.pool + (size_t)p * (NN / 2) + g * (PG / 2));
-                    const uint4 d0 = dp[0], d1 = dp[1];
-                    dv[0] = d0.x, dv[1] = d0.y, dv[2] = d0.z, dv[3] = d0.w;
-                    dv[4] = d1.x, dv[5] = d1.y, dv[6] = d1.z, dv[7] = d1.w;
+                const uint4* dp = reinterpret_cast<const uint4*>(a.tpool + ((size_t)tile * 32 + row) * 32 + g * (PG / 2));
+                const uint4 d0 = dp[0], d1 = dp[1];
+                const uint32_t dv[PG / 2] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w};
+                uint32_t dr[PG / 2]; // t = 1 pairs
+#pragma unroll
+                for (int o = 0; o < PG / 4; ++o) {
+                    dr[2 * o] = __builtin_amdgcn_alignbit(dv[2 * o + 1], dv[2 * o], 16);
+                    dr[2 * o + 1] = __builtin_amdgcn_alignbit(dv[2 * o], dv[2 * o + 1], 16);
                 }
-                const int nsd2 = p >= 0 ? a.negsd2[p] : 0;
+                uint32_t sd2 = 0;
+#pragma unroll
+                for (int q = 0; q < PG / 2; ++q)
+                    sd2 = __builtin_amdgcn_udot2(__builtin_bit_cast(ushort2_t, dv[q]), __builtin_bit_cast(ushort2_t, dv[q]),
+                                                 sd2, false);
+                sd2 += (uint32_t)__shfl_xor((int)sd2, 1, 64);
+                sd2 += (uint32_t)__shfl_xor((int)sd2, 2, 64);
+                const int nsd2 = -(int)sd2; // ΣD4² ≤ 64·1020² < 2^31
                 unsigned long long tk = kKeyNone;
 #pragma unroll
                 for (int t = 0; t < T; ++t) {
                     uint32_t X = 0;
 #pragma unroll
-                    for (int q = 0; q < PG / 2; ++q)
-                        X = __builtin_amdgcn_udot2(__builtin_bit_cast(ushort2_t, pk[t][q]),
-                                                   __builtin_bit_cast(ushort2_t, dv[q]), X, false);
+                    for (int q = 0; q < PG / 2; ++q) {
+                        // pair q of orbit q/2 for transform t (see the lane map above)
+                        const uint32_t dq = (t & 1) ? dr[q ^ (t >> 1)] : dv[q ^ (t >> 1)];
+                        X = __builtin_amdgcn_udot2(__builtin_bit_cast(ushort2_t, rp[q]), __builtin_bit_cast(ushort2_t, dq),
+                                                   X, false);
+                    }
                     X += (uint32_t)__shfl_xor((int)X, 1, 64);
                     X += (uint32_t)__shfl_xor((int)X, 2, 64);
                     // S16 = 16Σr² − 8X + ΣD4² ≤ 64·1020² < 2^31: exact in int32
@@ -654,6 +725,19 @@ __global__ void __launch_bounds__(256) resolve_dft(MfmaResolveArgs a)
     }
     if (lane == 0)
         a.best_key[r] = bestk;
+}
+
+// One wave per slot, in slot order (the 32 ranges of a block read the same entry lines back to
+// back). A grid of fewer, longer-lived waves striding over the slots measured slower (452 vs
+// 372 µs at C3 in the SEA tiled form).
+
+template <bool SORTED = false>
+__global__ void __launch_bounds__(256) resolve_dft(MfmaResolveArgs a)
+{
+    // the slot is wave-uniform: readfirstlane lets its loads go through the scalar unit
+    const uint32_t slot = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
+    if (slot < a.nslots)
+        resolve_dft_slot<SORTED>(a, slot, threadIdx.x & 63);
 }
 
 } // namespace fracenc

@@ -93,7 +93,7 @@ __device__ inline uint32_t pix_pair(const uint32_t (&pk)[(N * N + 3) / 4], int i
 }
 
 // Loads an N×N u8 block, four pixels per dword in row-major order.  Rows are read
-// as aligned dwords and realigned with v_alignbyte_b32 (any x), which keeps only a
+// as aligned dwords and realigned with v_alignbit_b32 (any x), which keeps only a
 // few loads in flight per row; the device plane has a slack row, so reading up to
 // 4 bytes past a row end stays in bounds.
 template <int N>
@@ -119,7 +119,7 @@ __device__ inline void load_range_packed(const uint8_t* __restrict__ plane, uint
                 w[i] = base[i];
 #pragma unroll
             for (int i = 0; i < W; ++i)
-                pk[r * W + i] = __builtin_amdgcn_alignbyte(w[i + 1], w[i], sh * 8u);
+                pk[r * W + i] = __builtin_amdgcn_alignbit(w[i + 1], w[i], sh * 8u); // shift in bits
         }
     }
 }
@@ -310,12 +310,9 @@ __device__ inline int group_sum_i(int v)
 }
 
 template <int N>
-__global__ void __launch_bounds__(256) fit_winner(FitArgs a)
+__device__ inline void fit_range(const FitArgs& a, uint32_t r, int sub)
 {
-    constexpr int NN = N * N, L = fit_lanes<N>(), PPL = NN / L, RPW = 64 / L;
-    const int lane = threadIdx.x & 63;
-    const uint32_t r = (blockIdx.x * 4u + (threadIdx.x >> 6)) * RPW + (uint32_t)(lane / L);
-    const int sub = lane % L;
+    constexpr int NN = N * N, L = fit_lanes<N>(), PPL = NN / L;
     // whole lane groups leave together below, so the group sums only read live lanes
     if (r >= a.nr)
         return;
@@ -400,6 +397,17 @@ __global__ void __launch_bounds__(256) fit_winner(FitArgs a)
     write_fit(a.out[r], rg, d, tsel, (double)sA, (double)sA2, (double)sD * 0.25, (double)X[tsel] * 0.25, Nd, a.smax,
               dist);
     a.aux[r] = RangeAux{p, flags};
+}
+
+// one wave per 64 / L ranges (a grid-stride form over fewer waves measured slower)
+
+template <int N>
+__global__ void __launch_bounds__(256) fit_winner(FitArgs a)
+{
+    constexpr int L = fit_lanes<N>(), RPW = 64 / L;
+    const int lane = threadIdx.x & 63;
+    const uint32_t w = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
+    fit_range<N>(a, w * RPW + (uint32_t)(lane / L), lane % L);
 }
 
 // ---------------------------------------------------------------------------

@@ -112,6 +112,7 @@ struct MfmaRangePrepArgs {
     uint32_t T;
     uint4* rfrags;             // [nblocks][T][KS][64]
     uint32_t* rconst;          // [nblocks*32]
+    uint32_t* rorb = nullptr;  // dft_range_prep: [nblocks*32][32] pixel pairs in orbit order (resolve_dft)
 };
 
 template <int N>
@@ -499,6 +500,11 @@ struct MfmaResolveArgs {
     uint32_t T;
     int64_t hitH;               // −1: no hits
     unsigned long long* best_key;
+    // resolve_dft only: waves walk the slots; D4 rows in tile order (dft_domain_build)
+    const int32_t* slot_range;  // [nslots] range of each slot, −1 padding
+    uint32_t nslots;
+    const uint32_t* tpool;      // [ntiles*32][32] D4 pairs in orbit order (dft_domain_build)
+    const uint32_t* rorb;       // [nslots][32] range pixel pairs in orbit order (dft_range_prep)
 };
 
 __device__ inline int fwd_rt(const Aff& a, int N, int q)

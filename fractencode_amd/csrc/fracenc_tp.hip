@@ -30,7 +30,7 @@ struct TpBuckets {
     uint32_t rng_begin[kTpMaxBuckets], rng_count[kTpMaxBuckets];   // sorted ranges
 };
 
-// range sort key: (bucket << 17) | ΣR (ΣR = 4Σr ≤ 65280)
+// range sort key: (bucket << 16) | ΣR (ΣR = 4Σr ≤ 65280 < 2^16)
 __global__ void __launch_bounds__(256) tp_range_keys(const uint8_t* __restrict__ tgt, uint32_t tstride,
                                                      const frac_grid_item* __restrict__ ranges,
                                                      const int32_t* __restrict__ rbucket_idx, uint32_t nr,
@@ -45,8 +45,48 @@ __global__ void __launch_bounds__(256) tp_range_keys(const uint8_t* __restrict__
 #pragma unroll
         for (int x = 0; x < 8; ++x)
             s += tgt[(size_t)(rg.y + y) * tstride + rg.x + x];
-    key[r] = ((uint32_t)rbucket_idx[r] << 17) | (4u * s);
+    key[r] = ((uint32_t)rbucket_idx[r] << 16) | (4u * s);
     idx[r] = r;
+}
+
+// domain sort key (bucket << 16) | ΣD4 straight from the plane — ΣD4 is the domain's pixel sum
+// (≤ 256·255 < 2^16) — so the pool is built once, by dft_domain_build, after the sort
+__device__ inline uint32_t byte_sum4(uint32_t w)
+{
+    const uint32_t t = (w & 0x00ff00ffu) + ((w >> 8) & 0x00ff00ffu);
+    return (t & 0xffffu) + (t >> 16);
+}
+
+__global__ void __launch_bounds__(256) tp_domain_keys(const uint8_t* __restrict__ src, uint32_t sstride,
+                                                      const frac_grid_item* __restrict__ doms,
+                                                      const uint32_t* __restrict__ porig, uint32_t P,
+                                                      const uint32_t* __restrict__ bucket_end, uint32_t nb,
+                                                      uint32_t* __restrict__ key, uint32_t* __restrict__ pos)
+{
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= P)
+        return;
+    const frac_grid_item d = doms[porig[p]];
+    const uint8_t* base = src + (size_t)d.y * sstride + d.x;
+    uint32_t sd = 0;
+    if ((((uintptr_t)base | sstride) & 7u) == 0) {
+#pragma unroll
+        for (int y = 0; y < 16; ++y) {
+            const uint2* row = reinterpret_cast<const uint2*>(base + (size_t)y * sstride);
+            const uint2 a = row[0], b = row[1];
+            sd += byte_sum4(a.x) + byte_sum4(a.y) + byte_sum4(b.x) + byte_sum4(b.y);
+        }
+    } else {
+        for (int y = 0; y < 16; ++y)
+#pragma unroll
+            for (int x = 0; x < 16; ++x)
+                sd += base[(size_t)y * sstride + x];
+    }
+    uint32_t b = 0;
+    while (b + 1 < nb && p >= bucket_end[b])
+        ++b;
+    key[p] = (b << 16) | sd;
+    pos[p] = p;
 }
 
 // tile rows from the sorted domain order; per tile [min, max] ΣD4 of its valid rows
@@ -66,8 +106,8 @@ __global__ void __launch_bounds__(256) tp_build_tiles(TpBuckets bk, const uint32
     tile_pos[gid] = valid ? (int32_t)spos[bk.dom_begin[b] + k] : -1;
     if (row == 0) {
         const uint32_t last = min(k + 31u, bk.dom_count[b] - 1u);
-        tile_sd[tile] = valid ? make_uint2(skey[bk.dom_begin[b] + k] & 0x1ffffu,
-                                           skey[bk.dom_begin[b] + last] & 0x1ffffu)
+        tile_sd[tile] = valid ? make_uint2(skey[bk.dom_begin[b] + k] & 0xffffu,
+                                           skey[bk.dom_begin[b] + last] & 0xffffu)
                               : make_uint2(0xffffffffu, 0u);
     }
 }
@@ -94,7 +134,7 @@ __global__ void __launch_bounds__(256) tp_build_slots(TpBuckets bk, const uint32
         range_slot[r] = gid;
     if (col == 0) {
         const uint32_t last = min(k + 31u, bk.rng_count[b] - 1u);
-        blk_sr[blk] = make_uint2(rkey[bk.rng_begin[b] + k] & 0x1ffffu, rkey[bk.rng_begin[b] + last] & 0x1ffffu);
+        blk_sr[blk] = make_uint2(rkey[bk.rng_begin[b] + k] & 0xffffu, rkey[bk.rng_begin[b] + last] & 0xffffu);
         blk_u[blk] = 0u;
     }
 }
@@ -121,8 +161,9 @@ __global__ void __launch_bounds__(256) tp_seed_work(const uint4* __restrict__ gr
     work[gi] = make_uint4(gr.x, gr.y, gr.z + lo, gr.z + lo + 1);
 }
 
-// per range slot: the seed search's maximum y over the seed tile → U = 16Σa² − y, the least
-// exact error over that tile (exact regime; else no bound), atomicMax into the block's bound
+// per block: the seed search's maximum y over the seed tile gives each slot U = 16Σa² − y, the
+// least exact error over that tile (exact regime; else no bound); the block's bound is the
+// greatest U over its slots (a 32-lane reduction, one writer per block)
 __global__ void __launch_bounds__(256) tp_seed_reduce(const uint2* __restrict__ blk_group,
                                                       const uint2* __restrict__ entries,
                                                       const int32_t* __restrict__ slot_range,
@@ -130,18 +171,25 @@ __global__ void __launch_bounds__(256) tp_seed_reduce(const uint2* __restrict__ 
                                                       uint32_t* __restrict__ blk_u)
 {
     const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
-    if (gid >= nblocks * 32u)
+    if (gid >= nblocks * 32u) // whole blocks: the 32 lanes of a block leave together
         return;
     const uint32_t b = gid >> 5, col = gid & 31u;
     const uint2 gw = blk_group[b];
-    if (gw.x == 0xffffffffu || slot_range[gid] < 0)
+    if (gw.x == 0xffffffffu)
         return;
-    const size_t e = ((size_t)gw.x * 8u + gw.y) * 64u + col;
-    const float y = fmaxf(__uint_as_float(entries[e].x), __uint_as_float(entries[e + 32].x));
-    const int64_t sa16 = (int64_t)rconst[gid];
-    // y = 16Σa² − min S16 is exact while min S16 < 2^24 (fracenc_dft.hip)
-    const uint32_t u = y > (float)(sa16 - kExactLimit) ? (uint32_t)(sa16 - (int64_t)y) : 0xffffffffu;
-    atomicMax(&blk_u[b], u);
+    uint32_t u = 0u;
+    if (slot_range[gid] >= 0) {
+        const size_t e = ((size_t)gw.x * 8u + gw.y) * 64u + col;
+        const float y = fmaxf(__uint_as_float(entries[e].x), __uint_as_float(entries[e + 32].x));
+        const int64_t sa16 = (int64_t)rconst[gid];
+        // y = 16Σa² − min S16 is exact while min S16 < 2^24 (fracenc_dft.hip)
+        u = y > (float)(sa16 - kExactLimit) ? (uint32_t)(sa16 - (int64_t)y) : 0xffffffffu;
+    }
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1)
+        u = max(u, (uint32_t)__shfl_xor((int)u, o, 64));
+    if (col == 0)
+        blk_u[b] = u;
 }
 
 // per group of ≤ 8 blocks: the tile window and its chunk count
@@ -154,6 +202,7 @@ struct TpWindowArgs {
     int64_t hitH;         // −1: no hits
     uint4* work;          // [ngroups] {first block, nblocks, t0, t1}
     uint32_t* nchunks;    // [ngroups]
+    uint32_t* pairs;      // [ngroups] block × tile pairs searched (frac_stats)
 };
 
 __global__ void __launch_bounds__(256) tp_windows(TpWindowArgs a)
@@ -196,6 +245,31 @@ __global__ void __launch_bounds__(256) tp_windows(TpWindowArgs a)
     }
     a.work[gi] = make_uint4(gr.x, gr.y, t0, t1);
     a.nchunks[gi] = (t1 - t0 + 3) / 4;
+    a.pairs[gi] = gr.y * (t1 - t0);
+}
+
+// the totals the host needs in one 16-byte copy: {chunks, block → entry links, Σ pairs (u64)}
+__global__ void __launch_bounds__(256) tp_totals(const uint32_t* __restrict__ choff, uint32_t ngroups,
+                                                 const uint32_t* __restrict__ blk_ptr, uint32_t nblocks,
+                                                 const uint32_t* __restrict__ pairs, uint32_t* __restrict__ tot)
+{
+    __shared__ unsigned long long part[4];
+    unsigned long long s = 0;
+    for (uint32_t g = threadIdx.x; g < ngroups; g += blockDim.x)
+        s += pairs[g];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1)
+        s += __shfl_xor(s, o, 64);
+    if ((threadIdx.x & 63u) == 0)
+        part[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned long long t = part[0] + part[1] + part[2] + part[3];
+        tot[0] = choff[ngroups];
+        tot[1] = blk_ptr[nblocks];
+        tot[2] = (uint32_t)t;
+        tot[3] = (uint32_t)(t >> 32);
+    }
 }
 
 // per block: entry count = its group's chunk count

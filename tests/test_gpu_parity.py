@@ -315,3 +315,26 @@ def test_sea_skips_most_candidates_with_identical_records():
     assert sa["evaluated_mappings"] == len(doms) * len(rngs)
     assert 0 < sb["evaluated_mappings"] < 0.2 * sa["evaluated_mappings"]
     assert sb["search_form"] == F.FORM_SEA
+
+
+@pytest.mark.parametrize("engine", ENGINES)
+@pytest.mark.parametrize("n", [4, 8])
+def test_unaligned_origins(oracle, engine, n):
+    """Ranges and domains at origins off the 4- and 8-pixel grid (a grid offset by (3, 5) with
+    odd strides): every engine's loaders realign the rows and match the oracle."""
+    rng = np.random.default_rng(11 + n)
+    W, H = 96, 80
+    p = rng.integers(0, 256, (H, W), dtype=np.uint8)
+
+    def grid(size, step, x0, y0):
+        out = [(x, y, size, size, 0) for y in range(y0, H - size + 1, step) for x in range(x0, W - size + 1, step)]
+        return np.array(out, dtype=F.GRID_ITEM)
+
+    doms = grid(2 * n, n + 1, 3, 5)
+    rngs = grid(n, n + 3, 1, 2)
+    with F.Engine(0, 4, False, 0.0, -1.0, engine) as e:
+        e.set_frame(p)
+        e.set_domains(doms)
+        out, _ = e.search(rngs)
+    want, _, _ = oracle.estimate(p, doms, rngs)
+    assert_same(out, {k: want[k] for k in FIELDS}, f"unaligned n={n}")
