@@ -203,6 +203,7 @@ struct frac_ctx {
     DBuf<uint2> d_dft_tguard;
     DBuf<uint32_t> d_dft_tpool; // pool rows in tile order (resolve_dft)
     DBuf<uint32_t> d_dft_rorb;  // range pixel pairs in orbit order, per slot (resolve_dft)
+    DBuf<uint4> d_rstat;        // per range: the winner's sums (resolve_dft → fit_rstat)
     DBuf<frac_grid_item> d_cls_items;
     DBuf<uint32_t> d_cls_list;
     DBuf<int32_t> d_cls_out;
@@ -244,6 +245,7 @@ struct frac_ctx {
     bool ran = false;
     uint32_t engine_ran = FRAC_ENGINE_VALU;
     uint32_t form_ran = FRAC_FORM_DOT2;
+    bool fit_rstat = false; // resolve_dft recorded the winners' sums (fit_rstat instead of fit_winner)
     uint64_t flops_ran = 0;
 
     int fail(int code, const std::string& msg)
@@ -984,6 +986,9 @@ inline int launch_dft(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride)
         v.nslots = c->nblocks * 32u;
         v.tpool = c->d_dft_tpool.ptr;
         v.rorb = c->d_dft_rorb.ptr;
+        FRAC_HIP(c, c->d_rstat.ensure(std::max<size_t>(nr, 1)));
+        v.rstat = c->d_rstat.ptr;
+        c->fit_rstat = true;
         resolve_dft<false><<<std::max(1u, (v.nslots + 3) / 4), 256, 0, c->stream>>>(v);
     }
     return FRAC_OK;
@@ -1236,6 +1241,9 @@ int launch_tp(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool timing)
     v.nslots = c->nblocks * 32u;
     v.tpool = c->d_dft_tpool.ptr;
     v.rorb = c->d_dft_rorb.ptr;
+    FRAC_HIP(c, c->d_rstat.ensure(std::max<size_t>(nr, 1)));
+    v.rstat = c->d_rstat.ptr;
+    c->fit_rstat = true;
     resolve_dft<true><<<std::max(1u, (v.nslots + 3) / 4), 256, 0, c->stream>>>(v);
     return FRAC_OK;
 }
@@ -1312,6 +1320,7 @@ int launch_all(frac_ctx* c)
     // a device-side fill, not an H2D copy from pageable host memory (which serialises the host
     // with the stream)
     FRAC_HIP(c, hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(c->d_fb_count.ptr), (int)fbc, 1, c->stream));
+    c->fit_rstat = false;
     const bool use_mfma = c->engine == FRAC_ENGINE_MFMA && !c->all_fallback;
     // the Fourier path and the SEA engine's tiled form build the pool in their fused domain pass
     // (dft_domain_build)
@@ -1388,8 +1397,11 @@ int launch_all(frac_ctx* c)
         f.aux = c->d_aux.ptr;
         f.fb_count = c->d_fb_count.ptr;
         f.fb_list = c->d_fb_list.ptr;
-        fit_winner<N><<<std::max(1u, (nr + 4 * (64 / fit_lanes<N>()) - 1) / (4 * (64 / fit_lanes<N>()))), 256, 0,
-                        c->stream>>>(f);
+        if (c->fit_rstat)
+            fit_rstat<N><<<(nr + 255) / 256, 256, 0, c->stream>>>(f, c->d_rstat.ptr);
+        else
+            fit_winner<N><<<std::max(1u, (nr + 4 * (64 / fit_lanes<N>()) - 1) / (4 * (64 / fit_lanes<N>()))), 256, 0,
+                            c->stream>>>(f);
     }
     if (nr) {
         FallbackArgs b;
@@ -1546,6 +1558,7 @@ void frac_destroy(frac_ctx* c)
     c->d_dft_tguard.release();
     c->d_dft_tpool.release();
     c->d_dft_rorb.release();
+    c->d_rstat.release();
     c->d_cls_items.release();
     c->d_cls_list.release();
     c->d_cls_out.release();

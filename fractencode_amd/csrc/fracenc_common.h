@@ -79,6 +79,27 @@ __host__ __device__ inline unsigned long long key_hit(uint32_t pos, uint32_t t)
     return ((unsigned long long)pos << 3) | t;
 }
 
+// Cross-lane exchanges without __shfl_xor's bounds checks (which cost 4 VALU per exchange):
+// xor 1 / xor 2 inside quads as DPP quad_perm moves (a VALU operand modifier), larger
+// distances as one ds_bpermute on a precomputed byte address. Every lane must be active.
+__device__ inline uint32_t quad_xor1(uint32_t v)
+{
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false); // quad_perm [1,0,3,2]
+}
+__device__ inline uint32_t quad_xor2(uint32_t v)
+{
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false); // quad_perm [2,3,0,1]
+}
+__device__ inline uint32_t quad_sum(uint32_t v)
+{
+    v += quad_xor1(v);
+    return v + quad_xor2(v);
+}
+__device__ inline uint32_t lane_xor(uint32_t v, int lane, int o)
+{
+    return (uint32_t)__builtin_amdgcn_ds_bpermute((lane ^ o) << 2, (int)v);
+}
+
 // S16 = Σ(4r − D4)² is the reference's fp32 error ×16 (image/metrics.h:37-50);
 // the fp32 sum is exact iff S16 < 2^24.
 constexpr int64_t kExactLimit = 1ll << 24;

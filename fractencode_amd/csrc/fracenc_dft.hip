@@ -591,13 +591,17 @@ __device__ inline void resolve_dft_slot(const MfmaResolveArgs& a, uint32_t slot,
     const uint4* rp4 = reinterpret_cast<const uint4*>(a.rorb + (size_t)slot * 32 + g * (PG / 2));
     const uint4 r0 = rp4[0], r1 = rp4[1];
     const uint32_t rp[PG / 2] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
-    uint32_t sr2u = 0;
+    constexpr uint32_t kOnes = 0x00010001u;
+    uint32_t sr2u = 0, sr1 = 0;
 #pragma unroll
-    for (int q = 0; q < PG / 2; ++q)
+    for (int q = 0; q < PG / 2; ++q) {
         sr2u = __builtin_amdgcn_udot2(__builtin_bit_cast(ushort2_t, rp[q]), __builtin_bit_cast(ushort2_t, rp[q]), sr2u,
                                       false);
-    sr2u += (uint32_t)__shfl_xor((int)sr2u, 1, 64);
-    sr2u += (uint32_t)__shfl_xor((int)sr2u, 2, 64);
+        sr1 = __builtin_amdgcn_udot2(__builtin_bit_cast(ushort2_t, rp[q]), __builtin_bit_cast(ushort2_t, kOnes), sr1,
+                                     false);
+    }
+    sr2u = quad_sum(sr2u);
+    sr1 = quad_sum(sr1);
     const int sr2 = (int)sr2u; // Σr² ≤ 64·255²
     const uint32_t e0 = a.blk_ptr[blk], e1 = a.blk_ptr[blk + 1];
     const uint32_t nent = (e1 - e0) * 2u;
@@ -612,7 +616,7 @@ __device__ inline void resolve_dft_slot(const MfmaResolveArgs& a, uint32_t slot,
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1)
-        vmax = __builtin_fmaxf(vmax, __shfl_xor(vmax, o, 64));
+        vmax = __builtin_fmaxf(vmax, __uint_as_float(lane_xor(__float_as_uint(vmax), lane, o)));
     if (!(vmax > -1.0e29f))
         return; // only padding rows: no eligible domain, best_key stays "none"
     const int64_t sa16 = (int64_t)a.rconst[slot];
@@ -621,6 +625,7 @@ __device__ inline void resolve_dft_slot(const MfmaResolveArgs& a, uint32_t slot,
     const int64_t target = exact && !sentinel ? sa16 - (int64_t)vmax : -1;
     const bool hit = a.hitH >= 0 && (sentinel || (target >= 0 && target <= a.hitH));
     unsigned long long bestk = kKeyNone;
+    uint32_t bx = 0, bs1 = 0, bs2 = 0; // X_t, ΣD4, ΣD4² of bestk's candidate (fit_rstat)
     const uint32_t vbits = __float_as_uint(vmax);
     // only the entries holding the maximum are re-evaluated (usually one): the lanes test 64
     // entries at a time and the wave walks the ballot of matches, so the cost does not grow
@@ -635,7 +640,7 @@ __device__ inline void resolve_dft_slot(const MfmaResolveArgs& a, uint32_t slot,
             const int src = __ffsll((long long)match) - 1;
             match &= match - 1;
             const uint32_t j = c0 + (uint32_t)src;
-            uint2 en = make_uint2(vbits, (uint32_t)__shfl((int)enl.y, src, 64));
+            uint2 en = make_uint2(vbits, (uint32_t)__builtin_amdgcn_readlane((int)enl.y, src));
             // SORTED entries carry the chunk's tile mask in bits 28..31 (search_dft CHUNKED)
             const uint32_t tmask = SORTED ? (en.y >> 28) : 0xfu;
             if constexpr (SORTED)
@@ -647,7 +652,7 @@ __device__ inline void resolve_dft_slot(const MfmaResolveArgs& a, uint32_t slot,
                 const int p = a.tile_pos[en.y * 32 + row];
                 const unsigned long long mask = __ballot(p >= 0 && g == 0);
                 if (mask) {
-                    const int pf = __shfl(p, __ffsll((long long)mask) - 1, 64);
+                    const int pf = __builtin_amdgcn_readlane(p, __ffsll((long long)mask) - 1);
                     bestk = min(bestk, key_miss((uint64_t)kExactLimit, (uint32_t)pf, 0));
                 }
                 continue;
@@ -667,15 +672,19 @@ __device__ inline void resolve_dft_slot(const MfmaResolveArgs& a, uint32_t slot,
                     dr[2 * o] = __builtin_amdgcn_alignbit(dv[2 * o + 1], dv[2 * o], 16);
                     dr[2 * o + 1] = __builtin_amdgcn_alignbit(dv[2 * o], dv[2 * o + 1], 16);
                 }
-                uint32_t sd2 = 0;
+                uint32_t sd2 = 0, sd1 = 0;
 #pragma unroll
-                for (int q = 0; q < PG / 2; ++q)
+                for (int q = 0; q < PG / 2; ++q) {
                     sd2 = __builtin_amdgcn_udot2(__builtin_bit_cast(ushort2_t, dv[q]), __builtin_bit_cast(ushort2_t, dv[q]),
                                                  sd2, false);
-                sd2 += (uint32_t)__shfl_xor((int)sd2, 1, 64);
-                sd2 += (uint32_t)__shfl_xor((int)sd2, 2, 64);
+                    sd1 = __builtin_amdgcn_udot2(__builtin_bit_cast(ushort2_t, dv[q]), __builtin_bit_cast(ushort2_t, kOnes),
+                                                 sd1, false);
+                }
+                sd2 = quad_sum(sd2);
+                sd1 = quad_sum(sd1);
                 const int nsd2 = -(int)sd2; // ΣD4² ≤ 64·1020² < 2^31
                 unsigned long long tk = kKeyNone;
+                uint32_t tx = 0, ts1 = 0, ts2 = 0;
 #pragma unroll
                 for (int t = 0; t < T; ++t) {
                     uint32_t X = 0;
@@ -686,8 +695,7 @@ __device__ inline void resolve_dft_slot(const MfmaResolveArgs& a, uint32_t slot,
                         X = __builtin_amdgcn_udot2(__builtin_bit_cast(ushort2_t, rp[q]), __builtin_bit_cast(ushort2_t, dq),
                                                    X, false);
                     }
-                    X += (uint32_t)__shfl_xor((int)X, 1, 64);
-                    X += (uint32_t)__shfl_xor((int)X, 2, 64);
+                    X = quad_sum(X);
                     // S16 = 16Σr² − 8X + ΣD4² ≤ 64·1020² < 2^31: exact in int32
                     const int64_t s16 = p >= 0 ? (int64_t)(16 * sr2 - 8 * (int32_t)X - nsd2) : 0;
                     const bool ok = p >= 0 && g == 0 && (hit ? (s16 <= a.hitH) : (s16 == target));
@@ -696,35 +704,61 @@ __device__ inline void resolve_dft_slot(const MfmaResolveArgs& a, uint32_t slot,
                         const unsigned long long k =
                             ok ? (hit ? key_hit((uint32_t)p, t) : key_miss((uint64_t)target, (uint32_t)p, T - 1 - t))
                                : kKeyNone;
-                        tk = k < tk ? k : tk;
+                        if (k < tk) {
+                            tk = k;
+                            tx = X;
+                        }
                     } else {
                         const unsigned long long mask = __ballot(ok);
                         if (mask) {
                             const int first = __ffsll((long long)mask) - 1;
-                            const int pf = __shfl(p, first, 64);
+                            const int pf = __builtin_amdgcn_readlane(p, first);
                             const unsigned long long k = hit ? key_hit((uint32_t)pf, t)
                                                              : key_miss((uint64_t)target, (uint32_t)pf, T - 1 - t);
-                            tk = k < tk ? k : tk;
+                            const uint32_t xf = (uint32_t)__builtin_amdgcn_readlane((int)X, first);
+                            const uint32_t s1f = (uint32_t)__builtin_amdgcn_readlane((int)sd1, first);
+                            const uint32_t s2f = (uint32_t)__builtin_amdgcn_readlane((int)sd2, first);
+                            if (k < tk) {
+                                tk = k;
+                                tx = xf;
+                                ts1 = s1f;
+                                ts2 = s2f;
+                            }
                         }
                     }
                 }
+                if constexpr (SORTED) {
+                    ts1 = sd1;
+                    ts2 = sd2;
+                }
                 if (tk != kKeyNone) {
-                    bestk = tk < bestk ? tk : bestk;
+                    if (tk < bestk) {
+                        bestk = tk;
+                        bx = tx;
+                        bs1 = ts1;
+                        bs2 = ts2;
+                    }
                     if constexpr (!SORTED)
                         break;
                 }
             }
         }
     }
+    const unsigned long long mine = bestk;
     if constexpr (SORTED) {
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) {
-            const unsigned long long ok2 = __shfl_xor(bestk, o, 64);
+            const unsigned long long ok2 = ((unsigned long long)lane_xor((uint32_t)(bestk >> 32), lane, o) << 32) |
+                                           lane_xor((uint32_t)bestk, lane, o);
             bestk = ok2 < bestk ? ok2 : bestk;
         }
     }
     if (lane == 0)
         a.best_key[r] = bestk;
+    // the winner's sums for fit_rstat, from the lane that evaluated it (keys are unique per
+    // (domain, transform); without SORTED every lane holds the same)
+    if (a.rstat && bestk != kKeyNone && (SORTED ? mine == bestk : lane == 0))
+        a.rstat[r] = make_uint4(bx, bs1 | (sr1 << 16), bs2, (uint32_t)sr2);
 }
 
 // One wave per slot, in slot order (the 32 ranges of a block read the same entry lines back to

@@ -399,6 +399,43 @@ __device__ inline void fit_range(const FitArgs& a, uint32_t r, int sub)
     a.aux[r] = RangeAux{p, flags};
 }
 
+// fit_rstat<N>: the fit for the Fourier path, whose resolve_dft recorded the winner's X_t,
+// ΣD4, ΣD4², Σr and Σr² (MfmaResolveArgs::rstat): one thread per range, no pixel or pool
+// reads; the transform comes from the selection key (resolve_dft emits hit-format keys for
+// every hit, so a miss-format key is a miss). Same formulas and fallback rule as fit_winner.
+template <int N>
+__global__ void __launch_bounds__(256) fit_rstat(FitArgs a, const uint4* __restrict__ rstat)
+{
+    constexpr int NN = N * N;
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= a.nr)
+        return;
+    const frac_grid_item rg = a.ranges[r];
+    const unsigned long long key = a.best_key[r];
+    if (key == kKeyNone) {
+        write_default(a.out[r], rg);
+        a.aux[r] = RangeAux{0u, (uint32_t)kAuxEmpty};
+        return;
+    }
+    const uint32_t p = key_pos(key);
+    const bool hit = (key >> 63) == 0;
+    const long long err = hit ? 0 : (long long)((key >> 27) & 0xffffffffull);
+    const int t = hit ? (int)(key & 7u) : (int)(a.T - 1 - (uint32_t)(key & 7u));
+    if (!hit && err >= kExactLimit) { // fp32 regime: fallback_fp32 writes the record
+        a.aux[r] = RangeAux{p, (uint32_t)kAuxFallback};
+        a.fb_list[atomicAdd(a.fb_count, 1u)] = r;
+        return;
+    }
+    const frac_grid_item d = a.doms[a.porig[p]];
+    const uint4 st = rstat[r];
+    const long long X = st.x, sD = st.y & 0xffffu, sA = st.y >> 16, sD2 = st.z, sA2 = st.w;
+    const long long S16 = 16 * sA2 - 8 * X + sD2;
+    const double dist = ((double)S16 * 0.0625) / (double)(d.w * d.h);
+    write_fit(a.out[r], rg, d, t, (double)sA, (double)sA2, (double)sD * 0.25, (double)X * 0.25, (double)NN, a.smax,
+              dist);
+    a.aux[r] = RangeAux{p, hit ? (uint32_t)kAuxHit : 0u};
+}
+
 // one wave per 64 / L ranges (a grid-stride form over fewer waves measured slower)
 
 template <int N>

@@ -505,6 +505,7 @@ struct MfmaResolveArgs {
     uint32_t nslots;
     const uint32_t* tpool;      // [ntiles*32][32] D4 pairs in orbit order (dft_domain_build)
     const uint32_t* rorb;       // [nslots][32] range pixel pairs in orbit order (dft_range_prep)
+    uint4* rstat = nullptr;     // [nr] the winner's {X_t, ΣD4 | Σr << 16, ΣD4², Σr²} (fit_rstat)
 };
 
 __device__ inline int fwd_rt(const Aff& a, int N, int q)
