@@ -223,7 +223,7 @@ struct frac_ctx {
     std::vector<uint2> tp_blk_group;
     DBuf<uint4> d_tp_groups;
     DBuf<uint2> d_tp_blk_group, d_tp_tile_sd, d_tp_blk_sr;
-    DBuf<uint32_t> d_tp_blk_u, d_tp_nch, d_tp_choff, d_tp_blkcnt, d_tp_tot, d_tp_iota, d_tp_pairs;
+    DBuf<uint32_t> d_tp_blk_u, d_tp_nch, d_tp_choff, d_tp_blkcnt, d_tp_tot, d_tp_iota, d_tp_pairs, d_tp_row_of;
     DBuf<int32_t> d_tp_rbk;
     DBuf<uint8_t> d_tp_tmp;
     size_t tp_tmp_bytes = 0;
@@ -748,6 +748,7 @@ int prepare(frac_ctx* c)
         FRAC_HIP(c, c->d_tp_groups.ensure(std::max<size_t>(ng, 1)));
         FRAC_HIP(c, c->d_tp_blk_group.ensure(std::max<size_t>(nbk, 1)));
         FRAC_HIP(c, c->d_tp_tile_sd.ensure(std::max<size_t>(nt, 1)));
+        FRAC_HIP(c, c->d_tp_row_of.ensure(std::max<size_t>(P, 1)));
         FRAC_HIP(c, c->d_tp_blk_sr.ensure(std::max<size_t>(nbk, 1)));
         FRAC_HIP(c, c->d_tp_blk_u.ensure(std::max<size_t>(nbk, 1)));
         FRAC_HIP(c, c->d_tp_nch.ensure(ng + 1));
@@ -877,7 +878,7 @@ inline int launch_dft(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride)
     b.negsd2 = c->d_negsd2.ptr;
     b.tpool = c->d_dft_tpool.ptr;
     if (c->ntiles)
-        dft_domain_build<<<(c->ntiles * 32 + 255) / 256, 256, 0, c->stream>>>(d, b, c->d_dft_tguard.ptr);
+        dft_domain_build<false><<<(c->ntiles * 32 + 255) / 256, 256, 0, c->stream>>>(d, b, c->d_dft_tguard.ptr);
     MfmaRangePrepArgs r;
     r.tgt = dtgt;
     r.tstride = tstride;
@@ -1105,8 +1106,9 @@ int launch_tp(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool timing)
                                    c->d_sea_dpos2.ptr, P, c->tp_key_bits, c->stream));
     }
     if (nt) {
-        tp_build_tiles<<<(nt * 32 + 255) / 256, 256, 0, c->stream>>>(c->tp_bk, c->d_sea_dkey2.ptr, c->d_sea_dpos2.ptr,
-                                                                     nt, c->d_m_tile_pos.ptr, c->d_tp_tile_sd.ptr);
+        tp_build_tiles<<<(nt * 32 + 255) / 256, 256, 0, c->stream>>>(
+            c->tp_bk, c->d_sea_dkey2.ptr, c->d_sea_dpos2.ptr, nt, c->d_m_tile_pos.ptr, c->d_tp_tile_sd.ptr,
+            c->d_tp_row_of.ptr, c->d_m_dtiles.ptr, c->d_m_dconst.ptr, c->d_dft_tguard.ptr);
         MfmaDomainPrepArgs d;
         d.pool = c->d_pool.ptr;
         d.negsd2 = c->d_negsd2.ptr;
@@ -1122,7 +1124,10 @@ int launch_tp(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool timing)
         b.pool = c->d_pool.ptr;
         b.negsd2 = c->d_negsd2.ptr;
         b.tpool = c->d_dft_tpool.ptr;
-        dft_domain_build<<<(nt * 32 + 255) / 256, 256, 0, c->stream>>>(d, b, c->d_dft_tguard.ptr);
+        b.row_of = c->d_tp_row_of.ptr;
+        b.npos = P;
+        if (P)
+            dft_domain_build<true><<<(P + 255) / 256, 256, 0, c->stream>>>(d, b, c->d_dft_tguard.ptr);
     }
     if (nr) {
         tp_range_keys<<<(nr + 255) / 256, 256, 0, c->stream>>>(dtgt, tstride, c->d_ranges.ptr, c->d_tp_rbk.ptr, nr,
@@ -1540,6 +1545,7 @@ void frac_destroy(frac_ctx* c)
     c->d_tp_blkcnt.release();
     c->d_tp_tot.release();
     c->d_tp_pairs.release();
+    c->d_tp_row_of.release();
     c->d_tp_iota.release();
     c->d_tp_rbk.release();
     c->d_tp_tmp.release();

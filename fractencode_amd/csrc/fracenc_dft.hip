@@ -128,6 +128,8 @@ struct DftDomainBuildArgs {
     uint32_t* pool;             // [P][32] packed u16 pairs of D4
     int32_t* negsd2;            // [P]
     uint32_t* tpool;            // [ntiles*32][32] the same rows in tile order, orbit order (resolve_dft)
+    const uint32_t* row_of = nullptr; // BYPOS: [P] tile row of each pool position (tp_build_tiles)
+    uint32_t npos = 0;                // BYPOS: P
 };
 
 __device__ inline uint32_t pair_sums(uint32_t w0, uint32_t w1)
@@ -136,15 +138,21 @@ __device__ inline uint32_t pair_sums(uint32_t w0, uint32_t w1)
     return (w0 & M) + ((w0 >> 8) & M) + (w1 & M) + ((w1 >> 8) & M);
 }
 
+// BYPOS (the SEA tiled form, whose tiles hold domains in ΣD4 order): one thread per pool
+// position in domain order, so neighbouring threads read overlapping plane rows, and the
+// outputs are scattered to the position's tile row; tp_build_tiles writes the padding rows and
+// zeroes the tile guards, which are then raised with atomics.
+template <bool BYPOS = false>
 __global__ void __launch_bounds__(256) dft_domain_build(MfmaDomainPrepArgs a, DftDomainBuildArgs s,
                                                         uint2* __restrict__ tguard)
 {
     constexpr int NN = 64, NO = 16;
-    const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
-    if (gid >= a.ntiles * 32u)
+    const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+    if (tid >= (BYPOS ? s.npos : a.ntiles * 32u))
         return;
+    const uint32_t gid = BYPOS ? s.row_of[tid] : tid;
     const uint32_t tile = gid >> 5, row = gid & 31u;
-    const int p = a.tile_pos[gid];
+    const int p = BYPOS ? (int)tid : a.tile_pos[gid];
     uint32_t w[NN / 2];
     if (p >= 0) {
         const frac_grid_item d = s.doms[s.porig[p]];
@@ -235,9 +243,14 @@ __global__ void __launch_bounds__(256) dft_domain_build(MfmaDomainPrepArgs a, Df
     const float ny = p >= 0 ? -(float)sb2 : kDftPadY;
     const uint32_t h = (row >> 2) & 1u, i = (row & 3u) + 4u * (row >> 3);
     a.dconst[(size_t)tile * 32 + h * 16 + i] = __float_as_uint(ny);
+    uint32_t gx = p >= 0 ? (uint32_t)(4 * dinf) : 0u, gy = p >= 0 ? (uint32_t)sb2 : 0u;
+    if constexpr (BYPOS) {
+        atomicMax(&tguard[tile].x, gx);
+        atomicMax(&tguard[tile].y, gy);
+        return;
+    }
     // the tile's guard terms over its valid rows: a 32-lane maximum (whole tiles leave together
     // above), one writer per tile
-    uint32_t gx = p >= 0 ? (uint32_t)(4 * dinf) : 0u, gy = p >= 0 ? (uint32_t)sb2 : 0u;
 #pragma unroll
     for (int o = 16; o > 0; o >>= 1) {
         gx = max(gx, (uint32_t)__shfl_xor((int)gx, o, 64));
@@ -252,7 +265,8 @@ __global__ void __launch_bounds__(256) dft_domain_build(MfmaDomainPrepArgs a, Df
 //   f0 = s_a, f1 = u_a, f2 = 4s_a, f3 = 4u_a, f4 = α, f5 = β, f6 = −α
 // (lane l: range slot l&31, orbit 8(l>>5) + j); U = [f0|f1], U' = [f1|f0] (×4: f2, f3),
 // Pr = [f4|f5], Pi = [f5|f6] against the domain K-steps [s_b|u_b], [γ|δ].  Also 16Σa² per
-// slot and the block's guard term max R1.  One thread per slot.
+// slot and the block's guard term max R1.  One thread per slot (a range-order variant with
+// scattered outputs measured slower for the SEA tiled form's ΣR-sorted slots: 61 vs 41 µs).
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) dft_range_prep(MfmaRangePrepArgs a, uint32_t* __restrict__ rguard)
 {

@@ -89,10 +89,14 @@ __global__ void __launch_bounds__(256) tp_domain_keys(const uint8_t* __restrict_
     pos[p] = p;
 }
 
-// tile rows from the sorted domain order; per tile [min, max] ΣD4 of its valid rows
+// tile rows from the sorted domain order; per tile [min, max] ΣD4 of its valid rows; for
+// dft_domain_build<BYPOS>: the tile row of each pool position, the padding rows' fragments
+// (b = 0) and epilogue constants, and zeroed tile guards
 __global__ void __launch_bounds__(256) tp_build_tiles(TpBuckets bk, const uint32_t* __restrict__ skey,
                                                       const uint32_t* __restrict__ spos, uint32_t ntiles,
-                                                      int32_t* __restrict__ tile_pos, uint2* __restrict__ tile_sd)
+                                                      int32_t* __restrict__ tile_pos, uint2* __restrict__ tile_sd,
+                                                      uint32_t* __restrict__ row_of, uint4* __restrict__ dtiles,
+                                                      uint32_t* __restrict__ dconst, uint2* __restrict__ tguard)
 {
     const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
     if (gid >= ntiles * 32u)
@@ -103,7 +107,21 @@ __global__ void __launch_bounds__(256) tp_build_tiles(TpBuckets bk, const uint32
         ++b;
     const uint32_t k = (tile - bk.tile_first[b]) * 32u + row;
     const bool valid = k < bk.dom_count[b];
-    tile_pos[gid] = valid ? (int32_t)spos[bk.dom_begin[b] + k] : -1;
+    const uint32_t p = valid ? spos[bk.dom_begin[b] + k] : 0u;
+    tile_pos[gid] = valid ? (int32_t)p : -1;
+    if (valid) {
+        row_of[p] = gid;
+    } else {
+#pragma unroll
+        for (int st = 0; st < 4; ++st)
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+                dtiles[((size_t)tile * 4 + st) * 64 + row + 32 * h] = make_uint4(0u, 0u, 0u, 0u);
+        const uint32_t hh = (row >> 2) & 1u, i = (row & 3u) + 4u * (row >> 3);
+        dconst[(size_t)tile * 32 + hh * 16 + i] = __float_as_uint(kDftPadY);
+    }
+    if (row == 0)
+        tguard[tile] = make_uint2(0u, 0u);
     if (row == 0) {
         const uint32_t last = min(k + 31u, bk.dom_count[b] - 1u);
         tile_sd[tile] = valid ? make_uint2(skey[bk.dom_begin[b] + k] & 0xffffu,
