@@ -343,12 +343,16 @@ int classify_on_device(frac_ctx* c, const std::vector<frac_grid_item>& items, co
     return FRAC_OK;
 }
 
-int upload_plane(frac_ctx* c, const HostPlane& hp, DBuf<uint8_t>& d, uint32_t& dstride)
+// the caller's plane straight to the device (no host copy): pageable memory, so the copy is
+// complete, and the caller's buffer free again, when the call returns
+int upload_plane(frac_ctx* c, const uint8_t* p, uint32_t w, uint32_t h, uint32_t stride, DBuf<uint8_t>& d,
+                 uint32_t& dstride)
 {
-    dstride = (hp.w + 63u) & ~63u;
+    dstride = (w + 63u) & ~63u;
     // one extra row + column of slack: kernels never read it, but keeps every 2×2 read in-bounds
-    FRAC_HIP(c, d.ensure((size_t)dstride * (hp.h + 1)));
-    FRAC_HIP(c, hipMemcpy2DAsync(d.ptr, dstride, hp.data.data(), hp.w, hp.w, hp.h, hipMemcpyHostToDevice, c->stream));
+    FRAC_HIP(c, d.ensure((size_t)dstride * (h + 1)));
+    FRAC_HIP(c, hipMemcpy2DAsync(d.ptr, dstride, p, stride, w, h, hipMemcpyHostToDevice, c->stream));
+    FRAC_HIP(c, hipStreamSynchronize(c->stream));
     return FRAC_OK;
 }
 
@@ -1317,6 +1321,7 @@ int launch_all(frac_ctx* c)
     const uint8_t* dsrc = c->d_src.ptr;
     const uint8_t* dtgt = c->same_plane ? c->d_src.ptr : c->d_tgt.ptr;
     const uint32_t tstride = c->same_plane ? c->d_sstride : c->d_tstride;
+    HostTrace tr("launch");
     if (timing)
         FRAC_HIP(c, hipEventRecord(c->ev[0], c->stream));
     if (nr)
@@ -1335,12 +1340,14 @@ int launch_all(frac_ctx* c)
         pool_build<N><<<(P + 3) / 4, 256, 0, c->stream>>>(dsrc, c->d_sstride, c->d_doms.ptr, c->d_porig.ptr, P,
                                                           c->d_pool.ptr, c->d_negsd2.ptr);
     const bool use_sea = c->engine == FRAC_ENGINE_SEA && !c->all_fallback;
+    tr.mark("memsets + pool");
     if (use_mfma)
         FRAC_TRY(launch_mfma<N>(c, dtgt, tstride));
     if constexpr (N <= 8) {
         if (use_sea)
             FRAC_TRY(launch_sea<N>(c, dtgt, tstride, timing));
     }
+    tr.mark("engine launch");
     const bool use_valu = !use_mfma && !use_sea;
     if (timing && use_valu)
         FRAC_HIP(c, hipEventRecord(c->ev[1], c->stream));
@@ -1429,6 +1436,7 @@ int launch_all(frac_ctx* c)
     if (timing)
         FRAC_HIP(c, hipEventRecord(c->ev[3], c->stream));
     FRAC_HIP(c, hipGetLastError());
+    tr.mark("fit + fallback");
     c->engine_ran = use_mfma ? FRAC_ENGINE_MFMA : use_sea ? FRAC_ENGINE_SEA : FRAC_ENGINE_VALU;
     if (!(use_sea && c->tp)) // the tiled form counted its evaluated pairs in launch_tp
         c->evaluated_ran = c->all_fallback ? 0 : c->eligible_pairs; // SEA: read back at fetch
@@ -1606,26 +1614,39 @@ static int copy_host_plane(HostPlane& hp, const uint8_t* p, uint32_t w, uint32_t
     return FRAC_OK;
 }
 
+// A new frame of the same geometry keeps the prepared range/domain structures unless the
+// classifier is on (categories depend on the pixels): without it a video frame costs the upload
+// and the search only.
+static void planes_changed(frac_ctx* c, uint32_t sw, uint32_t sh, uint32_t tw, uint32_t th, bool same)
+{
+    const bool geometry_kept = c->planes_set && c->src.w == sw && c->src.h == sh && c->tgt.w == tw &&
+                               c->tgt.h == th && c->same_plane == same;
+    if (!geometry_kept || c->p.use_classifier)
+        c->dirty = true;
+    c->src.w = sw;
+    c->src.h = sh;
+    c->tgt.w = tw;
+    c->tgt.h = th;
+    c->same_plane = same;
+    c->planes_set = true;
+    c->ran = false;
+}
+
 int frac_set_planes(frac_ctx* c, const uint8_t* src, uint32_t sw, uint32_t sh, uint32_t sstride, const uint8_t* tgt,
                     uint32_t tw, uint32_t th, uint32_t tstride)
 {
     if (!c)
         return FRAC_E_INVALID;
     FRAC_HIP(c, hipSetDevice(c->device));
-    if (copy_host_plane(c->src, src, sw, sh, sstride) != FRAC_OK)
+    if (!src || sw == 0 || sh == 0 || sstride < sw)
         return c->fail(FRAC_E_INVALID, "invalid source plane");
-    c->same_plane = tgt == nullptr || tgt == src;
-    if (!c->same_plane) {
-        if (copy_host_plane(c->tgt, tgt, tw, th, tstride) != FRAC_OK)
-            return c->fail(FRAC_E_INVALID, "invalid target plane");
-    } else {
-        c->tgt = c->src;
-    }
-    FRAC_TRY(upload_plane(c, c->src, c->d_src, c->d_sstride));
-    if (!c->same_plane)
-        FRAC_TRY(upload_plane(c, c->tgt, c->d_tgt, c->d_tstride));
-    c->planes_set = true;
-    c->dirty = true;
+    const bool same = tgt == nullptr || tgt == src;
+    if (!same && (tw == 0 || th == 0 || tstride < tw))
+        return c->fail(FRAC_E_INVALID, "invalid target plane");
+    FRAC_TRY(upload_plane(c, src, sw, sh, sstride, c->d_src, c->d_sstride));
+    if (!same)
+        FRAC_TRY(upload_plane(c, tgt, tw, th, tstride, c->d_tgt, c->d_tstride));
+    planes_changed(c, sw, sh, same ? sw : tw, same ? sh : th, same);
     return FRAC_OK;
 }
 
@@ -1642,17 +1663,11 @@ int frac_set_frame_device(frac_ctx* c, const void* d_plane, uint32_t w, uint32_t
         return c->fail(FRAC_E_INVALID, "invalid device plane");
     FRAC_HIP(c, hipSetDevice(c->device));
     // the frame stays on the device: the classifier pre-pass runs there too
-    c->src.w = w;
-    c->src.h = h;
-    c->src.data.clear();
     c->d_sstride = (w + 63u) & ~63u;
     FRAC_HIP(c, c->d_src.ensure((size_t)c->d_sstride * (h + 1)));
     FRAC_HIP(c, hipMemcpy2DAsync(c->d_src.ptr, c->d_sstride, d_plane, stride, w, h, hipMemcpyDeviceToDevice, c->stream));
     FRAC_HIP(c, hipStreamSynchronize(c->stream));
-    c->same_plane = true;
-    c->tgt = c->src;
-    c->planes_set = true;
-    c->dirty = true;
+    planes_changed(c, w, h, w, h, true);
     return FRAC_OK;
 }
 

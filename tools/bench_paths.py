@@ -7,6 +7,7 @@
   c4q       the same with the quadtree partition 16/8/4: ms per frame, items per size
   decode    Decoder2 on the GPU for the C3 winners: ms per iteration, HBM bytes per iteration
   stream    FRC1 pack of the C3 winners (host, numpy): ms
+  e2e       C3 from host buffers (PCIe-inclusive): H2D of the frame, search, D2H of the winners, per frame
 
 Run on the GPU box:  python tools/bench_paths.py [--only rgb2yuv c5 ...] [--steps K]
 """
@@ -126,6 +127,41 @@ def main():
                           "range_blocks_per_s": round(len(rngs) / sec, 1),
                           "rejected_mappings": st["rejected_mappings"], "total_mappings": st["total_mappings"],
                           "engine": st["engine"], "ms_search": round(st["ms_search"], 3)}), flush=True)
+
+    if want("e2e"):
+        # C3 through the host-buffer boundary: a new frame from host memory every step (H2D of the
+        # 16 MiB plane), the whole search pipeline, then the winners back to the host — the 64-byte
+        # encode_item_t records (frac_fetch) or the 32-byte tuples (frac_fetch_tuples)
+        frame = value_noise(4096, 4096, 1234)
+        frame2 = np.ascontiguousarray(frame[::-1])  # a different frame of the same statistics
+        doms = F.create_uniform_grid(4096, 4096, 16, 8)
+        rngs = F.create_uniform_grid(4096, 4096, 8, 8)
+        res = {}
+        with F.Engine(0, 4, False, timing=True) as e:
+            e.set_domains(doms)
+            e.set_ranges(rngs)
+            frames = [frame, frame2]
+            k = [0]
+
+            def step_records():
+                e.set_frame(frames[k[0] & 1])
+                k[0] += 1
+                e.run()
+                e.fetch()
+
+            def step_tuples():
+                e.set_frame(frames[k[0] & 1])
+                k[0] += 1
+                e.run()
+                e.fetch_tuples()
+
+            for name, fn in (("records_64B", step_records), ("tuples_32B", step_tuples)):
+                sec = timed(fn, args.steps, args.warmup, e.sync)
+                res[name] = {"ms_per_frame": round(sec * 1e3, 3), "range_blocks_per_s": round(len(rngs) / sec, 1)}
+            _, st = e.fetch()
+            res["device_ms_last"] = round(st["ms_device"], 3)
+        print(json.dumps({"path": "e2e", "workload": "C3 from host buffers: H2D of the 4096² frame, search, D2H of "
+                                                     "262,144 winners", "by_output": res}), flush=True)
 
     if want("c4q"):
         # C4 with the quadtree partition (16/8/4): the whole multi-level encode per frame
