@@ -48,11 +48,16 @@ class ColorEncoder:
             rgb = torch.from_numpy(np.ascontiguousarray(rgb, dtype=np.uint8)).to(f"cuda:{self.device}")
         planes = self.engines[0].rgb_to_yuv(rgb)
         self.planes = planes
-        self.ranges = []
         n, d = self.range_size, self.domain_size
-        for e, p in zip(self.engines, planes):
+        geom = [tuple(p.shape) for p in planes]
+        same = geom == getattr(self, "_geom", None)
+        if not same:
+            self.ranges = []
+        for k, (e, p) in enumerate(zip(self.engines, planes)):
             H, W = p.shape
             e.set_frame(p)
+            if same:
+                continue  # a frame of the same geometry keeps the grids (and, classifier off, the prepared state)
             # categories −1: with the classifier on, the engine classifies every item on the
             # device plane (main.cpp:155-162 preclassifies both grids on the same plane)
             doms = create_uniform_grid(W, H, d, d // 2)
@@ -60,6 +65,7 @@ class ColorEncoder:
             e.set_domains(doms)
             e.set_ranges(rngs)
             self.ranges.append(rngs)
+        self._geom = geom
 
     def run(self) -> None:
         """Enqueue the three searches (asynchronous; each engine on its own stream)."""
