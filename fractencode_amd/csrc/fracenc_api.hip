@@ -231,6 +231,9 @@ struct frac_ctx {
     DBuf<unsigned long long> d_frc_rec;
     DBuf<uint32_t> d_frc_words;
     std::vector<frac_encode_item> qt_res; // quadtree: one level's results (kept: no page faults per call)
+    // quadtree: the per-level domain grids (geometry only) of the last frame size, by log2(n)
+    uint32_t qt_w = 0, qt_h = 0;
+    std::vector<frac_grid_item> qt_doms[5];
     DBuf<uint8_t> d_sea_tmp;
     DBuf<unsigned long long> d_sea_count; // candidates the SEA search evaluated
     uint64_t eligible_pairs = 0;          // Σ over ranges of its bucket's domain count
@@ -443,11 +446,12 @@ int prepare(frac_ctx* c)
         const int b = c->range_bucket[i];
         c->rbucket[i] = make_uint2(c->bucket_begin[b], c->bucket_end[b]);
     }
-    // range slots: per bucket, padded to whole waves of 64
+    // range slots: per bucket, padded to whole waves of 64 (the VALU engine's work lists only)
     c->slot_range.clear();
     c->work.clear();
+    const bool valu_lists = c->p.engine == FRAC_ENGINE_VALU;
     std::vector<std::pair<uint32_t, int>> blocks; // (slot base, bucket)
-    for (int b = 0; b < nb; ++b) {
+    for (int b = 0; valu_lists && b < nb; ++b) {
         const uint32_t base = (uint32_t)c->slot_range.size();
         for (uint32_t k = rbeg[b]; k < rbeg[b + 1]; ++k)
             c->slot_range.push_back((int32_t)rord[k]);
@@ -1831,8 +1835,16 @@ int frac_encode_quadtree(frac_ctx* c, const frac_quadtree_params* qp, frac_encod
     emitted.reserve((size_t)(W / qp->min_size) * (H / qp->min_size));
     frac_stats total{};
     HostTrace tr("quadtree");
+    if (c->qt_w != W || c->qt_h != H) {
+        for (auto& g : c->qt_doms)
+            g.clear();
+        c->qt_w = W;
+        c->qt_h = H;
+    }
     for (uint32_t n = qp->max_size; !pending.empty() && n >= qp->min_size; n /= 2) {
-        const std::vector<frac_grid_item> doms = grid(2 * n, n);
+        std::vector<frac_grid_item>& doms = c->qt_doms[__builtin_ctz(n)];
+        if (doms.empty())
+            doms = grid(2 * n, n);
         FRAC_TRY(frac_set_domains(c, doms.data(), doms.size()));
         FRAC_TRY(frac_set_ranges(c, pending.data(), pending.size()));
         tr.mark("grids");

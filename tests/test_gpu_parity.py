@@ -338,3 +338,31 @@ def test_unaligned_origins(oracle, engine, n):
         out, _ = e.search(rngs)
     want, _, _ = oracle.estimate(p, doms, rngs)
     assert_same(out, {k: want[k] for k in FIELDS}, f"unaligned n={n}")
+
+
+@pytest.mark.parametrize("engine", ENGINES)
+@pytest.mark.parametrize("cls", [False, True])
+def test_new_frame_same_geometry(engine, cls):
+    """A second frame of the same geometry into a prepared context (the video case: the
+    classifier-off path keeps the prepared structures, the classifier-on path re-prepares)
+    gives the records a fresh context gives for that frame."""
+    rng = np.random.default_rng(21)
+    a = rng.integers(0, 256, (128, 128), dtype=np.uint8)
+    b = np.ascontiguousarray(np.rot90(a)) // 2 + rng.integers(0, 100, (128, 128), dtype=np.uint8)
+    doms = F.create_uniform_grid(128, 128, 16, 8)
+    rngs = F.create_uniform_grid(128, 128, 8, 8)
+    with F.Engine(0, 4, cls, 0.0, -1.0, engine) as e:
+        e.set_frame(a)
+        e.set_domains(doms)
+        e.set_ranges(rngs)
+        e.run()
+        first, _ = e.fetch()
+        e.set_frame(b)
+        e.run()
+        second, _ = e.fetch()
+    with F.Engine(0, 4, cls, 0.0, -1.0, engine) as e:
+        e.set_frame(b)
+        e.set_domains(doms)
+        want, _ = e.search(rngs)
+    assert second.tobytes() == want.tobytes()
+    assert first.tobytes() != second.tobytes()
