@@ -28,7 +28,7 @@ with F.Engine(0, 4, False, 0.0, -1.0, F.ENGINE_MFMA, timing=True) as e:
     for r in range(rounds + 1):
         for v in variants:
             os.environ["FRAC_MFMA_DFT"] = "1" if not v.isdigit() else "0"
-            os.environ["FRAC_MFMA_VARIANT"] = {"d": "2", "e": "1", "g": "3", "p": "4", "d8": "5",  "dm": "201", "dm0": "202", "dmD": "203", "dmB": "204", "dD": "205", "dB": "206",
+            os.environ["FRAC_MFMA_VARIANT"] = {"d": "2", "e": "1", "g": "3", "p": "4", "d8": "5", "dm": "201", "dm0": "202", "dmD": "203", "dmB": "204", "dD": "205", "dB": "206",
                                               "d0": "207", "em": "9", "ev": "17", "emL": "41", "emB": "73",
                                               "em0": "105", "eB": "65"}.get(v, v)
             e.run()
