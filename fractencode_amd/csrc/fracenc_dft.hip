@@ -417,26 +417,16 @@ __device__ inline float dft_tile_max(const half8_t (&af)[4], const half8_t (&bf)
         const floatx16_t v = mfma2(af[0], bf[1], af[1], bf[0], z);
         m0 = __builtin_fmaxf(m0, u[0] + v[0] + pr[0] + pi[0] + ny[0]);
     } else {
-        // exact path: U + |Pr| is folded while the U' and Pi MFMAs still run (the scheduler is
-        // asked to put four of those adds after each of the last four MFMAs: +1.1–1.6% in an
-        // in-process A/B against the unordered form, profiles/r01/ab_fourier_variants.log)
-        floatx16_t u = mfma2(af[0], bf[0], af[1], bf[1], z); // U
-#pragma unroll
-        for (int i = 0; i < 16; ++i)
-            u[i] = u[i] + __builtin_fabsf(pr[i]);
+        const floatx16_t u = mfma2(af[0], bf[0], af[1], bf[1], z);   // U
         const floatx16_t v = mfma2(af[0], bf[1], af[1], bf[0], z);   // U'
         const floatx16_t pi = mfma2(af[2], bf[5], af[3], bf[6], z);  // Pi
-        __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);           // the Pr and U MFMAs
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0); // one U' / Pi MFMA
-            __builtin_amdgcn_sched_group_barrier(0x002, 4, 0); // four of the U + |Pr| adds
-        }
 #pragma unroll
         for (int i = 0; i < 16; i += 2) {
-            const float y0 = __builtin_fmaf(__builtin_fmaxf(u[i], v[i] + __builtin_fabsf(pi[i])), 4.0f, ny[i]);
-            const float y1 =
-                __builtin_fmaf(__builtin_fmaxf(u[i + 1], v[i + 1] + __builtin_fabsf(pi[i + 1])), 4.0f, ny[i + 1]);
+            const float y0 = __builtin_fmaf(
+                __builtin_fmaxf(u[i] + __builtin_fabsf(pr[i]), v[i] + __builtin_fabsf(pi[i])), 4.0f, ny[i]);
+            const float y1 = __builtin_fmaf(
+                __builtin_fmaxf(u[i + 1] + __builtin_fabsf(pr[i + 1]), v[i + 1] + __builtin_fabsf(pi[i + 1])), 4.0f,
+                ny[i + 1]);
             m0 = __builtin_fmaxf(m0, __builtin_fmaxf(y0, y1));
         }
     }
