@@ -356,7 +356,7 @@ __global__ void __launch_bounds__(256) dft_range_prep(MfmaRangePrepArgs a, uint3
 // search_dft<HITS, VAR>: the search_mfma work decomposition (workgroup = 4 waves = 4 range
 // blocks of one bucket, domain tiles staged through LDS, 4 tiles per double-buffered
 // stage); per lane the chunk maximum of y over its 16 rows × the stage's tiles (all four
-// transforms folded in).  Entries: [nwork*4][64] {float bits of max y (+inf = hit), chunk tile | tile mask << 28}.
+// transforms folded in).  Entries: [nwork*4][64] {float bits of max y (+inf = hit), tile}.
 // VAR 1: exact path only (A/B of the guard).
 // ---------------------------------------------------------------------------
 __device__ inline floatx16_t mfma2(const half8_t& a0, const half8_t& b0, const half8_t& a1, const half8_t& b1,
@@ -515,7 +515,7 @@ __global__ void __launch_bounds__(64 * WAVES) search_dft(DftArgs d)
         hl = (float)((int32_t)a.rconst[blk * 32 + (lane & 31u)] - (int32_t)a.hitH);
 
     float best = -__builtin_inff();
-    uint32_t btile = 0, bmask = 0;
+    uint32_t btile = 0;
     uint32_t masks[2] = {0u, 0u};
     auto finish_stage = [&](float cm, uint32_t tb) {
         if constexpr (CHUNKED) {
@@ -535,20 +535,14 @@ __global__ void __launch_bounds__(64 * WAVES) search_dft(DftArgs d)
             masks[0] = masks[1] = 0u;
             return;
         }
-        // any hit in the chunk: the first-hit chunk wins; the entry's tile mask (bits 28..31) lists
-        // the chunk's tiles attaining the maximum, or holding a hit, for resolve_dft
-        uint32_t msk = masks[0];
+        // any hit in the chunk: the first-hit chunk wins. (A per-tile mask here, as the CHUNKED
+        // entries carry, cost 4% of this kernel in a 30-sample A/B for 0.1 ms less resolve: not kept.)
         if constexpr (HITS)
-            if (cm >= hl) {
-                cm = __builtin_inff();
-                msk = masks[1];
-            }
+            cm = cm >= hl ? __builtin_inff() : cm;
         if (cm > best) {
             best = cm;
             btile = tb;
-            bmask = msk;
         }
-        masks[0] = masks[1] = 0u;
     };
     const uint32_t nstage = (wk.w - wk.z + kTilesPerStage - 1) / kTilesPerStage;
     auto stage_nt = [&](uint32_t st) { return min((uint32_t)kTilesPerStage, wk.w - (wk.z + st * kTilesPerStage)); };
@@ -566,7 +560,7 @@ __global__ void __launch_bounds__(64 * WAVES) search_dft(DftArgs d)
             if (st + 1 < nstage && (!SKIPDMA || st == 0))
                 stage_tiles<KS, 64 * WAVES>(lds1, a.dtiles, a.dconst, tb + kTilesPerStage, stage_nt(st + 1));
             for (uint32_t c0 = 0; c0 < stage_nt(st); c0 += 4)
-                finish_stage(dft_compute_stage<VAR, true, HITS>(lds0, stage_nt(st), lane, bf, tb, d.tguard, r1, c0,
+                finish_stage(dft_compute_stage<VAR, CHUNKED, HITS>(lds0, stage_nt(st), lane, bf, tb, d.tguard, r1, c0,
                                                                    c0 + 4, masks, hl),
                              tb + c0);
         }
@@ -577,14 +571,13 @@ __global__ void __launch_bounds__(64 * WAVES) search_dft(DftArgs d)
             if (st + 2 < nstage && !SKIPDMA)
                 stage_tiles<KS, 64 * WAVES>(lds0, a.dtiles, a.dconst, tb + kTilesPerStage, stage_nt(st + 2));
             for (uint32_t c0 = 0; c0 < stage_nt(st + 1); c0 += 4)
-                finish_stage(dft_compute_stage<VAR, true, HITS>(lds1, stage_nt(st + 1), lane, bf, tb, d.tguard, r1,
+                finish_stage(dft_compute_stage<VAR, CHUNKED, HITS>(lds1, stage_nt(st + 1), lane, bf, tb, d.tguard, r1,
                                                                    c0, c0 + 4, masks, hl),
                              tb + c0);
         }
     }
     if (active && !CHUNKED)
-        a.entries[(size_t)(blockIdx.x * WAVES + wv) * 64 + lane] =
-            make_uint2(__float_as_uint(best), btile | (bmask << 28));
+        a.entries[(size_t)(blockIdx.x * WAVES + wv) * 64 + lane] = make_uint2(__float_as_uint(best), btile);
 }
 
 // ---------------------------------------------------------------------------
@@ -666,9 +659,10 @@ __device__ inline void resolve_dft_slot(const MfmaResolveArgs& a, uint32_t slot,
             match &= match - 1;
             const uint32_t j = c0 + (uint32_t)src;
             uint2 en = make_uint2(vbits, (uint32_t)__builtin_amdgcn_readlane((int)enl.y, src));
-            // entries carry the chunk's tile mask in bits 28..31 (search_dft)
-            const uint32_t tmask = en.y >> 28;
-            en.y &= 0x0fffffffu;
+            // SORTED entries carry the chunk's tile mask in bits 28..31 (search_dft CHUNKED)
+            const uint32_t tmask = SORTED ? (en.y >> 28) : 0xfu;
+            if constexpr (SORTED)
+                en.y &= 0x0fffffffu;
             const int row = (i & 3) + 8 * (i >> 2) + 4 * (int)(j & 1);
             if (!exact) {
                 // fp32 fallback regime: every candidate has S16 ≥ 2^24; any valid domain of the
