@@ -780,14 +780,14 @@ __device__ inline void resolve_dft_slot(const MfmaResolveArgs& a, uint32_t slot,
 }
 
 // One wave per slot, in slot order (the 32 ranges of a block read the same entry lines back to
-// back). A grid of fewer, longer-lived waves striding over the slots measured slower (452 vs
+// back); launched as one- or four-wave workgroups. A grid of fewer, longer-lived waves striding over the slots measured slower (452 vs
 // 372 µs at C3 in the SEA tiled form).
 
 template <bool SORTED = false>
 __global__ void __launch_bounds__(256) resolve_dft(MfmaResolveArgs a)
 {
     // the slot is wave-uniform: readfirstlane lets its loads go through the scalar unit
-    const uint32_t slot = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
+    const uint32_t slot = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
     if (slot < a.nslots)
         resolve_dft_slot<SORTED>(a, slot, threadIdx.x & 63);
 }
