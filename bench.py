@@ -6,17 +6,35 @@ Workload (BASELINE.json configs[2]): one 4096×4096 grayscale 
 (261,121), the reference's 4 transforms, exhaustive (no classifier), rms threshold 0.
 A step = one full search of the frame's ranges already resident in HBM: domain-pool
 build, search, winner fit, fp32 fallback and — for N > 1 — the RCCL all-gather of the
-32-byte (domain, transform, s, o, rms) winner tuples.  Ranges are sharded contiguously over ranks (fixed total work:
-strong scaling).
+32-byte (domain, transform, s, o, rms) winner tuples.  Ranges are sharded contiguously over
+ranks (fixed total work: strong scaling).
+
+Beside `value` the line carries:
+  roofline      the search kernel against the dense f16 MFMA peak: `achieved` = the matrix flops
+                the search issues per launch (its algorithm's count) ÷ the kernel's mean duration
+                over exactly the timed steps (library HIP events on the kernel's stream,
+                frac_timing_history); `direct_form` = the §8(d) direct-form op count over the same
+                time (an algorithmic-equivalent rate, not a hardware fraction); `traffic` = HBM
+                bytes per launch from the committed rocprofv3 PMC passes of THIS library build
+                (null when profiles/pmc_search.json was taken from another build)
+  e2e           the same workload through the host boundary (§8(d)): per step the frame H2D from
+                pinned memory, the search, and the tuples D2H into pinned memory
+  cpu_baseline  the unmodified reference (oracle/_ref) on a bounded sample, all the host cores this
+                process may use (affinity, capped by the cgroup CPU quota), CPU model recorded
 
 Run:  python bench.py [--gpus N] [--steps K] [--warmup W] [--engine valu|mfma|auto]
-N > 1 is launched by torch.distributed.run (one process per GPU, RCCL over xGMI).
+--gpus N > 1 without WORLD_SIZE in the environment: this process launches N ranks itself
+(torch.distributed.run as a child process, before anything touches the GPU) and exits with its
+status; under torch.distributed.run (WORLD_SIZE set) it runs one rank per GPU over RCCL.
 """
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -40,13 +58,52 @@ def parse():
     ap.add_argument("--size", type=int, default=4096)
     ap.add_argument("--transforms", type=int, default=4)
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of CPU-baseline sampling (0 = skip)")
-    ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every core this process may use")
     ap.add_argument("--alt-steps", type=int, default=2,
                     help="steps of the VALU engine (north_star's no-MFMA formulation) reported beside (0 = skip)")
+    ap.add_argument("--e2e-steps", type=int, default=-1, help="steps of the host-boundary leg (-1 = --steps)")
     return ap.parse_args()
 
 
-def cpu_baseline(frame: np.ndarray, budget: float, threads: int):
+def launch_ranks(args) -> int:
+    """N ranks on this node via torch.distributed.run (a child process; this parent never initialises
+    the GPU, so no exec happens after GPU init)."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *sys.argv[1:]]
+    return subprocess.call(cmd, env=env)
+
+
+def host_cores() -> tuple[int, dict]:
+    """Threads for the CPU baseline: the CPUs this process may run on (sched_getaffinity), capped by
+    the cgroup CPU quota when one is set; plus the host description recorded in the line."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    for path in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            q, per = open(path).read().split()[:2]
+            if q != "max":
+                quota = int(q) / int(per)
+        except (OSError, ValueError):
+            pass
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    threads = aff if quota is None else max(1, min(aff, int(quota)))
+    return threads, {"cpu_model": model, "affinity_cpus": aff, "cgroup_cpu_quota": quota}
+
+
+def cpu_baseline(frame: np.ndarray, budget: float, threads: int, host: dict):
     """Reference CPU path (oracle/_ref, the unmodified reference built by oracle/ref/Makefile)
     timed on this host on a bounded strided sample of the same workload; the oracle
     restatement ("port") when the reference build is absent."""
@@ -65,39 +122,55 @@ def cpu_baseline(frame: np.ndarray, budget: float, threads: int):
         _, _, done = O.estimate(frame, doms, rngs, T=4, threads=threads, budget_s=budget)
         kind = "port"
     dt = time.perf_counter() - t0
-    return {"value": done / dt, "unit": "range-blocks/s", "cores": threads, "kind": kind,
+    return {"value": done / dt, "unit": "range-blocks/s", "cores": threads, "kind": kind, **host,
             "sample": f"{done} ranges of the same {W}x{H} S1 frame (strided over all {n_ranges}), "
                       f"{threads} threads, {dt:.1f} s"}
 
 
-def load_traffic(engine_name: str):
-    """HBM bytes per search launch from the committed rocprofv3 PMC summary (profiles/),
-    corrected as MI355X_MICROARCH.md §HBM prescribes; None when absent."""
+def lib_sha16() -> str:
+    import fractencode_amd as F
+
+    with open(F.LIB_PATH, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()[:16]
+
+
+def load_traffic(form: str):
+    """HBM bytes per search launch from the committed rocprofv3 PMC summary (profiles/), corrected as
+    MI355X_MICROARCH.md §HBM prescribes — only when it was measured on this library build."""
     path = os.path.join(ROOT, "profiles", "pmc_search.json")
     if not os.path.exists(path):
-        return None
+        return None, "no PMC summary"
     with open(path) as f:
         d = json.load(f)
-    e = d.get(engine_name)
-    return None if e is None else e.get("hbm_bytes_per_launch")
+    e = d.get(form)
+    if e is None:
+        return None, f"no PMC entry for form {form}"
+    if e.get("lib_sha16") != lib_sha16():
+        return None, f"PMC entry is from library {e.get('lib_sha16')}, not this build"
+    return e.get("hbm_bytes_per_launch"), e.get("source")
 
 
-def main():
-    args = parse()
+def main(args):
     import torch
     import torch.distributed as dist
 
     import fractencode_amd as F
-    from fractencode_amd.distributed import TUPLE_BYTES, gather_tuples, shard_bounds, shard_capacity
+    from fractencode_amd.distributed import TUPLE_BYTES, gather_tuples, plan_capacity, shard_plan
     from fractencode_amd.synth import value_noise
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        where = [None] * world
+        dist.all_gather_object(where, (socket.gethostname(), local, torch.cuda.get_device_name(local)))
+        if len({(h, d) for h, d, _ in where}) != world:
+            raise SystemExit(f"bench.py: ranks share a GPU: {where}")
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", local if world > 1 else 0)
@@ -107,8 +180,8 @@ def main():
     doms = F.create_uniform_grid(S, S, 16, 8)
     rngs = F.create_uniform_grid(S, S, 8, 8)
     nr_total = len(rngs)
-    per = shard_capacity(nr_total, world)
-    start, stop = shard_bounds(nr_total, world, rank)
+    plan = shard_plan(nr_total, world)
+    start, stop = plan[rank]
     mine = rngs[start:stop]
     engine_id = {"auto": F.ENGINE_AUTO, "valu": F.ENGINE_VALU, "mfma": F.ENGINE_MFMA}[args.engine]
 
@@ -122,22 +195,22 @@ def main():
     eng.set_frame(d_frame)
     eng.set_domains(doms)
     eng.set_ranges(mine)
-    mine_bytes = torch.zeros(per * TUPLE_BYTES, dtype=torch.uint8, device=dev)
+    mine_bytes = torch.zeros(plan_capacity(plan) * TUPLE_BYTES, dtype=torch.uint8, device=dev)
 
     def step():
         eng.run()
         if world > 1:  # RCCL all-gather of the 32-byte (domain, t, s, o, rms) tuples (same stream)
             eng.copy_tuples_device(mine_bytes.data_ptr())
-            gather_tuples(mine_bytes, nr_total, world)
+            gather_tuples(mine_bytes, plan)
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
+    eng.timing_history()  # drop the warmup runs: the history now covers exactly the timed steps
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    search_ms = []
     for _ in range(args.steps):
         step()
     torch.cuda.synchronize(dev)
@@ -145,33 +218,46 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
-    # per-kernel device times of the last step (library HIP events on this stream)
+    hist = eng.timing_history()  # per-run HIP events of the K timed steps (on the kernel's stream)
+    assert len(hist) == args.steps, (len(hist), args.steps)
     _, st = eng.fetch()
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    # separate timed pass for the dominant kernel's average duration (HIP events around
-    # the search kernel on the stream it is launched on, recorded by the library)
-    for _ in range(max(3, min(args.steps, 10))):
-        eng.run()
-        _, st_i = eng.fetch()
-        search_ms.append(st_i["ms_search"])
-    avg_search_ms = float(np.mean(search_ms))
-
+    kernel_ms = float(np.mean(hist["ms_search"]))
     ms_per_step = 1000.0 * elapsed / args.steps
     value = nr_total / (elapsed / args.steps)
     engine_name = {1: "valu", 2: "mfma"}.get(st["engine"], "valu")
+    form = F.FORM_NAMES.get(st["search_form"], engine_name)
     n_d = len(doms)
-    ops_per_rb = 2 * 64 * args.transforms * n_d  # one MAC per pixel per candidate
-    ops_per_launch = ops_per_rb * len(mine)
-    achieved = ops_per_launch / (avg_search_ms * 1e-3) / 1e12
+    direct_ops = 2 * 64 * args.transforms * n_d * len(mine)  # one MAC per pixel per candidate
+    traffic, traffic_src = load_traffic(form)
     if engine_name == "mfma":
+        # the matrix flops the search issues: the Fourier form's own count (8 MFMA 32x32x16 per
+        # 32-range × 32-domain tile pair), half the direct form's §8(d) count for the same result
+        work = st["matrix_flops"]
         bound, peak, unit = "mfma", MFMA_F16_PEAK_TFLOPS, "TFLOP/s"
     else:
+        work = direct_ops
         bound, peak, unit = "valu", VALU_PEAK_TOPS, "TOP/s"
-    traffic = load_traffic(F.FORM_NAMES.get(st["search_form"], engine_name))
+    achieved = work / (kernel_ms * 1e-3) / 1e12
+    roof = {"bound": bound, "achieved": round(achieved, 2), "peak": peak, "unit": unit,
+            "frac": round(achieved / peak, 4), "traffic": traffic,
+            "kernel": {"fourier": "search_dft", "direct": "search_mfma"}.get(form, "search_valu"),
+            "kernel_ms": round(kernel_ms, 3), "kernel_ms_timed_steps": [round(float(x), 3) for x in hist["ms_search"]],
+            "flops_per_launch": int(work),
+            "direct_form": {"ops_per_launch": direct_ops,
+                            "rate": round(direct_ops / (kernel_ms * 1e-3) / 1e12, 2),
+                            "note": "SURVEY §8(d) direct-form count over the same kernel time: an "
+                                    "algorithmic-equivalent rate, not a hardware fraction"}}
+    if traffic:
+        roof["hbm_gbs"] = round(traffic / (kernel_ms * 1e-3) / 1e9, 3)
+        roof["hbm_frac"] = round(roof["hbm_gbs"] / HBM_PEAK_GBS, 6)
+        roof["traffic_source"] = traffic_src
+    else:
+        roof["traffic_note"] = traffic_src
     line = {
         "metric": METRIC,
         "value": round(value, 1),
@@ -188,28 +274,45 @@ def main():
         "config": {"workload": f"C3: {S}x{S} S1 value-noise frame (seed 1234), 8x8 ranges ({nr_total}), "
                                f"16x16 domains stride 8 ({n_d}), T={args.transforms}, exhaustive, rms 0",
                    "engine": engine_name, "ranges_per_gpu": len(mine), "parallelism": f"ranges/{world}"},
-        "roofline": {"bound": bound, "achieved": round(achieved, 2), "peak": peak, "unit": unit,
-                     "frac": round(achieved / peak, 4), "traffic": traffic,
-                     "kernel": "search", "kernel_ms": round(avg_search_ms, 3),
-                     "ops_per_launch": ops_per_launch},
-        "search_form": F.FORM_NAMES.get(st["search_form"], "?"),
-        "phases_ms": {"prep": round(st["ms_prep"], 3), "search": round(st["ms_search"], 3),
-                      "finish": round(st["ms_finish"], 3)},
+        "roofline": roof,
+        "search_form": form,
+        "phases_ms": {k: round(float(np.mean(hist["ms_" + k])), 3) for k in ("device", "prep", "search", "finish")},
         "fallback_ranges": st["fallback_ranges"],
+        "lib_sha16": lib_sha16(),
     }
-    if st["matrix_flops"]:
-        # the matrix-core work the search actually issued (the Fourier form needs 3/8 of the
-        # §8(d) direct-form count): the hardware utilisation beside the algorithmic figure
-        issued = st["matrix_flops"] / (avg_search_ms * 1e-3) / 1e12
-        line["roofline"]["issued"] = {"flops_per_launch": st["matrix_flops"], "achieved": round(issued, 2),
-                                      "frac": round(issued / MFMA_F16_PEAK_TFLOPS, 4)}
-    if traffic:
-        line["roofline"]["hbm_gbs"] = round(traffic / (avg_search_ms * 1e-3) / 1e9, 3)
-        line["roofline"]["hbm_frac"] = round(line["roofline"]["hbm_gbs"] / HBM_PEAK_GBS, 6)
+
+    # host boundary (§8(d) end-to-end): frame H2D from pinned memory + search + tuples D2H, per step
+    e2e_steps = args.steps if args.e2e_steps < 0 else args.e2e_steps
+    if e2e_steps > 0:
+        h_frame = torch.from_numpy(frame).pin_memory()
+        h_tuples = torch.empty(len(mine) * TUPLE_BYTES, dtype=torch.uint8).pin_memory()
+        tup = h_tuples.numpy().view(F.TUPLE)
+        eng.set_frame(h_frame.numpy())
+        eng.run()
+        eng.fetch_tuples(tup)
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(e2e_steps):
+            eng.set_frame(h_frame.numpy())  # same geometry: no re-preparation, the plane is re-uploaded
+            eng.run()
+            eng.fetch_tuples(tup)
+        e2e = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([e2e], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            e2e = float(t.item())
+        line["e2e"] = {"value": round(nr_total / (e2e / e2e_steps), 1), "ms_per_step": round(1e3 * e2e / e2e_steps, 3),
+                       "steps": e2e_steps,
+                       "step": "frame H2D (pinned, 16 MiB) + search + tuples D2H (pinned, 32 B per range)"
+                               + (" per rank; no gather" if world > 1 else "")}
+        eng.set_frame(d_frame)
+
     if world == 1 and engine_name == "mfma" and args.alt_steps > 0:
         # the same workload on the other engines, measured the same way: the VALU engine (packed-u16
         # v_dot2, north_star's no-MFMA formulation, exhaustive) and the SEA engine (successive
         # elimination: identical records, most candidates skipped by an exact bound, data-dependent)
+        main_out, _ = eng.fetch()
         line["alt_engines"] = {}
         for alt_name, alt_id in (("valu", F.ENGINE_VALU), ("sea", F.ENGINE_SEA)):
             with F.Engine(dev.index, args.transforms, False, 0.0, -1.0, alt_id, timing=True) as alt:
@@ -219,29 +322,30 @@ def main():
                 alt.set_ranges(mine)
                 alt.run()
                 torch.cuda.synchronize(dev)
+                alt.timing_history()
                 t0 = time.perf_counter()
                 for _ in range(args.alt_steps):
                     alt.run()
                 torch.cuda.synchronize(dev)
                 alt_sec = (time.perf_counter() - t0) / args.alt_steps
+                ah = alt.timing_history()
                 alt_out, ast = alt.fetch()
+            a_ms = float(np.mean(ah["ms_search"]))
             entry = {"value": round(nr_total / alt_sec, 1), "ms_per_step": round(alt_sec * 1e3, 3),
                      "steps": args.alt_steps, "dtype": "u16",
-                     "phases_ms": {"prep": round(ast["ms_prep"], 3), "search": round(ast["ms_search"], 3),
-                                   "finish": round(ast["ms_finish"], 3)}}
+                     "phases_ms": {k: round(float(np.mean(ah["ms_" + k])), 3) for k in ("prep", "search", "finish")}}
             if alt_name == "valu":
-                alt_ach = ops_per_launch / (ast["ms_search"] * 1e-3) / 1e12
+                alt_ach = direct_ops / (a_ms * 1e-3) / 1e12
                 entry["roofline"] = {"bound": "valu", "achieved": round(alt_ach, 2), "peak": VALU_PEAK_TOPS,
                                      "unit": "TOP/s", "frac": round(alt_ach / VALU_PEAK_TOPS, 4),
-                                     "kernel_ms": round(ast["ms_search"], 3)}
+                                     "kernel_ms": round(a_ms, 3)}
             else:
-                main_out, _ = eng.fetch()
                 entry["records_identical_to_exhaustive"] = bool(alt_out.tobytes() == main_out.tobytes())
                 entry["evaluated_frac"] = round(ast["evaluated_mappings"] / (len(mine) * n_d), 6)
             line["alt_engines"][alt_name] = entry
     if rank == 0 and world == 1 and args.cpu_budget > 0:
-        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
-        line["cpu_baseline"] = cpu_baseline(frame, args.cpu_budget, threads)
+        threads, host = host_cores()
+        line["cpu_baseline"] = cpu_baseline(frame, args.cpu_budget, args.cpu_threads or threads, host)
     eng.close()
     if rank == 0:
         print(json.dumps(line), flush=True)
@@ -250,4 +354,7 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    _args = parse()
+    if _args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(_args))
+    main(_args)

@@ -30,6 +30,8 @@ ENCODE_ITEM = np.dtype([("x", "<u4"), ("y", "<u4"), ("w", "<u4"), ("h", "<u4"),
 # frac_tuple: (domain index, transform, s, o, rms) — the 32-byte record of the multi-GPU gather
 TUPLE = np.dtype([("domain", "<u4"), ("transform", "<i4"), ("contrast", "<f8"), ("brightness", "<f8"),
                   ("distance", "<f8")])
+# frac_run_timing: per-run device times (frac_timing_history)
+RUN_TIMING = np.dtype([("ms_device", "<f8"), ("ms_prep", "<f8"), ("ms_search", "<f8"), ("ms_finish", "<f8")])
 NO_DOMAIN = 0xFFFFFFFF
 assert GRID_ITEM.itemsize == 20 and ENCODE_ITEM.itemsize == 64 and TUPLE.itemsize == 32
 
@@ -101,6 +103,7 @@ def lib() -> C.CDLL:
             "frac_run": (i32, [vp]),
             "frac_fetch": (i32, [vp, vp, C.POINTER(FracStats)]),
             "frac_sync": (i32, [vp]),
+            "frac_timing_history": (i32, [vp, vp, sz, C.POINTER(C.c_size_t)]),
             "frac_search": (i32, [vp, vp, sz, vp, C.POINTER(FracStats)]),
             "frac_set_stream": (i32, [vp, vp]),
             "frac_get_stream": (vp, [vp]),
@@ -225,7 +228,16 @@ class Engine:
         """Source == target plane (Encoder2).  numpy uint8 [H, W] or a CUDA torch tensor."""
         self._frame_wh = (int(plane.shape[1]), int(plane.shape[0]))
         if hasattr(plane, "is_cuda") and plane.is_cuda:
-            assert plane.dtype.itemsize == 1 and plane.dim() == 2
+            import torch
+
+            if plane.dtype != torch.uint8 or plane.dim() != 2:
+                raise FracError("set_frame: a device plane must be a 2-D uint8 tensor")
+            if plane.stride(1) != 1 or plane.stride(0) < plane.shape[1]:
+                raise FracError("set_frame: device plane rows must be contiguous (stride(1) == 1, "
+                                "stride(0) >= width)")
+            # the library copies on its own stream: work still pending on torch's current stream
+            # (e.g. the kernel producing this plane) must land first
+            torch.cuda.current_stream(plane.device).synchronize()
             self._check(lib().frac_set_frame_device(self._ctx, C.c_void_p(plane.data_ptr()), plane.shape[1],
                                                     plane.shape[0], plane.stride(0)))
             return
@@ -261,6 +273,15 @@ class Engine:
         self._check(lib().frac_fetch(self._ctx, out.ctypes.data if self._nr else None, C.byref(st)))
         return out, st.as_dict()
 
+    def timing_history(self) -> np.ndarray:
+        """Device times (ms: device, prep, search, finish) of every run since the previous call
+        (engine created with timing=True); waits for the stream."""
+        n = C.c_size_t(0)
+        self._check(lib().frac_timing_history(self._ctx, None, 0, C.byref(n)))
+        out = np.zeros(n.value, dtype=RUN_TIMING)
+        self._check(lib().frac_timing_history(self._ctx, out.ctypes.data if n.value else None, n.value, C.byref(n)))
+        return out[: n.value]
+
     def search(self, ranges: np.ndarray):
         """set_ranges + run + fetch → (encode items in range order, stats dict)."""
         self.set_ranges(ranges)
@@ -288,10 +309,14 @@ class Engine:
                                          n.value, C.byref(n)))
         return buf.tobytes()
 
-    def fetch_tuples(self) -> np.ndarray:
-        """The last run's tuples (TUPLE records) on the host."""
+    def fetch_tuples(self, out: np.ndarray | None = None) -> np.ndarray:
+        """The last run's tuples (TUPLE records) on the host; `out` (TUPLE array of the range count,
+        e.g. a view of pinned memory) is filled in place when given."""
         n = self._nr
-        out = np.zeros(n, dtype=TUPLE)
+        if out is None:
+            out = np.zeros(n, dtype=TUPLE)
+        elif out.dtype != TUPLE or len(out) != n or not out.flags.c_contiguous:
+            raise FracError("fetch_tuples: out must be a contiguous TUPLE array of the range count")
         if n:
             self._check(lib().frac_fetch_tuples(self._ctx, out.ctypes.data_as(C.c_void_p)))
         return out

@@ -53,10 +53,14 @@ class ColorEncoder:
         same = geom == getattr(self, "_geom", None)
         if not same:
             self.ranges = []
+        sharded = getattr(self, "_sharded", False)
+        self._sharded = False
         for k, (e, p) in enumerate(zip(self.engines, planes)):
             H, W = p.shape
             e.set_frame(p)
             if same:
+                if sharded:  # encode_sharded left each engine holding only this rank's shard
+                    e.set_ranges(self.ranges[k])
                 continue  # a frame of the same geometry keeps the grids (and, classifier off, the prepared state)
             # categories −1: with the classifier on, the engine classifies every item on the
             # device plane (main.cpp:155-162 preclassifies both grids on the same plane)
@@ -87,6 +91,7 @@ class ColorEncoder:
         on every rank.  `device` = a CUDA device for nccl, None for gloo (host tuples)."""
         from .distributed import encode_sharded
 
+        self._sharded = True  # the next load() of a same-geometry frame restores the full range lists
         out = []
         for e, rngs, p in zip(self.engines, self.ranges, self.planes):
             H, W = p.shape

@@ -245,6 +245,10 @@ struct frac_ctx {
 
     std::vector<RangeAux> h_aux;
     hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+    // FRAC_FLAG_TIMING: the same four boundaries (start | prep | search | finish) of every run
+    // since the last frac_timing_history call, a ring of kHistRuns runs (created on first use)
+    std::vector<hipEvent_t> hist;
+    uint64_t hist_runs = 0, hist_read = 0;
     bool ran = false;
     uint32_t engine_ran = FRAC_ENGINE_VALU;
     uint32_t form_ran = FRAC_FORM_DOT2;
@@ -272,6 +276,20 @@ struct frac_ctx {
             return _rc;                                                                                                \
     } while (0)
 #define FRAC_HIP(ctx, expr) FRAC_TRY((ctx)->hip((expr), #expr))
+
+namespace {
+constexpr uint32_t kHistRuns = 256;
+
+// Boundary k of the current run (0 start, 1 search begins, 2 search ends, 3 finish ends): the
+// last-run event (frac_stats) and the run's slot in the timing history (frac_timing_history)
+int mark_event(frac_ctx* c, int k)
+{
+    FRAC_HIP(c, hipEventRecord(c->ev[k], c->stream));
+    if (!c->hist.empty())
+        FRAC_HIP(c, hipEventRecord(c->hist[(size_t)(c->hist_runs % kHistRuns) * 4 + k], c->stream));
+    return FRAC_OK;
+}
+} // namespace
 
 namespace {
 
@@ -826,33 +844,62 @@ void launch_search_mfma_v(frac_ctx* c, const MfmaSearchArgs& a)
         search_mfma<N, T, false, VAR><<<(unsigned)c->m_work.size(), 256, 0, c->stream>>>(a);
 }
 
-// FRAC_MFMA_VARIANT (tuning knob, read per run): schedule variant of search_mfma
-inline int mfma_variant()
+// FRAC_MFMA_VARIANT (A/B knob, read per run): schedule variant of the MFMA searches. Every
+// value a product build accepts gives identical (exact) records; the ablations, which give
+// wrong results by design, are accepted — and compiled — only by a -DFRAC_TUNING build.
+// Any other value fails the run (FRAC_E_INVALID), so a stray variable cannot corrupt records.
+//   search_mfma: 0..7 schedule bits, 32 s_setprio, 64 late constants, 96, 98; ablations 8, 16
+//   search_dft:  default 8-wave exact form; 1 / 3 four-wave exact / guarded; 5 eight-tile
+//                stages; ablations 9, 17, 41, 73, 105, 65 (four-wave) and 201..207 (eight-wave)
+inline int mfma_variant(frac_ctx* c, int& var)
 {
     const char* v = getenv("FRAC_MFMA_VARIANT");
-    return v ? atoi(v) : kDefaultMfmaVariant;
+    var = kDefaultMfmaVariant;
+    if (!v || !*v)
+        return FRAC_OK;
+    char* end = nullptr;
+    const long x = strtol(v, &end, 10);
+    static const int exact[] = {0, 1, 2, 3, 4, 5, 6, 7, 32, 64, 96, 98};
+    static const int ablation[] = {8, 9, 16, 17, 41, 65, 73, 105, 201, 202, 203, 204, 205, 206, 207};
+    bool ok = end && *end == 0;
+    bool known = false;
+    for (int e : exact)
+        known |= x == e;
+    if (kTuningBuild)
+        for (int e : ablation)
+            known |= x == e;
+    if (!ok || !known)
+        return c->fail(FRAC_E_INVALID, std::string("FRAC_MFMA_VARIANT=") + v +
+                                           (kTuningBuild ? " is unknown" : " is not a product variant (ablations need "
+                                                                           "a -DFRAC_TUNING build)"));
+    var = (int)x;
+    return FRAC_OK;
 }
 
 template <int N, int T>
-void launch_search_mfma(frac_ctx* c, const MfmaSearchArgs& a)
+int launch_search_mfma(frac_ctx* c, const MfmaSearchArgs& a)
 {
-    switch (mfma_variant()) {
+    int var = 0;
+    FRAC_TRY(mfma_variant(c, var));
+    switch (var) {
     case 0: launch_search_mfma_v<N, T, 0>(c, a); break;
     case 1: launch_search_mfma_v<N, T, 1>(c, a); break;
-    case 2: launch_search_mfma_v<N, T, 2>(c, a); break;
     case 3: launch_search_mfma_v<N, T, 3>(c, a); break;
     case 4: launch_search_mfma_v<N, T, 4>(c, a); break;
     case 5: launch_search_mfma_v<N, T, 5>(c, a); break;
     case 6: launch_search_mfma_v<N, T, 6>(c, a); break;
     case 7: launch_search_mfma_v<N, T, 7>(c, a); break;
-    case 8: launch_search_mfma_v<N, T, 8>(c, a); break;   // ablation: 1-value epilogue
-    case 16: launch_search_mfma_v<N, T, 16>(c, a); break; // ablation: no MFMA
     case 32: launch_search_mfma_v<N, T, 32>(c, a); break; // s_setprio around MFMA clusters
     case 64: launch_search_mfma_v<N, T, 64>(c, a); break; // late epilogue-constant reads
     case 96: launch_search_mfma_v<N, T, 96>(c, a); break;
     case 98: launch_search_mfma_v<N, T, 98>(c, a); break;
+#ifdef FRAC_TUNING
+    case 8: launch_search_mfma_v<N, T, 8>(c, a); break;   // ablation: 1-value epilogue
+    case 16: launch_search_mfma_v<N, T, 16>(c, a); break; // ablation: no MFMA
+#endif
     default: launch_search_mfma_v<N, T, kDefaultMfmaVariant>(c, a); break;
     }
+    return FRAC_OK;
 }
 
 // FRAC_MFMA_DFT (tuning knob, read per run): 0 selects the direct n=8, T=4 MFMA search
@@ -901,11 +948,12 @@ inline int launch_dft(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride)
     if (c->nblocks)
         dft_range_prep<<<(c->nblocks * 32 + 255) / 256, 256, 0, c->stream>>>(r, c->d_dft_rguard.ptr);
     if (c->p.flags & FRAC_FLAG_TIMING)
-        FRAC_HIP(c, hipEventRecord(c->ev[1], c->stream));
+        FRAC_TRY(mark_event(c, 1));
     // FRAC_MFMA_VARIANT for this path (A/B knob): default = exact form in 8-wave workgroups;
     // 1 = exact form in 4-wave workgroups, 3 = guarded fast path (4 waves), odd values ≥ 9 =
     // ablations of variant 1 (tuning only: wrong results)
-    const int var = mfma_variant();
+    int var = 0;
+    FRAC_TRY(mfma_variant(c, var));
     const bool four = var == 1 || var == 3 || (var >= 9 && (var & 1));
     const std::vector<uint4>& work = four ? c->m_work : c->m8_work;
     c->form_ran = FRAC_FORM_FOURIER;
@@ -929,7 +977,8 @@ inline int launch_dft(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride)
         const unsigned nwg = (unsigned)work.size();
         const bool hits = c->hitH > 0;
         constexpr uint32_t W8 = kDftBlocksPerWG;
-        if (!four && var >= 200) { // ablations of the 8-wave exact form (tuning only, wrong results)
+        if (!four && var >= 200) {
+#ifdef FRAC_TUNING // ablations of the 8-wave exact form (wrong results by design)
             switch (var) {
             case 201: search_dft<false, 9, W8><<<nwg, 64 * W8, 0, c->stream>>>(da); break;   // MFMA-only
             case 202: search_dft<false, 73, W8><<<nwg, 64 * W8, 0, c->stream>>>(da); break;  // MFMA-only, no DMA/bar
@@ -939,6 +988,7 @@ inline int launch_dft(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride)
             case 206: search_dft<false, 513, W8><<<nwg, 64 * W8, 0, c->stream>>>(da); break; // full, no barrier
             default: search_dft<false, 65, W8><<<nwg, 64 * W8, 0, c->stream>>>(da); break;  // full, no DMA/bar
             }
+#endif
         } else if (!four && var == 5) { // 8-tile LDS stages
             if (hits)
                 search_dft<true, 1, W8, 8><<<nwg, 64 * W8, 0, c->stream>>>(da);
@@ -960,6 +1010,7 @@ inline int launch_dft(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride)
             else
                 search_dft<false, 0><<<nwg, 256, 0, c->stream>>>(da);
         } else {
+#ifdef FRAC_TUNING // ablations of the 4-wave exact form (wrong results by design)
             switch (var) {
             case 9: search_dft<false, 9><<<nwg, 256, 0, c->stream>>>(da); break;     // MFMA-only
             case 17: search_dft<false, 17><<<nwg, 256, 0, c->stream>>>(da); break;   // VALU-only
@@ -969,10 +1020,11 @@ inline int launch_dft(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride)
             case 65: search_dft<false, 65><<<nwg, 256, 0, c->stream>>>(da); break;   // full, no DMA/barrier
             default: search_dft<false, 1><<<nwg, 256, 0, c->stream>>>(da); break;
             }
+#endif
         }
     }
     if (c->p.flags & FRAC_FLAG_TIMING)
-        FRAC_HIP(c, hipEventRecord(c->ev[2], c->stream));
+        FRAC_TRY(mark_event(c, 2));
     if (nr) {
         MfmaResolveArgs v;
         v.tgt = dtgt;
@@ -1037,7 +1089,7 @@ int launch_mfma(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride)
         mfma_range_prep<N><<<(unsigned)((threads + 255) / 256), 256, 0, c->stream>>>(r);
     }
     if (c->p.flags & FRAC_FLAG_TIMING)
-        FRAC_HIP(c, hipEventRecord(c->ev[1], c->stream));
+        FRAC_TRY(mark_event(c, 1));
     c->form_ran = FRAC_FORM_DIRECT;
     c->flops_ran = 0;
     for (const uint4& w : c->m_work) // T·KS MFMA 32x32x16 per (range block, domain tile)
@@ -1067,12 +1119,12 @@ int launch_mfma(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride)
                     search_mfma16<4, false><<<nwg, 256, 0, c->stream>>>(a);
             }
         } else if (T == 8)
-            launch_search_mfma<N, 8>(c, a);
+            FRAC_TRY((launch_search_mfma<N, 8>(c, a)));
         else
-            launch_search_mfma<N, 4>(c, a);
+            FRAC_TRY((launch_search_mfma<N, 4>(c, a)));
     }
     if (c->p.flags & FRAC_FLAG_TIMING)
-        FRAC_HIP(c, hipEventRecord(c->ev[2], c->stream));
+        FRAC_TRY(mark_event(c, 2));
     if (nr) {
         MfmaResolveArgs v;
         v.tgt = dtgt;
@@ -1165,7 +1217,7 @@ int launch_tp(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool timing)
         dft_range_prep<<<(nbk * 32 + 255) / 256, 256, 0, c->stream>>>(r, c->d_dft_rguard.ptr);
     }
     if (timing)
-        FRAC_HIP(c, hipEventRecord(c->ev[1], c->stream));
+        FRAC_TRY(mark_event(c, 1));
     if (!nr || !ng) // no ranges, or no domain in any range's bucket: every record is the default
         return FRAC_OK;
     constexpr uint32_t W8 = kDftBlocksPerWG;
@@ -1234,7 +1286,7 @@ int launch_tp(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool timing)
     else
         search_dft<false, 1, W8, 4, true><<<ng, 64 * W8, 0, c->stream>>>(da);
     if (timing)
-        FRAC_HIP(c, hipEventRecord(c->ev[2], c->stream));
+        FRAC_TRY(mark_event(c, 2));
     MfmaResolveArgs v;
     v.tgt = dtgt;
     v.tstride = tstride;
@@ -1293,7 +1345,7 @@ int launch_sea(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool timing)
                                    c->d_sea_rord2.ptr, nr, 17, c->stream));
     }
     if (timing)
-        FRAC_HIP(c, hipEventRecord(c->ev[1], c->stream));
+        FRAC_TRY(mark_event(c, 1));
     FRAC_HIP(c, hipMemsetAsync(c->d_sea_count.ptr, 0, sizeof(unsigned long long), c->stream));
     if (nr) {
         SeaArgs a;
@@ -1328,8 +1380,13 @@ int launch_all(frac_ctx* c)
     const uint8_t* dtgt = c->same_plane ? c->d_src.ptr : c->d_tgt.ptr;
     const uint32_t tstride = c->same_plane ? c->d_sstride : c->d_tstride;
     HostTrace tr("launch");
+    if (timing && c->hist.empty()) {
+        c->hist.assign(4 * kHistRuns, nullptr);
+        for (auto& e : c->hist)
+            FRAC_HIP(c, hipEventCreate(&e));
+    }
     if (timing)
-        FRAC_HIP(c, hipEventRecord(c->ev[0], c->stream));
+        FRAC_TRY(mark_event(c, 0));
     if (nr)
         FRAC_HIP(c, hipMemsetAsync(c->d_best_key.ptr, 0xff, nr * sizeof(unsigned long long), c->stream));
     const uint32_t fbc = c->all_fallback ? nr : 0u;
@@ -1356,7 +1413,7 @@ int launch_all(frac_ctx* c)
     tr.mark("engine launch");
     const bool use_valu = !use_mfma && !use_sea;
     if (timing && use_valu)
-        FRAC_HIP(c, hipEventRecord(c->ev[1], c->stream));
+        FRAC_TRY(mark_event(c, 1));
     if (use_valu && !c->all_fallback && !c->work.empty()) {
         SearchArgs a;
         a.tgt = dtgt;
@@ -1396,7 +1453,7 @@ int launch_all(frac_ctx* c)
         }
     }
     if (timing && !use_mfma)
-        FRAC_HIP(c, hipEventRecord(c->ev[2], c->stream));
+        FRAC_TRY(mark_event(c, 2));
     if (!c->all_fallback && nr) {
         FitArgs f;
         f.tgt = dtgt;
@@ -1439,8 +1496,10 @@ int launch_all(frac_ctx* c)
         b.aux = c->d_aux.ptr;
         fallback_fp32<N><<<512, 256, 0, c->stream>>>(b);
     }
-    if (timing)
-        FRAC_HIP(c, hipEventRecord(c->ev[3], c->stream));
+    if (timing) {
+        FRAC_TRY(mark_event(c, 3));
+        ++c->hist_runs;
+    }
     FRAC_HIP(c, hipGetLastError());
     tr.mark("fit + fallback");
     c->engine_ran = use_mfma ? FRAC_ENGINE_MFMA : use_sea ? FRAC_ENGINE_SEA : FRAC_ENGINE_VALU;
@@ -1589,6 +1648,9 @@ void frac_destroy(frac_ctx* c)
     if (c->h_dec_sum)
         (void)hipHostFree(c->h_dec_sum);
     for (auto& ev : c->ev)
+        if (ev)
+            (void)hipEventDestroy(ev);
+    for (auto& ev : c->hist)
         if (ev)
             (void)hipEventDestroy(ev);
     if (c->own_stream)
@@ -1789,6 +1851,35 @@ int frac_fetch(frac_ctx* c, frac_encode_item* out, frac_stats* stats)
                 stats->ms_finish = ms;
         }
     }
+    return FRAC_OK;
+}
+
+int frac_timing_history(frac_ctx* c, frac_run_timing* out, size_t cap, size_t* n_out)
+{
+    if (!c || !n_out)
+        return FRAC_E_INVALID;
+    *n_out = 0;
+    if (!(c->p.flags & FRAC_FLAG_TIMING))
+        return c->fail(FRAC_E_STATE, "timing history needs FRAC_FLAG_TIMING");
+    FRAC_HIP(c, hipSetDevice(c->device));
+    FRAC_HIP(c, hipStreamSynchronize(c->stream));
+    const uint64_t first = std::max<uint64_t>(c->hist_read, c->hist_runs > kHistRuns ? c->hist_runs - kHistRuns : 0);
+    size_t k = 0;
+    for (uint64_t r = first; r < c->hist_runs; ++r, ++k) {
+        if (!out || k >= cap)
+            continue;
+        hipEvent_t* e = &c->hist[(size_t)(r % kHistRuns) * 4];
+        float ms[4] = {0.f, 0.f, 0.f, 0.f};
+        const int pairs[4][2] = {{0, 3}, {0, 1}, {1, 2}, {2, 3}};
+        for (int q = 0; q < 4; ++q)
+            if (hipEventElapsedTime(&ms[q], e[pairs[q][0]], e[pairs[q][1]]) != hipSuccess)
+                ms[q] = 0.f;
+        out[k] = frac_run_timing{ms[0], ms[1], ms[2], ms[3]};
+    }
+    (void)hipGetLastError(); // an unrecorded boundary leaves a sticky "not ready": not an error
+    *n_out = k;
+    if (out)
+        c->hist_read = c->hist_runs;
     return FRAC_OK;
 }
 

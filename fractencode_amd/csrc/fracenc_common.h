@@ -8,6 +8,15 @@
 
 namespace fracenc {
 
+// Ablation kernels (MFMA-only, VALU-only, no LDS-DMA, no barrier …) produce WRONG results by
+// design and exist only to locate time. They are compiled only into a -DFRAC_TUNING build
+// (tools/ab_mfma.py); the product library (__graft_entry__.build) holds none of them.
+#ifdef FRAC_TUNING
+constexpr bool kTuningBuild = true;
+#else
+constexpr bool kTuningBuild = false;
+#endif
+
 typedef unsigned short ushort2_t __attribute__((ext_vector_type(2)));
 
 // Dihedral transforms as the reference's 2×4 affine LUT (image/transform.h:32-41):

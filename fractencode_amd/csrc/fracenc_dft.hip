@@ -494,6 +494,8 @@ constexpr uint32_t kDftBlocksPerWG = 8; // waves (range blocks) sharing one LDS 
 template <bool HITS, int VAR, uint32_t WAVES = 4, uint32_t TPS = kTilesPerStage, bool CHUNKED = false>
 __global__ void __launch_bounds__(64 * WAVES) search_dft(DftArgs d)
 {
+    static_assert(kTuningBuild || (VAR & (8 | 16 | 32 | 64 | 256 | 512)) == 0,
+                  "search_dft ablations exist only in FRAC_TUNING builds");
     const MfmaSearchArgs& a = d.m;
     constexpr int KS = 4;
     constexpr uint32_t kTilesPerStage = TPS; // LDS stage; chunks stay 4 tiles (resolve_dft)

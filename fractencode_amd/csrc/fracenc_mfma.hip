@@ -308,6 +308,7 @@ __device__ inline void compute_stage(const uint4* __restrict__ la, uint32_t nt, 
 template <int N, int T, bool HITS, int VAR>
 __global__ void __launch_bounds__(256) search_mfma(MfmaSearchArgs a)
 {
+    static_assert(kTuningBuild || (VAR & (8 | 16)) == 0, "search_mfma ablations exist only in FRAC_TUNING builds");
     constexpr int KS = MfmaGeom<N>::KS;
     constexpr int STAGE = kTilesPerStage * KS * 64 + kTilesPerStage * 8; // uint4 per stage
     // two distinct LDS objects: the stage loop is unrolled by two so the LDS-DMA into

@@ -7,12 +7,19 @@ all-gathered as the 32-byte (domain, transform, s, o, rms) tuples north_star nam
 grids, so the 64-byte encode_item_t records are rebuilt locally from the tuples
 (records_from_tuples).  The same functions run on the ``gloo`` backend with CPU
 tensors (tests).
+
+Shards.  Without the classifier every range meets every domain, so equal-count slices
+are equal-cost.  With the classifier a range only meets the domains of its own category
+(Classifier2::compare, encode/Classifier2.cpp:70-81), so its cost is the size of its
+bucket: the slices are cut at equal fractions of the cost prefix sum, and
+the all-gather pads every shard to the largest one.
 """
 from __future__ import annotations
 
 import numpy as np
 
 TUPLE_BYTES = 32
+N_BUCKETS = 7  # category + 1: −1..5
 
 
 def shard_bounds(n_items: int, world: int, rank: int) -> tuple[int, int]:
@@ -26,20 +33,60 @@ def shard_capacity(n_items: int, world: int) -> int:
     return (n_items + world - 1) // world
 
 
-def gather_tuples(local, n_items: int, world: int, group=None):
-    """All-gathers per-rank tuple buffers (torch uint8 tensors of shard_capacity*32 bytes, on
-    the device for nccl or on the CPU for gloo) and returns the n_items*32 leading bytes in
-    global range order (rank 0's shard first, ...)."""
+def range_costs(ranges: np.ndarray, domains: np.ndarray) -> np.ndarray:
+    """Per-range search cost with the classifier on: the number of domains sharing the range's
+    category (both grids classified, categories −1..5), plus one for the range's own fixed work."""
+    cnt = np.bincount(np.asarray(domains["category"], np.int64) + 1, minlength=N_BUCKETS)
+    return cnt[np.asarray(ranges["category"], np.int64) + 1].astype(np.int64) + 1
+
+
+def shard_plan(n_items: int, world: int, costs: np.ndarray | None = None) -> list[tuple[int, int]]:
+    """[start, stop) of every rank: equal counts (costs None), else contiguous slices cut where the
+    cost prefix sum crosses k/world of the total (each rank's cost is within one range's cost of
+    the mean)."""
+    if costs is None:
+        return [shard_bounds(n_items, world, r) for r in range(world)]
+    costs = np.asarray(costs, np.int64)
+    assert len(costs) == n_items
+    csum = np.concatenate([[0], np.cumsum(costs)])
+    total = int(csum[-1])
+    cuts = [0]
+    for k in range(1, world):
+        # first boundary whose prefix reaches k/world of the total (ties to the nearer side)
+        goal = total * k / world
+        i = int(np.searchsorted(csum, goal, side="left"))
+        if 0 < i <= n_items and goal - csum[i - 1] < csum[i] - goal:
+            i -= 1
+        cuts.append(min(max(i, cuts[-1]), n_items))
+    cuts.append(n_items)
+    return [(cuts[r], cuts[r + 1]) for r in range(world)]
+
+
+def plan_capacity(plan: list[tuple[int, int]]) -> int:
+    return max((b - a for a, b in plan), default=0)
+
+
+def gather_tuples(local, plan: list[tuple[int, int]], group=None):
+    """All-gathers per-rank tuple buffers (torch uint8 tensors of plan_capacity·32 bytes, on the
+    device for nccl or on the CPU for gloo) and returns the tuples of every rank's shard in
+    global range order (rank 0's shard first, ...).  Runs the collective whenever a process group
+    is initialised, world size 1 included."""
     import torch
     import torch.distributed as dist
 
-    cap = shard_capacity(n_items, world) * TUPLE_BYTES
+    world = len(plan)
+    cap = plan_capacity(plan) * TUPLE_BYTES
     assert local.numel() == cap and local.dtype == torch.uint8
-    if world == 1:
-        return local[: n_items * TUPLE_BYTES]
+    if world == 1 and not dist.is_initialized():
+        return local[: (plan[0][1] - plan[0][0]) * TUPLE_BYTES]
+    assert dist.get_world_size(group) == world
     out = torch.empty(world * cap, dtype=torch.uint8, device=local.device)
     dist.all_gather_into_tensor(out, local, group=group)
-    return out[: n_items * TUPLE_BYTES]
+    if all(b - a == plan_capacity(plan) for a, b in plan[:-1]):  # equal shards: one view
+        n = plan[-1][1]
+        return out[: n * TUPLE_BYTES]
+    parts = [out[r * cap: r * cap + (b - a) * TUPLE_BYTES] for r, (a, b) in enumerate(plan)]
+    return torch.cat(parts)
 
 
 def tuples_from_bytes(buf) -> np.ndarray:
@@ -67,14 +114,33 @@ def records_from_tuples(tuples: np.ndarray, ranges: np.ndarray, domains: np.ndar
     return rec
 
 
+def classified_grids(engine, ranges: np.ndarray, domains: np.ndarray):
+    """Copies of both grids with every −1 category computed on the engine's device planes (the
+    same categories the search uses), so every rank derives the same cost-balanced plan."""
+    r, d = ranges, domains
+    if (np.asarray(d["category"]) == -1).any():
+        d = engine.classify(d, target_plane=False)
+    if (np.asarray(r["category"]) == -1).any():
+        r = engine.classify(r, target_plane=True)
+    return r, d
+
+
 def encode_sharded(engine, ranges: np.ndarray, domains: np.ndarray, rank: int, world: int, device=None,
-                   group=None) -> np.ndarray:
+                   group=None, use_classifier: bool | None = None) -> np.ndarray:
     """Search this rank's shard of `ranges` on `engine` (frame and `domains` already set), all-gather
-    every rank's tuples and return the full encode_item_t array on every rank."""
+    every rank's tuples and return the full encode_item_t array on every rank.  With the
+    classifier (engine parameter, or `use_classifier`) the shards are cost-balanced."""
     import torch
 
-    start, stop = shard_bounds(len(ranges), world, rank)
-    cap = shard_capacity(len(ranges), world) * TUPLE_BYTES
+    if use_classifier is None:
+        use_classifier = bool(getattr(getattr(engine, "_p", None), "use_classifier", 0))
+    if use_classifier and world > 1:
+        cr, cd = classified_grids(engine, ranges, domains)
+        plan = shard_plan(len(ranges), world, range_costs(cr, cd))
+    else:
+        plan = shard_plan(len(ranges), world)
+    start, stop = plan[rank]
+    cap = plan_capacity(plan) * TUPLE_BYTES
     local = torch.zeros(cap, dtype=torch.uint8, device=device)
     if local.is_cuda:
         torch.cuda.synchronize(local.device)  # the zero-fill must land before the engine's pack
@@ -87,4 +153,4 @@ def encode_sharded(engine, ranges: np.ndarray, domains: np.ndarray, rank: int, w
     elif stop > start:  # gloo: host tuples
         t = engine.fetch_tuples()
         local[: (stop - start) * TUPLE_BYTES] = torch.from_numpy(np.ascontiguousarray(t).view(np.uint8))
-    return records_from_tuples(tuples_from_bytes(gather_tuples(local, len(ranges), world, group)), ranges, domains)
+    return records_from_tuples(tuples_from_bytes(gather_tuples(local, plan, group)), ranges, domains)

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define FRAC_ABI_VERSION 3
+#define FRAC_ABI_VERSION 4
 
 /* error codes */
 #define FRAC_OK 0
@@ -141,6 +141,16 @@ int frac_set_ranges(frac_ctx* ctx, const frac_grid_item* ranges, size_t nr);
 int frac_run(frac_ctx* ctx);
 int frac_fetch(frac_ctx* ctx, frac_encode_item* out, frac_stats* stats);
 int frac_sync(frac_ctx* ctx);
+
+/* Per-run device times (FRAC_FLAG_TIMING): the ms_device / ms_prep / ms_search / ms_finish of
+ * every frac_run since the previous call that passed `out` (at most the last 256 runs), oldest
+ * first, from HIP events recorded on the context's stream around each phase.  Waits for the
+ * stream.  *n_out = the run count; writes min(count, cap) entries (out may be NULL to query).
+ * Lets a benchmark time the search kernel of exactly the runs of its timed region. */
+typedef struct frac_run_timing {
+    double ms_device, ms_prep, ms_search, ms_finish;
+} frac_run_timing;
+int frac_timing_history(frac_ctx* ctx, frac_run_timing* out, size_t cap, size_t* n_out);
 
 /* One-shot: set_ranges + run + fetch (the shape of AbstractEncodingEngine2::encode
  * applied to a batch of range items). */

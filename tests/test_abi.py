@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol():
     assert len(names) >= 20
     missing = [n for n in names if not hasattr(lib, n)]
     assert not missing, missing
-    assert lib.frac_abi_version() == 3
+    assert lib.frac_abi_version() == 4
 
 
 def test_record_layouts_match_reference_structs(tmp_path):
@@ -117,3 +117,19 @@ def test_engine_without_device_fails_loudly():
         pytest.skip("device present")
     with pytest.raises(F.FracError):
         F.Engine()
+
+
+def _kernel_instances(pattern):
+    """Demangled host-side launch stubs of one kernel template in the product library."""
+    out = subprocess.run(["nm", "-C", F.LIB_PATH], capture_output=True, text=True, check=True).stdout
+    return [m.group(1) for m in re.finditer(pattern, out)]
+
+
+def test_product_library_has_no_ablation_kernels():
+    # the "tuning only, wrong results" ablations exist only in a -DFRAC_TUNING build; unknown or
+    # ablation FRAC_MFMA_VARIANT values fail the run (fracenc_api.hip mfma_variant)
+    dft = _kernel_instances(r"fracenc::search_dft<(?:true|false), (\d+)")
+    mfma = _kernel_instances(r"fracenc::search_mfma<\d+, \d+, (?:true|false), (\d+)>")
+    assert dft and mfma
+    assert all(int(v) & (8 | 16 | 32 | 64 | 256 | 512) == 0 for v in dft), sorted(set(dft))
+    assert all(int(v) & (8 | 16) == 0 for v in mfma), sorted(set(mfma))

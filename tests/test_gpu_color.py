@@ -190,3 +190,46 @@ def test_c5_sharded_over_two_ranks_matches_single_rank(tmp_path):
         want = [o for o, _ in enc.fetch()]
     for k, w in zip("yuv", want):
         assert got[k].tobytes() == w.tobytes(), k
+
+
+def test_c5_load_after_sharded_encode_restores_full_ranges():
+    """encode_sharded leaves each engine holding one shard; the next load() of a same-geometry frame
+    must search every range again (world 1 without a process group: one shard = all ranges, so
+    the check uses world 2 / rank 1 and compares with a fresh encoder)."""
+    import torch.distributed as dist
+    from fractencode_amd.color import ColorEncoder
+    from fractencode_amd.distributed import shard_plan
+
+    assert not dist.is_initialized()
+    rgb = plane("lenna_rgb")
+    with ColorEncoder(0, 8, 16, 4) as enc:
+        enc.load(rgb)
+        # rank 1 of 2, without a collective: search only the shard (what encode_sharded leaves behind)
+        for e, rngs in zip(enc.engines, enc.ranges):
+            a, b = shard_plan(len(rngs), 2)[1]
+            e.set_ranges(rngs[a:b])
+            e.run()
+        enc._sharded = True
+        enc.load(rgb)
+        enc.run()
+        enc.sync()
+        again = [o for o, _ in enc.fetch()]
+    with ColorEncoder(0, 8, 16, 4) as fresh:
+        fresh.load(rgb)
+        fresh.run()
+        fresh.sync()
+        want = [o for o, _ in fresh.fetch()]
+    for g, w in zip(again, want):
+        assert len(g) == len(w) and g.tobytes() == w.tobytes()
+
+
+def test_set_frame_device_rejects_strided_columns():
+    import torch
+
+    t = torch.zeros((64, 128), dtype=torch.uint8, device="cuda")
+    with F.Engine(0) as e:
+        with pytest.raises(F.FracError):
+            e.set_frame(t[:, ::2])
+        with pytest.raises(F.FracError):
+            e.set_frame(t.to(torch.int16))
+        e.set_frame(t[:, :64])  # row stride 128 >= width 64: fine

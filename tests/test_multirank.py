@@ -10,7 +10,7 @@ import numpy as np
 import pytest
 import torch.multiprocessing as mp
 
-from fractencode_amd.distributed import shard_bounds, shard_capacity
+from fractencode_amd.distributed import plan_capacity, range_costs, shard_bounds, shard_capacity, shard_plan
 
 
 def test_shard_bounds_cover_all_items_once():
@@ -24,12 +24,39 @@ def test_shard_bounds_cover_all_items_once():
             assert seen == list(range(n))
 
 
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_cost_plan_balances_classifier_buckets(world):
+    # with the classifier a range costs |bucket(category)|; contiguous shards cut on
+    # the cost prefix sum stay within one range's cost of the mean, and cover every range once
+    rng = np.random.default_rng(11)
+    n = 5000
+    cost = rng.choice([1, 50, 4000, 20000], size=n, p=[0.2, 0.3, 0.3, 0.2]).astype(np.int64)
+    plan = shard_plan(n, world, cost)
+    assert plan[0][0] == 0 and plan[-1][1] == n
+    assert all(plan[r][1] == plan[r + 1][0] for r in range(world - 1))
+    per = [int(cost[a:b].sum()) for a, b in plan]
+    assert max(per) - cost.sum() / world <= cost.max()
+    eq = [int(cost[a:b].sum()) for a, b in shard_plan(n, world)]
+    assert max(per) <= max(eq)
+    assert plan_capacity(plan) >= max(b - a for a, b in plan)
+
+
+def test_range_costs_are_bucket_sizes():
+    import fractencode_amd as F
+    d = np.zeros(10, dtype=F.GRID_ITEM)
+    d["category"] = [-1, 0, 0, 1, 1, 1, 2, 5, 5, 5]
+    r = np.zeros(4, dtype=F.GRID_ITEM)
+    r["category"] = [0, 1, 3, -1]
+    np.testing.assert_array_equal(range_costs(r, d), [3, 4, 1, 2])
+
+
 class OracleEngine:
     """Engine-interface stand-in (CPU): set_ranges / run / fetch_tuples / sync."""
 
-    def __init__(self, plane, doms):
+    def __init__(self, plane, doms, use_classifier=False):
         from oracle import oracle as O
         self.O, self.plane, self.doms = O, plane, doms
+        self.use_classifier = use_classifier
         self.index = {(int(d["x"]), int(d["y"])): i for i, d in enumerate(doms)}
 
     def set_ranges(self, r):
@@ -37,12 +64,18 @@ class OracleEngine:
 
     def run(self):
         import fractencode_amd as F
-        out, _, _ = self.O.estimate(self.plane, self.doms, self.r.astype(self.O.ITEM_DTYPE), threads=2)
+        out, _, _ = self.O.estimate(self.plane, self.doms, self.r.astype(self.O.ITEM_DTYPE), threads=2,
+                                    use_classifier=self.use_classifier)
         rec = np.zeros(len(out), dtype=F.ENCODE_ITEM)
         rec["x"], rec["y"], rec["w"], rec["h"] = self.r["x"], self.r["y"], self.r["w"], self.r["h"]
         rec["distance"], rec["contrast"], rec["brightness"] = out["dist"], out["s"], out["o"]
         rec["transform"], rec["dx"], rec["dy"], rec["sw"], rec["sh"] = out["t"], out["dx"], out["dy"], out["dw"], out["dh"]
         self.rec = rec
+
+    def classify(self, items, target_plane=False):
+        out = items.copy()
+        out["category"] = self.O.classify(self.plane, items.astype(self.O.ITEM_DTYPE))["category"]
+        return out
 
     def fetch_tuples(self):
         import fractencode_amd as F
@@ -79,6 +112,28 @@ def _worker(rank, world, port, path):
     dist.destroy_process_group()
 
 
+def _cls_worker(rank, world, port, path):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import torch.distributed as dist
+
+    import fractencode_amd as F
+    from fractencode_amd.distributed import encode_sharded
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    rng = np.random.default_rng(5)
+    plane = rng.integers(0, 256, (64, 96), dtype=np.uint8)
+    doms = F.preclassify(plane, F.create_uniform_grid(96, 64, 16, 8))
+    rngs = F.preclassify(plane, F.create_uniform_grid(96, 64, 8, 8))
+    full = encode_sharded(OracleEngine(plane, doms, True), rngs, doms, rank, world, use_classifier=True)
+    if rank == 0:
+        np.save(path, full)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -103,6 +158,26 @@ def test_gloo_sharded_search_matches_single_rank(tmp_path, oracle, world):
     np.testing.assert_array_equal(full["distance"], want["dist"])
     np.testing.assert_array_equal(full["contrast"], want["s"])
     np.testing.assert_array_equal(full["brightness"], want["o"])
+
+
+def test_gloo_cost_balanced_classifier_shards_match_single_rank(tmp_path, oracle):
+    """Classifier on: cost-balanced (unequal-count) shards, padded all-gather, same records as one
+    rank (the oracle)."""
+    import fractencode_amd as F
+    path = str(tmp_path / "full.npy")
+    mp.spawn(_cls_worker, args=(2, _free_port(), path), nprocs=2, join=True)
+    full = np.load(path)
+    rng = np.random.default_rng(5)
+    plane = rng.integers(0, 256, (64, 96), dtype=np.uint8)
+    doms = F.preclassify(plane, F.create_uniform_grid(96, 64, 16, 8))
+    rngs = F.preclassify(plane, F.create_uniform_grid(96, 64, 8, 8))
+    plan = shard_plan(len(rngs), 2, range_costs(rngs, doms))
+    assert plan[0][1] - plan[0][0] != plan[1][1] - plan[1][0]  # the plan is not the equal split
+    want, _, _ = oracle.estimate(plane, doms.astype(oracle.ITEM_DTYPE), rngs.astype(oracle.ITEM_DTYPE),
+                                 use_classifier=True)
+    for a, b in (("dx", "dx"), ("dy", "dy"), ("transform", "t"), ("distance", "dist"), ("contrast", "s"),
+                 ("brightness", "o")):
+        np.testing.assert_array_equal(full[a], want[b], err_msg=a)
 
 
 def _gpu_worker(rank, world, port, path):
@@ -139,6 +214,91 @@ def test_two_ranks_with_hip_engines_match_reference(tmp_path):
     mp.spawn(_gpu_worker, args=(2, _free_port(), path), nprocs=2, join=True)
     full = np.load(path)
     rec, _ = golden("lenna_t4")
+    got = {"x": full["x"], "y": full["y"], "dx": full["dx"], "dy": full["dy"], "dw": full["sw"], "dh": full["sh"],
+           "t": full["transform"], "dist": full["distance"], "s": full["contrast"], "o": full["brightness"]}
+    for k in FIELDS:
+        np.testing.assert_array_equal(got[k], rec[k], err_msg=k)
+
+
+def _nccl_worker(rank, world, port, path):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import torch
+    import torch.distributed as dist
+
+    import fractencode_amd as F
+    from fractencode_amd.distributed import encode_sharded
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    torch.cuda.set_device(rank)
+    dev = torch.device("cuda", rank)
+    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    y = np.fromfile(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "lenna_y.u8"),
+                    dtype=np.uint8).reshape(512, 512)
+    doms = F.create_uniform_grid(512, 512, 16, 8)
+    with F.Engine(rank, 4) as e:
+        e.set_frame(y)
+        e.set_domains(doms)
+        # device tuples (frac_copy_tuples_device) through a real RCCL all_gather_into_tensor
+        full = encode_sharded(e, F.create_uniform_grid(512, 512, 8, 8), doms, rank, world, device=dev)
+    if rank == 0:
+        np.save(path, full)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_nccl_device_tuples_world1_match_reference(tmp_path):
+    """The nccl path bench.py uses at N > 1 — tuples packed on the device, all-gathered by RCCL —
+    run at world size 1 (one GPU per box; the collective still runs), against lenna_t4."""
+    from golden_util import FIELDS, golden
+
+    path = str(tmp_path / "full.npy")
+    mp.spawn(_nccl_worker, args=(1, _free_port(), path), nprocs=1, join=True)
+    full = np.load(path)
+    rec, _ = golden("lenna_t4")
+    got = {"x": full["x"], "y": full["y"], "dx": full["dx"], "dy": full["dy"], "dw": full["sw"], "dh": full["sh"],
+           "t": full["transform"], "dist": full["distance"], "s": full["contrast"], "o": full["brightness"]}
+    for k in FIELDS:
+        np.testing.assert_array_equal(got[k], rec[k], err_msg=k)
+
+
+def _gpu_cls_worker(rank, world, port, path):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import torch.distributed as dist
+
+    import fractencode_amd as F
+    from fractencode_amd.distributed import encode_sharded
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    y = np.fromfile(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "lenna_y.u8"),
+                    dtype=np.uint8).reshape(512, 512)
+    doms = F.create_uniform_grid(512, 512, 16, 8)  # categories −1: classified on the device
+    with F.Engine(0, 4, True) as e:
+        e.set_frame(y)
+        e.set_domains(doms)
+        full = encode_sharded(e, F.create_uniform_grid(512, 512, 8, 8), doms, rank, world)
+    if rank == 0:
+        np.save(path, full)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_two_ranks_cost_balanced_classifier_match_reference(tmp_path):
+    """Classifier on (lenna_cls): two ranks cut the ranges at equal bucket cost (unequal counts),
+    HIP engines, padded all-gather; records equal the reference golden."""
+    from golden_util import FIELDS, golden
+
+    path = str(tmp_path / "full.npy")
+    mp.spawn(_gpu_cls_worker, args=(2, _free_port(), path), nprocs=2, join=True)
+    full = np.load(path)
+    rec, _ = golden("lenna_cls")
     got = {"x": full["x"], "y": full["y"], "dx": full["dx"], "dy": full["dy"], "dw": full["sw"], "dh": full["sh"],
            "t": full["transform"], "dist": full["distance"], "s": full["contrast"], "o": full["brightness"]}
     for k in FIELDS:
