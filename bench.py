@@ -30,7 +30,6 @@ status; under torch.distributed.run (WORLD_SIZE set) it runs one rank per GPU ov
 from __future__ import annotations
 
 import argparse
-import hashlib
 import json
 import os
 import socket
@@ -130,8 +129,7 @@ def cpu_baseline(frame: np.ndarray, budget: float, threads: int, host: dict):
 def lib_sha16() -> str:
     import fractencode_amd as F
 
-    with open(F.LIB_PATH, "rb") as f:
-        return hashlib.sha256(f.read()).hexdigest()[:16]
+    return F.source_id()
 
 
 def load_traffic(form: str):
@@ -145,8 +143,8 @@ def load_traffic(form: str):
     e = d.get(form)
     if e is None:
         return None, f"no PMC entry for form {form}"
-    if e.get("lib_sha16") != lib_sha16():
-        return None, f"PMC entry is from library {e.get('lib_sha16')}, not this build"
+    if e.get("source_id") != lib_sha16():
+        return None, f"PMC entry is from sources {e.get('source_id')}, not this build's"
     return e.get("hbm_bytes_per_launch"), e.get("source")
 
 
@@ -278,8 +276,10 @@ def main(args):
         "search_form": form,
         "phases_ms": {k: round(float(np.mean(hist["ms_" + k])), 3) for k in ("device", "prep", "search", "finish")},
         "fallback_ranges": st["fallback_ranges"],
-        "lib_sha16": lib_sha16(),
+        "source_id": lib_sha16(),
     }
+
+    main_out, _ = eng.fetch()  # the timed steps' records (the SEA engine is checked against them)
 
     # host boundary (§8(d) end-to-end): frame H2D from pinned memory + search + tuples D2H, per step
     e2e_steps = args.steps if args.e2e_steps < 0 else args.e2e_steps
@@ -307,12 +307,12 @@ def main(args):
                        "step": "frame H2D (pinned, 16 MiB) + search + tuples D2H (pinned, 32 B per range)"
                                + (" per rank; no gather" if world > 1 else "")}
         eng.set_frame(d_frame)
+        eng.run()
 
     if world == 1 and engine_name == "mfma" and args.alt_steps > 0:
         # the same workload on the other engines, measured the same way: the VALU engine (packed-u16
         # v_dot2, north_star's no-MFMA formulation, exhaustive) and the SEA engine (successive
         # elimination: identical records, most candidates skipped by an exact bound, data-dependent)
-        main_out, _ = eng.fetch()
         line["alt_engines"] = {}
         for alt_name, alt_id in (("valu", F.ENGINE_VALU), ("sea", F.ENGINE_SEA)):
             with F.Engine(dev.index, args.transforms, False, 0.0, -1.0, alt_id, timing=True) as alt:

@@ -36,9 +36,9 @@ NO_DOMAIN = 0xFFFFFFFF
 assert GRID_ITEM.itemsize == 20 and ENCODE_ITEM.itemsize == 64 and TUPLE.itemsize == 32
 
 ENGINE_AUTO, ENGINE_VALU, ENGINE_MFMA, ENGINE_SEA = 0, 1, 2, 3
-FORM_DOT2, FORM_DIRECT, FORM_FOURIER, FORM_SEA, FORM_SEA_MFMA = 0, 1, 2, 3, 4
+FORM_DOT2, FORM_DIRECT, FORM_FOURIER, FORM_SEA, FORM_SEA_MFMA, FORM_SAMPLED = 0, 1, 2, 3, 4, 5
 FORM_NAMES = {FORM_DOT2: "dot2", FORM_DIRECT: "direct", FORM_FOURIER: "fourier", FORM_SEA: "sea",
-              FORM_SEA_MFMA: "sea_mfma"}
+              FORM_SEA_MFMA: "sea_mfma", FORM_SAMPLED: "sampled"}
 FLAG_TIMING = 1
 
 # Frac::TransformType (image/transform.h:16-25)
@@ -71,6 +71,21 @@ class FracError(RuntimeError):
 
 
 _lib = None
+
+
+def source_id() -> str:
+    """16 hex digits identifying the library's sources (csrc/, include/fracenc.h): the key under
+    which profiles/ records PMC measurements, so a measurement of another build is never reused."""
+    import hashlib
+
+    h = hashlib.sha256()
+    csrc = os.path.join(HERE, "csrc")
+    for name in sorted(os.listdir(csrc)):
+        with open(os.path.join(csrc, name), "rb") as f:
+            h.update(name.encode() + b"\0" + f.read())
+    with open(os.path.join(os.path.dirname(HERE), "include", "fracenc.h"), "rb") as f:
+        h.update(f.read())
+    return h.hexdigest()[:16]
 
 
 def lib() -> C.CDLL:
@@ -403,7 +418,7 @@ def encode(plane: np.ndarray, range_size: int = 8, domain_size: int | None = Non
     """Encoder2's search half for one plane, with grids built like main.cpp:142-162."""
     plane = np.ascontiguousarray(plane, dtype=np.uint8)
     H, W = plane.shape
-    dsz = domain_size or 2 * range_size
+    dsz = domain_size or 2 * range_size  # the reference's default pair is 16 -> 4 (encode_parameters.h:6-7)
     doms = create_uniform_grid(W, H, dsz, dsz // 2)
     rngs = create_uniform_grid(W, H, range_size, range_size)
     if use_classifier:

@@ -25,6 +25,7 @@
 #include "fracenc_sea.hip"
 #include "fracenc_stream.hip"
 #include "fracenc_tp.hip"
+#include "fracenc_gen.hip"
 
 using namespace fracenc;
 
@@ -158,6 +159,11 @@ struct frac_ctx {
 
     // prepared state
     int n = 0;
+    uint32_t S = 0;          // domain side
+    bool virt = false;       // sampled form (fracenc_gen.hip): one pool row per (domain, transform)
+    bool generic = false;    // sampled form with a range size no templated engine covers (gen_search)
+    uint32_t Teff = 4;       // transforms the engines search per pool row (1 in the sampled form)
+    uint32_t K2 = 0;         // dwords per pool row
     uint32_t G = 4, NG = 1;
     std::vector<uint32_t> porig;            // pool position → domain index
     std::vector<uint32_t> bucket_begin, bucket_end; // per bucket (category + 1)
@@ -383,8 +389,10 @@ int prepare(frac_ctx* c)
     if (!c->planes_set || !c->doms_set || !c->ranges_set)
         return c->fail(FRAC_E_STATE, "planes, domains and ranges must be set before frac_run");
     const uint32_t T = c->p.transforms;
-    // geometry: the engine implements the ratio-2 path of TransformMatcher (n×n ranges,
-    // 2n×2n domains), n ∈ {2, 4, 8, 16}
+    // geometry (TransformMatcher::matchTransformType, encode/transformmatcher.h:70-78): n×n ranges
+    // and S×S domains, S > n (main.cpp:99 rejects target >= source).  S = 2n with n ∈ {2, 4, 8, 16}
+    // is every engine's decimate-then-permute path; any other pair — the CLI default 16→4 among
+    // them — runs the sampled form (fracenc_gen.hip): one pool row per (domain, transform).
     int n = c->ranges.empty() ? 8 : (int)c->ranges[0].w;
     for (const auto& r : c->ranges) {
         if ((int)r.w != n || (int)r.h != n)
@@ -392,19 +400,28 @@ int prepare(frac_ctx* c)
         if ((uint64_t)r.x + r.w > c->tgt.w || (uint64_t)r.y + r.h > c->tgt.h)
             return c->fail(FRAC_E_INVALID, "range outside the target plane");
     }
-    if (n != 2 && n != 4 && n != 8 && n != 16)
-        return c->fail(FRAC_E_INVALID, "range size must be 2, 4, 8 or 16");
+    if (n < 2 || n > (int)kGenMaxN)
+        return c->fail(FRAC_E_INVALID, "range size must be 2..32");
+    const uint32_t S = c->doms.empty() ? 2u * (uint32_t)n : c->doms[0].w;
     for (const auto& d : c->doms) {
-        if ((int)d.w != 2 * n || (int)d.h != 2 * n)
-            return c->fail(FRAC_E_INVALID, "domains must be square with twice the range size");
+        if (d.w != S || d.h != S)
+            return c->fail(FRAC_E_INVALID, "all domains must be square and of one size");
         if ((uint64_t)d.x + d.w > c->src.w || (uint64_t)d.y + d.h > c->src.h)
             return c->fail(FRAC_E_INVALID, "domain outside the source plane");
     }
-    if (c->doms.size() >= (1u << 24))
-        return c->fail(FRAC_E_INVALID, "at most 2^24 - 1 domains");
+    if (S <= (uint32_t)n)
+        return c->fail(FRAC_E_INVALID, "domains must be larger than the ranges (main.cpp:99)");
+    const bool pow2 = n == 2 || n == 4 || n == 8 || n == 16;
+    c->virt = !(pow2 && S == 2u * (uint32_t)n);
+    c->generic = !pow2;
+    c->S = S;
+    c->Teff = c->virt ? 1u : T;
+    c->K2 = (uint32_t)(n * n + 1) / 2;
+    if ((uint64_t)c->doms.size() * (c->virt ? T : 1u) >= (1u << 24))
+        return c->fail(FRAC_E_INVALID, "at most 2^24 - 1 domains (domains x transforms in the sampled form)");
     c->n = n;
-    c->G = n == 16 ? 1u : (n <= 4 ? T : 4u);
-    c->NG = T / c->G;
+    c->G = c->virt ? 1u : (n == 16 ? 1u : (n <= 4 ? T : 4u));
+    c->NG = c->virt ? 1u : T / c->G;
 
     tr.mark("validate");
     // buckets: category + 1 (0 = category −1) with the classifier, a single bucket without
@@ -459,10 +476,17 @@ int prepare(frac_ctx* c)
     bucket_order(c->range_bucket, rord, rbeg);
     c->bucket_begin.assign(dbeg.begin(), dbeg.end() - 1);
     c->bucket_end.assign(dbeg.begin() + 1, dbeg.end());
+    // the engines' pool rows per bucket: pool positions, or T rows per position in the sampled form
+    const uint32_t VT = c->virt ? T : 1u;
+    std::vector<uint32_t> eb(nb), ee(nb);
+    for (int b = 0; b < nb; ++b) {
+        eb[b] = c->bucket_begin[b] * VT;
+        ee[b] = c->bucket_end[b] * VT;
+    }
     c->rbucket.resize(c->ranges.size());
     for (size_t i = 0; i < c->ranges.size(); ++i) {
         const int b = c->range_bucket[i];
-        c->rbucket[i] = make_uint2(c->bucket_begin[b], c->bucket_end[b]);
+        c->rbucket[i] = make_uint2(eb[b], ee[b]);
     }
     // range slots: per bucket, padded to whole waves of 64 (the VALU engine's work lists only)
     c->slot_range.clear();
@@ -483,12 +507,12 @@ int prepare(frac_ctx* c)
     }
     size_t total_blocks = 0;
     for (auto& bl : blocks)
-        if (c->bucket_end[bl.second] > c->bucket_begin[bl.second])
+        if (ee[bl.second] > eb[bl.second])
             total_blocks += c->NG;
     // domain splits: enough waves to fill 256 CUs several times over, ≥ 32 domains per wave
     const size_t target_waves = 8192;
     for (auto& bl : blocks) {
-        const uint32_t b0 = c->bucket_begin[bl.second], b1 = c->bucket_end[bl.second];
+        const uint32_t b0 = eb[bl.second], b1 = ee[bl.second];
         const uint32_t D = b1 - b0;
         if (D == 0)
             continue;
@@ -506,21 +530,22 @@ int prepare(frac_ctx* c)
     tr.mark("buckets + valu work");
     c->eligible_pairs = 0;
     for (size_t i = 0; i < c->ranges.size(); ++i)
-        c->eligible_pairs += c->rbucket[i].y - c->rbucket[i].x;
-    c->hitH = compute_hit_limit(c->p.rms_threshold, (uint32_t)(4 * n * n));
+        c->eligible_pairs += (c->rbucket[i].y - c->rbucket[i].x) / VT;
+    c->hitH = compute_hit_limit(c->p.rms_threshold, S * S); // the domain's area (image/metrics.h:49)
     c->all_fallback = c->hitH >= kExactLimit;
 
-    // engine: the MFMA encoding is exact for n <= 8 (|Σ(r−128)(D4−510)| < 2^22)
-    if (c->p.engine == FRAC_ENGINE_SEA && n > 8)
-        return c->fail(FRAC_E_INVALID, "the SEA engine supports range sizes 2, 4 and 8");
-    // MFMA: exact for every supported n (n = 16 through search_mfma16's integer epilogue)
-    c->engine = c->p.engine == FRAC_ENGINE_VALU  ? FRAC_ENGINE_VALU
-                : c->p.engine == FRAC_ENGINE_SEA ? FRAC_ENGINE_SEA
-                                                 : FRAC_ENGINE_MFMA;
+    // engine.  MFMA: exact for every templated n (n = 16 through search_mfma16's integer epilogue).
+    // SEA covers n ≤ 8 (its exact evaluation holds a candidate in one wave's VGPRs): larger ranges run
+    // the exhaustive MFMA search, which gives the same records.  Range sizes without a templated
+    // engine run gen_search (VALU) whatever the request.
+    c->engine = c->generic                                ? FRAC_ENGINE_VALU
+                : c->p.engine == FRAC_ENGINE_VALU          ? FRAC_ENGINE_VALU
+                : c->p.engine == FRAC_ENGINE_SEA && n <= 8 ? FRAC_ENGINE_SEA
+                                                           : FRAC_ENGINE_MFMA;
     // SEA, n = 8, T = 4: the tiled form (FRAC_SEA_TILED=0 keeps the per-range form, A/B knob)
     {
         const char* st = getenv("FRAC_SEA_TILED");
-        c->tp = c->engine == FRAC_ENGINE_SEA && n == 8 && T == 4 && (st ? atoi(st) != 0 : true);
+        c->tp = c->engine == FRAC_ENGINE_SEA && !c->virt && n == 8 && T == 4 && (st ? atoi(st) != 0 : true);
     }
     if (c->tp) {
         if (nb > kTpMaxBuckets)
@@ -583,7 +608,7 @@ int prepare(frac_ctx* c)
         std::vector<uint32_t> tile_first(nb, 0), tile_count(nb, 0);
         for (int b = 0; b < nb; ++b) {
             tile_first[b] = (uint32_t)(c->m_tile_pos.size() / 32);
-            for (uint32_t pp = c->bucket_begin[b]; pp < c->bucket_end[b]; ++pp)
+            for (uint32_t pp = eb[b]; pp < ee[b]; ++pp)
                 c->m_tile_pos.push_back((int32_t)pp);
             while (c->m_tile_pos.size() % 32)
                 c->m_tile_pos.push_back(-1);
@@ -684,7 +709,7 @@ int prepare(frac_ctx* c)
             build_work(1, 4096, c->m_work, c->m_blk_ptr, c->m_blk_ent, false);
         else
             build_work(4, 8192, c->m_work, c->m_blk_ptr, c->m_blk_ent, false);
-        if (n == 8 && c->p.transforms == 4) {
+        if (n == 8 && c->p.transforms == 4 && !c->virt) {
             // FRAC_DFT_WGS (tuning knob): target workgroup count of the Fourier search
             const char* tw = getenv("FRAC_DFT_WGS");
             const size_t wgs = tw ? (size_t)std::max(1, atoi(tw)) : 8192 / kDftBlocksPerWG * 4;
@@ -700,11 +725,11 @@ int prepare(frac_ctx* c)
     }
 
     tr.mark("engine work");
-    const size_t nr = c->ranges.size(), P = c->porig.size();
+    const size_t nr = c->ranges.size(), P = c->porig.size() * VT; // engine pool rows
     FRAC_HIP(c, c->d_doms.ensure(c->doms.size()));
     FRAC_HIP(c, c->d_ranges.ensure(nr));
-    FRAC_HIP(c, c->d_porig.ensure(P));
-    FRAC_HIP(c, c->d_pool.ensure(P * (size_t)(n * n / 2)));
+    FRAC_HIP(c, c->d_porig.ensure(c->porig.size()));
+    FRAC_HIP(c, c->d_pool.ensure(P * (size_t)c->K2));
     FRAC_HIP(c, c->d_negsd2.ensure(P));
     FRAC_HIP(c, c->d_slot_range.ensure(c->slot_range.size()));
     FRAC_HIP(c, c->d_work.ensure(c->work.size()));
@@ -719,7 +744,7 @@ int prepare(frac_ctx* c)
     };
     FRAC_TRY(up(c->d_doms.ptr, c->doms.data(), c->doms.size() * sizeof(frac_grid_item)));
     FRAC_TRY(up(c->d_ranges.ptr, c->ranges.data(), nr * sizeof(frac_grid_item)));
-    FRAC_TRY(up(c->d_porig.ptr, c->porig.data(), P * sizeof(uint32_t)));
+    FRAC_TRY(up(c->d_porig.ptr, c->porig.data(), c->porig.size() * sizeof(uint32_t)));
     FRAC_TRY(up(c->d_slot_range.ptr, c->slot_range.data(), c->slot_range.size() * sizeof(int32_t)));
     FRAC_TRY(up(c->d_work.ptr, c->work.data(), c->work.size() * sizeof(uint4)));
     FRAC_TRY(up(c->d_rbucket.ptr, c->rbucket.data(), nr * sizeof(uint2)));
@@ -745,7 +770,7 @@ int prepare(frac_ctx* c)
         FRAC_HIP(c, c->d_sea_rord2.ensure(std::max<size_t>(nr, 1)));
         FRAC_HIP(c, c->d_sea_bend.ensure(kSeaMaxBuckets));
         FRAC_HIP(c, c->d_sea_count.ensure(1));
-        FRAC_TRY(up(c->d_sea_bend.ptr, c->bucket_end.data(), c->bucket_end.size() * sizeof(uint32_t)));
+        FRAC_TRY(up(c->d_sea_bend.ptr, ee.data(), ee.size() * sizeof(uint32_t)));
         size_t t1 = 0, t2 = 0;
         FRAC_HIP(c, sort_pairs_u32(nullptr, t1, c->d_sea_dkey.ptr, c->d_sea_dkey2.ptr, c->d_sea_dpos.ptr,
                                    c->d_sea_dpos2.ptr, P, 20, c->stream));
@@ -810,8 +835,9 @@ int prepare(frac_ctx* c)
         FRAC_HIP(c, c->d_m_rconst.ensure((size_t)c->nblocks * 32));
         FRAC_HIP(c, c->d_m_dconst.ensure((size_t)c->ntiles * 32));
         FRAC_HIP(c, c->d_m_dtiles.ensure((size_t)c->ntiles * KS * 64));
-        FRAC_HIP(c, c->d_m_rfrags.ensure((size_t)c->nblocks * T * KS * 64));
-        FRAC_HIP(c, c->d_m_entries.ensure(std::max(c->m_work.size() * 4 * T, c->m8_work.size() * kDftBlocksPerWG) * 64));
+        FRAC_HIP(c, c->d_m_rfrags.ensure((size_t)c->nblocks * c->Teff * KS * 64));
+        FRAC_HIP(c, c->d_m_entries.ensure(std::max(c->m_work.size() * 4 * c->Teff, c->m8_work.size() * kDftBlocksPerWG) *
+                                          64));
         if (!c->m8_blk_ptr.empty()) { // built for n = 8, T = 4 (search_dft); may have no work
             FRAC_HIP(c, c->d_m8_work.ensure(std::max<size_t>(c->m8_work.size(), 1)));
             FRAC_HIP(c, c->d_m8_blk_ptr.ensure(c->m8_blk_ptr.size()));
@@ -1060,9 +1086,10 @@ inline int launch_dft(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride)
 template <int N>
 int launch_mfma(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride)
 {
-    const uint32_t nr = (uint32_t)c->ranges.size(), T = c->p.transforms;
+    // T = the transforms per pool row: 1 in the sampled form (one row per domain and transform)
+    const uint32_t nr = (uint32_t)c->ranges.size(), T = c->Teff;
     if constexpr (N == 8) {
-        if (T == 4 && mfma_dft_enabled())
+        if (T == 4 && !c->virt && mfma_dft_enabled())
             return launch_dft(c, dtgt, tstride);
     }
     if (c->ntiles) {
@@ -1112,6 +1139,11 @@ int launch_mfma(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride)
                     search_mfma16<8, true><<<nwg, 512, 0, c->stream>>>(a);
                 else
                     search_mfma16<8, false><<<nwg, 512, 0, c->stream>>>(a);
+            } else if (T == 1) {
+                if (hits)
+                    search_mfma16<1, true><<<nwg, 64, 0, c->stream>>>(a);
+                else
+                    search_mfma16<1, false><<<nwg, 64, 0, c->stream>>>(a);
             } else {
                 if (hits)
                     search_mfma16<4, true><<<nwg, 256, 0, c->stream>>>(a);
@@ -1120,6 +1152,8 @@ int launch_mfma(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride)
             }
         } else if (T == 8)
             FRAC_TRY((launch_search_mfma<N, 8>(c, a)));
+        else if (T == 1)
+            FRAC_TRY((launch_search_mfma<N, 1>(c, a)));
         else
             FRAC_TRY((launch_search_mfma<N, 4>(c, a)));
     }
@@ -1324,7 +1358,7 @@ int launch_sea(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool timing)
         if (c->tp)
             return launch_tp(c, dtgt, tstride, timing);
     }
-    const uint32_t nr = (uint32_t)c->ranges.size(), P = (uint32_t)c->porig.size();
+    const uint32_t nr = (uint32_t)c->ranges.size(), P = (uint32_t)c->porig.size() * (c->virt ? c->p.transforms : 1u);
     if (P) {
         sea_domain_keys<N><<<(P + 255) / 256, 256, 0, c->stream>>>(c->d_pool.ptr, P, c->d_sea_bend.ptr,
                                                                    (uint32_t)c->bucket_end.size(), c->d_sea_dkey.ptr,
@@ -1361,7 +1395,9 @@ int launch_sea(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool timing)
         a.hitH = c->hitH;
         a.best_key = c->d_best_key.ptr;
         a.evaluated = c->d_sea_count.ptr;
-        if (c->p.transforms == 8)
+        if (c->Teff == 1) // the sampled form: one pool row per (domain, transform)
+            sea_search<N, 1><<<(nr + 3) / 4, 256, 0, c->stream>>>(a);
+        else if (c->p.transforms == 8)
             sea_search<N, 8><<<(nr + 3) / 4, 256, 0, c->stream>>>(a);
         else
             sea_search<N, 4><<<(nr + 3) / 4, 256, 0, c->stream>>>(a);
@@ -1371,10 +1407,112 @@ int launch_sea(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool timing)
     return FRAC_OK;
 }
 
+// the sampled form's view of the context (fracenc_gen.hip)
+GenArgs gen_args(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride)
+{
+    GenArgs g;
+    g.src = c->d_src.ptr;
+    g.sstride = c->d_sstride;
+    g.tgt = dtgt;
+    g.tstride = tstride;
+    g.doms = c->d_doms.ptr;
+    g.ranges = c->d_ranges.ptr;
+    g.porig = c->d_porig.ptr;
+    g.n = (uint32_t)c->n;
+    g.S = c->S;
+    g.T = c->p.transforms;
+    g.K2 = c->K2;
+    g.pool = c->d_pool.ptr;
+    g.negsd2 = c->d_negsd2.ptr;
+    g.nrows = (uint32_t)c->porig.size() * c->p.transforms;
+    return g;
+}
+
+// the sampled form's fit (every range) and fp32 fallback (the flagged ones)
+int launch_gen_finish(frac_ctx* c, const GenArgs& g)
+{
+    const uint32_t nr = (uint32_t)c->ranges.size();
+    if (!nr)
+        return FRAC_OK;
+    if (!c->all_fallback) {
+        GenFitArgs f;
+        f.g = g;
+        f.best_key = c->d_best_key.ptr;
+        f.nr = nr;
+        f.hitH = c->hitH;
+        f.smax = c->p.s_max;
+        f.all_fallback = 0;
+        f.out = c->d_out.ptr;
+        f.aux = c->d_aux.ptr;
+        f.fb_count = c->d_fb_count.ptr;
+        f.fb_list = c->d_fb_list.ptr;
+        gen_fit<<<(nr + 255) / 256, 256, 0, c->stream>>>(f);
+    }
+    GenFallbackArgs b;
+    b.g = g;
+    b.rbucket = c->d_rbucket.ptr;
+    b.fb_count = c->d_fb_count.ptr;
+    b.fb_list = c->d_fb_list.ptr;
+    b.thr = c->p.rms_threshold;
+    b.smax = c->p.s_max;
+    b.out = c->d_out.ptr;
+    b.aux = c->d_aux.ptr;
+    gen_fallback<<<512, 256, 0, c->stream>>>(b);
+    return FRAC_OK;
+}
+
+// range sizes without a templated engine (n ∉ {2, 4, 8, 16}): the sampled form's pool, gen_search,
+// gen_fit and gen_fallback
+int launch_generic(frac_ctx* c)
+{
+    const uint32_t nr = (uint32_t)c->ranges.size();
+    const bool timing = (c->p.flags & FRAC_FLAG_TIMING) != 0;
+    const uint8_t* dtgt = c->same_plane ? c->d_src.ptr : c->d_tgt.ptr;
+    const uint32_t tstride = c->same_plane ? c->d_sstride : c->d_tstride;
+    if (timing && c->hist.empty()) {
+        c->hist.assign(4 * kHistRuns, nullptr);
+        for (auto& e : c->hist)
+            FRAC_HIP(c, hipEventCreate(&e));
+    }
+    if (timing)
+        FRAC_TRY(mark_event(c, 0));
+    if (nr)
+        FRAC_HIP(c, hipMemsetAsync(c->d_best_key.ptr, 0xff, nr * sizeof(unsigned long long), c->stream));
+    FRAC_HIP(c, hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(c->d_fb_count.ptr), (int)(c->all_fallback ? nr : 0u),
+                                  1, c->stream));
+    const GenArgs g = gen_args(c, dtgt, tstride);
+    if (g.nrows)
+        gen_pool_build<<<(g.nrows + 255) / 256, 256, 0, c->stream>>>(g);
+    if (timing)
+        FRAC_TRY(mark_event(c, 1));
+    if (nr && !c->all_fallback) {
+        GenSearchArgs a;
+        a.g = g;
+        a.rbucket = c->d_rbucket.ptr;
+        a.nr = nr;
+        a.hitH = c->hitH;
+        a.best_key = c->d_best_key.ptr;
+        gen_search<<<(nr + 3) / 4, 256, 0, c->stream>>>(a);
+    }
+    if (timing)
+        FRAC_TRY(mark_event(c, 2));
+    FRAC_TRY(launch_gen_finish(c, g));
+    if (timing) {
+        FRAC_TRY(mark_event(c, 3));
+        ++c->hist_runs;
+    }
+    FRAC_HIP(c, hipGetLastError());
+    c->engine_ran = FRAC_ENGINE_VALU;
+    c->form_ran = FRAC_FORM_SAMPLED;
+    c->flops_ran = 0;
+    c->evaluated_ran = c->all_fallback ? 0 : c->eligible_pairs;
+    return FRAC_OK;
+}
+
 template <int N>
 int launch_all(frac_ctx* c)
 {
-    const uint32_t nr = (uint32_t)c->ranges.size(), P = (uint32_t)c->porig.size();
+    const uint32_t nr = (uint32_t)c->ranges.size(), P = (uint32_t)c->porig.size() * (c->virt ? c->p.transforms : 1u);
     const bool timing = (c->p.flags & FRAC_FLAG_TIMING) != 0;
     const uint8_t* dsrc = c->d_src.ptr;
     const uint8_t* dtgt = c->same_plane ? c->d_src.ptr : c->d_tgt.ptr;
@@ -1397,9 +1535,13 @@ int launch_all(frac_ctx* c)
     const bool use_mfma = c->engine == FRAC_ENGINE_MFMA && !c->all_fallback;
     // the Fourier path and the SEA engine's tiled form build the pool in their fused domain pass
     // (dft_domain_build)
-    const bool fused_pool = N == 8 && ((use_mfma && c->p.transforms == 4 && mfma_dft_enabled()) ||
-                                       (c->engine == FRAC_ENGINE_SEA && !c->all_fallback && c->tp));
-    if (P && !fused_pool)
+    const bool fused_pool = N == 8 && !c->virt &&
+                            ((use_mfma && c->p.transforms == 4 && mfma_dft_enabled()) ||
+                             (c->engine == FRAC_ENGINE_SEA && !c->all_fallback && c->tp));
+    const GenArgs g = gen_args(c, dtgt, tstride);
+    if (P && c->virt) // the sampled form: one row per (domain, transform), fracenc_gen.hip
+        gen_pool_build<<<(P + 255) / 256, 256, 0, c->stream>>>(g);
+    else if (P && !fused_pool)
         pool_build<N><<<(P + 3) / 4, 256, 0, c->stream>>>(dsrc, c->d_sstride, c->d_doms.ptr, c->d_porig.ptr, P,
                                                           c->d_pool.ptr, c->d_negsd2.ptr);
     const bool use_sea = c->engine == FRAC_ENGINE_SEA && !c->all_fallback;
@@ -1428,7 +1570,7 @@ int launch_all(frac_ctx* c)
         a.best_key = c->d_best_key.ptr;
         const dim3 grid((a.nwork + 3) / 4), block(256);
         const bool hits = c->hitH > 0; // H = 0: the first maximum of w is the first hit
-        if constexpr (N == 16) {
+        if (N == 16 || c->G == 1) { // one copy: n = 16, or the sampled form's identity transform
             if (hits)
                 search_valu<N, 1, true><<<grid, block, 0, c->stream>>>(a);
             else
@@ -1454,7 +1596,9 @@ int launch_all(frac_ctx* c)
     }
     if (timing && !use_mfma)
         FRAC_TRY(mark_event(c, 2));
-    if (!c->all_fallback && nr) {
+    if (c->virt) {
+        FRAC_TRY(launch_gen_finish(c, g));
+    } else if (!c->all_fallback && nr) {
         FitArgs f;
         f.tgt = dtgt;
         f.tstride = tstride;
@@ -1478,7 +1622,7 @@ int launch_all(frac_ctx* c)
             fit_winner<N><<<std::max(1u, (nr + 4 * (64 / fit_lanes<N>()) - 1) / (4 * (64 / fit_lanes<N>()))), 256, 0,
                             c->stream>>>(f);
     }
-    if (nr) {
+    if (nr && !c->virt) {
         FallbackArgs b;
         b.tgt = dtgt;
         b.tstride = tstride;
@@ -1772,7 +1916,8 @@ int frac_run(frac_ctx* c)
     if (c->dirty)
         FRAC_TRY(prepare(c));
     int rc;
-    switch (c->n) {
+    switch (c->generic ? 0 : c->n) {
+    case 0: rc = launch_generic(c); break;
     case 2: rc = launch_all<2>(c); break;
     case 4: rc = launch_all<4>(c); break;
     case 16: rc = launch_all<16>(c); break;

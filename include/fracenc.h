@@ -14,6 +14,9 @@
  *    to the later transform; the first candidate with distance <= rms_threshold
  *    wins (early exit); distance is the reference's unfitted fp32 error;
  *  - contrast / brightness follow TransformMatcher::match_generic bit-for-bit;
+ *  - geometry: n x n ranges (2 <= n <= 32) and S x S domains with S > n, the pairs the reference
+ *    CLI accepts (main.cpp:99); S = 2n is the decimate-then-permute path, any other pair — the
+ *    CLI default 16 -> 4 (match_16to4) included — samples as RootMeanSquare does;
  *  - results are returned in the order the ranges were given.
  * All entry points return 0 on success and a negative FRAC_E* code on error;
  * frac_last_error() gives the message.  Not thread-safe per context.
@@ -112,6 +115,8 @@ typedef struct frac_stats {
 #define FRAC_FORM_FOURIER 2 /* MFMA engine, n = 8, T = 4: rotation-group Fourier form (96 MACs)    */
 #define FRAC_FORM_SEA 3     /* SEA engine: bound-pruned exact evaluation (v_dot2)                */
 #define FRAC_FORM_SEA_MFMA 4 /* SEA engine, n = 8, T = 4: the bound per tile pair, Fourier MFMA search */
+#define FRAC_FORM_SAMPLED 5 /* range sizes outside {2,4,8,16}: per range an exact integer scan of the */
+                            /* pool rows, one per (domain, transform), sampled as RootMeanSquare does  */
 
 typedef struct frac_ctx frac_ctx;
 

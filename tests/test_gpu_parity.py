@@ -12,8 +12,8 @@ from golden_util import FIELDS, GOLDEN_NAMES, golden, plane, selection
 
 pytestmark = pytest.mark.gpu
 
-# fixture name → engine support (the engine implements the ratio-2 path, n ∈ {2,4,8,16})
-RATIO2 = [n for n in GOLDEN_NAMES if n != "lenna_16to4"]
+# every golden runs on every engine: the ratio-2 path (domain = 2 × range, n ∈ {2, 4, 8, 16}) and
+# the sampled form for every other geometry (16→4 — the CLI default — 32→8, 12→8, 8→3, 64→32 ...)
 ENGINES = [F.ENGINE_VALU, F.ENGINE_MFMA, F.ENGINE_SEA]
 
 
@@ -23,8 +23,6 @@ def as_oracle_fields(out):
 
 
 def run_engine(p, meta, engine, tgt=None, ranges_idx=None):
-    if engine == F.ENGINE_SEA and meta["tgt"] > 8:
-        pytest.skip("the SEA engine covers n <= 8")
     H, W = p.shape
     doms = F.create_uniform_grid(W, H, meta["src"], meta["src"] // 2)
     rngs = F.create_uniform_grid(W, H, meta["tgt"], meta["tgt"])
@@ -46,7 +44,7 @@ def assert_same(got, want, what):
 
 
 @pytest.mark.parametrize("engine", ENGINES)
-@pytest.mark.parametrize("name", RATIO2)
+@pytest.mark.parametrize("name", GOLDEN_NAMES)
 def test_engine_matches_reference_goldens(name, engine):
     rec, meta = golden(name)
     p = plane(meta["plane"])
@@ -175,12 +173,20 @@ def test_edge_cases(oracle, engine):
 
 @pytest.mark.parametrize("engine", ENGINES)
 def test_invalid_geometry_is_an_error(engine):
+    # what the reference CLI rejects (main.cpp:99: target >= source) or cannot express
     p = np.zeros((64, 64), np.uint8)
     with F.Engine(0, 4, engine=engine) as e:
         e.set_frame(p)
-        e.set_domains(F.create_uniform_grid(64, 64, 12, 6))  # ratio 12/8 is not the ratio-2 path
+        e.set_domains(F.create_uniform_grid(64, 64, 8, 4))  # domains no larger than the ranges
         with pytest.raises(F.FracError):
             e.search(F.create_uniform_grid(64, 64, 8, 8))
+        mixed = np.concatenate([F.create_uniform_grid(64, 64, 16, 8), F.create_uniform_grid(64, 64, 12, 6)])
+        e.set_domains(mixed)  # domains of two sizes
+        with pytest.raises(F.FracError):
+            e.search(F.create_uniform_grid(64, 64, 8, 8))
+        e.set_domains(F.create_uniform_grid(64, 64, 64, 32))
+        with pytest.raises(F.FracError):  # ranges above the 32×32 limit
+            e.search(np.array([(0, 0, 48, 48, -1)], dtype=F.GRID_ITEM))
         e.set_domains(F.create_uniform_grid(64, 64, 16, 8))
         bad = np.array([(60, 60, 8, 8, -1)], dtype=F.GRID_ITEM)  # outside the plane
         with pytest.raises(F.FracError):
@@ -223,13 +229,12 @@ def test_full_4096_frame(engine):
     assert (out["sw"] == 16).all()
 
 
-def test_sea_rejects_n16():
-    p = np.zeros((64, 64), np.uint8)
-    with F.Engine(0, 4, engine=F.ENGINE_SEA) as e:
-        e.set_frame(p)
-        e.set_domains(F.create_uniform_grid(64, 64, 32, 16))
-        with pytest.raises(F.FracError):
-            e.search(F.create_uniform_grid(64, 64, 16, 16))
+def test_sea_n16_runs_the_exhaustive_search():
+    """SEA covers n ≤ 8; a valid 32→16 geometry runs the exhaustive MFMA search (same records)."""
+    rec, meta = golden("lenna_n16")
+    out, st = run_engine(plane("lenna_y"), meta, F.ENGINE_SEA)
+    assert_same(out, rec, "lenna_n16 via SEA")
+    assert st["engine"] == F.ENGINE_MFMA
 
 
 def test_engines_agree_on_stress_frame():
@@ -366,3 +371,75 @@ def test_new_frame_same_geometry(engine, cls):
         want, _ = e.search(rngs)
     assert second.tobytes() == want.tobytes()
     assert first.tobytes() != second.tobytes()
+
+
+# the sampled form (fracenc_gen.hip): domain sizes other than 2n, and range sizes outside {2,4,8,16}
+GEN_CASES = [
+    # W, H, src, tgt, T, classifier, thr, smax, kind
+    (64, 64, 16, 4, 4, False, 0.0, -1.0, "noise"),    # the CLI default (match_16to4)
+    (64, 64, 16, 4, 8, True, 0.0, -1.0, "uniform"),
+    (64, 64, 16, 4, 4, False, 3.0, -1.0, "flat"),     # threshold hits: first (domain, t)
+    (96, 64, 32, 8, 4, False, 0.0, 0.8, "noise"),
+    (48, 48, 24, 8, 8, True, 0.0, -1.0, "flat"),      # ratio 3, ties
+    (48, 48, 12, 8, 4, False, 0.0, -1.0, "noise"),    # metric ratio 1, fit at (x·12)/8
+    (60, 60, 10, 4, 4, False, 0.0, -1.0, "uniform"),  # ratio 2 in the metric, 2.5 in the fit
+    (48, 48, 12, 6, 4, True, 0.0, -1.0, "noise"),     # n = 6: gen_search
+    (48, 48, 9, 3, 8, False, 2.0, -1.0, "flat"),      # n = 3, threshold
+    (64, 64, 64, 16, 4, False, 0.0, -1.0, "noise"),   # n = 16, ratio 4
+    (64, 64, 64, 32, 4, False, 0.0, -1.0, "uniform"), # n = 32 (fp32 fallback regime)
+    (40, 40, 20, 5, 4, False, 1e9, -1.0, "noise"),    # every candidate hits: all-fallback mode
+]
+
+
+@pytest.mark.parametrize("engine", ENGINES)
+@pytest.mark.parametrize("case", range(len(GEN_CASES)))
+def test_sampled_form_matches_oracle_random(oracle, case, engine):
+    W, H, src, tgt, T, cls, thr, smax, kind = GEN_CASES[case]
+    rng = np.random.default_rng(3000 + case)
+    p = _random_plane(rng, W, H, kind)
+    meta = dict(src=src, tgt=tgt, T=T, cls=cls, thr=thr, smax=smax)
+    out, st = run_engine(p, meta, engine)
+    doms = oracle.uniform_grid(W, H, src, src // 2)
+    rngs = oracle.uniform_grid(W, H, tgt, tgt)
+    if cls:
+        doms = oracle.classify(p, doms)
+        rngs = oracle.classify(p, rngs)
+    want, rej, _ = oracle.estimate(p, doms, rngs, T=T, thr=thr, smax=smax, use_classifier=cls)
+    assert_same(out, {k: want[k] for k in FIELDS}, f"case {GEN_CASES[case]}")
+    assert st["rejected_mappings"] == rej
+    if tgt not in (2, 4, 8, 16):
+        assert st["search_form"] == F.FORM_SAMPLED
+
+
+@pytest.mark.parametrize("engine", ENGINES)
+def test_default_cli_geometry_4096(engine):
+    """The reference's default geometry (16→4, encode_parameters.h:6-7) on the 4096² C3 frame —
+    1,048,576 ranges × 261,121 domains × 4 transforms: every reported distance is the exact error of
+    the reported (domain, transform) sampled as match_16to4 does (numpy), and a strided sample of
+    ranges matches the oracle."""
+    p = plane("s1_4096")
+    doms = F.create_uniform_grid(4096, 4096, 16, 8)
+    rngs = F.create_uniform_grid(4096, 4096, 4, 4)
+    with F.Engine(0, 4, False, 0.0, -1.0, engine, timing=True) as e:
+        e.set_frame(p)
+        e.set_domains(doms)
+        out, st = e.search(rngs)
+    # exact error of each winner: 2×2 sums at the transformed (4x, 4y) corners (transform.h:96-109)
+    lut = [(1, 0, 0, 0, 0, 1, 0, 0), (0, 1, 0, 0, -1, 0, 1, 0), (-1, 0, 1, 0, 0, -1, 0, 1), (0, -1, 0, 1, 1, 0, 0, 0)]
+    A = np.array(lut, np.int64)[out["transform"].astype(np.int64)]
+    yy, xx = np.divmod(np.arange(16), 4)
+    lx, ly = 4 * xx[None, :], 4 * yy[None, :]
+    S = 16
+    px = out["dx"].astype(np.int64)[:, None] + A[:, 0:1] * lx + A[:, 1:2] * ly + (A[:, 2:3] + A[:, 3:4]) * (S - 1)
+    py = out["dy"].astype(np.int64)[:, None] + A[:, 4:5] * lx + A[:, 5:6] * ly + (A[:, 6:7] + A[:, 7:8]) * (S - 1)
+    pi = p.astype(np.int64)
+    D = (pi[py, px] + pi[py + A[:, 4:5], px + A[:, 0:1]] + pi[py + A[:, 5:6], px + A[:, 1:2]]
+         + pi[py + A[:, 4:5] + A[:, 5:6], px + A[:, 0:1] + A[:, 1:2]])
+    r = p[out["y"].astype(np.int64)[:, None] + yy[None, :], out["x"].astype(np.int64)[:, None] + xx[None, :]]
+    s16 = ((4 * r.astype(np.int64) - D) ** 2).sum(1)
+    np.testing.assert_array_equal(out["distance"], (s16 / 16.0) / 256.0)
+    assert st["fallback_ranges"] == 0 and (out["sw"] == 16).all()
+    from oracle import oracle as O
+    sel = np.arange(0, len(rngs), 8191)
+    want, _, _ = O.estimate(p, O.uniform_grid(4096, 4096, 16, 8), O.uniform_grid(4096, 4096, 4, 4)[sel], threads=16)
+    assert_same(out[sel], {k: want[k] for k in FIELDS}, "16to4 4096 sample")

@@ -124,6 +124,9 @@ def main():
     planes["inexact64"] = inexact
     yy, xx = np.mgrid[0:64, 0:64]
     planes["checker64"] = np.where(((yy // 8) + (xx // 8)) % 2 == 0, 0, 255).astype(np.uint8)
+    planes["crop48"] = np.ascontiguousarray(y[256:304, 256:304])
+    planes["crop60"] = np.ascontiguousarray(y[256:316, 256:316])
+    planes["inexact48"] = np.ascontiguousarray(inexact[:48, :48])
     # Lenna RGB (the reference's own test input, decoded losslessly; checked against the
     # reference loader's planes below) and a seeded synthetic RGB frame with odd sizes
     from PIL import Image
@@ -168,6 +171,23 @@ def main():
         ("inexact64_t4", "inexact64", dict(src=16, tgt=8, T=4)),
         ("checker64_t8", "checker64", dict(src=16, tgt=8, T=8)),
         ("checker64_thr", "checker64", dict(src=16, tgt=8, T=4, thr=8200.0)),
+        # geometry other than domain = 2 × range (RootMeanSquare's sampler at ratio S/n, the fit at
+        # (x·S)/n: image/metrics.h:40-45, encode/transformmatcher.h:94-95,113-144)
+        ("lenna_32to8", "lenna_y", dict(src=32, tgt=8, T=4)),
+        ("lenna_16to4_t8", "lenna_y", dict(src=16, tgt=4, T=8)),
+        ("lenna_16to4_cls", "lenna_y", dict(src=16, tgt=4, T=4, cls=True)),
+        ("lenna_16to4_thr", "lenna_y", dict(src=16, tgt=4, T=4, thr=2.0)),
+        ("lenna_64to16", "lenna_y", dict(src=64, tgt=16, T=4)),
+        ("lenna_64to32", "lenna_y", dict(src=64, tgt=32, T=4)),
+        # createUniformGrid asserts the frame is a multiple of the item size (image/partition2.hpp:119)
+        ("crop48_12to8", "crop48", dict(src=12, tgt=8, T=4)),
+        ("crop48_24to8_t8", "crop48", dict(src=24, tgt=8, T=8)),
+        ("crop48_12to6", "crop48", dict(src=12, tgt=6, T=4)),
+        ("crop48_8to3_t8", "crop48", dict(src=8, tgt=3, T=8)),
+        ("crop60_20to6_cls", "crop60", dict(src=20, tgt=6, T=4, cls=True)),
+        ("crop60_5to4", "crop60", dict(src=5, tgt=4, T=4)),
+        ("inexact64_32to8_t8", "inexact64", dict(src=32, tgt=8, T=8)),
+        ("inexact48_12to6", "inexact48", dict(src=12, tgt=6, T=4)),
     ]
     for name, pk, p in jobs:
         if not want(name):

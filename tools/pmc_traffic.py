@@ -4,7 +4,6 @@ runs, kB per dispatch) of bench.py: HBM-side bytes per search launch, FETCH_SIZE
 (MI355X_MICROARCH.md §HBM: 16-B/lane streaming reads are tallied at half their bytes).
 usage: tools/pmc_traffic.py FORM KERNEL_PREFIX FETCH_CSV WRITE_CSV SOURCE_NOTE"""
 import csv
-import hashlib
 import json
 import os
 import sys
@@ -28,9 +27,10 @@ d = json.load(open(path)) if os.path.exists(path) else {}
 d["_doc"] = ("HBM-side bytes per search launch from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes, "
              "kB units), corrected per MI355X_MICROARCH.md §HBM: FETCH_SIZE doubled on gfx950, WRITE_SIZE as "
              "reported.  Keyed by frac_stats.search_form.")
-root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sha = hashlib.sha256(open(os.path.join(root, "fractencode_amd", "libfracenc.so"), "rb").read()).hexdigest()[:16]
-d[form] = {"kernel": prefix, "lib_sha16": sha, "fetch_size_kb": round(f, 1), "write_size_kb": round(w, 1), "dispatches": [nf, nw],
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from fractencode_amd import source_id  # noqa: E402
+
+d[form] = {"kernel": prefix, "source_id": source_id(), "fetch_size_kb": round(f, 1), "write_size_kb": round(w, 1), "dispatches": [nf, nw],
            "hbm_bytes_per_launch": int(round((2 * f + w) * 1024)), "source": note}
 json.dump(d, open(path, "w"), indent=1)
 print(json.dumps(d[form]))
