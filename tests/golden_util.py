@@ -24,11 +24,31 @@ def plane(name: str) -> np.ndarray:
     elif name == "s1_2048":
         from fractencode_amd.synth import value_noise
         p = value_noise(4096, 4096, 1234)[:2048, :2048].copy()
+    elif name in ("c5_y", "c5_u", "c5_v"):
+        p = c5_planes()[("c5_y", "c5_u", "c5_v").index(name)]
     else:
         p = np.fromfile(os.path.join(GOLD, name + ".u8"), dtype=np.uint8).reshape(m["shape"])
     from fractencode_amd.synth import sha256
     assert sha256(p) == m["sha256"], f"fixture plane {name} drifted"
     return p
+
+
+def c5_rgb() -> np.ndarray:
+    """C5's frame: the S1 RGB 4096² (value noise seeds 1234, 1235, 1236 as R, G, B)."""
+    from fractencode_amd.synth import value_noise
+    return np.stack([value_noise(4096, 4096, 1234 + k) for k in range(3)], -1)
+
+
+_C5 = None
+
+
+def c5_planes():
+    """Y, U, V of the C5 frame by the oracle's rgb2yuv (its digests are the reference's, manifest)."""
+    global _C5
+    if _C5 is None:
+        from oracle import oracle as O
+        _C5 = O.rgb2yuv(c5_rgb())
+    return _C5
 
 
 def golden(name: str):

@@ -1,0 +1,178 @@
+"""BASELINE configs C4 and C5 at their full size on the GPU (configs_untested).
+
+C4 — 2048² S1, classifier on, quadtree 16/8/4 (BASELINE configs[3]):
+  * the leaves tile the frame exactly once, each aligned to its size;
+  * every leaf meets the split rule (include/fracenc.h frac_encode_quadtree): a leaf larger than
+    the minimum has distance ≤ split, and every split block's own best distance exceeds it;
+  * every leaf's distance is the exact error of the (domain, transform) it reports (numpy), and
+    that domain is in the leaf's classifier bucket;
+  * per level, the leaves that fall in the reference's strided samples of the level's full grid
+    (s1_2048_cls_n16 / s1_2048_cls / s1_2048_cls_n4, tools/make_golden.py) are bit-identical to
+    them, and a strided sample of every level's leaves matches the oracle.
+C5 — 4096² RGB, three planes, Quantizer, decoded PSNR (BASELINE configs[4]):
+  * the device rgb2yuv planes have the reference's digests;
+  * per plane, the reference's strided sample (c5_*_sample) is matched bit for bit, and every
+    range's distance is the exact error of its reported (domain, transform);
+  * the device FRC1 stream equals the host packer and round-trips (domain, transform, codes);
+  * the GPU decode of the dequantized records equals the oracle's decode: planes, iteration
+    counts and rms, hence PSNR.
+"""
+import numpy as np
+import pytest
+
+import fractencode_amd as F
+from golden_util import FIELDS, c5_rgb, golden, manifest, oracle_records, plane, selection
+
+pytestmark = pytest.mark.gpu
+
+
+def _fields(out):
+    return {"x": out["x"], "y": out["y"], "dx": out["dx"], "dy": out["dy"], "dw": out["sw"], "dh": out["sh"],
+            "t": out["transform"], "dist": out["distance"], "s": out["contrast"], "o": out["brightness"]}
+
+
+def _assert_same(out, want, what):
+    g = _fields(out)
+    for k in FIELDS:
+        np.testing.assert_array_equal(g[k], want[k], err_msg=f"{what}: field {k}")
+
+
+def exact_s16(p, out, n):
+    """Σ(4r − D4)² of each record's (domain, transform) at ratio 2, recomputed in numpy."""
+    rx, ry, dx, dy, t = (out[k].astype(np.int64) for k in ("x", "y", "dx", "dy", "transform"))
+    yy, xx = np.divmod(np.arange(n * n), n)
+    fwd = np.array([[F.transform_index(n, tt, q) for q in range(n * n)] for tt in range(8)])
+    pi = p.astype(np.int64)
+    s = np.zeros(len(out), np.int64)
+    for c0 in range(0, len(out), 1 << 16):  # bounded temporaries
+        sl = slice(c0, c0 + (1 << 16))
+        r = pi[ry[sl, None] + yy[None, :], rx[sl, None] + xx[None, :]]
+        qy, qx = np.divmod(fwd[t[sl]], n)
+        X0 = dx[sl, None] + 2 * qx
+        Y0 = dy[sl, None] + 2 * qy
+        D = pi[Y0, X0] + pi[Y0, X0 + 1] + pi[Y0 + 1, X0] + pi[Y0 + 1, X0 + 1]
+        s[sl] = ((4 * r - D) ** 2).sum(1)
+    return s
+
+
+def check_exact_distances(p, out, n):
+    s16 = exact_s16(p, out, n)
+    exact = s16 < (1 << 24)
+    np.testing.assert_array_equal(out["distance"][exact], (s16[exact] / 16.0) / (4.0 * n * n))
+    return int((~exact).sum())
+
+
+C4_SPLIT = 0.5
+
+
+def test_c4_quadtree_2048_classifier(oracle):
+    p = plane("s1_2048")
+    W = H = 2048
+    with F.Engine(0, 4, True, 0.0, -1.0) as e:
+        e.set_frame(p)
+        items, st = e.encode_quadtree(16, 4, C4_SPLIT)
+        sizes = items["w"].astype(np.int64)
+        assert set(np.unique(sizes)) <= {4, 8, 16} and (items["h"] == items["w"]).all()
+        # tiling: every pixel in exactly one leaf, every leaf aligned to its size
+        cov = np.zeros((H, W), np.int32)
+        for s in (4, 8, 16):
+            m = sizes == s
+            xs, ys = items["x"][m].astype(np.int64), items["y"][m].astype(np.int64)
+            assert (xs % s == 0).all() and (ys % s == 0).all()
+            blk = np.zeros((H // s, W // s), np.int32)
+            np.add.at(blk, (ys // s, xs // s), 1)
+            cov += np.kron(blk, np.ones((s, s), np.int32))
+        assert (cov == 1).all()
+        # split rule: leaves above the minimum size met the split distance ...
+        assert (items["distance"][sizes > 4] <= C4_SPLIT).all()
+        # ... and every block that was split did not (its own level search, classifier on)
+        for s in (16, 8):
+            covered = np.zeros((H // s, W // s), bool)
+            m = sizes >= s
+            for t in (4, 8, 16):
+                mt = m & (sizes == t)
+                if t >= s and mt.any():
+                    yy, xx = items["y"][mt].astype(np.int64) // s, items["x"][mt].astype(np.int64) // s
+                    for oy in range(t // s):
+                        for ox in range(t // s):
+                            covered[yy + oy, xx + ox] = True
+            split_y, split_x = np.nonzero(~covered)
+            if s == 8:  # an 8-block is only searched when its 16-parent was split
+                parent = np.zeros((H // 16, W // 16), bool)
+                pm = sizes == 16
+                parent[items["y"][pm] // 16, items["x"][pm] // 16] = True
+                keep = ~parent[split_y // 2, split_x // 2]
+                split_y, split_x = split_y[keep], split_x[keep]
+            blocks = np.zeros(len(split_y), dtype=F.GRID_ITEM)
+            blocks["x"], blocks["y"], blocks["w"], blocks["h"], blocks["category"] = split_x * s, split_y * s, s, s, -1
+            e.set_domains(F.create_uniform_grid(W, H, 2 * s, s))
+            par, _ = e.search(blocks)
+            assert (par["distance"] > C4_SPLIT).all(), s
+    # exact errors and bucket membership of every leaf
+    fallbacks = 0
+    for s in (4, 8, 16):
+        leaves = items[sizes == s]
+        fallbacks += check_exact_distances(p, leaves, s)
+        cat = F.preclassify(p, np.array(list(zip(leaves["x"], leaves["y"], leaves["w"], leaves["h"],
+                                                 [-1] * len(leaves))), dtype=F.GRID_ITEM))["category"]
+        dom = np.zeros(len(leaves), dtype=F.GRID_ITEM)
+        dom["x"], dom["y"], dom["w"], dom["h"], dom["category"] = leaves["dx"], leaves["dy"], 2 * s, 2 * s, -1
+        dcat = F.preclassify(p, dom)["category"]
+        has = leaves["sw"] > 0
+        np.testing.assert_array_equal(dcat[has], cat[has])
+    assert st["fallback_ranges"] == fallbacks
+    # per level: the leaves in the reference's samples of the level grid, and an oracle sample
+    for s, gname in ((16, "s1_2048_cls_n16_sample"), (8, "s1_2048_cls_sample"), (4, "s1_2048_cls_n4_sample")):
+        rec, meta = golden(gname)
+        idx = selection(meta, (W // s) * (H // s))
+        leaves = items[sizes == s]
+        lid = (leaves["y"].astype(np.int64) // s) * (W // s) + leaves["x"].astype(np.int64) // s
+        common, li, gi = np.intersect1d(lid, idx, return_indices=True)
+        assert len(common) > 0, f"level {s}: no leaf in the reference sample"
+        _assert_same(leaves[li], {k: rec[k][gi] for k in FIELDS}, f"C4 level {s} vs reference")
+        pick = leaves[:: max(1, len(leaves) // 64)]
+        doms = oracle.classify(p, oracle.uniform_grid(W, H, 2 * s, s))
+        rg = np.zeros(len(pick), dtype=oracle.ITEM_DTYPE)
+        for k in ("x", "y", "w", "h"):
+            rg[k] = pick[k]
+        rg = oracle.classify(p, rg)
+        want, _, _ = oracle.estimate(p, doms, rg, T=4, use_classifier=True, threads=16)
+        _assert_same(pick, {k: want[k] for k in FIELDS}, f"C4 level {s} vs oracle")
+
+
+def test_c5_rgb_4096_three_planes_quantized_decode(oracle):
+    from fractencode_amd import codec
+    from fractencode_amd.color import ColorEncoder
+    from fractencode_amd.synth import sha256
+
+    man = manifest()
+    with ColorEncoder(0, 8, 16, 4) as enc:
+        enc.load(c5_rgb())  # uploaded once, rgb2yuv on the device
+        enc.run()
+        enc.sync()
+        results = enc.fetch()
+        planes = enc.host_planes()
+        streams = [e.pack_frc1() for e in enc.engines]
+        for k, name in enumerate(("c5_y", "c5_u", "c5_v")):
+            p, (out, st), buf = planes[k], results[k], streams[k]
+            H, W = p.shape
+            assert sha256(p) == man[name]["sha256"], f"{name}: device rgb2yuv differs from the reference"
+            rec, meta = golden(name + "_sample")
+            sel = selection(meta, len(out))
+            _assert_same(out[sel], rec, name)
+            assert st["fallback_ranges"] == check_exact_distances(p, out, 8)
+            # FRC1: the device packer equals the host packer; the records round-trip
+            assert buf == codec.pack_stream(out, W, H, 8)
+            back, hdr = codec.unpack_stream(buf)
+            for f in ("x", "y", "dx", "dy", "sw", "sh", "transform"):
+                np.testing.assert_array_equal(back[f], out[f], err_msg=f"{name} FRC1 {f}")
+            qs = codec.Quantizer(hdr["contrast_min"], hdr["contrast_max"], codec.CONTRAST_BITS)
+            qo = codec.Quantizer(hdr["brightness_min"], hdr["brightness_max"], codec.BRIGHTNESS_BITS)
+            np.testing.assert_array_equal(back["contrast"], qs.value(qs.quantized(out["contrast"])))
+            np.testing.assert_array_equal(back["brightness"], qo.value(qo.quantized(out["brightness"])))
+            # decoded PSNR parity: GPU Decoder2 vs the oracle decoder on the same records
+            dec, it, rms = enc.engines[k].decode(back, W, H)
+            want, wit, wrms = oracle.decode(oracle_records(back), 8, W, H)
+            assert (it, rms) == (wit, wrms), name
+            np.testing.assert_array_equal(dec, want, err_msg=name)
+            assert codec.psnr(p, dec) == codec.psnr(p, want)

@@ -25,7 +25,9 @@ def _grids(O, p, meta):
 
 
 # Large fixtures are checked on a strided subset here (the full check is `slow`).
-_SUBSET = {"s1_4096_sample": 16, "s1_2048_cls_sample": 8, "lenna_n4": 4, "lenna_16to4": 4}
+_SUBSET = {"s1_4096_sample": 16, "s1_2048_cls_sample": 8, "lenna_n4": 4, "lenna_16to4": 4, "lenna_16to4_t8": 8,
+           "lenna_16to4_cls": 4, "lenna_16to4_thr": 4, "c5_y_sample": 16, "c5_u_sample": 8, "c5_v_sample": 8,
+           "s1_2048_cls_n16_sample": 8, "s1_2048_cls_n4_sample": 8}
 
 
 @pytest.mark.parametrize("name", GOLDEN_NAMES)

@@ -238,6 +238,32 @@ def main():
         save("s1_2048_cls_sample", "s1_2048", rec, rej, dict(src=16, tgt=8, T=4, thr=0.0, smax=-1.0, cls=True,
                                                              sel="arange(0,65536,64)"),
              {"seconds": round(time.time() - t0, 2)})
+    # C4 levels: the quadtree's 16/8/4 level searches at 2048² with the classifier (n = 8 above)
+    for name, src, tgt, nr, step in (("s1_2048_cls_n16_sample", 32, 16, 16384, 16),
+                                     ("s1_2048_cls_n4_sample", 8, 4, 262144, 256)):
+        if not want(name):
+            continue
+        t0 = time.time()
+        s1 = value_noise(4096, 4096, 1234)[:2048, :2048].copy()
+        sel = np.arange(0, nr, step, dtype=np.uint32)
+        rec, rej = ref_estimate(lib, s1, src, tgt, 4, cls=True, sel=sel)
+        save(name, "s1_2048", rec, rej, dict(src=src, tgt=tgt, T=4, thr=0.0, smax=-1.0, cls=True,
+                                             sel=f"arange(0,{nr},{step})"), {"seconds": round(time.time() - t0, 2)})
+    # C5: the S1 RGB frame (value_noise seeds 1234/1235/1236 as R, G, B) through the reference's
+    # rgb2yuv; digests of its Y/U/V planes and reference samples of each plane's search
+    if want("c5"):
+        t0 = time.time()
+        rgb = np.stack([value_noise(4096, 4096, 1234 + k) for k in range(3)], -1)
+        cy, cu, cv = ref_rgb2yuv(lib, rgb)
+        for pk, pl in (("c5_y", cy), ("c5_u", cu), ("c5_v", cv)):
+            manifest[pk] = {"shape": list(pl.shape), "sha256": sha256(pl),
+                            "generator": "reference rgb2yuv of stack(value_noise(4096,4096,1234+k), k<3)"}
+        for pk, pl, nr, step in (("c5_y", cy, 262144, 256), ("c5_u", cu, 65536, 128), ("c5_v", cv, 65536, 128)):
+            sel = np.arange(0, nr, step, dtype=np.uint32)
+            rec, rej = ref_estimate(lib, pl, 16, 8, 4, sel=sel)
+            save(pk + "_sample", pk, rec, rej, dict(src=16, tgt=8, T=4, thr=0.0, smax=-1.0, cls=False,
+                                                    sel=f"arange(0,{nr},{step})"))
+        print(f"  c5 goldens: {time.time() - t0:.1f} s")
     path = os.path.join(GOLD, "manifest.json")
     old = json.load(open(path)) if os.path.exists(path) else {}
     old.update(manifest)
