@@ -1,0 +1,102 @@
+// core_driver.cpp — runs the REFERENCE's EncodingEngineCore2 (encode/EncodingEngine2.hpp:115-180,
+// EncodingEngine2.cpp:7-30, compiled unmodified from /root/reference) with the HIP engine of
+// integration/HipEncodingEngine2.hpp registered and the CPU engines off (--nocpu, main.cpp:83-84).
+//
+// TEST INFRASTRUCTURE (tests/test_integration.py).  The reference registers accelerator engines
+// inside EncodingEngineCore2's constructor (EncodingEngine2.cpp:21-29, the commented OpenCL block);
+// a maintainer adds the three lines there.  This driver cannot edit the reference, so it performs
+// the same push_back into the core's private engine list through the standard explicit-
+// instantiation access idiom (access checks do not apply to explicit instantiations,
+// [temp.spec.general]/6) — the registration itself, nothing else.
+//
+// usage: core_driver PLANE.u8 W H SRC TGT CLASSIFIER(0|1) RMS_THR SMAX OUT.bin
+//   OUT.bin: the core's result().encoded (encode_item_t, 64 B each) in the core's order, then the
+//   HIP engine's rejected-mapping count (u64).
+#include "encode/EncodingEngine2.hpp"
+#include "encode/Classifier2.hpp"
+#include "encode/TransformEstimator2.hpp"
+#include "image/partition2.hpp"
+#include "HipEncodingEngine2.hpp"
+
+#include <cstdio>
+#include <cstdlib>
+#include <fstream>
+#include <memory>
+#include <vector>
+
+using namespace Frac2;
+
+namespace {
+using Engines = std::vector<std::unique_ptr<AbstractEncodingEngine2>>;
+template <Engines EncodingEngineCore2::*M>
+struct EnginesOf {
+    friend Engines& engines_of(EncodingEngineCore2& c) { return c.*M; }
+};
+Engines& engines_of(EncodingEngineCore2& c);
+template struct EnginesOf<&EncodingEngineCore2::_engines>;
+
+struct NullReporter : ProgressReporter2 {
+    void log(size_t, size_t) override {}
+};
+} // namespace
+
+int main(int argc, char** argv)
+{
+    if (argc != 10) {
+        std::fprintf(stderr, "usage: %s PLANE W H SRC TGT CLS THR SMAX OUT\n", argv[0]);
+        return 2;
+    }
+    const uint32_t W = std::atoi(argv[2]), H = std::atoi(argv[3]);
+    encode_parameters_t params;
+    params.sourceGridSize = std::atoi(argv[4]);
+    params.targetGridSize = std::atoi(argv[5]);
+    params.noclassifier = std::atoi(argv[6]) == 0;
+    params.rmsThreshold = std::atof(argv[7]);
+    params.sMax = std::atof(argv[8]);
+    params.nocpu = true;
+    std::vector<uint8_t> buf(size_t(W) * H);
+    {
+        std::ifstream f(argv[1], std::ios::binary);
+        f.read(reinterpret_cast<char*>(buf.data()), buf.size());
+        if (!f)
+            return 3;
+    }
+    ImagePlane image(Size32u(W, H), W, std::move(buf));
+    // grids and classifier exactly as encode_image2 builds them (main.cpp:142-162)
+    const Size32u gridSizeTarget(params.targetGridSize, params.targetGridSize);
+    const Size32u gridSizeSource(params.sourceGridSize, params.sourceGridSize);
+    const Size32u gridOffset = gridSizeSource / params.latticeSize;
+    std::unique_ptr<Classifier2> classifier = std::make_unique<BrightnessBlocksClassifier2>(image, image);
+    if (params.noclassifier)
+        classifier = std::make_unique<DummyClassifier>(image, image);
+    auto cb = [&](const Point2du& origin, const Size32u& size) {
+        UniformGridItem::ExtraData data;
+        classifier->preclassify(origin, size, data);
+        return data;
+    };
+    auto sourceGrid = createUniformGrid(image.size(), gridSizeSource, gridOffset, cb);
+    auto targetGrid = createUniformGrid(image.size(), gridSizeTarget, gridSizeTarget, cb);
+    // Encoder2's estimator (encode/Encoder2.hpp:36) and core (:38)
+    TransformEstimator2 estimator(image, image, std::move(classifier),
+                                  std::make_shared<TransformMatcher>(params.rmsThreshold, params.sMax), sourceGrid);
+    NullReporter reporter;
+    EncodingEngineCore2 core(params, image, sourceGrid, estimator, &reporter);
+    uint64_t rejected = 0;
+    HipEncodingEngine2* hip = nullptr;
+    try { // EncodingEngine2.cpp:21-29, filled in
+        auto engine = std::make_unique<HipEncodingEngine2>(params, image, sourceGrid);
+        engine->setName("HIP");
+        hip = engine.get();
+        engines_of(core).push_back(std::move(engine));
+    } catch (const std::exception& exc) {
+        std::printf("failed to create engine: %s\n", exc.what());
+        return 4;
+    }
+    core.encode(targetGrid);
+    rejected = hip->rejectedMappings();
+    const auto data = core.result();
+    std::ofstream out(argv[9], std::ios::binary);
+    out.write(reinterpret_cast<const char*>(data.encoded.data()), data.encoded.size() * sizeof(Frac::encode_item_t));
+    out.write(reinterpret_cast<const char*>(&rejected), sizeof(rejected));
+    return out ? 0 : 5;
+}
