@@ -26,6 +26,7 @@
 #include "fracenc_stream.hip"
 #include "fracenc_tp.hip"
 #include "fracenc_gen.hip"
+#include "fracenc_bucket.hip"
 
 using namespace fracenc;
 
@@ -165,11 +166,14 @@ struct frac_ctx {
     uint32_t Teff = 4;       // transforms the engines search per pool row (1 in the sampled form)
     uint32_t K2 = 0;         // dwords per pool row
     uint32_t G = 4, NG = 1;
-    std::vector<uint32_t> porig;            // pool position → domain index
-    std::vector<uint32_t> bucket_begin, bucket_end; // per bucket (category + 1)
-    std::vector<int32_t> range_bucket;      // per range
-    std::vector<uint2> rbucket;             // per range pool slice
-    std::vector<int32_t> slot_range;
+    uint32_t npos = 0;                      // pool positions (= domains); d_porig maps them to domain indices
+    std::vector<uint32_t> bucket_begin, bucket_end; // per bucket (category + 1): pool positions
+    BucketLayout layout{};                  // per-bucket counts and offsets (fracenc_bucket.hip); VALU slots
+    BucketLayout mlayout{};                 // the same with the MFMA engine's 32-slot blocks and tiles
+    uint32_t nvslots = 0;                   // VALU engine: range slots (64 per wave)
+    bool doms_uploaded = false;             // d_doms holds c->doms
+    bool doms_trusted = false;              // c->doms built by this library (quadtree levels): not re-validated
+    std::vector<uint32_t> h_rkey, h_porig;  // frac_fetch: per-range bucket, pool order (classifier stats)
     std::vector<uint4> work;
     int64_t hitH = -1;
     bool all_fallback = false;
@@ -180,6 +184,10 @@ struct frac_ctx {
     DBuf<int32_t> d_negsd2, d_slot_range;
     DBuf<uint4> d_work;
     DBuf<uint2> d_rbucket;
+    DBuf<uint32_t> d_rord, d_rkey;           // bucket-sorted range order; per range bucket
+    DBuf<uint32_t> d_bk_keys, d_bk_keys2, d_bk_iota, d_bk_first, d_bk_err;
+    DBuf<uint8_t> d_bk_tmp;
+    size_t bk_tmp_bytes = 0;
     DBuf<unsigned long long> d_best_key;
     DBuf<frac_encode_item> d_out;
     DBuf<RangeAux> d_aux;
@@ -187,9 +195,6 @@ struct frac_ctx {
     // MFMA engine layout
     uint32_t engine = FRAC_ENGINE_VALU;    // engine chosen for the current geometry
     uint32_t nblocks = 0, ntiles = 0;
-    std::vector<int32_t> m_slot_range;     // [nblocks*32]
-    std::vector<uint32_t> m_range_slot;    // [nr]
-    std::vector<int32_t> m_tile_pos;       // [ntiles*32]
     std::vector<uint4> m_work;             // per WG (4 range blocks: search_mfma)
     std::vector<uint32_t> m_blk_ptr, m_blk_ent;
     std::vector<uint4> m8_work;            // per WG (8 range blocks: search_dft)
@@ -240,6 +245,8 @@ struct frac_ctx {
     // quadtree: the per-level domain grids (geometry only) of the last frame size, by log2(n)
     uint32_t qt_w = 0, qt_h = 0;
     std::vector<frac_grid_item> qt_doms[5];
+    DBuf<frac_grid_item> qt_ddoms[5];     // their device copies
+    bool qt_dvalid[5] = {false, false, false, false, false};
     DBuf<uint8_t> d_sea_tmp;
     DBuf<unsigned long long> d_sea_count; // candidates the SEA search evaluated
     uint64_t eligible_pairs = 0;          // Σ over ranges of its bucket's domain count
@@ -383,6 +390,70 @@ int upload_plane(frac_ctx* c, const uint8_t* p, uint32_t w, uint32_t h, uint32_t
     return FRAC_OK;
 }
 
+// The classifier buckets on the device (fracenc_bucket.hip): d_porig (pool position → domain index),
+// d_rord (ranges in bucket order), d_rkey (per range bucket); first[b] / rfirst[b] = the first pool
+// position / bucket-sorted range of bucket b (b = 0..kMaxBuckets).  One small synchronous copy.
+int device_buckets(frac_ctx* c, int nb, uint32_t* dfirst, uint32_t* rfirst)
+{
+    const uint32_t nd = (uint32_t)c->doms.size(), nr = (uint32_t)c->ranges.size();
+    if (nb == 1) { // one bucket: the pool is the domain list, the ranges keep their order
+        if (nd)
+            fill_iota<<<(nd + 255) / 256, 256, 0, c->stream>>>(c->d_porig.ptr, nd);
+        if (nr) {
+            fill_iota<<<(nr + 255) / 256, 256, 0, c->stream>>>(c->d_rord.ptr, nr);
+            FRAC_HIP(c, hipMemsetAsync(c->d_rkey.ptr, 0, nr * sizeof(uint32_t), c->stream));
+        }
+        for (int b = 0; b <= kMaxBuckets; ++b) {
+            dfirst[b] = b == 0 ? 0u : nd;
+            rfirst[b] = b == 0 ? 0u : nr;
+        }
+        return FRAC_OK;
+    }
+    const uint32_t m = std::max(std::max(nd, nr), 1u);
+    FRAC_HIP(c, c->d_bk_keys.ensure(m));
+    FRAC_HIP(c, c->d_bk_keys2.ensure(m));
+    FRAC_HIP(c, c->d_bk_iota.ensure(m));
+    FRAC_HIP(c, c->d_bk_first.ensure(2 * (kMaxBuckets + 1) + 1));
+    size_t need = 0;
+    FRAC_HIP(c, sort_pairs_u32(nullptr, need, c->d_bk_keys.ptr, c->d_bk_keys2.ptr, c->d_bk_iota.ptr, c->d_porig.ptr, m,
+                               3, c->stream));
+    if (need > c->bk_tmp_bytes) {
+        FRAC_HIP(c, c->d_bk_tmp.ensure(need));
+        c->bk_tmp_bytes = need;
+    }
+    uint32_t* first = c->d_bk_first.ptr;
+    uint32_t* err = first + 2 * (kMaxBuckets + 1);
+    FRAC_HIP(c, hipMemsetAsync(err, 0, sizeof(uint32_t), c->stream));
+    const uint8_t* tplane = c->same_plane ? c->d_src.ptr : c->d_tgt.ptr;
+    const uint32_t tstride = c->same_plane ? c->d_sstride : c->d_tstride;
+    size_t tb = c->bk_tmp_bytes;
+    if (nd) { // a stored −1 is classified on the item's own plane (Classifier2::compare, Classifier2.cpp:70-81)
+        bucket_keys<<<(nd + 3) / 4, 256, 0, c->stream>>>(c->d_doms.ptr, nd, c->d_src.ptr, c->d_sstride, c->d_bk_keys.ptr,
+                                                        c->d_bk_iota.ptr, err);
+        FRAC_HIP(c, sort_pairs_u32(c->d_bk_tmp.ptr, tb, c->d_bk_keys.ptr, c->d_bk_keys2.ptr, c->d_bk_iota.ptr,
+                                   c->d_porig.ptr, nd, 3, c->stream));
+    }
+    bucket_bounds<<<1, 64, 0, c->stream>>>(c->d_bk_keys2.ptr, nd, first);
+    tb = c->bk_tmp_bytes;
+    if (nr) {
+        bucket_keys<<<(nr + 3) / 4, 256, 0, c->stream>>>(c->d_ranges.ptr, nr, tplane, tstride, c->d_rkey.ptr,
+                                                        c->d_bk_iota.ptr, err);
+        FRAC_HIP(c, sort_pairs_u32(c->d_bk_tmp.ptr, tb, c->d_rkey.ptr, c->d_bk_keys2.ptr, c->d_bk_iota.ptr,
+                                   c->d_rord.ptr, nr, 3, c->stream));
+    }
+    bucket_bounds<<<1, 64, 0, c->stream>>>(c->d_bk_keys2.ptr, nr, first + kMaxBuckets + 1);
+    uint32_t h[2 * (kMaxBuckets + 1) + 1];
+    FRAC_HIP(c, hipMemcpyAsync(h, first, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+    FRAC_HIP(c, hipStreamSynchronize(c->stream));
+    if (h[2 * (kMaxBuckets + 1)])
+        return c->fail(FRAC_E_INVALID, "item category outside -1..5");
+    for (int b = 0; b <= kMaxBuckets; ++b) {
+        dfirst[b] = h[b];
+        rfirst[b] = h[kMaxBuckets + 1 + b];
+    }
+    return FRAC_OK;
+}
+
 int prepare(frac_ctx* c)
 {
     HostTrace tr("prepare");
@@ -403,7 +474,8 @@ int prepare(frac_ctx* c)
     if (n < 2 || n > (int)kGenMaxN)
         return c->fail(FRAC_E_INVALID, "range size must be 2..32");
     const uint32_t S = c->doms.empty() ? 2u * (uint32_t)n : c->doms[0].w;
-    for (const auto& d : c->doms) {
+    for (size_t i = 0; !c->doms_trusted && i < c->doms.size(); ++i) {
+        const frac_grid_item& d = c->doms[i];
         if (d.w != S || d.h != S)
             return c->fail(FRAC_E_INVALID, "all domains must be square and of one size");
         if ((uint64_t)d.x + d.w > c->src.w || (uint64_t)d.y + d.h > c->src.h)
@@ -424,86 +496,56 @@ int prepare(frac_ctx* c)
     c->NG = c->virt ? 1u : T / c->G;
 
     tr.mark("validate");
-    // buckets: category + 1 (0 = category −1) with the classifier, a single bucket without
+    // buckets: category + 1 (0 = category −1) with the classifier, a single bucket without.  Every
+    // per-item step runs on the device (device_buckets); the host works from the bucket counts.
     const int nb = c->p.use_classifier ? 7 : 1;
-    std::vector<int32_t> dbk(c->doms.size(), 0);
-    c->range_bucket.assign(c->ranges.size(), 0);
-    if (c->p.use_classifier) {
-        // a stored −1 is recomputed on the item's own plane (BrightnessBlocksClassifier2::compare,
-        // encode/Classifier2.cpp:70-81) — on the device (fracenc_classify.hip)
-        std::vector<uint32_t> dl, rl;
-        for (size_t i = 0; i < c->doms.size(); ++i)
-            if (c->doms[i].category == -1)
-                dl.push_back((uint32_t)i);
-        for (size_t i = 0; i < c->ranges.size(); ++i)
-            if (c->ranges[i].category == -1)
-                rl.push_back((uint32_t)i);
-        std::vector<int32_t> dcat, rcat;
-        FRAC_TRY(classify_on_device(c, c->doms, dl, c->d_src.ptr, c->d_sstride, dcat));
-        FRAC_TRY(classify_on_device(c, c->ranges, rl, c->same_plane ? c->d_src.ptr : c->d_tgt.ptr,
-                                    c->same_plane ? c->d_sstride : c->d_tstride, rcat));
-        for (size_t i = 0; i < c->doms.size(); ++i)
-            dbk[i] = c->doms[i].category + 1;
-        for (size_t k = 0; k < dl.size(); ++k)
-            dbk[dl[k]] = dcat[k] + 1;
-        for (size_t i = 0; i < c->ranges.size(); ++i)
-            c->range_bucket[i] = c->ranges[i].category + 1;
-        for (size_t k = 0; k < rl.size(); ++k)
-            c->range_bucket[rl[k]] = rcat[k] + 1;
-        for (size_t i = 0; i < c->doms.size(); ++i)
-            if (dbk[i] < 0 || dbk[i] >= nb)
-                return c->fail(FRAC_E_INVALID, "domain category outside -1..5");
-        for (size_t i = 0; i < c->ranges.size(); ++i)
-            if (c->range_bucket[i] < 0 || c->range_bucket[i] >= nb)
-                return c->fail(FRAC_E_INVALID, "range category outside -1..5");
-    }
-    tr.mark("classify");
-    // stable counting sort of item indices by bucket: order[beg[b] .. beg[b + 1]) = bucket b
-    auto bucket_order = [nb](const std::vector<int32_t>& key, std::vector<uint32_t>& order,
-                             std::vector<uint32_t>& beg) {
-        beg.assign(nb + 1, 0);
-        for (int32_t k : key)
-            ++beg[k + 1];
-        for (int b = 0; b < nb; ++b)
-            beg[b + 1] += beg[b];
-        order.resize(key.size());
-        std::vector<uint32_t> pos(beg.begin(), beg.end() - 1);
-        for (size_t i = 0; i < key.size(); ++i)
-            order[pos[key[i]]++] = (uint32_t)i;
+    const size_t nd = c->doms.size(), nr = c->ranges.size();
+    auto up = [&](void* dst, const void* srcp, size_t bytes) {
+        return bytes ? c->hip(hipMemcpyAsync(dst, srcp, bytes, hipMemcpyHostToDevice, c->stream), "upload") : 0;
     };
-    std::vector<uint32_t> dbeg, rord, rbeg;
-    bucket_order(dbk, c->porig, dbeg);
-    bucket_order(c->range_bucket, rord, rbeg);
-    c->bucket_begin.assign(dbeg.begin(), dbeg.end() - 1);
-    c->bucket_end.assign(dbeg.begin() + 1, dbeg.end());
+    FRAC_HIP(c, c->d_doms.ensure(nd));
+    FRAC_HIP(c, c->d_ranges.ensure(nr));
+    FRAC_HIP(c, c->d_porig.ensure(nd));
+    FRAC_HIP(c, c->d_rord.ensure(nr));
+    FRAC_HIP(c, c->d_rkey.ensure(nr));
+    if (!c->doms_uploaded) {
+        FRAC_TRY(up(c->d_doms.ptr, c->doms.data(), nd * sizeof(frac_grid_item)));
+        c->doms_uploaded = true;
+    }
+    FRAC_TRY(up(c->d_ranges.ptr, c->ranges.data(), nr * sizeof(frac_grid_item)));
+    uint32_t dfirst[kMaxBuckets + 1], rfirst[kMaxBuckets + 1];
+    FRAC_TRY(device_buckets(c, nb, dfirst, rfirst));
+    tr.mark("buckets (device)");
+    c->npos = (uint32_t)nd;
+    c->bucket_begin.assign(dfirst, dfirst + nb);
+    c->bucket_end.assign(dfirst + 1, dfirst + nb + 1);
+    std::vector<uint32_t> rbeg(rfirst, rfirst + nb + 1);
     // the engines' pool rows per bucket: pool positions, or T rows per position in the sampled form
     const uint32_t VT = c->virt ? T : 1u;
     std::vector<uint32_t> eb(nb), ee(nb);
+    BucketLayout L{};
+    L.nb = (uint32_t)nb;
+    L.VT = VT;
     for (int b = 0; b < nb; ++b) {
         eb[b] = c->bucket_begin[b] * VT;
         ee[b] = c->bucket_end[b] * VT;
+        L.dbeg[b] = c->bucket_begin[b];
+        L.dcnt[b] = c->bucket_end[b] - c->bucket_begin[b];
+        L.rbeg[b] = rbeg[b];
+        L.rcnt[b] = rbeg[b + 1] - rbeg[b];
     }
-    c->rbucket.resize(c->ranges.size());
-    for (size_t i = 0; i < c->ranges.size(); ++i) {
-        const int b = c->range_bucket[i];
-        c->rbucket[i] = make_uint2(eb[b], ee[b]);
-    }
+    c->layout = L;
     // range slots: per bucket, padded to whole waves of 64 (the VALU engine's work lists only)
-    c->slot_range.clear();
     c->work.clear();
-    const bool valu_lists = c->p.engine == FRAC_ENGINE_VALU;
+    c->nvslots = 0;
+    const bool valu_lists = c->p.engine == FRAC_ENGINE_VALU && !c->generic;
     std::vector<std::pair<uint32_t, int>> blocks; // (slot base, bucket)
     for (int b = 0; valu_lists && b < nb; ++b) {
-        const uint32_t base = (uint32_t)c->slot_range.size();
-        for (uint32_t k = rbeg[b]; k < rbeg[b + 1]; ++k)
-            c->slot_range.push_back((int32_t)rord[k]);
-        const uint32_t cnt = (uint32_t)c->slot_range.size() - base;
-        if (cnt == 0)
-            continue;
-        while (c->slot_range.size() % 64)
-            c->slot_range.push_back(-1);
-        for (uint32_t s = base; s < c->slot_range.size(); s += 64)
-            blocks.emplace_back(s, b);
+        c->layout.slot_first[b] = c->nvslots; // used by the VALU slot fill below
+        const uint32_t cnt = L.rcnt[b];
+        for (uint32_t s0 = 0; s0 < cnt; s0 += 64)
+            blocks.emplace_back(c->nvslots + s0, b);
+        c->nvslots += (cnt + 63) / 64 * 64;
     }
     size_t total_blocks = 0;
     for (auto& bl : blocks)
@@ -529,8 +571,8 @@ int prepare(frac_ctx* c)
     }
     tr.mark("buckets + valu work");
     c->eligible_pairs = 0;
-    for (size_t i = 0; i < c->ranges.size(); ++i)
-        c->eligible_pairs += (c->rbucket[i].y - c->rbucket[i].x) / VT;
+    for (int b = 0; b < nb; ++b)
+        c->eligible_pairs += (uint64_t)L.rcnt[b] * L.dcnt[b];
     c->hitH = compute_hit_limit(c->p.rms_threshold, S * S); // the domain's area (image/metrics.h:49)
     c->all_fallback = c->hitH >= kExactLimit;
 
@@ -588,33 +630,25 @@ int prepare(frac_ctx* c)
         }
     }
     if (c->engine == FRAC_ENGINE_MFMA) {
-        // range blocks of 32 slots per bucket; domain tiles of 32 pool positions per bucket
-        c->m_slot_range.clear();
-        c->m_range_slot.assign(c->ranges.size(), 0);
-        std::vector<uint32_t> blk_first(nb, 0), blk_count(nb, 0);
+        // range blocks of 32 slots per bucket; domain tiles of 32 engine pool rows per bucket (the
+        // maps themselves are filled on the device below)
+        std::vector<uint32_t> blk_first(nb, 0), blk_count(nb, 0), tile_first(nb, 0), tile_count(nb, 0);
+        uint32_t nbk = 0, nt = 0;
         for (int b = 0; b < nb; ++b) {
-            blk_first[b] = (uint32_t)(c->m_slot_range.size() / 32);
-            for (uint32_t k = rbeg[b]; k < rbeg[b + 1]; ++k) {
-                const uint32_t i = rord[k];
-                c->m_range_slot[i] = (uint32_t)c->m_slot_range.size();
-                c->m_slot_range.push_back((int32_t)i);
-            }
-            while (c->m_slot_range.size() % 32)
-                c->m_slot_range.push_back(-1);
-            blk_count[b] = (uint32_t)(c->m_slot_range.size() / 32) - blk_first[b];
+            blk_first[b] = nbk;
+            blk_count[b] = (L.rcnt[b] + 31) / 32;
+            nbk += blk_count[b];
+            tile_first[b] = nt;
+            tile_count[b] = (ee[b] - eb[b] + 31) / 32;
+            nt += tile_count[b];
         }
-        c->nblocks = (uint32_t)(c->m_slot_range.size() / 32);
-        c->m_tile_pos.clear();
-        std::vector<uint32_t> tile_first(nb, 0), tile_count(nb, 0);
+        c->nblocks = nbk;
+        c->ntiles = nt;
+        c->mlayout = L;
         for (int b = 0; b < nb; ++b) {
-            tile_first[b] = (uint32_t)(c->m_tile_pos.size() / 32);
-            for (uint32_t pp = eb[b]; pp < ee[b]; ++pp)
-                c->m_tile_pos.push_back((int32_t)pp);
-            while (c->m_tile_pos.size() % 32)
-                c->m_tile_pos.push_back(-1);
-            tile_count[b] = (uint32_t)(c->m_tile_pos.size() / 32) - tile_first[b];
+            c->mlayout.slot_first[b] = 32 * blk_first[b];
+            c->mlayout.tile_first[b] = tile_first[b];
         }
-        c->ntiles = (uint32_t)(c->m_tile_pos.size() / 32);
         // work items: groups of up to BPW blocks of one bucket × splits of its tiles, plus the
         // CSR map block → entry bases (work·BPW + wave) the resolve kernels read
         auto build_work = [&](uint32_t bpw, size_t target_wgs, std::vector<uint4>& work,
@@ -725,13 +759,10 @@ int prepare(frac_ctx* c)
     }
 
     tr.mark("engine work");
-    const size_t nr = c->ranges.size(), P = c->porig.size() * VT; // engine pool rows
-    FRAC_HIP(c, c->d_doms.ensure(c->doms.size()));
-    FRAC_HIP(c, c->d_ranges.ensure(nr));
-    FRAC_HIP(c, c->d_porig.ensure(c->porig.size()));
+    const size_t P = (size_t)c->npos * VT; // engine pool rows
     FRAC_HIP(c, c->d_pool.ensure(P * (size_t)c->K2));
     FRAC_HIP(c, c->d_negsd2.ensure(P));
-    FRAC_HIP(c, c->d_slot_range.ensure(c->slot_range.size()));
+    FRAC_HIP(c, c->d_slot_range.ensure(c->nvslots));
     FRAC_HIP(c, c->d_work.ensure(c->work.size()));
     FRAC_HIP(c, c->d_rbucket.ensure(nr));
     FRAC_HIP(c, c->d_best_key.ensure(nr));
@@ -739,21 +770,15 @@ int prepare(frac_ctx* c)
     FRAC_HIP(c, c->d_aux.ensure(nr));
     FRAC_HIP(c, c->d_fb_list.ensure(nr));
     FRAC_HIP(c, c->d_fb_count.ensure(1));
-    auto up = [&](void* dst, const void* srcp, size_t bytes) {
-        return bytes ? c->hip(hipMemcpyAsync(dst, srcp, bytes, hipMemcpyHostToDevice, c->stream), "upload") : 0;
-    };
-    FRAC_TRY(up(c->d_doms.ptr, c->doms.data(), c->doms.size() * sizeof(frac_grid_item)));
-    FRAC_TRY(up(c->d_ranges.ptr, c->ranges.data(), nr * sizeof(frac_grid_item)));
-    FRAC_TRY(up(c->d_porig.ptr, c->porig.data(), c->porig.size() * sizeof(uint32_t)));
-    FRAC_TRY(up(c->d_slot_range.ptr, c->slot_range.data(), c->slot_range.size() * sizeof(int32_t)));
     FRAC_TRY(up(c->d_work.ptr, c->work.data(), c->work.size() * sizeof(uint4)));
-    FRAC_TRY(up(c->d_rbucket.ptr, c->rbucket.data(), nr * sizeof(uint2)));
-    if (c->all_fallback) {
-        c->fb_iota.resize(nr);
-        for (size_t i = 0; i < nr; ++i)
-            c->fb_iota[i] = (uint32_t)i;
-        FRAC_TRY(up(c->d_fb_list.ptr, c->fb_iota.data(), nr * sizeof(uint32_t)));
-    }
+    if (nr)
+        fill_rbucket<<<(unsigned)((nr + 255) / 256), 256, 0, c->stream>>>(L, c->d_rkey.ptr, (uint32_t)nr,
+                                                                         c->d_rbucket.ptr);
+    if (c->nvslots)
+        fill_range_slots<<<(c->nvslots + 255) / 256, 256, 0, c->stream>>>(c->layout, c->d_rord.ptr, c->nvslots,
+                                                                          c->d_slot_range.ptr, nullptr);
+    if (c->all_fallback && nr)
+        fill_iota<<<(unsigned)((nr + 255) / 256), 256, 0, c->stream>>>(c->d_fb_list.ptr, (uint32_t)nr);
     if (c->engine == FRAC_ENGINE_SEA) {
         if (c->bucket_end.size() > (size_t)kSeaMaxBuckets)
             return c->fail(FRAC_E_INVALID, "SEA: too many classifier buckets");
@@ -810,7 +835,9 @@ int prepare(frac_ctx* c)
         FRAC_HIP(c, c->d_tp_rbk.ensure(std::max<size_t>(nr, 1)));
         FRAC_TRY(up(c->d_tp_groups.ptr, c->tp_groups.data(), ng * sizeof(uint4)));
         FRAC_TRY(up(c->d_tp_blk_group.ptr, c->tp_blk_group.data(), nbk * sizeof(uint2)));
-        FRAC_TRY(up(c->d_tp_rbk.ptr, c->range_bucket.data(), nr * sizeof(int32_t)));
+        if (nr)
+            FRAC_HIP(c, hipMemcpyAsync(c->d_tp_rbk.ptr, c->d_rkey.ptr, nr * sizeof(int32_t), hipMemcpyDeviceToDevice,
+                                       c->stream));
         c->tp_iota.resize(ng);
         for (size_t g = 0; g < ng; ++g)
             c->tp_iota[g] = (uint32_t)g;
@@ -826,9 +853,9 @@ int prepare(frac_ctx* c)
     }
     if (c->engine == FRAC_ENGINE_MFMA) {
         const int KS = (n * n + 15) / 16;
-        FRAC_HIP(c, c->d_m_slot_range.ensure(c->m_slot_range.size()));
+        FRAC_HIP(c, c->d_m_slot_range.ensure((size_t)c->nblocks * 32));
         FRAC_HIP(c, c->d_m_range_slot.ensure(nr));
-        FRAC_HIP(c, c->d_m_tile_pos.ensure(c->m_tile_pos.size()));
+        FRAC_HIP(c, c->d_m_tile_pos.ensure((size_t)c->ntiles * 32));
         FRAC_HIP(c, c->d_m_work.ensure(c->m_work.size()));
         FRAC_HIP(c, c->d_m_blk_ptr.ensure(c->m_blk_ptr.size()));
         FRAC_HIP(c, c->d_m_blk_ent.ensure(c->m_blk_ent.size()));
@@ -846,9 +873,12 @@ int prepare(frac_ctx* c)
             FRAC_TRY(up(c->d_m8_blk_ptr.ptr, c->m8_blk_ptr.data(), c->m8_blk_ptr.size() * sizeof(uint32_t)));
             FRAC_TRY(up(c->d_m8_blk_ent.ptr, c->m8_blk_ent.data(), c->m8_blk_ent.size() * sizeof(uint32_t)));
         }
-        FRAC_TRY(up(c->d_m_slot_range.ptr, c->m_slot_range.data(), c->m_slot_range.size() * sizeof(int32_t)));
-        FRAC_TRY(up(c->d_m_range_slot.ptr, c->m_range_slot.data(), nr * sizeof(uint32_t)));
-        FRAC_TRY(up(c->d_m_tile_pos.ptr, c->m_tile_pos.data(), c->m_tile_pos.size() * sizeof(int32_t)));
+        if (c->nblocks)
+            fill_range_slots<<<(c->nblocks * 32 + 255) / 256, 256, 0, c->stream>>>(
+                c->mlayout, c->d_rord.ptr, c->nblocks * 32, c->d_m_slot_range.ptr, c->d_m_range_slot.ptr);
+        if (c->ntiles)
+            fill_tile_pos<<<(c->ntiles * 32 + 255) / 256, 256, 0, c->stream>>>(c->mlayout, c->ntiles * 32,
+                                                                              c->d_m_tile_pos.ptr);
         FRAC_TRY(up(c->d_m_work.ptr, c->m_work.data(), c->m_work.size() * sizeof(uint4)));
         FRAC_TRY(up(c->d_m_blk_ptr.ptr, c->m_blk_ptr.data(), c->m_blk_ptr.size() * sizeof(uint32_t)));
         FRAC_TRY(up(c->d_m_blk_ent.ptr, c->m_blk_ent.data(), c->m_blk_ent.size() * sizeof(uint32_t)));
@@ -1187,7 +1217,7 @@ int launch_mfma(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride)
 // One host synchronisation sizes the entry arrays (their count depends on the windows).
 int launch_tp(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool timing)
 {
-    const uint32_t nr = (uint32_t)c->ranges.size(), P = (uint32_t)c->porig.size();
+    const uint32_t nr = (uint32_t)c->ranges.size(), P = c->npos;
     const uint32_t nt = c->ntiles, nbk = c->nblocks, ng = (uint32_t)c->tp_groups.size();
     c->form_ran = FRAC_FORM_SEA_MFMA;
     c->flops_ran = 0;
@@ -1358,7 +1388,7 @@ int launch_sea(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool timing)
         if (c->tp)
             return launch_tp(c, dtgt, tstride, timing);
     }
-    const uint32_t nr = (uint32_t)c->ranges.size(), P = (uint32_t)c->porig.size() * (c->virt ? c->p.transforms : 1u);
+    const uint32_t nr = (uint32_t)c->ranges.size(), P = c->npos * (c->virt ? c->p.transforms : 1u);
     if (P) {
         sea_domain_keys<N><<<(P + 255) / 256, 256, 0, c->stream>>>(c->d_pool.ptr, P, c->d_sea_bend.ptr,
                                                                    (uint32_t)c->bucket_end.size(), c->d_sea_dkey.ptr,
@@ -1424,7 +1454,7 @@ GenArgs gen_args(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride)
     g.K2 = c->K2;
     g.pool = c->d_pool.ptr;
     g.negsd2 = c->d_negsd2.ptr;
-    g.nrows = (uint32_t)c->porig.size() * c->p.transforms;
+    g.nrows = c->npos * c->p.transforms;
     return g;
 }
 
@@ -1512,7 +1542,7 @@ int launch_generic(frac_ctx* c)
 template <int N>
 int launch_all(frac_ctx* c)
 {
-    const uint32_t nr = (uint32_t)c->ranges.size(), P = (uint32_t)c->porig.size() * (c->virt ? c->p.transforms : 1u);
+    const uint32_t nr = (uint32_t)c->ranges.size(), P = c->npos * (c->virt ? c->p.transforms : 1u);
     const bool timing = (c->p.flags & FRAC_FLAG_TIMING) != 0;
     const uint8_t* dsrc = c->d_src.ptr;
     const uint8_t* dtgt = c->same_plane ? c->d_src.ptr : c->d_tgt.ptr;
@@ -1787,6 +1817,16 @@ void frac_destroy(frac_ctx* c)
     c->d_cls_out.release();
     c->d_dft_rguard.release();
     c->d_dec_tgt.release();
+    c->d_rord.release();
+    for (auto& q : c->qt_ddoms)
+        q.release();
+    c->d_rkey.release();
+    c->d_bk_keys.release();
+    c->d_bk_keys2.release();
+    c->d_bk_iota.release();
+    c->d_bk_first.release();
+    c->d_bk_err.release();
+    c->d_bk_tmp.release();
     c->d_dec_items.release();
     c->d_dec_sum.release();
     if (c->h_dec_sum)
@@ -1891,6 +1931,8 @@ int frac_set_domains(frac_ctx* c, const frac_grid_item* d, size_t nd)
         return c->fail(FRAC_E_INVALID, "domains is NULL");
     c->doms.assign(d, d + nd);
     c->doms_set = true;
+    c->doms_uploaded = false;
+    c->doms_trusted = false;
     c->dirty = true;
     return FRAC_OK;
 }
@@ -1948,6 +1990,11 @@ int frac_fetch(frac_ctx* c, frac_encode_item* out, frac_stats* stats)
     if (nr)
         FRAC_HIP(c, hipMemcpyAsync(c->h_aux.data(), c->d_aux.ptr, nr * sizeof(RangeAux), hipMemcpyDeviceToHost,
                                    c->stream));
+    if (nr && stats && c->p.use_classifier) { // the per-range buckets of the reject count
+        c->h_rkey.resize(nr);
+        FRAC_HIP(c, hipMemcpyAsync(c->h_rkey.data(), c->d_rkey.ptr, nr * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                                   c->stream));
+    }
     unsigned long long sea_count = 0;
     const bool sea_ran = c->engine_ran == FRAC_ENGINE_SEA && c->form_ran == FRAC_FORM_SEA;
     if (sea_ran)
@@ -1964,9 +2011,20 @@ int frac_fetch(frac_ctx* c, frac_encode_item* out, frac_stats* stats)
         stats->matrix_flops = c->flops_ran;
         stats->evaluated_mappings = c->evaluated_ran;
         const uint64_t nd = c->doms.size();
+        if (c->p.use_classifier) { // a hit's rejects depend on its domain's grid index: the pool order
+            bool any_hit = false;
+            for (size_t r = 0; r < nr && !any_hit; ++r)
+                any_hit = (c->h_aux[r].flags & kAuxHit) && !(c->h_aux[r].flags & kAuxEmpty);
+            if (any_hit) {
+                c->h_porig.resize(c->npos);
+                FRAC_HIP(c, hipMemcpyAsync(c->h_porig.data(), c->d_porig.ptr, c->npos * sizeof(uint32_t),
+                                           hipMemcpyDeviceToHost, c->stream));
+                FRAC_HIP(c, hipStreamSynchronize(c->stream));
+            }
+        }
         for (size_t r = 0; r < nr; ++r) {
             const RangeAux& ax = c->h_aux[r];
-            const int b = c->range_bucket[r];
+            const int b = c->p.use_classifier ? (int)c->h_rkey[r] : 0;
             const uint64_t bsize = c->bucket_end[b] - c->bucket_begin[b];
             if (ax.flags & kAuxEmpty) {
                 ++stats->empty_ranges;
@@ -1979,7 +2037,7 @@ int frac_fetch(frac_ctx* c, frac_encode_item* out, frac_stats* stats)
             if (ax.flags & kAuxHit) {
                 ++stats->hit_ranges;
                 if (c->p.use_classifier)
-                    stats->rejected_mappings += (uint64_t)c->porig[ax.pos] - (ax.pos - c->bucket_begin[b]);
+                    stats->rejected_mappings += (uint64_t)c->h_porig[ax.pos] - (ax.pos - c->bucket_begin[b]);
             } else if (c->p.use_classifier) {
                 stats->rejected_mappings += nd - bsize;
             }
@@ -2076,14 +2134,45 @@ int frac_encode_quadtree(frac_ctx* c, const frac_quadtree_params* qp, frac_encod
     if (c->qt_w != W || c->qt_h != H) {
         for (auto& g : c->qt_doms)
             g.clear();
+        for (auto& v : c->qt_dvalid)
+            v = false;
         c->qt_w = W;
         c->qt_h = H;
     }
+    // every level's domain grid (geometry only) stays on the host and the device across frames: the
+    // level swaps them in (no copy, no upload, no re-validation) and back out afterwards
+    struct LevelGrid {
+        frac_ctx* c;
+        int lv = -1;
+        void in(int level)
+        {
+            lv = level;
+            std::swap(c->doms, c->qt_doms[lv]);
+            std::swap(c->d_doms, c->qt_ddoms[lv]);
+            c->doms_set = true;
+            c->doms_uploaded = c->qt_dvalid[lv];
+            c->doms_trusted = true;
+            c->dirty = true;
+        }
+        void out()
+        {
+            if (lv < 0)
+                return;
+            c->qt_dvalid[lv] = c->doms_uploaded;
+            std::swap(c->doms, c->qt_doms[lv]);
+            std::swap(c->d_doms, c->qt_ddoms[lv]);
+            c->doms_uploaded = false;
+            c->doms_trusted = false;
+            c->dirty = true;
+            lv = -1;
+        }
+        ~LevelGrid() { out(); }
+    } level{c};
     for (uint32_t n = qp->max_size; !pending.empty() && n >= qp->min_size; n /= 2) {
-        std::vector<frac_grid_item>& doms = c->qt_doms[__builtin_ctz(n)];
-        if (doms.empty())
-            doms = grid(2 * n, n);
-        FRAC_TRY(frac_set_domains(c, doms.data(), doms.size()));
+        const int lv = __builtin_ctz(n);
+        if (c->qt_doms[lv].empty())
+            c->qt_doms[lv] = grid(2 * n, n);
+        level.in(lv);
         FRAC_TRY(frac_set_ranges(c, pending.data(), pending.size()));
         tr.mark("grids");
         FRAC_TRY(frac_run(c));
@@ -2092,6 +2181,7 @@ int frac_encode_quadtree(frac_ctx* c, const frac_quadtree_params* qp, frac_encod
         std::vector<frac_encode_item>& res = c->qt_res;
         frac_stats st{};
         FRAC_TRY(frac_fetch(c, res.data(), &st));
+        level.out();
         tr.mark("fetch (sync)");
         total.rejected_mappings += st.rejected_mappings;
         total.total_mappings += st.total_mappings;
