@@ -173,6 +173,8 @@ struct frac_ctx {
     uint32_t nvslots = 0;                   // VALU engine: range slots (64 per wave)
     bool doms_uploaded = false;             // d_doms holds c->doms
     bool doms_trusted = false;              // c->doms built by this library (quadtree levels): not re-validated
+    bool ranges_dev = false;                // d_ranges was filled on the device (quadtree level): nr_dev items of n_dev
+    uint32_t nr_dev = 0, n_dev = 0;
     std::vector<uint32_t> h_rkey, h_porig;  // frac_fetch: per-range bucket, pool order (classifier stats)
     std::vector<uint4> work;
     int64_t hitH = -1;
@@ -246,6 +248,11 @@ struct frac_ctx {
     uint32_t qt_w = 0, qt_h = 0;
     std::vector<frac_grid_item> qt_doms[5];
     DBuf<frac_grid_item> qt_ddoms[5];     // their device copies
+    DBuf<frac_grid_item> d_qt_next;       // the next level's ranges, built on the device
+    DBuf<frac_encode_item> d_qt_leaves;   // the frame's leaves, in output order
+    DBuf<uint32_t> d_qt_flags, d_qt_offs, d_qt_count;
+    DBuf<uint8_t> d_qt_tmp;
+    size_t qt_tmp_bytes = 0;
     bool qt_dvalid[5] = {false, false, false, false, false};
     DBuf<uint8_t> d_sea_tmp;
     DBuf<unsigned long long> d_sea_count; // candidates the SEA search evaluated
@@ -281,6 +288,9 @@ struct frac_ctx {
         return fail(FRAC_E_DEVICE, std::string(what) + ": " + hipGetErrorString(e));
     }
 };
+
+// ranges of the current search: the caller's list, or (quadtree levels) a list the device built
+inline size_t nranges(const frac_ctx* c) { return c->ranges_dev ? c->nr_dev : c->ranges.size(); }
 
 #define FRAC_TRY(expr)                                                                                                 \
     do {                                                                                                               \
@@ -395,7 +405,7 @@ int upload_plane(frac_ctx* c, const uint8_t* p, uint32_t w, uint32_t h, uint32_t
 // position / bucket-sorted range of bucket b (b = 0..kMaxBuckets).  One small synchronous copy.
 int device_buckets(frac_ctx* c, int nb, uint32_t* dfirst, uint32_t* rfirst)
 {
-    const uint32_t nd = (uint32_t)c->doms.size(), nr = (uint32_t)c->ranges.size();
+    const uint32_t nd = (uint32_t)c->doms.size(), nr = (uint32_t)nranges(c);
     if (nb == 1) { // one bucket: the pool is the domain list, the ranges keep their order
         if (nd)
             fill_iota<<<(nd + 255) / 256, 256, 0, c->stream>>>(c->d_porig.ptr, nd);
@@ -409,6 +419,7 @@ int device_buckets(frac_ctx* c, int nb, uint32_t* dfirst, uint32_t* rfirst)
         }
         return FRAC_OK;
     }
+    HostTrace tr("buckets");
     const uint32_t m = std::max(std::max(nd, nr), 1u);
     FRAC_HIP(c, c->d_bk_keys.ensure(m));
     FRAC_HIP(c, c->d_bk_keys2.ensure(m));
@@ -421,6 +432,7 @@ int device_buckets(frac_ctx* c, int nb, uint32_t* dfirst, uint32_t* rfirst)
         FRAC_HIP(c, c->d_bk_tmp.ensure(need));
         c->bk_tmp_bytes = need;
     }
+    tr.mark("alloc");
     uint32_t* first = c->d_bk_first.ptr;
     uint32_t* err = first + 2 * (kMaxBuckets + 1);
     FRAC_HIP(c, hipMemsetAsync(err, 0, sizeof(uint32_t), c->stream));
@@ -443,8 +455,10 @@ int device_buckets(frac_ctx* c, int nb, uint32_t* dfirst, uint32_t* rfirst)
     }
     bucket_bounds<<<1, 64, 0, c->stream>>>(c->d_bk_keys2.ptr, nr, first + kMaxBuckets + 1);
     uint32_t h[2 * (kMaxBuckets + 1) + 1];
+    tr.mark("enqueue");
     FRAC_HIP(c, hipMemcpyAsync(h, first, sizeof(h), hipMemcpyDeviceToHost, c->stream));
     FRAC_HIP(c, hipStreamSynchronize(c->stream));
+    tr.mark("D2H + sync");
     if (h[2 * (kMaxBuckets + 1)])
         return c->fail(FRAC_E_INVALID, "item category outside -1..5");
     for (int b = 0; b <= kMaxBuckets; ++b) {
@@ -464,8 +478,10 @@ int prepare(frac_ctx* c)
     // and S×S domains, S > n (main.cpp:99 rejects target >= source).  S = 2n with n ∈ {2, 4, 8, 16}
     // is every engine's decimate-then-permute path; any other pair — the CLI default 16→4 among
     // them — runs the sampled form (fracenc_gen.hip): one pool row per (domain, transform).
-    int n = c->ranges.empty() ? 8 : (int)c->ranges[0].w;
+    int n = c->ranges_dev ? (int)c->n_dev : c->ranges.empty() ? 8 : (int)c->ranges[0].w;
     for (const auto& r : c->ranges) {
+        if (c->ranges_dev)
+            break; // built on the device from validated parents (frac_encode_quadtree)
         if ((int)r.w != n || (int)r.h != n)
             return c->fail(FRAC_E_INVALID, "all ranges must be square and of one size");
         if ((uint64_t)r.x + r.w > c->tgt.w || (uint64_t)r.y + r.h > c->tgt.h)
@@ -499,7 +515,7 @@ int prepare(frac_ctx* c)
     // buckets: category + 1 (0 = category −1) with the classifier, a single bucket without.  Every
     // per-item step runs on the device (device_buckets); the host works from the bucket counts.
     const int nb = c->p.use_classifier ? 7 : 1;
-    const size_t nd = c->doms.size(), nr = c->ranges.size();
+    const size_t nd = c->doms.size(), nr = nranges(c);
     auto up = [&](void* dst, const void* srcp, size_t bytes) {
         return bytes ? c->hip(hipMemcpyAsync(dst, srcp, bytes, hipMemcpyHostToDevice, c->stream), "upload") : 0;
     };
@@ -512,7 +528,8 @@ int prepare(frac_ctx* c)
         FRAC_TRY(up(c->d_doms.ptr, c->doms.data(), nd * sizeof(frac_grid_item)));
         c->doms_uploaded = true;
     }
-    FRAC_TRY(up(c->d_ranges.ptr, c->ranges.data(), nr * sizeof(frac_grid_item)));
+    if (!c->ranges_dev)
+        FRAC_TRY(up(c->d_ranges.ptr, c->ranges.data(), nr * sizeof(frac_grid_item)));
     uint32_t dfirst[kMaxBuckets + 1], rfirst[kMaxBuckets + 1];
     FRAC_TRY(device_buckets(c, nb, dfirst, rfirst));
     tr.mark("buckets (device)");
@@ -969,7 +986,7 @@ inline bool mfma_dft_enabled()
 // n = 8, T = 4: the C4-Fourier search (6 MFMAs per 32×32 tile pair instead of 16)
 inline int launch_dft(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride)
 {
-    const uint32_t nr = (uint32_t)c->ranges.size();
+    const uint32_t nr = (uint32_t)nranges(c);
     MfmaDomainPrepArgs d;
     d.pool = c->d_pool.ptr;
     d.negsd2 = c->d_negsd2.ptr;
@@ -1117,7 +1134,7 @@ template <int N>
 int launch_mfma(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride)
 {
     // T = the transforms per pool row: 1 in the sampled form (one row per domain and transform)
-    const uint32_t nr = (uint32_t)c->ranges.size(), T = c->Teff;
+    const uint32_t nr = (uint32_t)nranges(c), T = c->Teff;
     if constexpr (N == 8) {
         if (T == 4 && !c->virt && mfma_dft_enabled())
             return launch_dft(c, dtgt, tstride);
@@ -1217,7 +1234,7 @@ int launch_mfma(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride)
 // One host synchronisation sizes the entry arrays (their count depends on the windows).
 int launch_tp(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool timing)
 {
-    const uint32_t nr = (uint32_t)c->ranges.size(), P = c->npos;
+    const uint32_t nr = (uint32_t)nranges(c), P = c->npos;
     const uint32_t nt = c->ntiles, nbk = c->nblocks, ng = (uint32_t)c->tp_groups.size();
     c->form_ran = FRAC_FORM_SEA_MFMA;
     c->flops_ran = 0;
@@ -1388,7 +1405,7 @@ int launch_sea(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool timing)
         if (c->tp)
             return launch_tp(c, dtgt, tstride, timing);
     }
-    const uint32_t nr = (uint32_t)c->ranges.size(), P = c->npos * (c->virt ? c->p.transforms : 1u);
+    const uint32_t nr = (uint32_t)nranges(c), P = c->npos * (c->virt ? c->p.transforms : 1u);
     if (P) {
         sea_domain_keys<N><<<(P + 255) / 256, 256, 0, c->stream>>>(c->d_pool.ptr, P, c->d_sea_bend.ptr,
                                                                    (uint32_t)c->bucket_end.size(), c->d_sea_dkey.ptr,
@@ -1461,7 +1478,7 @@ GenArgs gen_args(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride)
 // the sampled form's fit (every range) and fp32 fallback (the flagged ones)
 int launch_gen_finish(frac_ctx* c, const GenArgs& g)
 {
-    const uint32_t nr = (uint32_t)c->ranges.size();
+    const uint32_t nr = (uint32_t)nranges(c);
     if (!nr)
         return FRAC_OK;
     if (!c->all_fallback) {
@@ -1495,7 +1512,7 @@ int launch_gen_finish(frac_ctx* c, const GenArgs& g)
 // gen_fit and gen_fallback
 int launch_generic(frac_ctx* c)
 {
-    const uint32_t nr = (uint32_t)c->ranges.size();
+    const uint32_t nr = (uint32_t)nranges(c);
     const bool timing = (c->p.flags & FRAC_FLAG_TIMING) != 0;
     const uint8_t* dtgt = c->same_plane ? c->d_src.ptr : c->d_tgt.ptr;
     const uint32_t tstride = c->same_plane ? c->d_sstride : c->d_tstride;
@@ -1542,7 +1559,7 @@ int launch_generic(frac_ctx* c)
 template <int N>
 int launch_all(frac_ctx* c)
 {
-    const uint32_t nr = (uint32_t)c->ranges.size(), P = c->npos * (c->virt ? c->p.transforms : 1u);
+    const uint32_t nr = (uint32_t)nranges(c), P = c->npos * (c->virt ? c->p.transforms : 1u);
     const bool timing = (c->p.flags & FRAC_FLAG_TIMING) != 0;
     const uint8_t* dsrc = c->d_src.ptr;
     const uint8_t* dtgt = c->same_plane ? c->d_src.ptr : c->d_tgt.ptr;
@@ -1820,6 +1837,12 @@ void frac_destroy(frac_ctx* c)
     c->d_rord.release();
     for (auto& q : c->qt_ddoms)
         q.release();
+    c->d_qt_next.release();
+    c->d_qt_leaves.release();
+    c->d_qt_flags.release();
+    c->d_qt_offs.release();
+    c->d_qt_count.release();
+    c->d_qt_tmp.release();
     c->d_rkey.release();
     c->d_bk_keys.release();
     c->d_bk_keys2.release();
@@ -1945,6 +1968,7 @@ int frac_set_ranges(frac_ctx* c, const frac_grid_item* r, size_t nr)
         return c->fail(FRAC_E_INVALID, "ranges is NULL");
     c->ranges.assign(r, r + nr);
     c->ranges_set = true;
+    c->ranges_dev = false;
     c->dirty = true;
     c->ran = false;
     return FRAC_OK;
@@ -1984,7 +2008,7 @@ int frac_fetch(frac_ctx* c, frac_encode_item* out, frac_stats* stats)
         return FRAC_E_INVALID;
     if (!c->ran)
         return c->fail(FRAC_E_STATE, "frac_fetch before frac_run");
-    const size_t nr = c->ranges.size();
+    const size_t nr = nranges(c);
     if (nr && out)
         FRAC_HIP(c, hipMemcpyAsync(out, c->d_out.ptr, nr * sizeof(frac_encode_item), hipMemcpyDeviceToHost, c->stream));
     if (nr)
@@ -2127,8 +2151,6 @@ int frac_encode_quadtree(frac_ctx* c, const frac_quadtree_params* qp, frac_encod
         return g;
     };
     std::vector<frac_grid_item> pending = grid(qp->max_size, qp->max_size);
-    std::vector<frac_encode_item> emitted;
-    emitted.reserve((size_t)(W / qp->min_size) * (H / qp->min_size));
     frac_stats total{};
     HostTrace tr("quadtree");
     if (c->qt_w != W || c->qt_h != H) {
@@ -2166,23 +2188,38 @@ int frac_encode_quadtree(frac_ctx* c, const frac_quadtree_params* qp, frac_encod
             c->dirty = true;
             lv = -1;
         }
-        ~LevelGrid() { out(); }
+        ~LevelGrid()
+        {
+            out();
+            c->ranges_dev = false;
+        }
     } level{c};
-    for (uint32_t n = qp->max_size; !pending.empty() && n >= qp->min_size; n /= 2) {
+    // the level-to-level step runs on the device (qt_flags, scan, qt_scatter): each level's leaves are
+    // appended to d_qt_leaves and its split ranges' quadrants become the next level's device range list;
+    // the host reads one count per level and the leaves once at the end
+    const size_t max_leaves = (size_t)(W / qp->min_size) * (H / qp->min_size);
+    FRAC_HIP(c, c->d_qt_leaves.ensure(std::max<size_t>(max_leaves, 1)));
+    // the level range lists swap between d_ranges and d_qt_next: both at the worst-case size up front, so
+    // no level (of this or a later frame) reallocates one (hipFree would also synchronise the device)
+    FRAC_HIP(c, c->d_ranges.ensure(std::max<size_t>(max_leaves, 1)));
+    FRAC_HIP(c, c->d_qt_next.ensure(std::max<size_t>(max_leaves, 1)));
+    FRAC_HIP(c, c->d_qt_count.ensure(1));
+    uint32_t n_leaves = 0;
+    size_t level_nr = pending.size();
+    FRAC_TRY(frac_set_ranges(c, pending.data(), pending.size()));
+    for (uint32_t n = qp->max_size; level_nr && n >= qp->min_size; n /= 2) {
         const int lv = __builtin_ctz(n);
         if (c->qt_doms[lv].empty())
             c->qt_doms[lv] = grid(2 * n, n);
         level.in(lv);
-        FRAC_TRY(frac_set_ranges(c, pending.data(), pending.size()));
+        c->dirty = true;
         tr.mark("grids");
         FRAC_TRY(frac_run(c));
         tr.mark("run (enqueue)");
-        c->qt_res.resize(pending.size());
-        std::vector<frac_encode_item>& res = c->qt_res;
         frac_stats st{};
-        FRAC_TRY(frac_fetch(c, res.data(), &st));
+        FRAC_TRY(frac_fetch(c, nullptr, stats ? &st : nullptr)); // statistics only: the records stay on the device
         level.out();
-        tr.mark("fetch (sync)");
+        tr.mark("fetch stats (sync)");
         total.rejected_mappings += st.rejected_mappings;
         total.total_mappings += st.total_mappings;
         total.hit_ranges += st.hit_ranges;
@@ -2196,25 +2233,48 @@ int frac_encode_quadtree(frac_ctx* c, const frac_quadtree_params* qp, frac_encod
         total.search_form = st.search_form;
         total.matrix_flops += st.matrix_flops;
         total.evaluated_mappings += st.evaluated_mappings;
-        std::vector<frac_grid_item> next;
-        for (size_t i = 0; i < res.size(); ++i) {
-            const frac_grid_item& r = pending[i];
-            if (n > qp->min_size && res[i].match.score.distance > qp->split_distance) {
-                const uint32_t h = n / 2;
-                next.push_back(frac_grid_item{r.x, r.y, h, h, -1});
-                next.push_back(frac_grid_item{r.x + h, r.y, h, h, -1});
-                next.push_back(frac_grid_item{r.x, r.y + h, h, h, -1});
-                next.push_back(frac_grid_item{r.x + h, r.y + h, h, h, -1});
-            } else {
-                emitted.push_back(res[i]);
-            }
+        const uint32_t nr = (uint32_t)level_nr;
+        FRAC_HIP(c, c->d_qt_flags.ensure(nr));
+        FRAC_HIP(c, c->d_qt_offs.ensure(nr));
+        size_t need = 0;
+        FRAC_HIP(c, hipcub::DeviceScan::ExclusiveSum(nullptr, need, c->d_qt_flags.ptr, c->d_qt_offs.ptr, (int)nr,
+                                                     c->stream));
+        if (need > c->qt_tmp_bytes) {
+            FRAC_HIP(c, c->d_qt_tmp.ensure(need));
+            c->qt_tmp_bytes = need;
         }
-        pending.swap(next);
-        tr.mark("split");
+        qt_flags<<<(nr + 255) / 256, 256, 0, c->stream>>>(c->d_out.ptr, nr, n > qp->min_size ? 1 : 0,
+                                                         qp->split_distance, c->d_qt_flags.ptr);
+        size_t tb = c->qt_tmp_bytes;
+        FRAC_HIP(c, hipcub::DeviceScan::ExclusiveSum(c->d_qt_tmp.ptr, tb, c->d_qt_flags.ptr, c->d_qt_offs.ptr, (int)nr,
+                                                     c->stream));
+        FRAC_HIP(c, c->d_qt_next.ensure(std::max<size_t>(4 * (size_t)nr, 1)));
+        qt_scatter<<<(nr + 255) / 256, 256, 0, c->stream>>>(c->d_out.ptr, c->d_ranges.ptr, nr, c->d_qt_flags.ptr,
+                                                           c->d_qt_offs.ptr, c->d_qt_leaves.ptr, n_leaves,
+                                                           c->d_qt_next.ptr, c->d_qt_count.ptr);
+        uint32_t nsplit = 0;
+        FRAC_HIP(c, hipMemcpyAsync(&nsplit, c->d_qt_count.ptr, sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
+        FRAC_HIP(c, hipStreamSynchronize(c->stream));
+        n_leaves += nr - nsplit;
+        level_nr = 4 * (size_t)nsplit;
+        // the next level searches the device-built quadrants
+        std::swap(c->d_ranges, c->d_qt_next);
+        c->ranges_dev = true;
+        c->nr_dev = (uint32_t)level_nr;
+        c->n_dev = n / 2;
+        c->ranges_set = true;
+        c->ran = false;
+        tr.mark("split (device)");
     }
-    *n_out = emitted.size();
-    if (out)
-        std::memcpy(out, emitted.data(), std::min(cap, emitted.size()) * sizeof(frac_encode_item));
+    c->ranges_dev = false;
+    c->ranges.clear();
+    c->dirty = true;
+    c->ran = false;
+    *n_out = n_leaves;
+    if (out && n_leaves)
+        FRAC_HIP(c, hipMemcpy(out, c->d_qt_leaves.ptr, std::min<size_t>(cap, n_leaves) * sizeof(frac_encode_item),
+                              hipMemcpyDeviceToHost));
+    tr.mark("leaves D2H");
     if (stats)
         *stats = total;
     return FRAC_OK;
@@ -2492,8 +2552,8 @@ int frac_decode_results(frac_ctx* c, uint32_t w, uint32_t h, int max_iter, doubl
     // the fused form needs every range written: no empty (domain-less) record among the results
     bool fused = covers_exactly(c->ranges, w, h);
     if (fused && !c->ranges.empty()) {
-        c->h_aux.resize(c->ranges.size());
-        FRAC_HIP(c, hipMemcpyAsync(c->h_aux.data(), c->d_aux.ptr, c->ranges.size() * sizeof(RangeAux),
+        c->h_aux.resize(nranges(c));
+        FRAC_HIP(c, hipMemcpyAsync(c->h_aux.data(), c->d_aux.ptr, nranges(c) * sizeof(RangeAux),
                                    hipMemcpyDeviceToHost, c->stream));
         FRAC_HIP(c, hipStreamSynchronize(c->stream));
         for (const RangeAux& x : c->h_aux)
@@ -2502,7 +2562,7 @@ int frac_decode_results(frac_ctx* c, uint32_t w, uint32_t h, int max_iter, doubl
                 break;
             }
     }
-    return decode_impl(c, c->d_out.ptr, c->ranges.size(), w, h, max_iter, rms_eps, plane, iterations, rms, fused);
+    return decode_impl(c, c->d_out.ptr, nranges(c), w, h, max_iter, rms_eps, plane, iterations, rms, fused);
 }
 
 int frac_copy_tuples_device(frac_ctx* c, void* d_dst)
@@ -2511,7 +2571,7 @@ int frac_copy_tuples_device(frac_ctx* c, void* d_dst)
         return FRAC_E_INVALID;
     if (!c->ran)
         return c->fail(FRAC_E_STATE, "no results: frac_run has not been called");
-    const uint32_t nr = (uint32_t)c->ranges.size();
+    const uint32_t nr = (uint32_t)nranges(c);
     if (nr) {
         if (!d_dst)
             return c->fail(FRAC_E_INVALID, "copy_tuples: NULL destination");
@@ -2553,7 +2613,7 @@ int frac_pack_frc1(frac_ctx* c, uint32_t cbits, uint32_t bbits, uint8_t* out, si
         return c->fail(FRAC_E_INVALID, "pack_frc1: ranges are not the row-major range grid");
     if (!same_grid(c->doms, 2 * n, n))
         return c->fail(FRAC_E_INVALID, "pack_frc1: domains are not the domain lattice (size 2n, stride n)");
-    const uint32_t nr = (uint32_t)c->ranges.size(), nd = (uint32_t)c->doms.size(), T = c->p.transforms;
+    const uint32_t nr = (uint32_t)nranges(c), nd = (uint32_t)c->doms.size(), T = c->p.transforms;
     auto bitlen = [](uint64_t v) { uint32_t b = 0; while (v) { ++b; v >>= 1; } return b; };
     const uint32_t ib = std::max(1u, bitlen(nd)), tb = std::max(1u, bitlen(T - 1));
     const uint32_t width = ib + tb + cbits + bbits;
@@ -2627,7 +2687,7 @@ int frac_fetch_tuples(frac_ctx* c, frac_tuple* out)
         return FRAC_E_INVALID;
     if (!c->ran)
         return c->fail(FRAC_E_STATE, "no results: frac_run has not been called");
-    const size_t nr = c->ranges.size();
+    const size_t nr = nranges(c);
     if (!nr)
         return FRAC_OK;
     if (!out)
@@ -2645,7 +2705,7 @@ int frac_copy_results_device(frac_ctx* c, void* d_dst)
         return FRAC_E_INVALID;
     if (!c->ran)
         return c->fail(FRAC_E_STATE, "no results: frac_run has not been called");
-    const size_t nr = c->ranges.size();
+    const size_t nr = nranges(c);
     if (nr)
         FRAC_HIP(c, hipMemcpyAsync(d_dst, c->d_out.ptr, nr * sizeof(frac_encode_item), hipMemcpyDeviceToDevice,
                                    c->stream));

@@ -149,4 +149,41 @@ __global__ void __launch_bounds__(256) fill_rbucket(BucketLayout L, const uint32
     rbucket[r] = make_uint2(L.VT * L.dbeg[b], L.VT * (L.dbeg[b] + L.dcnt[b]));
 }
 
+// ---- quadtree level transitions on the device (frac_encode_quadtree) ----
+// A level's record i splits (flag 1) when the level may split and its distance exceeds the
+// threshold; the level's leaves are appended, in search order, to the frame's leaf list, and the
+// split ranges' four quadrants (top-left, top-right, bottom-left, bottom-right) become the next
+// level's ranges in their parents' order.  offs = exclusive scan of the flags.
+__global__ void __launch_bounds__(256) qt_flags(const frac_encode_item* __restrict__ out, uint32_t n, int can_split,
+                                                double split, uint32_t* __restrict__ flags)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n)
+        flags[i] = (can_split && out[i].match.score.distance > split) ? 1u : 0u;
+}
+
+__global__ void __launch_bounds__(256) qt_scatter(const frac_encode_item* __restrict__ out,
+                                                  const frac_grid_item* __restrict__ ranges, uint32_t n,
+                                                  const uint32_t* __restrict__ flags, const uint32_t* __restrict__ offs,
+                                                  frac_encode_item* __restrict__ leaves, uint32_t leaf_base,
+                                                  frac_grid_item* __restrict__ next, uint32_t* __restrict__ nsplit)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n)
+        return;
+    const uint32_t o = offs[i];
+    if (flags[i]) {
+        const frac_grid_item r = ranges[i];
+        const uint32_t h = r.w / 2;
+        next[4 * o + 0] = frac_grid_item{r.x, r.y, h, h, -1};
+        next[4 * o + 1] = frac_grid_item{r.x + h, r.y, h, h, -1};
+        next[4 * o + 2] = frac_grid_item{r.x, r.y + h, h, h, -1};
+        next[4 * o + 3] = frac_grid_item{r.x + h, r.y + h, h, h, -1};
+    } else {
+        leaves[leaf_base + (i - o)] = out[i];
+    }
+    if (i == n - 1)
+        *nsplit = o + flags[i];
+}
+
 } // namespace fracenc

@@ -170,7 +170,8 @@ def main():
         for split in (0.05, 0.5):
             with F.Engine(0, 4, True, timing=True) as e:
                 e.set_frame(frame)
-                e.encode_quadtree(16, 4, split)
+                for _ in range(max(2, args.warmup)):  # the first calls allocate the per-level buffers
+                    e.encode_quadtree(16, 4, split)
                 t0 = time.perf_counter()
                 for _ in range(args.steps):
                     items, st = e.encode_quadtree(16, 4, split)

@@ -13,6 +13,6 @@ with F.Engine(0, 4, True, timing=True) as e:
     e.set_frame(frame)
     e.encode_quadtree(16, 4, split)
     os.environ["FRAC_TRACE"] = "1"
-    for _ in range(2):
+    for _ in range(int(os.environ.get("QT_CALLS", "2"))):
         items, st = e.encode_quadtree(16, 4, split)
     print("items", len(items), "ms_search", st["ms_search"], "ms_device", st["ms_device"], file=sys.stderr)
