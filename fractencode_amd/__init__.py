@@ -20,7 +20,8 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libfracenc.so")
+# FRAC_LIB: an explicitly built alternative (tools/build_tuning.py's A/B library); the product is libfracenc.so
+LIB_PATH = os.environ.get("FRAC_LIB") or os.path.join(HERE, "libfracenc.so")
 
 GRID_ITEM = np.dtype([("x", "<u4"), ("y", "<u4"), ("w", "<u4"), ("h", "<u4"), ("category", "<i4")])
 ENCODE_ITEM = np.dtype([("x", "<u4"), ("y", "<u4"), ("w", "<u4"), ("h", "<u4"),

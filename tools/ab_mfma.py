@@ -4,6 +4,8 @@ median/min search-kernel and finish (resolve + fit) ms (library HIP events).
 Variants: "d" = the C4-Fourier search (FRAC_MFMA_DFT=1, default: software-pipelined exact
 form), "e" = its unpipelined exact form, "g" = the guarded fast-path form, "p" = pipelined with a forced interleave, "em"/"ev" = MFMA-only / VALU-only ablations of "e", an integer v = the direct
 search_mfma with FRAC_MFMA_VARIANT=v (FRAC_MFMA_DFT=0).
+Ablation variants need the tuning library: python tools/build_tuning.py, then
+FRAC_LIB=fractencode_amd/libfracenc_tuning.so tools/ab_mfma.py ...
 usage: tools/ab_mfma.py d,2 [rounds]"""
 import os
 import sys

@@ -1,0 +1,17 @@
+#!/usr/bin/env python3
+"""Builds the A/B tuning library: the product sources with -DFRAC_TUNING, so the ablation
+variants of FRAC_MFMA_VARIANT (MFMA-only, VALU-only, no LDS-DMA, no barrier — wrong results by
+design) exist.  Output fractencode_amd/libfracenc_tuning.so; use it with FRAC_LIB=<that path>
+(tools/ab_mfma.py).  The product build (__graft_entry__.build) never sets FRAC_TUNING."""
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import __graft_entry__ as G  # noqa: E402
+
+out = os.path.join(ROOT, "fractencode_amd", "libfracenc_tuning.so")
+subprocess.check_call([G._hipcc(), *G.HIPCC_FLAGS, "-DFRAC_TUNING", "-o", out,
+                       os.path.join(G.CSRC, "fracenc_api.hip")], cwd=G.CSRC)
+print(out)
