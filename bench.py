@@ -18,7 +18,9 @@ Beside `value` the line carries:
                 bytes per launch from the committed rocprofv3 PMC passes of THIS library build
                 (null when profiles/pmc_search.json was taken from another build)
   e2e           the same workload through the host boundary (§8(d)): per step the frame H2D from
-                pinned memory, the search, and the tuples D2H into pinned memory
+                pinned memory, the search, and the tuples D2H into pinned memory; `pipelined` = the same
+                with two contexts alternating frames, so frame k+1's upload and frame k−1's download
+                overlap frame k's search
   cpu_baseline  the unmodified reference (oracle/_ref) on a bounded sample, all the host cores this
                 process may use (affinity, capped by the cgroup CPU quota), CPU model recorded
 
@@ -306,6 +308,33 @@ def main(args):
                        "steps": e2e_steps,
                        "step": "frame H2D (pinned, 16 MiB) + search + tuples D2H (pinned, 32 B per range)"
                                + (" per rank; no gather" if world > 1 else "")}
+        # the same through two contexts in turn (a frame stream): frame k+1 uploads on one context's stream
+        # while frame k searches on the other's, and frame k's tuples come back while k+1 searches
+        with F.Engine(dev.index, args.transforms, False, 0.0, -1.0, engine_id) as eng2:
+            eng2.set_frame(h_frame.numpy())
+            eng2.set_domains(doms)
+            eng2.set_ranges(mine)
+            eng2.run()
+            eng2.fetch_tuples(tup)
+            ctxs = (eng, eng2)
+            tups = (tup, torch.empty(len(mine) * TUPLE_BYTES, dtype=torch.uint8).pin_memory().numpy().view(F.TUPLE))
+            if world > 1:
+                dist.barrier()
+            t0 = time.perf_counter()
+            for k in range(e2e_steps + 1):
+                if k < e2e_steps:
+                    ctxs[k & 1].set_frame(h_frame.numpy())  # waits for this context's own upload only
+                    ctxs[k & 1].run()
+                if k > 0:
+                    ctxs[(k - 1) & 1].fetch_tuples(tups[(k - 1) & 1])  # frame k−1's winners
+            e2p = time.perf_counter() - t0
+            if world > 1:
+                t = torch.tensor([e2p], dtype=torch.float64, device=dev)
+                dist.all_reduce(t, op=dist.ReduceOp.MAX)
+                e2p = float(t.item())
+            line["e2e"]["pipelined"] = {"value": round(nr_total / (e2p / e2e_steps), 1),
+                                        "ms_per_step": round(1e3 * e2p / e2e_steps, 3),
+                                        "step": "the same per frame, two contexts alternating frames"}
         eng.set_frame(d_frame)
         eng.run()
 
