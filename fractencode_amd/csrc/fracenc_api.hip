@@ -923,7 +923,7 @@ void launch_search_mfma_v(frac_ctx* c, const MfmaSearchArgs& a)
 // Any other value fails the run (FRAC_E_INVALID), so a stray variable cannot corrupt records.
 //   search_mfma: 0..7 schedule bits, 32 s_setprio, 64 late constants, 96, 98; ablations 8, 16
 //   search_dft:  default 8-wave exact form; 1 / 3 four-wave exact / guarded; 5 eight-tile
-//                stages; ablations 9, 17, 41, 73, 105, 65 (four-wave) and 201..207 (eight-wave)
+//                stages; 6 pairwise-tree row maximum; ablations 9, 17, 41, 73, 105, 65 (four-wave) and 201..207 (eight-wave)
 inline int mfma_variant(frac_ctx* c, int& var)
 {
     const char* v = getenv("FRAC_MFMA_VARIANT");
@@ -1022,8 +1022,9 @@ inline int launch_dft(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride)
         dft_range_prep<<<(c->nblocks * 32 + 255) / 256, 256, 0, c->stream>>>(r, c->d_dft_rguard.ptr);
     if (c->p.flags & FRAC_FLAG_TIMING)
         FRAC_TRY(mark_event(c, 1));
-    // FRAC_MFMA_VARIANT for this path (A/B knob): default = exact form in 8-wave workgroups;
-    // 1 = exact form in 4-wave workgroups, 3 = guarded fast path (4 waves), odd values ≥ 9 =
+    // FRAC_MFMA_VARIANT for this path (A/B knob): default = exact form in 8-wave workgroups
+    // with the v_max3-chain row maximum; 6 = the same with a pairwise-tree row maximum; 5 =
+    // 8-tile stages; 1 = exact form in 4-wave workgroups, 3 = guarded fast path (4 waves), odd values ≥ 9 =
     // ablations of variant 1 (tuning only: wrong results)
     int var = 0;
     FRAC_TRY(mfma_variant(c, var));
@@ -1064,14 +1065,19 @@ inline int launch_dft(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride)
 #endif
         } else if (!four && var == 5) { // 8-tile LDS stages
             if (hits)
-                search_dft<true, 1, W8, 8><<<nwg, 64 * W8, 0, c->stream>>>(da);
+                search_dft<true, 1 | kDftChain, W8, 8><<<nwg, 64 * W8, 0, c->stream>>>(da);
             else
-                search_dft<false, 1, W8, 8><<<nwg, 64 * W8, 0, c->stream>>>(da);
-        } else if (!four) {
+                search_dft<false, 1 | kDftChain, W8, 8><<<nwg, 64 * W8, 0, c->stream>>>(da);
+        } else if (!four && var == 6) { // the pairwise-tree row maximum (round 1's default, A/B)
             if (hits)
                 search_dft<true, 1, W8><<<nwg, 64 * W8, 0, c->stream>>>(da);
             else
                 search_dft<false, 1, W8><<<nwg, 64 * W8, 0, c->stream>>>(da);
+        } else if (!four) {
+            if (hits)
+                search_dft<true, 1 | kDftChain, W8><<<nwg, 64 * W8, 0, c->stream>>>(da);
+            else
+                search_dft<false, 1 | kDftChain, W8><<<nwg, 64 * W8, 0, c->stream>>>(da);
         } else if (var == 1) {
             if (hits)
                 search_dft<true, 1><<<nwg, 256, 0, c->stream>>>(da);
@@ -1321,7 +1327,7 @@ int launch_tp(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool timing)
     FRAC_HIP(c, c->d_m_entries.ensure((size_t)ng * W8 * 64));
     da.m.entries = c->d_m_entries.ptr;
     da.choff = c->d_tp_iota.ptr;
-    search_dft<false, 1, W8, 4, true><<<ng, 64 * W8, 0, c->stream>>>(da);
+    search_dft<false, 1 | kDftChain, W8, 4, true><<<ng, 64 * W8, 0, c->stream>>>(da);
     tp_seed_reduce<<<(nbk * 32 + 255) / 256, 256, 0, c->stream>>>(c->d_tp_blk_group.ptr, c->d_m_entries.ptr,
                                                                    c->d_m_slot_range.ptr, c->d_m_rconst.ptr, nbk,
                                                                    c->d_tp_blk_u.ptr);
@@ -1363,9 +1369,9 @@ int launch_tp(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool timing)
     da.m.entries = c->d_m_entries.ptr;
     da.choff = c->d_tp_choff.ptr;
     if (c->hitH > 0)
-        search_dft<true, 1, W8, 4, true><<<ng, 64 * W8, 0, c->stream>>>(da);
+        search_dft<true, 1 | kDftChain, W8, 4, true><<<ng, 64 * W8, 0, c->stream>>>(da);
     else
-        search_dft<false, 1, W8, 4, true><<<ng, 64 * W8, 0, c->stream>>>(da);
+        search_dft<false, 1 | kDftChain, W8, 4, true><<<ng, 64 * W8, 0, c->stream>>>(da);
     if (timing)
         FRAC_TRY(mark_event(c, 2));
     MfmaResolveArgs v;
