@@ -251,6 +251,7 @@ struct frac_ctx {
     DBuf<frac_grid_item> d_qt_next;       // the next level's ranges, built on the device
     DBuf<frac_encode_item> d_qt_leaves;   // the frame's leaves, in output order
     DBuf<uint32_t> d_qt_flags, d_qt_offs, d_qt_count;
+    DBuf<unsigned long long> d_qt_stats; // quadtree: the levels' frac_stats counters (qt_level_stats)
     DBuf<uint8_t> d_qt_tmp;
     size_t qt_tmp_bytes = 0;
     bool qt_dvalid[5] = {false, false, false, false, false};
@@ -440,16 +441,16 @@ int device_buckets(frac_ctx* c, int nb, uint32_t* dfirst, uint32_t* rfirst)
     const uint32_t tstride = c->same_plane ? c->d_sstride : c->d_tstride;
     size_t tb = c->bk_tmp_bytes;
     if (nd) { // a stored −1 is classified on the item's own plane (Classifier2::compare, Classifier2.cpp:70-81)
-        bucket_keys<<<(nd + 3) / 4, 256, 0, c->stream>>>(c->d_doms.ptr, nd, c->d_src.ptr, c->d_sstride, c->d_bk_keys.ptr,
-                                                        c->d_bk_iota.ptr, err);
+        launch_bucket_keys(c->d_doms.ptr, nd, c->S, c->d_src.ptr, c->d_sstride, c->d_bk_keys.ptr, c->d_bk_iota.ptr,
+                           err, c->stream);
         FRAC_HIP(c, sort_pairs_u32(c->d_bk_tmp.ptr, tb, c->d_bk_keys.ptr, c->d_bk_keys2.ptr, c->d_bk_iota.ptr,
                                    c->d_porig.ptr, nd, 3, c->stream));
     }
     bucket_bounds<<<1, 64, 0, c->stream>>>(c->d_bk_keys2.ptr, nd, first);
     tb = c->bk_tmp_bytes;
     if (nr) {
-        bucket_keys<<<(nr + 3) / 4, 256, 0, c->stream>>>(c->d_ranges.ptr, nr, tplane, tstride, c->d_rkey.ptr,
-                                                        c->d_bk_iota.ptr, err);
+        launch_bucket_keys(c->d_ranges.ptr, nr, (uint32_t)c->n, tplane, tstride, c->d_rkey.ptr, c->d_bk_iota.ptr, err,
+                           c->stream);
         FRAC_HIP(c, sort_pairs_u32(c->d_bk_tmp.ptr, tb, c->d_rkey.ptr, c->d_bk_keys2.ptr, c->d_bk_iota.ptr,
                                    c->d_rord.ptr, nr, 3, c->stream));
     }
@@ -467,6 +468,12 @@ int device_buckets(frac_ctx* c, int nb, uint32_t* dfirst, uint32_t* rfirst)
     }
     return FRAC_OK;
 }
+
+inline int mfma_variant(frac_ctx* c, int& var);
+inline bool mfma_dft_enabled();
+// the Fourier search variants that run 4-wave workgroups (and read m_work): 1, 3 and the odd
+// ablations below 200; every other variant runs 8-wave workgroups on m8_work
+inline bool dft_four_wave(int var) { return var == 1 || var == 3 || (var >= 9 && var < 200 && (var & 1)); }
 
 int prepare(frac_ctx* c)
 {
@@ -675,13 +682,31 @@ int prepare(frac_ctx* c)
             for (int b = 0; b < nb; ++b)
                 if (tile_count[b])
                     groups += (blk_count[b] + bpw - 1) / bpw;
-            std::vector<std::vector<uint32_t>> blk_list(c->nblocks);
-            work.clear();
+            // every block of bucket b gets one entry per domain split of b: the CSR map is
+            // sized by a count pass, then filled in work order (no per-block lists)
+            std::vector<uint32_t> nsplit(nb, 0);
+            blk_ptr.assign(c->nblocks + 1, 0);
             for (int b = 0; b < nb; ++b) {
                 if (!tile_count[b] || !blk_count[b])
                     continue;
                 size_t splits = groups ? (target_wgs + groups - 1) / groups : 1;
                 splits = std::max<size_t>(1, std::min<size_t>(splits, std::max<uint32_t>(1u, tile_count[b] / 4u)));
+                uint32_t ns = 0;
+                for (size_t sp = 0; sp < splits; ++sp)
+                    ns += (uint64_t)tile_count[b] * (sp + 1) / splits > (uint64_t)tile_count[b] * sp / splits;
+                nsplit[b] = (uint32_t)splits;
+                for (uint32_t k = 0; k < blk_count[b]; ++k)
+                    blk_ptr[blk_first[b] + k + 1] = ns;
+            }
+            for (uint32_t b = 0; b < c->nblocks; ++b)
+                blk_ptr[b + 1] += blk_ptr[b];
+            blk_ent.assign(blk_ptr[c->nblocks], 0);
+            std::vector<uint32_t> cur(blk_ptr.begin(), blk_ptr.end() - 1);
+            work.clear();
+            for (int b = 0; b < nb; ++b) {
+                if (!nsplit[b])
+                    continue;
+                const size_t splits = nsplit[b];
                 for (uint32_t g = 0; g < blk_count[b]; g += bpw) {
                     const uint32_t nbk = std::min(bpw, blk_count[b] - g);
                     for (size_t sp = 0; sp < splits; ++sp) {
@@ -693,7 +718,7 @@ int prepare(frac_ctx* c)
                         work.push_back(make_uint4(blk_first[b] + g, nbk, t0, t1));
                         split_of.push_back((uint32_t)sp);
                         for (uint32_t k = 0; k < nbk; ++k)
-                            blk_list[blk_first[b] + g + k].push_back(w * bpw + k);
+                            blk_ent[cur[blk_first[b] + g + k]++] = w * bpw + k;
                     }
                 }
             }
@@ -744,22 +769,23 @@ int prepare(frac_ctx* c)
                     inv[order[n]] = n;
                 }
                 work.swap(nw);
-                for (auto& lst : blk_list)
-                    for (uint32_t& e : lst)
-                        e = inv[e / bpw] * bpw + e % bpw;
+                for (uint32_t& e : blk_ent)
+                    e = inv[e / bpw] * bpw + e % bpw;
             }
-            blk_ptr.assign(c->nblocks + 1, 0);
-            blk_ent.clear();
-            for (uint32_t b = 0; b < c->nblocks; ++b) {
-                blk_ptr[b] = (uint32_t)blk_ent.size();
-                blk_ent.insert(blk_ent.end(), blk_list[b].begin(), blk_list[b].end());
-            }
-            blk_ptr[c->nblocks] = (uint32_t)blk_ent.size();
         };
+        const bool fourier = n == 8 && c->p.transforms == 4 && !c->virt && mfma_dft_enabled();
+        int var = 0;
+        FRAC_TRY(mfma_variant(c, var));
+        const bool four_wave = dft_four_wave(var);
         if (n == 16) // search_mfma16: one range block per workgroup (T waves)
             build_work(1, 4096, c->m_work, c->m_blk_ptr, c->m_blk_ent, false);
-        else
+        else if (!fourier || four_wave) // the 8-wave Fourier search reads only its own list
             build_work(4, 8192, c->m_work, c->m_blk_ptr, c->m_blk_ent, false);
+        else {
+            c->m_work.clear();
+            c->m_blk_ptr.assign(c->nblocks + 1, 0);
+            c->m_blk_ent.clear();
+        }
         if (n == 8 && c->p.transforms == 4 && !c->virt) {
             // FRAC_DFT_WGS (tuning knob): target workgroup count of the Fourier search
             const char* tw = getenv("FRAC_DFT_WGS");
@@ -1028,7 +1054,7 @@ inline int launch_dft(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride)
     // ablations of variant 1 (tuning only: wrong results)
     int var = 0;
     FRAC_TRY(mfma_variant(c, var));
-    const bool four = var == 1 || var == 3 || (var >= 9 && (var & 1));
+    const bool four = dft_four_wave(var);
     const std::vector<uint4>& work = four ? c->m_work : c->m8_work;
     c->form_ran = FRAC_FORM_FOURIER;
     c->flops_ran = 0;
@@ -1848,6 +1874,7 @@ void frac_destroy(frac_ctx* c)
     c->d_qt_flags.release();
     c->d_qt_offs.release();
     c->d_qt_count.release();
+    c->d_qt_stats.release();
     c->d_qt_tmp.release();
     c->d_rkey.release();
     c->d_bk_keys.release();
@@ -2210,6 +2237,9 @@ int frac_encode_quadtree(frac_ctx* c, const frac_quadtree_params* qp, frac_encod
     FRAC_HIP(c, c->d_ranges.ensure(std::max<size_t>(max_leaves, 1)));
     FRAC_HIP(c, c->d_qt_next.ensure(std::max<size_t>(max_leaves, 1)));
     FRAC_HIP(c, c->d_qt_count.ensure(1));
+    FRAC_HIP(c, c->d_qt_stats.ensure(5));
+    if (stats)
+        FRAC_HIP(c, hipMemsetAsync(c->d_qt_stats.ptr, 0, 5 * sizeof(unsigned long long), c->stream));
     uint32_t n_leaves = 0;
     size_t level_nr = pending.size();
     FRAC_TRY(frac_set_ranges(c, pending.data(), pending.size()));
@@ -2222,24 +2252,29 @@ int frac_encode_quadtree(frac_ctx* c, const frac_quadtree_params* qp, frac_encod
         tr.mark("grids");
         FRAC_TRY(frac_run(c));
         tr.mark("run (enqueue)");
-        frac_stats st{};
-        FRAC_TRY(frac_fetch(c, nullptr, stats ? &st : nullptr)); // statistics only: the records stay on the device
-        level.out();
-        tr.mark("fetch stats (sync)");
-        total.rejected_mappings += st.rejected_mappings;
-        total.total_mappings += st.total_mappings;
-        total.hit_ranges += st.hit_ranges;
-        total.fallback_ranges += st.fallback_ranges;
-        total.empty_ranges += st.empty_ranges;
-        total.engine = st.engine;
-        total.ms_device += st.ms_device;
-        total.ms_search += st.ms_search;
-        total.ms_prep += st.ms_prep;
-        total.ms_finish += st.ms_finish;
-        total.search_form = st.search_form;
-        total.matrix_flops += st.matrix_flops;
-        total.evaluated_mappings += st.evaluated_mappings;
+        // the level's statistics accumulate on the device (no per-level download or host loop); the
+        // counters are read once after the last level, the event times after this level's count
         const uint32_t nr = (uint32_t)level_nr;
+        if (stats) {
+            QtBuckets qb{};
+            qb.nb = (uint32_t)c->bucket_begin.size();
+            for (uint32_t b = 0; b < qb.nb && b < (uint32_t)kMaxBuckets; ++b) {
+                qb.beg[b] = c->bucket_begin[b];
+                qb.end[b] = c->bucket_end[b];
+            }
+            const bool sea_ran = c->engine_ran == FRAC_ENGINE_SEA && c->form_ran == FRAC_FORM_SEA;
+            qt_level_stats<<<(nr + 255) / 256, 256, 0, c->stream>>>(
+                c->d_aux.ptr, c->d_rkey.ptr, c->d_porig.ptr, nr, (uint64_t)c->doms.size(), c->p.use_classifier ? 1 : 0,
+                qb, sea_ran ? c->d_sea_count.ptr : nullptr, c->d_qt_stats.ptr);
+            total.total_mappings += (uint64_t)c->doms.size() * nr;
+            total.engine = c->engine_ran;
+            total.search_form = c->form_ran;
+            total.matrix_flops += c->flops_ran;
+            if (!sea_ran)
+                total.evaluated_mappings += c->evaluated_ran;
+        }
+        level.out();
+        tr.mark("level stats (enqueue)");
         FRAC_HIP(c, c->d_qt_flags.ensure(nr));
         FRAC_HIP(c, c->d_qt_offs.ensure(nr));
         size_t need = 0;
@@ -2261,6 +2296,17 @@ int frac_encode_quadtree(frac_ctx* c, const frac_quadtree_params* qp, frac_encod
         uint32_t nsplit = 0;
         FRAC_HIP(c, hipMemcpyAsync(&nsplit, c->d_qt_count.ptr, sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
         FRAC_HIP(c, hipStreamSynchronize(c->stream));
+        if (stats && (c->p.flags & FRAC_FLAG_TIMING)) { // the level's run has completed
+            float ms = 0.f;
+            if (hipEventElapsedTime(&ms, c->ev[0], c->ev[3]) == hipSuccess)
+                total.ms_device += ms;
+            if (hipEventElapsedTime(&ms, c->ev[0], c->ev[1]) == hipSuccess)
+                total.ms_prep += ms;
+            if (hipEventElapsedTime(&ms, c->ev[1], c->ev[2]) == hipSuccess)
+                total.ms_search += ms;
+            if (hipEventElapsedTime(&ms, c->ev[2], c->ev[3]) == hipSuccess)
+                total.ms_finish += ms;
+        }
         n_leaves += nr - nsplit;
         level_nr = 4 * (size_t)nsplit;
         // the next level searches the device-built quadrants
@@ -2281,8 +2327,16 @@ int frac_encode_quadtree(frac_ctx* c, const frac_quadtree_params* qp, frac_encod
         FRAC_HIP(c, hipMemcpy(out, c->d_qt_leaves.ptr, std::min<size_t>(cap, n_leaves) * sizeof(frac_encode_item),
                               hipMemcpyDeviceToHost));
     tr.mark("leaves D2H");
-    if (stats)
+    if (stats) {
+        unsigned long long acc[5] = {0ull, 0ull, 0ull, 0ull, 0ull};
+        FRAC_HIP(c, hipMemcpy(acc, c->d_qt_stats.ptr, sizeof(acc), hipMemcpyDeviceToHost));
+        total.rejected_mappings = acc[0];
+        total.hit_ranges = acc[1];
+        total.fallback_ranges = acc[2];
+        total.empty_ranges = acc[3];
+        total.evaluated_mappings += acc[4];
         *stats = total;
+    }
     return FRAC_OK;
 }
 

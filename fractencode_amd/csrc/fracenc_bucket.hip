@@ -10,6 +10,8 @@
 // boundaries, and the fills of the per-slot / per-tile / per-range maps the engines read.  The
 // host sees only the 2 × 8 bucket counts, from which it derives the small per-bucket layout
 // (BucketLayout) and the work lists — no per-item host loop and no per-item transfer.
+#include <type_traits>
+
 #include "fracenc_common.h"
 
 namespace fracenc {
@@ -69,6 +71,87 @@ __global__ void __launch_bounds__(256) bucket_keys(const frac_grid_item* __restr
         key[k] = (uint32_t)(cat + 1);
         iota[k] = k;
     }
+}
+
+// The same for items at most 64 rows high: L lanes per item (L = the item height rounded up to
+// a power of two), lane j sums the two halves of row j (dword loads and v_dot4 when the row
+// and the half width are 4-byte aligned, else bytes), and the group reduces the quadrants.
+// 64/L items per wave instead of one.
+template <uint32_t L>
+__global__ void __launch_bounds__(256) bucket_keys_rows(const frac_grid_item* __restrict__ items, uint32_t n,
+                                                        const uint8_t* __restrict__ plane, uint32_t stride,
+                                                        uint32_t* __restrict__ key, uint32_t* __restrict__ iota,
+                                                        uint32_t* __restrict__ err)
+{
+    static_assert(L >= 1 && L <= 64 && (L & (L - 1)) == 0, "lanes per item: a power of two up to 64");
+    const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t k = gid / L, j = gid % L;
+    frac_grid_item it{0, 0, 0, 0, 0};
+    if (k < n)
+        it = items[k];
+    const uint32_t hw = it.w / 2, hh = it.h / 2;
+    uint32_t lo = 0, hi = 0;
+    if (k < n && it.category == -1 && j < 2 * hh) {
+        const uint8_t* row = plane + (size_t)(it.y + j) * stride + it.x;
+        if (((((uintptr_t)row) | hw) & 3u) == 0) {
+            for (uint32_t c = 0; c < hw; c += 4) {
+                lo = __builtin_amdgcn_udot4(*reinterpret_cast<const uint32_t*>(row + c), 0x01010101u, lo, false);
+                hi = __builtin_amdgcn_udot4(*reinterpret_cast<const uint32_t*>(row + hw + c), 0x01010101u, hi, false);
+            }
+        } else {
+            for (uint32_t c = 0; c < hw; ++c) {
+                lo += row[c];
+                hi += row[hw + c];
+            }
+        }
+    }
+    uint32_t q[4] = {j < hh ? lo : 0u, j < hh ? hi : 0u, j < hh ? 0u : lo, j < hh ? 0u : hi};
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (uint32_t o = L / 2; o > 0; o >>= 1)
+            q[i] += (uint32_t)__shfl_xor((int)q[i], (int)o, 64);
+    if (j != 0 || k >= n)
+        return;
+    int cat = it.category;
+    if (cat == -1) {
+        if (hw <= 16)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                q[i] &= 0xffffu;
+        cat = category4_dev(q[0], q[1], q[2], q[3]);
+    }
+    if (cat < -1 || cat > 5) {
+        atomicOr(err, 1u);
+        cat = -1;
+    }
+    key[k] = (uint32_t)(cat + 1);
+    iota[k] = k;
+}
+
+// bucket keys of `cnt` items of height h (every item of a grid has the size of the first)
+inline void launch_bucket_keys(const frac_grid_item* items, uint32_t cnt, uint32_t h, const uint8_t* plane,
+                               uint32_t stride, uint32_t* key, uint32_t* iota, uint32_t* err, hipStream_t s)
+{
+    auto rows = [&](auto lanes) {
+        constexpr uint32_t L = decltype(lanes)::value;
+        const uint64_t threads = (uint64_t)cnt * L;
+        bucket_keys_rows<L><<<(unsigned)((threads + 255) / 256), 256, 0, s>>>(items, cnt, plane, stride, key, iota, err);
+    };
+    if (h <= 2)
+        rows(std::integral_constant<uint32_t, 2>());
+    else if (h <= 4)
+        rows(std::integral_constant<uint32_t, 4>());
+    else if (h <= 8)
+        rows(std::integral_constant<uint32_t, 8>());
+    else if (h <= 16)
+        rows(std::integral_constant<uint32_t, 16>());
+    else if (h <= 32)
+        rows(std::integral_constant<uint32_t, 32>());
+    else if (h <= 64)
+        rows(std::integral_constant<uint32_t, 64>());
+    else
+        bucket_keys<<<(cnt + 3) / 4, 256, 0, s>>>(items, cnt, plane, stride, key, iota, err);
 }
 
 __global__ void __launch_bounds__(256) fill_iota(uint32_t* __restrict__ out, uint32_t n)
@@ -160,6 +243,54 @@ __global__ void __launch_bounds__(256) qt_flags(const frac_encode_item* __restri
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n)
         flags[i] = (can_split && out[i].match.score.distance > split) ? 1u : 0u;
+}
+
+// A level's frac_stats counters, added on the device into acc = {rejected, hit, fallback, empty,
+// evaluated} (frac_fetch's host loop, restated): an empty range rejects every domain (classifier
+// on), a hit rejects the ineligible domains before its own in grid order (porig of its pool
+// position minus the eligible ones before it), any other range every domain outside its bucket.
+struct QtBuckets {
+    uint32_t nb;
+    uint32_t beg[kMaxBuckets];
+    uint32_t end[kMaxBuckets];
+};
+
+__global__ void __launch_bounds__(256) qt_level_stats(const RangeAux* __restrict__ aux,
+                                                      const uint32_t* __restrict__ rkey,
+                                                      const uint32_t* __restrict__ porig, uint32_t nr, uint64_t nd,
+                                                      int classifier, QtBuckets B,
+                                                      const unsigned long long* __restrict__ sea_count,
+                                                      unsigned long long* __restrict__ acc)
+{
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    unsigned long long v[4] = {0ull, 0ull, 0ull, 0ull}; // rejected, hit, fallback, empty
+    if (r < nr) {
+        const RangeAux ax = aux[r];
+        const uint32_t b = classifier ? rkey[r] : 0u;
+        if (ax.flags & kAuxEmpty) {
+            v[3] = 1;
+            v[0] = classifier ? nd : 0ull;
+        } else {
+            v[2] = (ax.flags & kAuxFallback) ? 1ull : 0ull;
+            if (ax.flags & kAuxHit) {
+                v[1] = 1;
+                if (classifier)
+                    v[0] = (unsigned long long)porig[ax.pos] - (ax.pos - B.beg[b]);
+            } else if (classifier) {
+                v[0] = nd - (B.end[b] - B.beg[b]);
+            }
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1)
+            v[i] += (unsigned long long)__shfl_xor((long long)v[i], o, 64);
+        if ((threadIdx.x & 63u) == 0 && v[i])
+            atomicAdd(&acc[i], v[i]);
+    }
+    if (sea_count && r == 0)
+        atomicAdd(&acc[4], *sea_count);
 }
 
 __global__ void __launch_bounds__(256) qt_scatter(const frac_encode_item* __restrict__ out,

@@ -516,12 +516,27 @@ __device__ inline int fwd_rt(const Aff& a, int N, int q)
 }
 
 // One wave per range.  Lane l covers tile row i = l>>2 of a candidate entry's lane half
-// and pixel slice g = l&3 (n²/4 pixels), so the 16 rows of a tile are evaluated at once
-// with exact integers; a ballot picks the first row (domain order) that matches.
+// and slice g = l&3 of the pool row (n²/8 packed u16 pairs), so the 16 rows of a tile are
+// evaluated at once with exact integers; a ballot picks the first row (domain order) that
+// matches.  Per transform the lane holds its slice of the range's inverse-permuted copy
+// (the pixels that meet the slice's domain cells under t, as u16 pairs), so a row is one
+// contiguous load of pool words and v_dot2_u32_u16 per word (Σ r·D4 < 2^32 for n ≤ 16).
+// Matching entries in a chunk after the tile of the best key so far are skipped: their rows
+// are later pool positions of the same bucket, so they can neither win nor tie.
+template <int N>
+__device__ inline uint32_t range_pix_inv(const uint8_t* __restrict__ tgt, uint32_t tstride, const frac_grid_item& rg,
+                                         const Aff& af, int q)
+{
+    const int qx = q % N, qy = q / N;
+    const int dx = qx - (af.a2 + af.a3) * (N - 1), dy = qy - (af.a6 + af.a7) * (N - 1);
+    const int px = af.a0 * dx + af.a4 * dy, py = af.a1 * dx + af.a5 * dy;
+    return tgt[(size_t)(rg.y + py) * tstride + rg.x + px];
+}
+
 template <int N>
 __global__ void __launch_bounds__(256) resolve_mfma(MfmaResolveArgs a)
 {
-    constexpr int NN = N * N, PG = (NN + 3) / 4; // pixels per slice
+    constexpr int NN = N * N, K2 = NN / 2, WPL = K2 >= 4 ? K2 / 4 : 1; // pool words per lane slice
     const uint32_t r = blockIdx.x * 4u + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     if (r >= a.nr)
@@ -542,20 +557,32 @@ __global__ void __launch_bounds__(256) resolve_mfma(MfmaResolveArgs a)
         return; // no eligible domain: best_key stays "none"
     const frac_grid_item rg = a.ranges[r];
     const int i = lane >> 2, g = lane & 3;
-    int px[PG];
-    int64_t sr2 = 0;
+    // the lane's slice of the copy under transform ct (rebuilt when an entry's t differs)
+    uint32_t cp[WPL];
+    int ct = -1;
+    auto build_copy = [&](int t) {
+        const Aff af = lut(t);
 #pragma unroll
-    for (int u = 0; u < PG; ++u) {
-        const int q = g * PG + u;
-        px[u] = q < NN ? (int)a.tgt[(size_t)(rg.y + q / N) * a.tstride + rg.x + (q % N)] : 0;
-        sr2 += px[u] * px[u];
-    }
-    sr2 += __shfl_xor(sr2, 1, 64);
-    sr2 += __shfl_xor(sr2, 2, 64);
+        for (int w = 0; w < WPL; ++w) {
+            const int k = g * WPL + w;
+            cp[w] = k < K2 ? range_pix_inv<N>(a.tgt, a.tstride, rg, af, 2 * k) |
+                                 (range_pix_inv<N>(a.tgt, a.tstride, rg, af, 2 * k + 1) << 16)
+                           : 0u;
+        }
+        ct = t;
+    };
+    build_copy(0);
+    uint32_t sr2u = 0; // Σr² (every pixel meets exactly one domain cell)
+#pragma unroll
+    for (int w = 0; w < WPL; ++w)
+        sr2u = __builtin_amdgcn_udot2(__builtin_bit_cast(ushort2_t, cp[w]), __builtin_bit_cast(ushort2_t, cp[w]), sr2u,
+                                      false);
+    const int64_t sr2 = (int64_t)quad_sum(sr2u);
     const int64_t target = (int64_t)vmin - (int64_t)a.rconst[slot]; // best S16 (when vmin != sentinel)
     // hits: the sentinel 0 (kernel run with H > 0), or a best error that meets H = 0
     const bool hit = a.hitH >= 0 && (vmin == 0 || target <= a.hitH);
     unsigned long long bestk = kKeyNone;
+    uint32_t best_tile = 0xffffffffu;
     // only the entries holding the minimum are re-evaluated: the lanes test 64 entries at a
     // time and the wave walks the ballot of matches (the cost does not grow with the splits)
     for (uint32_t c0 = 0; c0 < nent; c0 += 64) {
@@ -571,28 +598,44 @@ __global__ void __launch_bounds__(256) resolve_mfma(MfmaResolveArgs a)
             match &= match - 1;
             const uint32_t j = c0 + (uint32_t)src;
             const uint32_t t = (j >> 1) % a.T, h = j & 1u;
-            const uint2 en = make_uint2(vmin, (uint32_t)__shfl((int)enl.y, src, 64));
+            const uint32_t ctile = (uint32_t)__builtin_amdgcn_readlane((int)enl.y, src);
+            if (ctile > best_tile)
+                continue;
+            if ((int)t != ct)
+                build_copy((int)t);
             const int row = (i & 3) + 8 * (i >> 2) + 4 * (int)h;
-            const Aff af = lut((int)t);
             // the entry names the first tile of the chunk that attained the minimum: scan the
             // chunk's tiles in order; the first matching row is the earliest domain
-            for (uint32_t tile = en.y; tile < min(en.y + (uint32_t)kTilesPerStage, a.ntiles); ++tile) {
+            for (uint32_t tile = ctile; tile < min(ctile + (uint32_t)kTilesPerStage, a.ntiles); ++tile) {
                 const int p = a.tile_pos[tile * 32 + row];
-                int64_t X = 0;
-                if (p >= 0) {
-                    const uint32_t* dp = a.pool + (size_t)p * (NN / 2);
+                uint32_t d[WPL];
+                if (p >= 0 && g * WPL < K2) {
+                    const uint32_t* dp = a.pool + (size_t)p * K2 + g * WPL;
+                    if constexpr (WPL % 4 == 0) {
 #pragma unroll
-                    for (int u = 0; u < PG; ++u) {
-                        const int q = g * PG + u;
-                        if (q < NN) {
-                            const int f = fwd_rt(af, N, q);
-                            const uint32_t w = dp[f >> 1];
-                            X += (int64_t)px[u] * (int64_t)((f & 1) ? (w >> 16) : (w & 0xffffu));
+                        for (int w = 0; w < WPL; w += 4) {
+                            const uint4 v = *reinterpret_cast<const uint4*>(dp + w);
+                            d[w] = v.x;
+                            d[w + 1] = v.y;
+                            d[w + 2] = v.z;
+                            d[w + 3] = v.w;
                         }
+                    } else {
+#pragma unroll
+                        for (int w = 0; w < WPL; ++w)
+                            d[w] = dp[w];
                     }
+                } else {
+#pragma unroll
+                    for (int w = 0; w < WPL; ++w)
+                        d[w] = 0u;
                 }
-                X += __shfl_xor(X, 1, 64);
-                X += __shfl_xor(X, 2, 64);
+                uint32_t xu = 0;
+#pragma unroll
+                for (int w = 0; w < WPL; ++w)
+                    xu = __builtin_amdgcn_udot2(__builtin_bit_cast(ushort2_t, cp[w]), __builtin_bit_cast(ushort2_t, d[w]),
+                                                xu, false);
+                const int64_t X = (int64_t)quad_sum(xu);
                 const int64_t s16 = p >= 0 ? 16 * sr2 - 8 * X - (int64_t)a.negsd2[p] : 0;
                 const bool ok = p >= 0 && g == 0 && (hit ? (s16 <= a.hitH) : (s16 == target));
                 const unsigned long long mask = __ballot(ok);
@@ -602,7 +645,10 @@ __global__ void __launch_bounds__(256) resolve_mfma(MfmaResolveArgs a)
                     const int pf = __shfl(p, first, 64);
                     const unsigned long long k =
                         hit ? key_hit((uint32_t)pf, t) : key_miss((uint64_t)s16f, (uint32_t)pf, a.T - 1 - t);
-                    bestk = k < bestk ? k : bestk;
+                    if (k < bestk) {
+                        bestk = k;
+                        best_tile = tile;
+                    }
                     break;
                 }
             }
