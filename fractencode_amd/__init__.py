@@ -353,22 +353,29 @@ class Engine:
                                           height, max_iter, rms_eps, plane.ctypes.data, C.byref(it), C.byref(rms)))
         return plane, it.value, rms.value
 
-    def encode_quadtree(self, max_size: int = 16, min_size: int = 4, split_distance: float = 10.0):
+    def encode_quadtree(self, max_size: int = 16, min_size: int = 4, split_distance: float = 10.0, out=None):
         """Quadtree partition of the frame set on this engine (frac_encode_quadtree): ranges of
         max_size split into quadrants while their best distance exceeds split_distance, down to
-        min_size.  Returns (encode items of mixed sizes, summed stats dict)."""
+        min_size.  Returns (encode items of mixed sizes, summed stats dict).  With `out` (an
+        ENCODE_ITEM array of at least (W/min_size)·(H/min_size) items, e.g. pinned host memory)
+        the items are written there and a view of it is returned, without a copy."""
         qp = FracQuadtreeParams(max_size, min_size, split_distance)
         n = C.c_size_t(0)
         st = FracStats()
-        # one pass with a worst-case capacity (every range at min_size), in a buffer kept across
-        # calls: a fresh one costs a page fault per 4 KiB on first touch
         W, H = self._frame_wh
         cap = max((W // min_size) * (H // min_size), 1)
-        buf = getattr(self, "_qt_buf", None)
-        if buf is None or len(buf) < cap:
-            buf = self._qt_buf = np.empty(cap, dtype=ENCODE_ITEM)
+        if out is not None:
+            if out.dtype != ENCODE_ITEM or not out.flags.c_contiguous or len(out) < cap:
+                raise ValueError(f"out must be a contiguous ENCODE_ITEM array of at least {cap} items")
+            buf = out
+        else:
+            # one pass with a worst-case capacity (every range at min_size), in a buffer kept across
+            # calls: a fresh one costs a page fault per 4 KiB on first touch
+            buf = getattr(self, "_qt_buf", None)
+            if buf is None or len(buf) < cap:
+                buf = self._qt_buf = np.empty(cap, dtype=ENCODE_ITEM)
         self._check(lib().frac_encode_quadtree(self._ctx, C.byref(qp), buf.ctypes.data, cap, C.byref(n), C.byref(st)))
-        return buf[: n.value].copy(), st.as_dict()
+        return (buf[: n.value] if out is not None else buf[: n.value].copy()), st.as_dict()
 
     def classify(self, items: np.ndarray, target_plane: bool = False) -> np.ndarray:
         """BrightnessBlocksClassifier2 categories of `items` computed on the device plane set by

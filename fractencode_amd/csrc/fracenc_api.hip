@@ -270,6 +270,7 @@ struct frac_ctx {
     // since the last frac_timing_history call, a ring of kHistRuns runs (created on first use)
     std::vector<hipEvent_t> hist;
     uint64_t hist_runs = 0, hist_read = 0;
+    int prep_knobs = -1; // FRAC_MFMA_VARIANT / FRAC_MFMA_DFT as of the last prepare (frac_run)
     bool ran = false;
     uint32_t engine_ran = FRAC_ENGINE_VALU;
     uint32_t form_ran = FRAC_FORM_DOT2;
@@ -1192,6 +1193,8 @@ int launch_mfma(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride)
         r.rfrags = c->d_m_rfrags.ptr;
         r.rconst = c->d_m_rconst.ptr;
         const size_t threads = (size_t)c->nblocks * T * MfmaGeom<N>::KS * 64;
+        // rconst is a sum of per-pixel terms, accumulated by the transform-0 threads
+        FRAC_HIP(c, hipMemsetAsync(c->d_m_rconst.ptr, 0, (size_t)c->nblocks * 32 * sizeof(uint32_t), c->stream));
         mfma_range_prep<N><<<(unsigned)((threads + 255) / 256), 256, 0, c->stream>>>(r);
     }
     if (c->p.flags & FRAC_FLAG_TIMING)
@@ -1620,9 +1623,11 @@ int launch_all(frac_ctx* c)
     const GenArgs g = gen_args(c, dtgt, tstride);
     if (P && c->virt) // the sampled form: one row per (domain, transform), fracenc_gen.hip
         gen_pool_build<<<(P + 255) / 256, 256, 0, c->stream>>>(g);
-    else if (P && !fused_pool)
-        pool_build<N><<<(P + 3) / 4, 256, 0, c->stream>>>(dsrc, c->d_sstride, c->d_doms.ptr, c->d_porig.ptr, P,
-                                                          c->d_pool.ptr, c->d_negsd2.ptr);
+    else if (P && !fused_pool) { // groups of min(n²/2, 64) lanes per pool position
+        const unsigned nblk = (unsigned)(((uint64_t)P * std::min(N * N / 2, 64) + 255) / 256);
+        pool_build<N><<<nblk, 256, 0, c->stream>>>(dsrc, c->d_sstride, c->d_doms.ptr, c->d_porig.ptr, P, c->d_pool.ptr,
+                                                   c->d_negsd2.ptr);
+    }
     const bool use_sea = c->engine == FRAC_ENGINE_SEA && !c->all_fallback;
     tr.mark("memsets + pool");
     if (use_mfma)
@@ -2012,6 +2017,15 @@ int frac_run(frac_ctx* c)
     if (!c)
         return FRAC_E_INVALID;
     FRAC_HIP(c, hipSetDevice(c->device));
+    {
+        // the work lists prepare() builds depend on the A/B knobs: a change re-prepares
+        int var = 0;
+        FRAC_TRY(mfma_variant(c, var));
+        const int knobs = var * 2 + (mfma_dft_enabled() ? 1 : 0);
+        if (knobs != c->prep_knobs)
+            c->dirty = true;
+        c->prep_knobs = knobs;
+    }
     if (c->dirty)
         FRAC_TRY(prepare(c));
     int rc;

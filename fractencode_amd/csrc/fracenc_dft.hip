@@ -579,7 +579,7 @@ __global__ void __launch_bounds__(64 * WAVES) search_dft(DftArgs d)
         {
             const uint32_t tb = wk.z + st * kTilesPerStage;
             if (!SKIPBAR || st < 2)
-                __syncthreads();
+                stage_barrier();
             if (st + 1 < nstage && (!SKIPDMA || st == 0))
                 stage_tiles<KS, 64 * WAVES>(lds1, a.dtiles, a.dconst, tb + kTilesPerStage, stage_nt(st + 1));
             for (uint32_t c0 = 0; c0 < stage_nt(st); c0 += 4)
@@ -590,7 +590,7 @@ __global__ void __launch_bounds__(64 * WAVES) search_dft(DftArgs d)
         if (st + 1 < nstage) {
             const uint32_t tb = wk.z + (st + 1) * kTilesPerStage;
             if (!SKIPBAR || st < 2)
-                __syncthreads();
+                stage_barrier();
             if (st + 2 < nstage && !SKIPDMA)
                 stage_tiles<KS, 64 * WAVES>(lds0, a.dtiles, a.dconst, tb + kTilesPerStage, stage_nt(st + 2));
             for (uint32_t c0 = 0; c0 < stage_nt(st + 1); c0 += 4)

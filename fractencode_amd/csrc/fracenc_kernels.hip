@@ -30,8 +30,9 @@ __device__ inline long long wave_sum_ll(long long v)
 }
 
 // ---------------------------------------------------------------------------
-// pool_build: one wave per domain pool position p (bucket order).  D4[i][j] is the
-// 2×2 sum at domain pixel (2j, 2i): SamplerBilinear::sample's integer sum
+// pool_build: one group of LPD = min(64, n²/2) lanes per domain pool position p (bucket
+// order), 64/LPD positions per wave; lane k of a group writes pool words k, k + LPD, ...
+// D4[i][j] is the 2×2 sum at domain pixel (2j, 2i): SamplerBilinear::sample's integer sum
 // (image/sampler.h:21-38) for the identity transform at range pixel (j, i).
 // ---------------------------------------------------------------------------
 template <int N>
@@ -40,32 +41,30 @@ __global__ void __launch_bounds__(256) pool_build(const uint8_t* __restrict__ sr
                                                   const uint32_t* __restrict__ porig, uint32_t P,
                                                   uint32_t* __restrict__ pool, int32_t* __restrict__ negsd2)
 {
-    constexpr int NN = N * N, K2 = NN / 2;
-    const uint32_t p = blockIdx.x * 4u + (threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    if (p >= P)
-        return;
-    const frac_grid_item d = doms[porig[p]];
+    constexpr int NN = N * N, K2 = NN / 2, LPD = K2 < 64 ? K2 : 64;
+    const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t p = gid / LPD;
+    const int k0 = (int)(gid % LPD);
     int sq = 0;
-    for (int q0 = 0; q0 < NN; q0 += 128) {
-        const int q = q0 + 2 * lane;
-        uint32_t packed = 0;
-        if (q < NN) {
+    if (p < P) {
+        const frac_grid_item d = doms[porig[p]];
+        for (int k = k0; k < K2; k += LPD) {
             int v[2];
 #pragma unroll
             for (int e = 0; e < 2; ++e) {
-                const int qi = q + e;
+                const int qi = 2 * k + e;
                 const uint32_t x = d.x + 2u * (qi % N), y = d.y + 2u * (qi / N);
                 const uint8_t* r0 = src + (size_t)y * sstride + x;
                 v[e] = (int)r0[0] + (int)r0[1] + (int)r0[sstride] + (int)r0[sstride + 1];
                 sq += v[e] * v[e];
             }
-            packed = (uint32_t)v[0] | ((uint32_t)v[1] << 16);
-            pool[(size_t)p * K2 + (q >> 1)] = packed;
+            pool[(size_t)p * K2 + k] = (uint32_t)v[0] | ((uint32_t)v[1] << 16);
         }
     }
-    sq = wave_sum_i(sq);
-    if (lane == 0)
+#pragma unroll
+    for (int o = LPD / 2; o > 0; o >>= 1)
+        sq += __shfl_xor(sq, o, 64);
+    if (p < P && k0 == 0)
         negsd2[p] = -sq;
 }
 

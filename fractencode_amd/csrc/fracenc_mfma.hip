@@ -130,6 +130,7 @@ __global__ void __launch_bounds__(256) mfma_range_prep(MfmaRangePrepArgs a)
     _Float16 v8[8];
     if (ri >= 0) {
         const frac_grid_item rg = a.ranges[ri];
+        int32_t part = 0; // this thread's share of rconst (transform 0 covers every pixel once)
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             const int k = 16 * (int)s + 8 * (int)h + j;
@@ -137,24 +138,21 @@ __global__ void __launch_bounds__(256) mfma_range_prep(MfmaRangePrepArgs a)
             if (k < NN) {
                 const int pix = inv_index<N>((int)t, k);
                 rv = a.tgt[(size_t)(rg.y + pix / N) * a.tstride + rg.x + (pix % N)];
+                part += 4080 * rv - 16 * rv * rv;
             }
             v8[j] = (_Float16)(128 - rv);
         }
-        if (t == 0 && s == 0 && h == 0) {
-            int64_t sr = 0, sr2 = 0;
-            for (int q = 0; q < NN; ++q) {
-                const int rv = a.tgt[(size_t)(rg.y + q / N) * a.tstride + rg.x + (q % N)];
-                sr += rv;
-                sr2 += rv * rv;
-            }
-            a.rconst[b * 32 + col] = mfma_range_const(NN, sr, sr2);
+        // rconst = −16Σr² + 4080Σr + const (mfma_range_const) mod 2^32: the transform-0 threads add
+        // their pixels' terms to the zeroed word, the first of them the constant
+        if (t == 0) {
+            if (s == 0 && h == 0)
+                part += (int32_t)mfma_range_const(NN, 0, 0);
+            atomicAdd(&a.rconst[b * 32 + col], (uint32_t)part);
         }
     } else {
 #pragma unroll
         for (int j = 0; j < 8; ++j)
             v8[j] = (_Float16)0.0f;
-        if (t == 0 && s == 0 && h == 0)
-            a.rconst[b * 32 + col] = 0;
     }
     a.rfrags[((size_t)(b * a.T + t) * KS + s) * 64 + lane] = __builtin_bit_cast(uint4, v8);
 }
@@ -187,6 +185,17 @@ __device__ inline void stage_tiles(uint4* dst, const uint4* __restrict__ dtiles,
         __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)src,
                                          (__attribute__((address_space(3))) void*)(dst + (i - lane)), 16, 0, 0);
     }
+}
+
+// The stage hand-off of every LDS-DMA search loop: this wave's own pieces have landed
+// (LDS-DMA is counted by vmcnt only), then the workgroup barrier covers the other waves'.
+// __syncthreads() alone is not enough: the compiler emits only lgkmcnt(0) before a barrier
+// whose preceding DMA it cannot match to a later ds_read (seen at the loop head of
+// search_dft: a stage could be read before all of its pieces had landed).
+__device__ inline void stage_barrier()
+{
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
 }
 
 template <int N, int T, bool PRIO = false>
@@ -363,7 +372,7 @@ __global__ void __launch_bounds__(256) search_mfma(MfmaSearchArgs a)
         // even stage: read lds0, prefetch stage st+1 into lds1
         {
             const uint32_t tb = wk.z + st * kTilesPerStage;
-            __syncthreads();
+            stage_barrier();
             if (st + 1 < nstage)
                 stage_tiles<KS>(buf1, a.dtiles, a.dconst, tb + kTilesPerStage, stage_nt(st + 1));
             uint32_t cm[T];
@@ -376,7 +385,7 @@ __global__ void __launch_bounds__(256) search_mfma(MfmaSearchArgs a)
         if (st + 1 < nstage) {
             // odd stage: read lds1, prefetch stage st+2 into lds0
             const uint32_t tb = wk.z + (st + 1) * kTilesPerStage;
-            __syncthreads();
+            stage_barrier();
             if (st + 2 < nstage)
                 stage_tiles<KS>(buf0, a.dtiles, a.dconst, tb + kTilesPerStage, stage_nt(st + 2));
             uint32_t cm[T];
@@ -463,12 +472,12 @@ __global__ void __launch_bounds__(64 * T) search_mfma16(MfmaSearchArgs a)
         stage_tiles<KS, 64 * T>(lds0, a.dtiles, a.dconst, wk.z, stage_nt(0));
     for (uint32_t st = 0; st < nstage; st += 2) {
         const uint32_t tb = wk.z + st * kTilesPerStage16;
-        __syncthreads();
+        stage_barrier();
         if (st + 1 < nstage)
             stage_tiles<KS, 64 * T>(lds1, a.dtiles, a.dconst, tb + kTilesPerStage16, stage_nt(st + 1));
         compute(lds0, stage_nt(st), tb);
         if (st + 1 < nstage) {
-            __syncthreads();
+            stage_barrier();
             if (st + 2 < nstage)
                 stage_tiles<KS, 64 * T>(lds0, a.dtiles, a.dconst, tb + 2 * kTilesPerStage16, stage_nt(st + 2));
             compute(lds1, stage_nt(st + 1), tb);

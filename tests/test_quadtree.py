@@ -62,3 +62,45 @@ def test_gpu_quadtree_matches_oracle(oracle, cls, split):
     np.testing.assert_array_equal(dec, wdec)
     from fractencode_amd.codec import psnr
     assert psnr(p, dec) > 25.0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cls,thr", [(True, 0.0), (True, 2.0), (False, 2.0)])
+def test_gpu_quadtree_stats_are_the_levels_stats(cls, thr):
+    # the quadtree's summed statistics (accumulated on the device level by level) equal the sum of
+    # the same levels searched one by one; the caller's `out` buffer receives the same items
+    p = plane("lenna_y")
+    split = 8.0
+    with F.Engine(0, 4, cls, thr) as e:
+        e.set_frame(p)
+        buf = np.empty((512 // 4) ** 2, dtype=F.ENCODE_ITEM)
+        items, st = e.encode_quadtree(16, 4, split, out=buf)
+        assert np.shares_memory(items, buf)
+        items2, st2 = e.encode_quadtree(16, 4, split)
+        np.testing.assert_array_equal(items, items2)
+        keys = ("rejected_mappings", "total_mappings", "hit_ranges", "fallback_ranges", "empty_ranges")
+        want = dict.fromkeys(keys, 0)
+        ranges = F.create_uniform_grid(512, 512, 16, 16)
+        leaves = []
+        for n in (16, 8, 4):
+            e.set_domains(F.create_uniform_grid(512, 512, 2 * n, n))
+            out, s = e.search(ranges)
+            for k in keys:
+                want[k] += s[k]
+            if n == 4:
+                leaves.append(out)
+                break
+            sp = out["distance"] > split
+            leaves.append(out[~sp])
+            par = ranges[sp]
+            h = n // 2
+            nxt = np.zeros(4 * len(par), dtype=F.GRID_ITEM)
+            for q, (ox, oy) in enumerate(((0, 0), (h, 0), (0, h), (h, h))):
+                nxt["x"][q::4], nxt["y"][q::4] = par["x"] + ox, par["y"] + oy
+            nxt["w"], nxt["h"], nxt["category"] = h, h, -1
+            ranges = nxt
+        assert st["hit_ranges"] > 0 or thr == 0.0
+        for k in keys:
+            assert st[k] == want[k], k
+            assert st2[k] == want[k], k
+        np.testing.assert_array_equal(items, np.concatenate(leaves))

@@ -165,16 +165,21 @@ def main():
 
     if want("c4q"):
         # C4 with the quadtree partition (16/8/4): the whole multi-level encode per frame
+        import torch
+
         frame = value_noise(4096, 4096, 1234)[:2048, :2048].copy()
+        # the leaves land in pinned host memory owned by the caller (as a C++ caller would pass its buffer)
+        cap = (2048 // 4) ** 2
+        leaves = torch.empty(cap * F.ENCODE_ITEM.itemsize, dtype=torch.uint8).pin_memory().numpy().view(F.ENCODE_ITEM)
         res = {}
         for split in (0.05, 0.5):
             with F.Engine(0, 4, True, timing=True) as e:
                 e.set_frame(frame)
                 for _ in range(max(2, args.warmup)):  # the first calls allocate the per-level buffers
-                    e.encode_quadtree(16, 4, split)
+                    e.encode_quadtree(16, 4, split, out=leaves)
                 t0 = time.perf_counter()
                 for _ in range(args.steps):
-                    items, st = e.encode_quadtree(16, 4, split)
+                    items, st = e.encode_quadtree(16, 4, split, out=leaves)
                 sec = (time.perf_counter() - t0) / args.steps
             sizes, counts = np.unique(items["w"], return_counts=True)
             res[str(split)] = {"ms_per_frame": round(sec * 1e3, 3), "items": int(len(items)),
