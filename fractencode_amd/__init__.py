@@ -420,13 +420,15 @@ class Engine:
         return lib().frac_device_results(self._ctx) or 0
 
 
-def encode(plane: np.ndarray, range_size: int = 8, domain_size: int | None = None, transforms: int = 4,
-           use_classifier: bool = False, rms_threshold: float = 0.0, s_max: float = -1.0, device: int = 0,
+def encode(plane: np.ndarray, range_size: int = 4, domain_size: int = 16, transforms: int = 4,
+           use_classifier: bool = True, rms_threshold: float = 0.0, s_max: float = -1.0, device: int = 0,
            engine: int = ENGINE_AUTO):
-    """Encoder2's search half for one plane, with grids built like main.cpp:142-162."""
+    """Encoder2's search half for one plane, with grids built like main.cpp:142-162 and the CLI's
+    defaults (encode/encode_parameters.h:6-13): 16×16 domains at offset 16 / latticeSize 2, 4×4
+    ranges, the classifier on, rms threshold 0, sMax −1."""
     plane = np.ascontiguousarray(plane, dtype=np.uint8)
     H, W = plane.shape
-    dsz = domain_size or 2 * range_size  # the reference's default pair is 16 -> 4 (encode_parameters.h:6-7)
+    dsz = domain_size
     doms = create_uniform_grid(W, H, dsz, dsz // 2)
     rngs = create_uniform_grid(W, H, range_size, range_size)
     if use_classifier:

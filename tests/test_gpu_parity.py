@@ -443,3 +443,12 @@ def test_default_cli_geometry_4096(engine):
     sel = np.arange(0, len(rngs), 8191)
     want, _, _ = O.estimate(p, O.uniform_grid(4096, 4096, 16, 8), O.uniform_grid(4096, 4096, 4, 4)[sel], threads=16)
     assert_same(out[sel], {k: want[k] for k in FIELDS}, "16to4 4096 sample")
+
+
+def test_encode_defaults_are_the_reference_cli_defaults():
+    # fractencode_amd.encode() with no options = the CLI's encode_parameters_t (16 -> 4, offset 8,
+    # classifier on, threshold 0, sMax -1): the reference's own run of that configuration
+    rec, meta = golden("lenna_16to4_cls")
+    out, st = F.encode(plane(meta["plane"]))
+    assert_same(out, rec, "encode() defaults")
+    assert st["rejected_mappings"] == meta["rejected"]
