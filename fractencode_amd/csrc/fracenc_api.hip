@@ -948,7 +948,8 @@ void launch_search_mfma_v(frac_ctx* c, const MfmaSearchArgs& a)
 // value a product build accepts gives identical (exact) records; the ablations, which give
 // wrong results by design, are accepted — and compiled — only by a -DFRAC_TUNING build.
 // Any other value fails the run (FRAC_E_INVALID), so a stray variable cannot corrupt records.
-//   search_mfma: 0..7 schedule bits, 32 s_setprio, 64 late constants, 96, 98; ablations 8, 16
+//   search_mfma: 0..7 schedule bits, 32 s_setprio, 64 late constants, 96, 98, 128 / 130 (default)
+//                the minimum over transforms first; ablations 8, 16
 //   search_dft:  default 8-wave exact form; 1 / 3 four-wave exact / guarded; 5 eight-tile
 //                stages; 6 pairwise-tree row maximum; ablations 9, 17, 41, 73, 105, 65 (four-wave) and 201..207 (eight-wave)
 inline int mfma_variant(frac_ctx* c, int& var)
@@ -959,7 +960,7 @@ inline int mfma_variant(frac_ctx* c, int& var)
         return FRAC_OK;
     char* end = nullptr;
     const long x = strtol(v, &end, 10);
-    static const int exact[] = {0, 1, 2, 3, 4, 5, 6, 7, 32, 64, 96, 98};
+    static const int exact[] = {0, 1, 2, 3, 4, 5, 6, 7, 32, 64, 96, 98, 128, 130};
     static const int ablation[] = {8, 9, 16, 17, 41, 65, 73, 105, 201, 202, 203, 204, 205, 206, 207};
     bool ok = end && *end == 0;
     bool known = false;
@@ -984,6 +985,7 @@ int launch_search_mfma(frac_ctx* c, const MfmaSearchArgs& a)
     switch (var) {
     case 0: launch_search_mfma_v<N, T, 0>(c, a); break;
     case 1: launch_search_mfma_v<N, T, 1>(c, a); break;
+    case 2: launch_search_mfma_v<N, T, 2>(c, a); break;
     case 3: launch_search_mfma_v<N, T, 3>(c, a); break;
     case 4: launch_search_mfma_v<N, T, 4>(c, a); break;
     case 5: launch_search_mfma_v<N, T, 5>(c, a); break;
@@ -993,6 +995,8 @@ int launch_search_mfma(frac_ctx* c, const MfmaSearchArgs& a)
     case 64: launch_search_mfma_v<N, T, 64>(c, a); break; // late epilogue-constant reads
     case 96: launch_search_mfma_v<N, T, 96>(c, a); break;
     case 98: launch_search_mfma_v<N, T, 98>(c, a); break;
+    case 128: launch_search_mfma_v<N, T, 128>(c, a); break; // minimum over transforms first
+    case 130: launch_search_mfma_v<N, T, 130>(c, a); break;
 #ifdef FRAC_TUNING
     case 8: launch_search_mfma_v<N, T, 8>(c, a); break;   // ablation: 1-value epilogue
     case 16: launch_search_mfma_v<N, T, 16>(c, a); break; // ablation: no MFMA
@@ -1259,6 +1263,9 @@ int launch_mfma(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride)
         v.T = T;
         v.hitH = c->hitH;
         v.best_key = c->d_best_key.ptr;
+        int var = 0;
+        FRAC_TRY(mfma_variant(c, var));
+        v.merged = (N != 16 && T > 1 && (var & 128)) ? 1 : 0; // search_mfma's entries merged over t
         resolve_mfma<N><<<(nr + 3) / 4, 256, 0, c->stream>>>(v);
     }
     return FRAC_OK;

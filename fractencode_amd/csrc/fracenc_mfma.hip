@@ -26,7 +26,7 @@ typedef float floatx16_t __attribute__((ext_vector_type(16)));
 
 constexpr uint32_t kMfmaPadConst = 0x70000000u; // e' of padding domains: v ≈ 1.9e9, never wins
 constexpr int kTilesPerStage = 4; // domain tiles per LDS stage (double-buffered)
-constexpr int kDefaultMfmaVariant = 2; // two v_min3 chains (A/B: tools/ab_mfma.py)
+constexpr int kDefaultMfmaVariant = 130; // the minimum over transforms first (128), two v_min3 chains (2)
 
 template <int N>
 struct MfmaGeom {
@@ -301,6 +301,32 @@ __device__ inline void compute_stage(const uint4* __restrict__ la, uint32_t nt, 
                     acc[i] = __builtin_bit_cast(float, (uint32_t)__builtin_bit_cast(uint4, af[i & (KS - 1)]).x + i + t);
                 cm[t] = epilogue_min<false>(acc, e, cm[t]);
             }
+        } else if constexpr ((VAR & 128) != 0 && T > 1) {
+            // the minimum over the T transforms first, on the accumulator bits (monotone in −Z,
+            // one u32 min per candidate: v_min3 over pairs of transforms), then one v_lshl_add per
+            // row: T/2 + 1.5 VALU per row instead of 1.5·T.  The lane's entry keeps the merged
+            // minimum (slot t = 0) and resolve_mfma evaluates every transform of a matching chunk.
+            uint32_t mb[16];
+            {
+                const floatx16_t a0 = mfma_tile<N, T>(af, bf[0], cinit);
+                const floatx16_t a1 = mfma_tile<N, T>(af, bf[1], cinit);
+#pragma unroll
+                for (int i = 0; i < 16; ++i)
+                    mb[i] = min(__float_as_uint(a0[i]), __float_as_uint(a1[i]));
+            }
+#pragma unroll
+            for (int t = 2; t < T; t += 2) {
+                const floatx16_t x = mfma_tile<N, T>(af, bf[t], cinit);
+                const floatx16_t y = mfma_tile<N, T>(af, bf[t + 1], cinit);
+#pragma unroll
+                for (int i = 0; i < 16; ++i)
+                    mb[i] = min(min(mb[i], __float_as_uint(x[i])), __float_as_uint(y[i]));
+            }
+            uint32_t m = cm[0];
+#pragma unroll
+            for (int i = 0; i < 16; i += 2)
+                m = min(min(m, (mb[i] << 3) + e[i]), (mb[i + 1] << 3) + e[i + 1]);
+            cm[0] = m;
         } else {
 #pragma unroll
             for (int t = 0; t < T; ++t)
@@ -314,6 +340,8 @@ __device__ inline void compute_stage(const uint4* __restrict__ la, uint32_t nt, 
 //   2: two independent v_min3 chains in the epilogue
 //   4: the two LDS stage buffers are distinct __shared__ objects (the LDS-DMA into one
 //      provably does not alias ds_reads of the other, so no vmcnt(0) before each tile)
+//   128: the minimum over the transforms on the accumulator bits first (entries merged over
+//      t; resolve_mfma with MfmaResolveArgs::merged evaluates every transform of a match)
 template <int N, int T, bool HITS, int VAR>
 __global__ void __launch_bounds__(256) search_mfma(MfmaSearchArgs a)
 {
@@ -516,6 +544,7 @@ struct MfmaResolveArgs {
     const uint32_t* tpool;      // [ntiles*32][32] D4 pairs in orbit order (dft_domain_build)
     const uint32_t* rorb;       // [nslots][32] range pixel pairs in orbit order (dft_range_prep)
     uint4* rstat = nullptr;     // [nr] the winner's {X_t, ΣD4 | Σr << 16, ΣD4², Σr²} (fit_rstat)
+    int merged = 0;             // resolve_mfma: entries hold the minimum over every transform (search_mfma VAR 128)
 };
 
 __device__ inline int fwd_rt(const Aff& a, int N, int q)
@@ -610,55 +639,61 @@ __global__ void __launch_bounds__(256) resolve_mfma(MfmaResolveArgs a)
             const uint32_t ctile = (uint32_t)__builtin_amdgcn_readlane((int)enl.y, src);
             if (ctile > best_tile)
                 continue;
-            if ((int)t != ct)
-                build_copy((int)t);
             const int row = (i & 3) + 8 * (i >> 2) + 4 * (int)h;
-            // the entry names the first tile of the chunk that attained the minimum: scan the
-            // chunk's tiles in order; the first matching row is the earliest domain
-            for (uint32_t tile = ctile; tile < min(ctile + (uint32_t)kTilesPerStage, a.ntiles); ++tile) {
-                const int p = a.tile_pos[tile * 32 + row];
-                uint32_t d[WPL];
-                if (p >= 0 && g * WPL < K2) {
-                    const uint32_t* dp = a.pool + (size_t)p * K2 + g * WPL;
-                    if constexpr (WPL % 4 == 0) {
+            // merged entries: every transform of the chunk; per transform the first matching row in
+            // tile order is its least key, and no tile after the best key's can win or tie
+            const uint32_t tlo = a.merged ? 0u : t, thi = a.merged ? a.T : t + 1u;
+            for (uint32_t tt = tlo; tt < thi; ++tt) {
+                if ((int)tt != ct)
+                    build_copy((int)tt);
+                // the entry names the first tile of the chunk that attained the minimum: scan the
+                // chunk's tiles in order; the first matching row is the earliest domain
+                for (uint32_t tile = ctile; tile < min(ctile + (uint32_t)kTilesPerStage, a.ntiles) && tile <= best_tile;
+                     ++tile) {
+                    const int p = a.tile_pos[tile * 32 + row];
+                    uint32_t d[WPL];
+                    if (p >= 0 && g * WPL < K2) {
+                        const uint32_t* dp = a.pool + (size_t)p * K2 + g * WPL;
+                        if constexpr (WPL % 4 == 0) {
 #pragma unroll
-                        for (int w = 0; w < WPL; w += 4) {
-                            const uint4 v = *reinterpret_cast<const uint4*>(dp + w);
-                            d[w] = v.x;
-                            d[w + 1] = v.y;
-                            d[w + 2] = v.z;
-                            d[w + 3] = v.w;
+                            for (int w = 0; w < WPL; w += 4) {
+                                const uint4 v = *reinterpret_cast<const uint4*>(dp + w);
+                                d[w] = v.x;
+                                d[w + 1] = v.y;
+                                d[w + 2] = v.z;
+                                d[w + 3] = v.w;
+                            }
+                        } else {
+#pragma unroll
+                            for (int w = 0; w < WPL; ++w)
+                                d[w] = dp[w];
                         }
                     } else {
 #pragma unroll
                         for (int w = 0; w < WPL; ++w)
-                            d[w] = dp[w];
+                            d[w] = 0u;
                     }
-                } else {
+                    uint32_t xu = 0;
 #pragma unroll
                     for (int w = 0; w < WPL; ++w)
-                        d[w] = 0u;
-                }
-                uint32_t xu = 0;
-#pragma unroll
-                for (int w = 0; w < WPL; ++w)
-                    xu = __builtin_amdgcn_udot2(__builtin_bit_cast(ushort2_t, cp[w]), __builtin_bit_cast(ushort2_t, d[w]),
-                                                xu, false);
-                const int64_t X = (int64_t)quad_sum(xu);
-                const int64_t s16 = p >= 0 ? 16 * sr2 - 8 * X - (int64_t)a.negsd2[p] : 0;
-                const bool ok = p >= 0 && g == 0 && (hit ? (s16 <= a.hitH) : (s16 == target));
-                const unsigned long long mask = __ballot(ok);
-                if (mask) {
-                    const int first = __ffsll((long long)mask) - 1; // lowest lane = lowest row of the half
-                    const int64_t s16f = __shfl(s16, first, 64);
-                    const int pf = __shfl(p, first, 64);
-                    const unsigned long long k =
-                        hit ? key_hit((uint32_t)pf, t) : key_miss((uint64_t)s16f, (uint32_t)pf, a.T - 1 - t);
-                    if (k < bestk) {
-                        bestk = k;
-                        best_tile = tile;
+                        xu = __builtin_amdgcn_udot2(__builtin_bit_cast(ushort2_t, cp[w]),
+                                                    __builtin_bit_cast(ushort2_t, d[w]), xu, false);
+                    const int64_t X = (int64_t)quad_sum(xu);
+                    const int64_t s16 = p >= 0 ? 16 * sr2 - 8 * X - (int64_t)a.negsd2[p] : 0;
+                    const bool ok = p >= 0 && g == 0 && (hit ? (s16 <= a.hitH) : (s16 == target));
+                    const unsigned long long mask = __ballot(ok);
+                    if (mask) {
+                        const int first = __ffsll((long long)mask) - 1; // lowest lane = lowest row of the half
+                        const int64_t s16f = __shfl(s16, first, 64);
+                        const int pf = __shfl(p, first, 64);
+                        const unsigned long long k =
+                            hit ? key_hit((uint32_t)pf, tt) : key_miss((uint64_t)s16f, (uint32_t)pf, a.T - 1 - tt);
+                        if (k < bestk) {
+                            bestk = k;
+                            best_tile = tile;
+                        }
+                        break;
                     }
-                    break;
                 }
             }
         }

@@ -452,3 +452,28 @@ def test_encode_defaults_are_the_reference_cli_defaults():
     out, st = F.encode(plane(meta["plane"]))
     assert_same(out, rec, "encode() defaults")
     assert st["rejected_mappings"] == meta["rejected"]
+
+
+PRODUCT_VARIANTS = ("0", "1", "2", "3", "4", "5", "6", "7", "32", "64", "96", "98", "128", "130")
+
+
+@pytest.mark.parametrize("n,T,dft", [(8, 4, "0"), (4, 4, "0"), (8, 8, "0"), (8, 4, "1")])
+def test_every_product_variant_gives_the_same_records(monkeypatch, n, T, dft):
+    # FRAC_MFMA_VARIANT is an A/B knob: every value a product build accepts must give the records of
+    # the exhaustive VALU engine (the launch switch and the resolve's entry layout must agree)
+    from fractencode_amd.synth import value_noise
+    S = 256
+    p = value_noise(S, S, 77)
+    doms, rngs = F.create_uniform_grid(S, S, 2 * n, n), F.create_uniform_grid(S, S, n, n)
+    with F.Engine(0, T, False, 0.0, -1.0, F.ENGINE_VALU) as e:
+        e.set_frame(p)
+        e.set_domains(doms)
+        want, _ = e.search(rngs)
+    monkeypatch.setenv("FRAC_MFMA_DFT", dft)
+    for v in PRODUCT_VARIANTS:
+        monkeypatch.setenv("FRAC_MFMA_VARIANT", v)
+        with F.Engine(0, T, False, 0.0, -1.0, F.ENGINE_MFMA) as e:
+            e.set_frame(p)
+            e.set_domains(doms)
+            out, _ = e.search(rngs)
+        assert out.tobytes() == want.tobytes(), f"variant {v} (n={n}, T={T}, dft={dft})"
