@@ -271,6 +271,7 @@ struct frac_ctx {
     std::vector<hipEvent_t> hist;
     uint64_t hist_runs = 0, hist_read = 0;
     int prep_knobs = -1; // FRAC_MFMA_VARIANT / FRAC_MFMA_DFT as of the last prepare (frac_run)
+    int mfma_var_ran = 0; // the schedule variant search_mfma last ran with (its entry layout)
     bool ran = false;
     uint32_t engine_ran = FRAC_ENGINE_VALU;
     uint32_t form_ran = FRAC_FORM_DOT2;
@@ -936,6 +937,7 @@ int prepare(frac_ctx* c)
 template <int N, int T, int VAR>
 void launch_search_mfma_v(frac_ctx* c, const MfmaSearchArgs& a)
 {
+    c->mfma_var_ran = VAR; // the resolve reads the entry layout this launch writes (VAR 128: merged over t)
     // H = 0 (the default threshold): a hit is S16 = 0, the smallest possible error, so
     // the plain first-minimum search already finds the first hit
     if (c->hitH > 0)
@@ -951,7 +953,8 @@ void launch_search_mfma_v(frac_ctx* c, const MfmaSearchArgs& a)
 //   search_mfma: 0..7 schedule bits, 32 s_setprio, 64 late constants, 96, 98, 128 / 130 (default)
 //                the minimum over transforms first; ablations 8, 16
 //   search_dft:  default 8-wave exact form; 1 / 3 four-wave exact / guarded; 5 eight-tile
-//                stages; 6 pairwise-tree row maximum; ablations 9, 17, 41, 73, 105, 65 (four-wave) and 201..207 (eight-wave)
+//                stages; 6 pairwise-tree row maximum; 12 two range blocks per wave (search_dft2);
+//                ablations 9, 17, 41, 73, 105, 65 (four-wave) and 201..207 (eight-wave)
 inline int mfma_variant(frac_ctx* c, int& var)
 {
     const char* v = getenv("FRAC_MFMA_VARIANT");
@@ -960,7 +963,7 @@ inline int mfma_variant(frac_ctx* c, int& var)
         return FRAC_OK;
     char* end = nullptr;
     const long x = strtol(v, &end, 10);
-    static const int exact[] = {0, 1, 2, 3, 4, 5, 6, 7, 32, 64, 96, 98, 128, 130};
+    static const int exact[] = {0, 1, 2, 3, 4, 5, 6, 7, 12, 32, 64, 96, 98, 128, 130};
     static const int ablation[] = {8, 9, 16, 17, 41, 65, 73, 105, 201, 202, 203, 204, 205, 206, 207};
     bool ok = end && *end == 0;
     bool known = false;
@@ -1099,6 +1102,12 @@ inline int launch_dft(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride)
                 search_dft<true, 1 | kDftChain, W8, 8><<<nwg, 64 * W8, 0, c->stream>>>(da);
             else
                 search_dft<false, 1 | kDftChain, W8, 8><<<nwg, 64 * W8, 0, c->stream>>>(da);
+        } else if (!four && var == 12) { // two range blocks per wave (4-wave workgroups, the 8-block lists)
+            static_assert(kDftBlocksPerWG == 8, "search_dft2 covers 8 blocks per workgroup");
+            if (hits)
+                search_dft2<true><<<nwg, 256, 0, c->stream>>>(da);
+            else
+                search_dft2<false><<<nwg, 256, 0, c->stream>>>(da);
         } else if (!four && var == 6) { // the pairwise-tree row maximum (round 1's default, A/B)
             if (hits)
                 search_dft<true, 1, W8><<<nwg, 64 * W8, 0, c->stream>>>(da);
@@ -1263,9 +1272,7 @@ int launch_mfma(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride)
         v.T = T;
         v.hitH = c->hitH;
         v.best_key = c->d_best_key.ptr;
-        int var = 0;
-        FRAC_TRY(mfma_variant(c, var));
-        v.merged = (N != 16 && T > 1 && (var & 128)) ? 1 : 0; // search_mfma's entries merged over t
+        v.merged = (N != 16 && T > 1 && (c->mfma_var_ran & 128)) ? 1 : 0; // search_mfma's entries merged over t
         resolve_mfma<N><<<(nr + 3) / 4, 256, 0, c->stream>>>(v);
     }
     return FRAC_OK;

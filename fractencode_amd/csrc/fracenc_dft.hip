@@ -604,6 +604,98 @@ __global__ void __launch_bounds__(64 * WAVES) search_dft(DftArgs d)
 }
 
 // ---------------------------------------------------------------------------
+// search_dft2<HITS>: the exact form with two range blocks per wave (4-wave workgroups, 8 blocks
+// per workgroup, the entry layout of search_dft<…, 8>): a tile's A fragments and −Σb² row
+// constants are read from LDS once for both blocks, half the LDS bytes per (block, tile) pair.
+// 3 waves per SIMD (3 workgroups per CU) instead of 4.
+// ---------------------------------------------------------------------------
+template <bool HITS>
+__global__ void __launch_bounds__(256, 3) search_dft2(DftArgs d)
+{
+    const MfmaSearchArgs& a = d.m;
+    constexpr int KS = 4, VAR = 1 | kDftChain;
+    constexpr int STAGE = kTilesPerStage * KS * 64 + kTilesPerStage * 8;
+    __shared__ uint4 lds0[STAGE];
+    __shared__ uint4 lds1[STAGE];
+    const uint4 wk = a.work[blockIdx.x];
+    const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    bool act[2];
+    half8_t bf[2][kDftRangeFrags];
+    float hl[2] = {0.0f, 0.0f}, best[2];
+    uint32_t btile[2] = {0u, 0u};
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const uint32_t b = 2 * wv + k;
+        act[k] = b < wk.y;
+        const uint32_t blk = wk.x + (act[k] ? b : 0u);
+#pragma unroll
+        for (int f = 0; f < kDftRangeFrags; ++f)
+            bf[k][f] = __builtin_bit_cast(half8_t, a.rfrags[((size_t)blk * kDftRangeFrags + f) * 64 + lane]);
+        if constexpr (HITS)
+            hl[k] = (float)((int32_t)a.rconst[blk * 32 + (lane & 31u)] - (int32_t)a.hitH);
+        best[k] = -__builtin_inff();
+    }
+    const uint32_t h = lane >> 5;
+    auto compute = [&](const uint4* la, uint32_t nt, uint32_t tb) {
+        const uint4* lc = la + nt * 4u * 64u;
+        float cm[2] = {-__builtin_inff(), -__builtin_inff()};
+        for (uint32_t q = 0; q < nt; ++q) {
+            half8_t af[4];
+#pragma unroll
+            for (int s = 0; s < 4; ++s)
+                af[s] = __builtin_bit_cast(half8_t, la[(q * 4 + s) * 64 + lane]);
+            floatx16_t ny;
+#pragma unroll
+            for (int c4 = 0; c4 < 4; ++c4) {
+                const uint4 v = lc[q * 8 + h * 4 + c4];
+                ny[4 * c4 + 0] = __uint_as_float(v.x);
+                ny[4 * c4 + 1] = __uint_as_float(v.y);
+                ny[4 * c4 + 2] = __uint_as_float(v.z);
+                ny[4 * c4 + 3] = __uint_as_float(v.w);
+            }
+#pragma unroll
+            for (int k = 0; k < 2; ++k)
+                cm[k] = dft_tile_max<VAR>(af, bf[k], ny, false, cm[k]);
+        }
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            float c = cm[k];
+            if constexpr (HITS) // any hit in the chunk: the first-hit chunk wins
+                c = c >= hl[k] ? __builtin_inff() : c;
+            if (c > best[k]) {
+                best[k] = c;
+                btile[k] = tb;
+            }
+        }
+    };
+    const uint32_t nstage = (wk.w - wk.z + kTilesPerStage - 1) / kTilesPerStage;
+    auto stage_nt = [&](uint32_t st) { return min((uint32_t)kTilesPerStage, wk.w - (wk.z + st * kTilesPerStage)); };
+    if (nstage)
+        stage_tiles<KS, 256>(lds0, a.dtiles, a.dconst, wk.z, stage_nt(0));
+    for (uint32_t st = 0; st < nstage; st += 2) {
+        {
+            const uint32_t tb = wk.z + st * kTilesPerStage;
+            stage_barrier();
+            if (st + 1 < nstage)
+                stage_tiles<KS, 256>(lds1, a.dtiles, a.dconst, tb + kTilesPerStage, stage_nt(st + 1));
+            compute(lds0, stage_nt(st), tb);
+        }
+        if (st + 1 < nstage) {
+            const uint32_t tb = wk.z + (st + 1) * kTilesPerStage;
+            stage_barrier();
+            if (st + 2 < nstage)
+                stage_tiles<KS, 256>(lds0, a.dtiles, a.dconst, tb + kTilesPerStage, stage_nt(st + 2));
+            compute(lds1, stage_nt(st + 1), tb);
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+        if (act[k])
+            a.entries[(size_t)(blockIdx.x * kDftBlocksPerWG + 2 * wv + k) * 64 + lane] =
+                make_uint2(__float_as_uint(best[k]), btile[k]);
+}
+
+// ---------------------------------------------------------------------------
 // resolve_dft: one wave per range (resolve_mfma's lane map: tile row i = l>>2, pixel
 // slice g = l&3).  The greatest entry y over the block's splits and lane halves gives the
 // target error S16 = 16Σa² − y (exact regime) or flags the range for the fp32 fallback;
