@@ -476,6 +476,8 @@ inline bool mfma_dft_enabled();
 // the Fourier search variants that run 4-wave workgroups (and read m_work): 1, 3 and the odd
 // ablations below 200; every other variant runs 8-wave workgroups on m8_work
 inline bool dft_four_wave(int var) { return var == 1 || var == 3 || (var >= 9 && var < 200 && (var & 1)); }
+// the Fourier form's domain/range fragment layout: 4 (8 MFMA per tile pair), 5 (kDft5, variant 20)
+inline int dft_form(int var) { return var == 20 ? 5 : 4; }
 
 int prepare(frac_ctx* c)
 {
@@ -963,7 +965,7 @@ inline int mfma_variant(frac_ctx* c, int& var)
         return FRAC_OK;
     char* end = nullptr;
     const long x = strtol(v, &end, 10);
-    static const int exact[] = {0, 1, 2, 3, 4, 5, 6, 7, 12, 32, 64, 96, 98, 128, 130};
+    static const int exact[] = {0, 1, 2, 3, 4, 5, 6, 7, 12, 20, 32, 64, 96, 98, 128, 130};
     static const int ablation[] = {8, 9, 16, 17, 41, 65, 73, 105, 201, 202, 203, 204, 205, 206, 207};
     bool ok = end && *end == 0;
     bool known = false;
@@ -1031,6 +1033,17 @@ inline int launch_dft(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride)
     FRAC_HIP(c, c->d_dft_tguard.ensure(std::max<size_t>(c->ntiles, 1)));
     FRAC_HIP(c, c->d_dft_tpool.ensure(std::max<size_t>((size_t)c->ntiles * 32 * 32, 1)));
     FRAC_HIP(c, c->d_dft_rguard.ensure(std::max<size_t>(c->nblocks, 1)));
+    // FRAC_MFMA_VARIANT for this path (A/B knob): default = exact form in 8-wave workgroups
+    // with the v_max3-chain row maximum; 20 = the five-MFMA form (kDft5) in the same
+    // workgroups; 6 = the pairwise-tree row maximum; 5 = 8-tile stages; 12 = two range blocks
+    // per wave; 1 = exact form in 4-wave workgroups, 3 = guarded fast path (4 waves), odd
+    // values ≥ 9 = ablations of variant 1 (tuning only: wrong results)
+    int var = 0;
+    FRAC_TRY(mfma_variant(c, var));
+    const int form = dft_form(var);
+    const bool f5 = form == 5; // five domain fragments per tile
+    FRAC_HIP(c, c->d_m_dtiles.ensure(std::max<size_t>((size_t)c->ntiles * (f5 ? 5 : 4) * 64, 1)));
+    d.dtiles = c->d_m_dtiles.ptr;
     DftDomainBuildArgs b;
     b.src = c->d_src.ptr;
     b.sstride = c->d_sstride;
@@ -1039,8 +1052,12 @@ inline int launch_dft(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride)
     b.pool = c->d_pool.ptr;
     b.negsd2 = c->d_negsd2.ptr;
     b.tpool = c->d_dft_tpool.ptr;
-    if (c->ntiles)
-        dft_domain_build<false><<<(c->ntiles * 32 + 255) / 256, 256, 0, c->stream>>>(d, b, c->d_dft_tguard.ptr);
+    if (c->ntiles) {
+        if (f5)
+            dft_domain_build<false, true><<<(c->ntiles * 32 + 255) / 256, 256, 0, c->stream>>>(d, b, c->d_dft_tguard.ptr);
+        else
+            dft_domain_build<false><<<(c->ntiles * 32 + 255) / 256, 256, 0, c->stream>>>(d, b, c->d_dft_tguard.ptr);
+    }
     MfmaRangePrepArgs r;
     r.tgt = dtgt;
     r.tstride = tstride;
@@ -1052,22 +1069,21 @@ inline int launch_dft(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride)
     r.rconst = c->d_m_rconst.ptr;
     FRAC_HIP(c, c->d_dft_rorb.ensure(std::max<size_t>((size_t)r.nblocks * 32 * 32, 1)));
     r.rorb = c->d_dft_rorb.ptr;
-    if (c->nblocks)
-        dft_range_prep<<<(c->nblocks * 32 + 255) / 256, 256, 0, c->stream>>>(r, c->d_dft_rguard.ptr);
+    if (c->nblocks) {
+        const unsigned g = (c->nblocks * 32 + 255) / 256;
+        if (form == 5)
+            dft_range_prep<5><<<g, 256, 0, c->stream>>>(r, c->d_dft_rguard.ptr);
+        else
+            dft_range_prep<4><<<g, 256, 0, c->stream>>>(r, c->d_dft_rguard.ptr);
+    }
     if (c->p.flags & FRAC_FLAG_TIMING)
         FRAC_TRY(mark_event(c, 1));
-    // FRAC_MFMA_VARIANT for this path (A/B knob): default = exact form in 8-wave workgroups
-    // with the v_max3-chain row maximum; 6 = the same with a pairwise-tree row maximum; 5 =
-    // 8-tile stages; 1 = exact form in 4-wave workgroups, 3 = guarded fast path (4 waves), odd values ≥ 9 =
-    // ablations of variant 1 (tuning only: wrong results)
-    int var = 0;
-    FRAC_TRY(mfma_variant(c, var));
     const bool four = dft_four_wave(var);
     const std::vector<uint4>& work = four ? c->m_work : c->m8_work;
     c->form_ran = FRAC_FORM_FOURIER;
     c->flops_ran = 0;
-    for (const uint4& w : work) // 8 MFMA 32x32x16 (32768 flops each) per (range block, domain tile)
-        c->flops_ran += (uint64_t)w.y * (w.w - w.z) * 8ull * 32768ull;
+    for (const uint4& w : work) // 8 (five-MFMA form: 5) MFMA 32x32x16 (32768 flops each) per (block, tile)
+        c->flops_ran += (uint64_t)w.y * (w.w - w.z) * (f5 ? 5ull : 8ull) * 32768ull;
     if (!work.empty()) {
         MfmaSearchArgs a;
         a.dtiles = c->d_m_dtiles.ptr;
@@ -1097,6 +1113,11 @@ inline int launch_dft(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride)
             default: search_dft<false, 65, W8><<<nwg, 64 * W8, 0, c->stream>>>(da); break;  // full, no DMA/bar
             }
 #endif
+        } else if (form == 5) { // the five-MFMA form
+            if (hits)
+                search_dft<true, 1 | kDftChain | kDft5, W8><<<nwg, 64 * W8, 0, c->stream>>>(da);
+            else
+                search_dft<false, 1 | kDftChain | kDft5, W8><<<nwg, 64 * W8, 0, c->stream>>>(da);
         } else if (!four && var == 5) { // 8-tile LDS stages
             if (hits)
                 search_dft<true, 1 | kDftChain, W8, 8><<<nwg, 64 * W8, 0, c->stream>>>(da);
@@ -1344,7 +1365,7 @@ int launch_tp(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool timing)
         r.rconst = c->d_m_rconst.ptr;
         FRAC_HIP(c, c->d_dft_rorb.ensure(std::max<size_t>((size_t)r.nblocks * 32 * 32, 1)));
         r.rorb = c->d_dft_rorb.ptr;
-        dft_range_prep<<<(nbk * 32 + 255) / 256, 256, 0, c->stream>>>(r, c->d_dft_rguard.ptr);
+        dft_range_prep<4><<<(nbk * 32 + 255) / 256, 256, 0, c->stream>>>(r, c->d_dft_rguard.ptr);
     }
     if (timing)
         FRAC_TRY(mark_event(c, 1));

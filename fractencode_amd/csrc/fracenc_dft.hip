@@ -101,6 +101,30 @@ constexpr Orbits4<8> kOrb8 = make_orbits4<8>();
 constexpr float kDftPadY = -1.0e30f; // −Σb² of padding rows: y ≈ −1e30 never wins
 constexpr int kDftRangeFrags = 7;     // s, u, 4s, 4u, α, β, −α
 
+// VAR bit of search_dft: the five-MFMA form (DC / Nyquist bins + a three-product complex bin).
+// The length-4 DFT of the per-orbit correlation has two real bins and one complex bin, so with
+// P = Σ(s_a + u_a)(s_b + u_b) = U + U' and M = Σ(s_a − u_a)(s_b − u_b) = U − U' (one K = 16
+// GEMM each) and the complex bin Pr + iPi = Σ(α + iβ)(γ − iδ) by Gauss's three products
+//   k1 = Σγ(α + β),  Pr = k1 + Σ(γ − δ)(−β),  Pi = k1 + Σ(−δ − γ)α
+// (the last two accumulate onto k1 inside the MFMA), a tile pair costs 5 MFMA 32x32x16
+// instead of 8.  The range operands of the complex bin are doubled so that
+//   y = fma(max(P + M + |2Pr|, P − M + |2Pi|), 2, −Σb²)   (= 4·max(U + |Pr|, U' + |Pi|) − Σb²).
+// Exactness (a ∈ [−128, 127], b ∈ [−512, 508]; every value an integer):
+//   operands  |s_b ± u_b|, |γ − δ|, |δ + γ| ≤ 2048, |γ| ≤ 1020; |s_a ± u_a| ≤ 512,
+//             |2(α + β)| ≤ 1020, |2α|, |2β| ≤ 510: exact in f16;
+//   P         partial sums ≤ 16·512·2048 = 2^24; M ≤ 16·510·2040 < 2^24: exact;
+//   2Pr, 2Pi  partial sums ≤ 2·(16·510·1020 + 16·255·2040) = 33,292,800 < 2^25, all even: exact;
+//   P ± M     = 2U, 2U' (|·| ≤ 2^24): exact; + |2Pr| = 4·max(Z_0, Z_2) (≤ 2^24): exact;
+//   y         one rounding, exact whenever |y| ≤ 2^24 — the exact-form argument below.
+constexpr int kDft5 = 2048;
+
+template <int VAR>
+struct DftForm {
+    static constexpr bool F5 = (VAR & kDft5) != 0;
+    static constexpr int KS = F5 ? 5 : 4;              // domain fragments per tile
+    static constexpr int NBF = F5 ? 5 : kDftRangeFrags; // range fragments per block
+};
+
 struct DftArgs {
     MfmaSearchArgs m;
     uint32_t* rguard;     // [nblocks]  max over the block's ranges of R1 = Σ_o(|s_a| + |u_a|)
@@ -142,11 +166,12 @@ __device__ inline uint32_t pair_sums(uint32_t w0, uint32_t w1)
 // position in domain order, so neighbouring threads read overlapping plane rows, and the
 // outputs are scattered to the position's tile row; tp_build_tiles writes the padding rows and
 // zeroes the tile guards, which are then raised with atomics.
-template <bool BYPOS = false>
+// F5: the five-MFMA form's fragments [s_b + u_b | s_b − u_b | γ | γ − δ | −δ − γ] (kDft5)
+template <bool BYPOS = false, bool F5 = false>
 __global__ void __launch_bounds__(256) dft_domain_build(MfmaDomainPrepArgs a, DftDomainBuildArgs s,
                                                         uint2* __restrict__ tguard)
 {
-    constexpr int NN = 64, NO = 16;
+    constexpr int NN = 64, NO = 16, KS = F5 ? 5 : 4;
     const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
     if (tid >= (BYPOS ? s.npos : a.ntiles * 32u))
         return;
@@ -218,27 +243,35 @@ __global__ void __launch_bounds__(256) dft_domain_build(MfmaDomainPrepArgs a, Df
 #pragma unroll
     for (int k = 0; k < NN; ++k)
         sb2 += b[k] * b[k];
-    _Float16 comp[4][NO];
+    _Float16 comp[KS][NO];
     int dinf = 0;
 #pragma unroll
     for (int o = 0; o < NO; ++o) {
         const int b0 = b[kOrb8.p[o][0]], b1 = b[kOrb8.p[o][1]], b2 = b[kOrb8.p[o][2]], b3 = b[kOrb8.p[o][3]];
-        const int sb = b0 + b2, ub = b1 + b3;
+        const int sb = b0 + b2, ub = b1 + b3, gb = b0 - b2, db = b1 - b3;
         dinf = max(dinf, max(abs(sb), abs(ub)));
-        comp[0][o] = (_Float16)sb;
-        comp[1][o] = (_Float16)ub;
-        comp[2][o] = (_Float16)(b0 - b2);
-        comp[3][o] = (_Float16)(b1 - b3);
+        if constexpr (F5) {
+            comp[0][o] = (_Float16)(sb + ub);
+            comp[1][o] = (_Float16)(sb - ub);
+            comp[2][o] = (_Float16)gb;
+            comp[3][o] = (_Float16)(gb - db);
+            comp[4][o] = (_Float16)(-db - gb);
+        } else {
+            comp[0][o] = (_Float16)sb;
+            comp[1][o] = (_Float16)ub;
+            comp[2][o] = (_Float16)gb;
+            comp[3][o] = (_Float16)db;
+        }
     }
 #pragma unroll
-    for (int st = 0; st < 4; ++st)
+    for (int st = 0; st < KS; ++st)
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             _Float16 v8[8];
 #pragma unroll
             for (int j = 0; j < 8; ++j)
                 v8[j] = comp[st][8 * h + j];
-            a.dtiles[((size_t)tile * 4 + st) * 64 + row + 32 * h] = __builtin_bit_cast(uint4, v8);
+            a.dtiles[((size_t)tile * KS + st) * 64 + row + 32 * h] = __builtin_bit_cast(uint4, v8);
         }
     const float ny = p >= 0 ? -(float)sb2 : kDftPadY;
     const uint32_t h = (row >> 2) & 1u, i = (row & 3u) + 4u * (row >> 3);
@@ -268,9 +301,11 @@ __global__ void __launch_bounds__(256) dft_domain_build(MfmaDomainPrepArgs a, Df
 // slot and the block's guard term max R1.  One thread per slot (a range-order variant with
 // scattered outputs measured slower for the SEA tiled form's ΣR-sorted slots: 61 vs 41 µs).
 // ---------------------------------------------------------------------------
+// FORM 5: the five-MFMA form's fragments [s_a + u_a | s_a − u_a | 2(α + β) | −2β | 2α] (kDft5)
+template <int FORM = 4>
 __global__ void __launch_bounds__(256) dft_range_prep(MfmaRangePrepArgs a, uint32_t* __restrict__ rguard)
 {
-    constexpr int N = 8, NN = 64, NO = 16;
+    constexpr int N = 8, NN = 64, NO = 16, NBF = FORM == 5 ? 5 : kDftRangeFrags;
     const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
     if (gid >= a.nblocks * 32u)
         return;
@@ -303,30 +338,38 @@ __global__ void __launch_bounds__(256) dft_range_prep(MfmaRangePrepArgs a, uint3
         for (int q = 0; q < NN; ++q)
             av[q] = 0;
     }
-    _Float16 comp[kDftRangeFrags][NO];
+    _Float16 comp[NBF][NO];
     int r1 = 0;
 #pragma unroll
     for (int o = 0; o < NO; ++o) {
         const int a0 = av[kOrb8.p[o][0]], a1 = av[kOrb8.p[o][1]], a2 = av[kOrb8.p[o][2]], a3 = av[kOrb8.p[o][3]];
-        const int sa = a0 + a2, ua = a1 + a3;
+        const int sa = a0 + a2, ua = a1 + a3, al = a0 - a2, be = a1 - a3;
         r1 += abs(sa) + abs(ua);
-        comp[0][o] = (_Float16)sa;
-        comp[1][o] = (_Float16)ua;
-        comp[2][o] = (_Float16)(4 * sa);
-        comp[3][o] = (_Float16)(4 * ua);
-        comp[4][o] = (_Float16)(a0 - a2);
-        comp[5][o] = (_Float16)(a1 - a3);
-        comp[6][o] = (_Float16)(a2 - a0);
+        if constexpr (FORM == 5) {
+            comp[0][o] = (_Float16)(sa + ua);
+            comp[1][o] = (_Float16)(sa - ua);
+            comp[2][o] = (_Float16)(2 * (al + be));
+            comp[3][o] = (_Float16)(-2 * be);
+            comp[4][o] = (_Float16)(2 * al);
+        } else {
+            comp[0][o] = (_Float16)sa;
+            comp[1][o] = (_Float16)ua;
+            comp[2][o] = (_Float16)(4 * sa);
+            comp[3][o] = (_Float16)(4 * ua);
+            comp[4][o] = (_Float16)al;
+            comp[5][o] = (_Float16)be;
+            comp[6][o] = (_Float16)(-al);
+        }
     }
 #pragma unroll
-    for (int f = 0; f < kDftRangeFrags; ++f)
+    for (int f = 0; f < NBF; ++f)
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             _Float16 v8[8];
 #pragma unroll
             for (int j = 0; j < 8; ++j)
                 v8[j] = comp[f][8 * h + j];
-            a.rfrags[((size_t)b * kDftRangeFrags + f) * 64 + col + 32 * h] = __builtin_bit_cast(uint4, v8);
+            a.rfrags[((size_t)b * NBF + f) * 64 + col + 32 * h] = __builtin_bit_cast(uint4, v8);
         }
     a.rconst[gid] = ri >= 0 ? (uint32_t)(16 * sa2) : 0u; // 16Σa² ≤ 2^24
     if (a.rorb) {
@@ -368,9 +411,40 @@ __device__ inline floatx16_t mfma2(const half8_t& a0, const half8_t& b0, const h
 
 constexpr int kDftChain = 1024;  // VAR bit: v_max3 chain for the row maximum
 
+typedef float float2v_t __attribute__((ext_vector_type(2)));
+
+// the five-MFMA form (kDft5): af = [s_b + u_b, s_b − u_b, γ, γ − δ, −δ − γ],
+// bf = [s_a + u_a, s_a − u_a, 2(α + β), −2β, 2α]
+__device__ inline float dft_tile_max5(const half8_t (&af)[5], const half8_t (&bf)[5], const floatx16_t& ny, float m)
+{
+    const floatx16_t z = {};
+    const floatx16_t k1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[2], bf[2], z, 0, 0, 0); // 2k1
+    const floatx16_t p = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[0], bf[0], z, 0, 0, 0);  // P = U + U'
+    const floatx16_t q = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[1], bf[1], z, 0, 0, 0);  // M = U − U'
+    const floatx16_t pr = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[3], bf[3], k1, 0, 0, 0); // 2Pr
+    const floatx16_t pi = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[4], bf[4], k1, 0, 0, 0); // 2Pi
+    float y[16];
+#pragma unroll
+    for (int i = 0; i < 16; i += 2) {
+        // two rows per packed instruction where no |·| modifier is needed
+        const float2v_t P2 = {p[i], p[i + 1]}, M2 = {q[i], q[i + 1]};
+        const float2v_t X = P2 + M2, Xp = P2 - M2; // 2U, 2U'
+        const float2v_t t = {__builtin_fmaxf(X.x + __builtin_fabsf(pr[i]), Xp.x + __builtin_fabsf(pi[i])),
+                             __builtin_fmaxf(X.y + __builtin_fabsf(pr[i + 1]), Xp.y + __builtin_fabsf(pi[i + 1]))};
+        const float2v_t N2 = {ny[i], ny[i + 1]};
+        const float2v_t yy = __builtin_elementwise_fma(t, (float2v_t){2.0f, 2.0f}, N2);
+        y[i] = yy.x;
+        y[i + 1] = yy.y;
+    }
+#pragma unroll
+    for (int i = 0; i < 16; i += 2)
+        m = __builtin_fmaxf(__builtin_fmaxf(m, y[i]), y[i + 1]);
+    return m;
+}
+
 template <int VAR>
-__device__ inline float dft_tile_max(const half8_t (&af)[4], const half8_t (&bf)[kDftRangeFrags],
-                                     const floatx16_t& ny, bool fast, float m)
+__device__ inline float dft_tile_max4(const half8_t (&af)[4], const half8_t (&bf)[kDftRangeFrags],
+                                      const floatx16_t& ny, bool fast, float m)
 {
     const floatx16_t z = {};
     // af: [s_b, u_b, γ, δ];  bf: [s_a, u_a, 4s_a, 4u_a, α, β, −α]
@@ -451,15 +525,29 @@ __device__ inline float dft_tile_max(const half8_t (&af)[4], const half8_t (&bf)
     return __builtin_fmaxf(m0, m1);
 }
 
+template <int VAR>
+__device__ inline float dft_tile_max(const half8_t (&af)[DftForm<VAR>::KS], const half8_t (&bf)[DftForm<VAR>::NBF],
+                                     const floatx16_t& ny, bool fast, float m)
+{
+    if constexpr (DftForm<VAR>::F5) {
+        static_assert((VAR & 1) != 0, "the five-MFMA form has no guarded fast path");
+        (void)fast;
+        return dft_tile_max5(af, bf, ny, m);
+    } else {
+        return dft_tile_max4<VAR>(af, bf, ny, fast, m);
+    }
+}
+
 // MASK (CHUNKED search): masks[0] gets the chunk tiles attaining the lane's maximum, masks[1]
 // (HITS) the tiles holding a hit (y ≥ hl), bit k for tile q0 + k
 template <int VAR, bool MASK = false, bool HITS = false>
 __device__ inline float dft_compute_stage(const uint4* __restrict__ la, uint32_t nt, uint32_t lane,
-                                          const half8_t (&bf)[kDftRangeFrags], uint32_t tb,
+                                          const half8_t (&bf)[DftForm<VAR>::NBF], uint32_t tb,
                                           const uint2* __restrict__ tguard, uint32_t r1, uint32_t q0 = 0,
                                           uint32_t q1 = ~0u, uint32_t* masks = nullptr, float hl = 0.0f)
 {
-    const uint4* lc = la + nt * 4u * 64u;
+    constexpr int KS = DftForm<VAR>::KS;
+    const uint4* lc = la + nt * (uint32_t)KS * 64u;
     const uint32_t h = lane >> 5;
     float cm = -__builtin_inff();
     // the chunk's fast-path guards, loaded up front (wave-uniform scalar loads)
@@ -475,10 +563,10 @@ __device__ inline float dft_compute_stage(const uint4* __restrict__ la, uint32_t
     auto tile = [&](uint32_t q) {
         // ABLATION bit 32 (tuning only, wrong results): every tile reuses tile 0's operands
         const uint32_t qq = (VAR & 32) ? 0u : q;
-        half8_t af[4];
+        half8_t af[KS];
 #pragma unroll
-        for (int s = 0; s < 4; ++s)
-            af[s] = __builtin_bit_cast(half8_t, la[(qq * 4 + s) * 64 + lane]);
+        for (int s = 0; s < KS; ++s)
+            af[s] = __builtin_bit_cast(half8_t, la[(qq * KS + s) * 64 + lane]);
         floatx16_t ny;
 #pragma unroll
         for (int c4 = 0; c4 < 4; ++c4) {
@@ -518,7 +606,7 @@ __global__ void __launch_bounds__(64 * WAVES) search_dft(DftArgs d)
     static_assert(kTuningBuild || (VAR & (8 | 16 | 32 | 64 | 256 | 512)) == 0,
                   "search_dft ablations exist only in FRAC_TUNING builds");
     const MfmaSearchArgs& a = d.m;
-    constexpr int KS = 4;
+    constexpr int KS = DftForm<VAR>::KS, NBF = DftForm<VAR>::NBF;
     constexpr uint32_t kTilesPerStage = TPS; // LDS stage; chunks stay 4 tiles (resolve_dft)
     constexpr int STAGE = kTilesPerStage * KS * 64 + kTilesPerStage * 8;
     __shared__ uint4 lds0[STAGE];
@@ -529,10 +617,10 @@ __global__ void __launch_bounds__(64 * WAVES) search_dft(DftArgs d)
     const uint32_t blk = wk.x + (active ? wv : 0u);
     const uint32_t r1 = __builtin_amdgcn_readfirstlane(d.rguard[blk]);
 
-    half8_t bf[kDftRangeFrags];
+    half8_t bf[NBF];
 #pragma unroll
-    for (int f = 0; f < kDftRangeFrags; ++f)
-        bf[f] = __builtin_bit_cast(half8_t, a.rfrags[((size_t)blk * kDftRangeFrags + f) * 64 + lane]);
+    for (int f = 0; f < NBF; ++f)
+        bf[f] = __builtin_bit_cast(half8_t, a.rfrags[((size_t)blk * NBF + f) * 64 + lane]);
     float hl = 0.0f;
     if constexpr (HITS) // S16 ≤ H  ⇔  y ≥ 16Σa² − H  (exact integers below 2^24)
         hl = (float)((int32_t)a.rconst[blk * 32 + (lane & 31u)] - (int32_t)a.hitH);

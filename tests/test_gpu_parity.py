@@ -265,10 +265,14 @@ DFT_CASES = [
 ]
 
 
-@pytest.mark.parametrize("dft", ["1", "0"])
+@pytest.mark.parametrize("dft", ["1", "0", "1/20"])
 @pytest.mark.parametrize("case", range(len(DFT_CASES)))
 def test_mfma_fourier_and_direct_match_oracle(oracle, monkeypatch, case, dft):
+    # "1/20": the five-MFMA Fourier form (FRAC_MFMA_VARIANT=20)
+    dft, _, var = dft.partition("/")
     monkeypatch.setenv("FRAC_MFMA_DFT", dft)
+    if var:
+        monkeypatch.setenv("FRAC_MFMA_VARIANT", var)
     W, H, cls, thr, smax, kind = DFT_CASES[case]
     rng = np.random.default_rng(2000 + case)
     p = _random_plane(rng, W, H, kind)
@@ -282,6 +286,53 @@ def test_mfma_fourier_and_direct_match_oracle(oracle, monkeypatch, case, dft):
     want, rej, _ = oracle.estimate(p, doms, rngs, T=4, thr=thr, smax=smax, use_classifier=cls)
     assert_same(out, {k: want[k] for k in FIELDS}, f"dft={dft} case {DFT_CASES[case]}")
     assert st["rejected_mappings"] == rej
+
+
+def _extreme_plane(rng, S, kind):
+    # frames that drive the Fourier operands to their bounds: pixels only 0 or 255, as i.i.d.
+    # noise, as 8×8 / 2×2 constant blocks, and as per-orbit patterns (one rotation orbit of an
+    # 8×8 block bright, its image under Rotate_90 dark: |α|, |β|, |γ|, |δ| at their maxima)
+    if kind == "binary":
+        return (rng.integers(0, 2, (S, S)) * 255).astype(np.uint8)
+    if kind == "blocks8":
+        return (rng.integers(0, 2, (S // 8, S // 8)) * 255).astype(np.uint8).repeat(8, 0).repeat(8, 1)
+    if kind == "blocks2":
+        return (rng.integers(0, 2, (S // 2, S // 2)) * 255).astype(np.uint8).repeat(2, 0).repeat(2, 1)
+    # "orbits": every 8×8 block and every 2×2-decimated 16×16 block alternates 0/255 around
+    # each rotation orbit, with a random phase per block
+    yy, xx = np.mgrid[0:8, 0:8]
+    ring = ((yy + xx) % 2) ^ ((yy < 4) & (xx < 4)).astype(int)
+    tiles = [ring, np.rot90(ring), 1 - ring, np.rot90(1 - ring)]
+    pick = rng.integers(0, 4, (S // 8, S // 8))
+    out = np.block([[tiles[k] for k in row] for row in pick]) * 255
+    return out.astype(np.uint8)
+
+
+@pytest.mark.parametrize("var", ["20"])
+@pytest.mark.parametrize("kind", ["binary", "blocks8", "blocks2", "orbits"])
+def test_five_mfma_form_at_operand_extremes(monkeypatch, kind, var):
+    """The five-MFMA Fourier form (FRAC_MFMA_VARIANT=20) has the tightest exactness margins (2Pr /
+    2Pi partial sums up to 33.3M < 2^25, P up to 2^24): on 0/255 frames that drive every operand
+    to its bound it returns the exhaustive VALU engine's records, with and without the
+    classifier."""
+    rng = np.random.default_rng(hash(kind) & 0xffff)
+    S = 256
+    p = _extreme_plane(rng, S, kind)
+    doms, rngs = F.create_uniform_grid(S, S, 16, 8), F.create_uniform_grid(S, S, 8, 8)
+    for cls in (False, True):
+        with F.Engine(0, 4, cls, 0.0, -1.0, F.ENGINE_VALU) as e:
+            e.set_frame(p)
+            e.set_domains(doms)
+            want, wst = e.search(rngs)
+        monkeypatch.setenv("FRAC_MFMA_DFT", "1")
+        monkeypatch.setenv("FRAC_MFMA_VARIANT", var)
+        with F.Engine(0, 4, cls, 0.0, -1.0, F.ENGINE_MFMA) as e:
+            e.set_frame(p)
+            e.set_domains(doms)
+            out, st = e.search(rngs)
+        monkeypatch.delenv("FRAC_MFMA_VARIANT")
+        assert out.tobytes() == want.tobytes(), f"{kind} cls={cls}"
+        assert st["rejected_mappings"] == wst["rejected_mappings"]
 
 
 def test_fourier_direct_and_valu_agree_on_stress_frame(monkeypatch):
@@ -454,7 +505,7 @@ def test_encode_defaults_are_the_reference_cli_defaults():
     assert st["rejected_mappings"] == meta["rejected"]
 
 
-PRODUCT_VARIANTS = ("0", "1", "2", "3", "4", "5", "6", "7", "12", "32", "64", "96", "98", "128", "130")
+PRODUCT_VARIANTS = ("0", "1", "2", "3", "4", "5", "6", "7", "12", "20", "32", "64", "96", "98", "128", "130")
 
 
 @pytest.mark.parametrize("n,T,dft", [(8, 4, "0"), (4, 4, "0"), (8, 8, "0"), (8, 4, "1")])

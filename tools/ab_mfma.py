@@ -2,7 +2,7 @@
 """Interleaved in-process A/B of MFMA search variants on the C3 frame; prints per-variant
 median/min search-kernel and finish (resolve + fit) ms (library HIP events).
 Variants: "d" = the C4-Fourier search (FRAC_MFMA_DFT=1, default: software-pipelined exact
-form), "e" = its unpipelined exact form, "g" = the guarded fast-path form, "dt" = "d" with the pairwise-tree row maximum (the default uses one v_max3 chain), "p" = pipelined with a forced interleave, "em"/"ev" = MFMA-only / VALU-only ablations of "e", an integer v = the direct
+form), "e" = its unpipelined exact form, "g" = the guarded fast-path form, "d5" = the five-MFMA form (variant 20), "dt" = "d" with the pairwise-tree row maximum (the default uses one v_max3 chain), "p" = pipelined with a forced interleave, "em"/"ev" = MFMA-only / VALU-only ablations of "e", an integer v = the direct
 search_mfma with FRAC_MFMA_VARIANT=v (FRAC_MFMA_DFT=0).
 Ablation variants need the tuning library: python tools/build_tuning.py, then
 FRAC_LIB=fractencode_amd/libfracenc_tuning.so tools/ab_mfma.py ...
@@ -30,14 +30,14 @@ with F.Engine(0, 4, False, 0.0, -1.0, F.ENGINE_MFMA, timing=True) as e:
     for r in range(rounds + 1):
         for v in variants:
             os.environ["FRAC_MFMA_DFT"] = "1" if not v.isdigit() else "0"
-            os.environ["FRAC_MFMA_VARIANT"] = {"d": "2", "e": "1", "g": "3", "p": "4", "d8": "5", "dt": "6", "d2": "12", "dm": "201", "dm0": "202", "dmD": "203", "dmB": "204", "dD": "205", "dB": "206",
+            os.environ["FRAC_MFMA_VARIANT"] = {"d": "2", "e": "1", "g": "3", "p": "4", "d8": "5", "dt": "6", "d2": "12", "d5": "20", "dm": "201", "dm0": "202", "dmD": "203", "dmB": "204", "dD": "205", "dB": "206",
                                               "d0": "207", "em": "9", "ev": "17", "emL": "41", "emB": "73",
                                               "em0": "105", "eB": "65"}.get(v, v)
             e.run()
             out, st = e.fetch()
             if ref is None:
                 ref = out.tobytes()
-            if v in ("d", "e", "g", "p", "d8", "dt", "d2") or (v.isdigit() and (int(v) < 8 or int(v) in (32, 64, 96, 98, 128, 130))):  # 8, 16 are ablations (results intentionally wrong)
+            if v in ("d", "e", "g", "p", "d8", "dt", "d2", "d5") or (v.isdigit() and (int(v) < 8 or int(v) in (32, 64, 96, 98, 128, 130))):  # 8, 16 are ablations (results intentionally wrong)
                 assert out.tobytes() == ref, f"variant {v} differs"
             if r:
                 res[v].append(st["ms_search"])
