@@ -475,9 +475,17 @@ inline int mfma_variant(frac_ctx* c, int& var);
 inline bool mfma_dft_enabled();
 // the Fourier search variants that run 4-wave workgroups (and read m_work): 1, 3 and the odd
 // ablations below 200; every other variant runs 8-wave workgroups on m8_work
-inline bool dft_four_wave(int var) { return var == 1 || var == 3 || (var >= 9 && var < 200 && (var & 1)); }
-// the Fourier form's domain/range fragment layout: 4 (8 MFMA per tile pair), 5 (kDft5, variant 20)
-inline int dft_form(int var) { return var == 20 ? 5 : 4; }
+// the variants that run search_dft in 4-wave workgroups over the 4-block work lists: 1, 3 and the
+// tuning ablations of 1 (the other odd A/B values, e.g. 21, are 8-block forms)
+inline bool dft_four_wave(int var)
+{
+    return var == 1 || var == 3 || var == 9 || var == 17 || var == 41 || var == 65 || var == 73 || var == 105;
+}
+// the Fourier form's domain/range fragment layout: 4 (8 MFMA per tile pair), 5 (kDft5, variants 20, 22),
+// 6 (kDft6, variants 21, 23)
+constexpr int kTpVar = 1 | kDftChain | (kDftTpForm == 6 ? kDft6 : 0); // the SEA tiled form's search_dft
+constexpr uint32_t kTpKS = kDftTpForm == 4 ? 4u : 5u;                    // its domain fragments per tile
+inline int dft_form(int var) { return var == 20 || var == 22 ? 5 : var == 21 || var == 23 ? 6 : 4; }
 
 int prepare(frac_ctx* c)
 {
@@ -859,7 +867,7 @@ int prepare(frac_ctx* c)
         FRAC_HIP(c, c->d_m_slot_range.ensure(std::max<size_t>(nbk * 32, 1)));
         FRAC_HIP(c, c->d_m_range_slot.ensure(std::max<size_t>(nr, 1)));
         FRAC_HIP(c, c->d_m_tile_pos.ensure(std::max<size_t>(nt * 32, 1)));
-        FRAC_HIP(c, c->d_m_dtiles.ensure(std::max<size_t>(nt * 4 * 64, 1)));
+        FRAC_HIP(c, c->d_m_dtiles.ensure(std::max<size_t>(nt * kTpKS * 64, 1)));
         FRAC_HIP(c, c->d_m_dconst.ensure(std::max<size_t>(nt * 32, 1)));
         FRAC_HIP(c, c->d_m_rfrags.ensure(std::max<size_t>(nbk * 7 * 64, 1)));
         FRAC_HIP(c, c->d_m_rconst.ensure(std::max<size_t>(nbk * 32, 1)));
@@ -965,7 +973,7 @@ inline int mfma_variant(frac_ctx* c, int& var)
         return FRAC_OK;
     char* end = nullptr;
     const long x = strtol(v, &end, 10);
-    static const int exact[] = {0, 1, 2, 3, 4, 5, 6, 7, 12, 20, 32, 64, 96, 98, 128, 130};
+    static const int exact[] = {0, 1, 2, 3, 4, 5, 6, 7, 12, 20, 21, 22, 23, 32, 64, 96, 98, 128, 130};
     static const int ablation[] = {8, 9, 16, 17, 41, 65, 73, 105, 201, 202, 203, 204, 205, 206, 207};
     bool ok = end && *end == 0;
     bool known = false;
@@ -1041,7 +1049,7 @@ inline int launch_dft(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride)
     int var = 0;
     FRAC_TRY(mfma_variant(c, var));
     const int form = dft_form(var);
-    const bool f5 = form == 5; // five domain fragments per tile
+    const bool f5 = form != 4; // five domain fragments per tile (forms 5 and 6)
     FRAC_HIP(c, c->d_m_dtiles.ensure(std::max<size_t>((size_t)c->ntiles * (f5 ? 5 : 4) * 64, 1)));
     d.dtiles = c->d_m_dtiles.ptr;
     DftDomainBuildArgs b;
@@ -1073,6 +1081,8 @@ inline int launch_dft(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride)
         const unsigned g = (c->nblocks * 32 + 255) / 256;
         if (form == 5)
             dft_range_prep<5><<<g, 256, 0, c->stream>>>(r, c->d_dft_rguard.ptr);
+        else if (form == 6)
+            dft_range_prep<6><<<g, 256, 0, c->stream>>>(r, c->d_dft_rguard.ptr);
         else
             dft_range_prep<4><<<g, 256, 0, c->stream>>>(r, c->d_dft_rguard.ptr);
     }
@@ -1082,8 +1092,8 @@ inline int launch_dft(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride)
     const std::vector<uint4>& work = four ? c->m_work : c->m8_work;
     c->form_ran = FRAC_FORM_FOURIER;
     c->flops_ran = 0;
-    for (const uint4& w : work) // 8 (five-MFMA form: 5) MFMA 32x32x16 (32768 flops each) per (block, tile)
-        c->flops_ran += (uint64_t)w.y * (w.w - w.z) * (f5 ? 5ull : 8ull) * 32768ull;
+    for (const uint4& w : work) // 8 (forms 5 / 6: 5 / 6) MFMA 32x32x16 (32768 flops each) per (block, tile)
+        c->flops_ran += (uint64_t)w.y * (w.w - w.z) * (form == 5 ? 5ull : form == 6 ? 6ull : 8ull) * 32768ull;
     if (!work.empty()) {
         MfmaSearchArgs a;
         a.dtiles = c->d_m_dtiles.ptr;
@@ -1113,6 +1123,21 @@ inline int launch_dft(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride)
             default: search_dft<false, 65, W8><<<nwg, 64 * W8, 0, c->stream>>>(da); break;  // full, no DMA/bar
             }
 #endif
+        } else if (form == 6 && var == 23) { // the six-MFMA form, two range blocks per wave (search_dft2)
+            if (hits)
+                search_dft2<true, true><<<nwg, 256, 0, c->stream>>>(da);
+            else
+                search_dft2<false, true><<<nwg, 256, 0, c->stream>>>(da);
+        } else if (form == 6) { // the six-MFMA form
+            if (hits)
+                search_dft<true, 1 | kDftChain | kDft6, W8><<<nwg, 64 * W8, 0, c->stream>>>(da);
+            else
+                search_dft<false, 1 | kDftChain | kDft6, W8><<<nwg, 64 * W8, 0, c->stream>>>(da);
+        } else if (var == 22) { // the five-MFMA form, unpacked epilogue
+            if (hits)
+                search_dft<true, 1 | kDftChain | kDft5 | kDftScalar, W8><<<nwg, 64 * W8, 0, c->stream>>>(da);
+            else
+                search_dft<false, 1 | kDftChain | kDft5 | kDftScalar, W8><<<nwg, 64 * W8, 0, c->stream>>>(da);
         } else if (form == 5) { // the five-MFMA form
             if (hits)
                 search_dft<true, 1 | kDftChain | kDft5, W8><<<nwg, 64 * W8, 0, c->stream>>>(da);
@@ -1321,7 +1346,7 @@ int launch_tp(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool timing)
     if (nt) {
         tp_build_tiles<<<(nt * 32 + 255) / 256, 256, 0, c->stream>>>(
             c->tp_bk, c->d_sea_dkey2.ptr, c->d_sea_dpos2.ptr, nt, c->d_m_tile_pos.ptr, c->d_tp_tile_sd.ptr,
-            c->d_tp_row_of.ptr, c->d_m_dtiles.ptr, c->d_m_dconst.ptr, c->d_dft_tguard.ptr);
+            c->d_tp_row_of.ptr, c->d_m_dtiles.ptr, c->d_m_dconst.ptr, c->d_dft_tguard.ptr, kTpKS);
         MfmaDomainPrepArgs d;
         d.pool = c->d_pool.ptr;
         d.negsd2 = c->d_negsd2.ptr;
@@ -1340,7 +1365,7 @@ int launch_tp(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool timing)
         b.row_of = c->d_tp_row_of.ptr;
         b.npos = P;
         if (P)
-            dft_domain_build<true><<<(P + 255) / 256, 256, 0, c->stream>>>(d, b, c->d_dft_tguard.ptr);
+            dft_domain_build<true, kDftTpForm != 4><<<(P + 255) / 256, 256, 0, c->stream>>>(d, b, c->d_dft_tguard.ptr);
     }
     if (nr) {
         tp_range_keys<<<(nr + 255) / 256, 256, 0, c->stream>>>(dtgt, tstride, c->d_ranges.ptr, c->d_tp_rbk.ptr, nr,
@@ -1365,7 +1390,7 @@ int launch_tp(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool timing)
         r.rconst = c->d_m_rconst.ptr;
         FRAC_HIP(c, c->d_dft_rorb.ensure(std::max<size_t>((size_t)r.nblocks * 32 * 32, 1)));
         r.rorb = c->d_dft_rorb.ptr;
-        dft_range_prep<4><<<(nbk * 32 + 255) / 256, 256, 0, c->stream>>>(r, c->d_dft_rguard.ptr);
+        dft_range_prep<kDftTpForm><<<(nbk * 32 + 255) / 256, 256, 0, c->stream>>>(r, c->d_dft_rguard.ptr);
     }
     if (timing)
         FRAC_TRY(mark_event(c, 1));
@@ -1391,7 +1416,7 @@ int launch_tp(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool timing)
     FRAC_HIP(c, c->d_m_entries.ensure((size_t)ng * W8 * 64));
     da.m.entries = c->d_m_entries.ptr;
     da.choff = c->d_tp_iota.ptr;
-    search_dft<false, 1 | kDftChain, W8, 4, true><<<ng, 64 * W8, 0, c->stream>>>(da);
+    search_dft<false, kTpVar, W8, 4, true><<<ng, 64 * W8, 0, c->stream>>>(da);
     tp_seed_reduce<<<(nbk * 32 + 255) / 256, 256, 0, c->stream>>>(c->d_tp_blk_group.ptr, c->d_m_entries.ptr,
                                                                    c->d_m_slot_range.ptr, c->d_m_rconst.ptr, nbk,
                                                                    c->d_tp_blk_u.ptr);
@@ -1428,14 +1453,14 @@ int launch_tp(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool timing)
                                                               c->d_m8_blk_ptr.ptr, nbk, c->d_m8_blk_ent.ptr);
     // issued matrix work (8 MFMA 32×32×16 per block × tile) and evaluated (slot, domain row) pairs
     const uint64_t pairs = (uint64_t)tot[2] | ((uint64_t)tot[3] << 32);
-    c->flops_ran = pairs * 8ull * 32768ull;
+    c->flops_ran = pairs * (kDftTpForm == 6 ? 6ull : 8ull) * 32768ull;
     c->evaluated_ran = pairs * 32ull * 32ull;
     da.m.entries = c->d_m_entries.ptr;
     da.choff = c->d_tp_choff.ptr;
     if (c->hitH > 0)
-        search_dft<true, 1 | kDftChain, W8, 4, true><<<ng, 64 * W8, 0, c->stream>>>(da);
+        search_dft<true, kTpVar, W8, 4, true><<<ng, 64 * W8, 0, c->stream>>>(da);
     else
-        search_dft<false, 1 | kDftChain, W8, 4, true><<<ng, 64 * W8, 0, c->stream>>>(da);
+        search_dft<false, kTpVar, W8, 4, true><<<ng, 64 * W8, 0, c->stream>>>(da);
     if (timing)
         FRAC_TRY(mark_event(c, 2));
     MfmaResolveArgs v;

@@ -117,12 +117,18 @@ constexpr int kDftRangeFrags = 7;     // s, u, 4s, 4u, α, β, −α
 //   P ± M     = 2U, 2U' (|·| ≤ 2^24): exact; + |2Pr| = 4·max(Z_0, Z_2) (≤ 2^24): exact;
 //   y         one rounding, exact whenever |y| ≤ 2^24 — the exact-form argument below.
 constexpr int kDft5 = 2048;
+constexpr int kDftScalar = 4096; // with kDft5: the P ± M and the fma one row per instruction
+constexpr int kDft6 = 8192;      // the six-MFMA form (dft_tile_max6)
+
+// the form the SEA engine's tiled search (fracenc_tp.hip) runs: 4 or 6
+constexpr int kDftTpForm = 4;
 
 template <int VAR>
 struct DftForm {
     static constexpr bool F5 = (VAR & kDft5) != 0;
-    static constexpr int KS = F5 ? 5 : 4;              // domain fragments per tile
-    static constexpr int NBF = F5 ? 5 : kDftRangeFrags; // range fragments per block
+    static constexpr bool F6 = (VAR & kDft6) != 0;
+    static constexpr int KS = (F5 || F6) ? 5 : 4;                 // domain fragments per tile
+    static constexpr int NBF = F6 ? 6 : F5 ? 5 : kDftRangeFrags; // range fragments per block
 };
 
 struct DftArgs {
@@ -301,11 +307,12 @@ __global__ void __launch_bounds__(256) dft_domain_build(MfmaDomainPrepArgs a, Df
 // slot and the block's guard term max R1.  One thread per slot (a range-order variant with
 // scattered outputs measured slower for the SEA tiled form's ΣR-sorted slots: 61 vs 41 µs).
 // ---------------------------------------------------------------------------
-// FORM 5: the five-MFMA form's fragments [s_a + u_a | s_a − u_a | 2(α + β) | −2β | 2α] (kDft5)
+// FORM 5: the five-MFMA form's fragments [s_a + u_a | s_a − u_a | 2(α + β) | −2β | 2α] (kDft5);
+// FORM 6: the six-MFMA form's [s_a + u_a | s_a − u_a | u_a − s_a | 2(α + β) | −2β | 2α] (kDft6)
 template <int FORM = 4>
 __global__ void __launch_bounds__(256) dft_range_prep(MfmaRangePrepArgs a, uint32_t* __restrict__ rguard)
 {
-    constexpr int N = 8, NN = 64, NO = 16, NBF = FORM == 5 ? 5 : kDftRangeFrags;
+    constexpr int N = 8, NN = 64, NO = 16, NBF = FORM == 6 ? 6 : FORM == 5 ? 5 : kDftRangeFrags;
     const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
     if (gid >= a.nblocks * 32u)
         return;
@@ -351,6 +358,13 @@ __global__ void __launch_bounds__(256) dft_range_prep(MfmaRangePrepArgs a, uint3
             comp[2][o] = (_Float16)(2 * (al + be));
             comp[3][o] = (_Float16)(-2 * be);
             comp[4][o] = (_Float16)(2 * al);
+        } else if constexpr (FORM == 6) {
+            comp[0][o] = (_Float16)(sa + ua);
+            comp[1][o] = (_Float16)(sa - ua);
+            comp[2][o] = (_Float16)(ua - sa);
+            comp[3][o] = (_Float16)(2 * (al + be));
+            comp[4][o] = (_Float16)(-2 * be);
+            comp[5][o] = (_Float16)(2 * al);
         } else {
             comp[0][o] = (_Float16)sa;
             comp[1][o] = (_Float16)ua;
@@ -413,8 +427,10 @@ constexpr int kDftChain = 1024;  // VAR bit: v_max3 chain for the row maximum
 
 typedef float float2v_t __attribute__((ext_vector_type(2)));
 
+
 // the five-MFMA form (kDft5): af = [s_b + u_b, s_b − u_b, γ, γ − δ, −δ − γ],
 // bf = [s_a + u_a, s_a − u_a, 2(α + β), −2β, 2α]
+template <bool PK = true>
 __device__ inline float dft_tile_max5(const half8_t (&af)[5], const half8_t (&bf)[5], const floatx16_t& ny, float m)
 {
     const floatx16_t z = {};
@@ -424,6 +440,18 @@ __device__ inline float dft_tile_max5(const half8_t (&af)[5], const half8_t (&bf
     const floatx16_t pr = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[3], bf[3], k1, 0, 0, 0); // 2Pr
     const floatx16_t pi = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[4], bf[4], k1, 0, 0, 0); // 2Pi
     float y[16];
+    if constexpr (!PK) {
+        // one row per instruction (A/B of the packed P ± M and fma below)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const float X = p[i] + q[i], Xp = p[i] - q[i];
+            y[i] = __builtin_fmaf(__builtin_fmaxf(X + __builtin_fabsf(pr[i]), Xp + __builtin_fabsf(pi[i])), 2.0f, ny[i]);
+        }
+#pragma unroll
+        for (int i = 0; i < 16; i += 2)
+            m = __builtin_fmaxf(__builtin_fmaxf(m, y[i]), y[i + 1]);
+        return m;
+    }
 #pragma unroll
     for (int i = 0; i < 16; i += 2) {
         // two rows per packed instruction where no |·| modifier is needed
@@ -440,6 +468,63 @@ __device__ inline float dft_tile_max5(const half8_t (&af)[5], const half8_t (&bf
     for (int i = 0; i < 16; i += 2)
         m = __builtin_fmaxf(__builtin_fmaxf(m, y[i]), y[i + 1]);
     return m;
+}
+
+// the six-MFMA form (kDft6): af as dft_tile_max5, bf = [s_a + u_a, s_a − u_a, u_a − s_a, 2(α + β), −2β, 2α].
+// The M GEMM accumulates onto P once with +(s_a − u_a) and once with −(s_a − u_a), giving 2U and 2U'
+// in the MFMA (the five-MFMA form's two VALU per candidate for P ± M go away).  Exact in any
+// accumulation order: with A0 = s_a + u_a, A2 = s_a − u_a (B0, B2 on the domain side),
+// |A0| + |A2| = 2·max(|s_a|, |u_a|) ≤ 512 and |B0|, |B2| ≤ 2048, so every partial sum of P ± M is
+// bounded by Σ_o (|A0·B0| + |A2·B2|) ≤ 16·2048·512 = 2^24.  Then the exact form's epilogue:
+//   y = fma(max(2U + |2Pr|, 2U' + |2Pi|), 2, −Σb²).
+__device__ inline float dft_tile_max6(const half8_t (&af)[5], const half8_t (&bf)[6], const floatx16_t& ny, float m)
+{
+    const floatx16_t z = {};
+    const floatx16_t p = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[0], bf[0], z, 0, 0, 0);  // P
+    const floatx16_t k1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[2], bf[3], z, 0, 0, 0); // 2k1
+    const floatx16_t u = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[1], bf[1], p, 0, 0, 0);  // P + M = 2U
+    const floatx16_t pr = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[3], bf[4], k1, 0, 0, 0); // 2Pr
+    const floatx16_t v = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[1], bf[2], p, 0, 0, 0);  // P − M = 2U'
+    const floatx16_t pi = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[4], bf[5], k1, 0, 0, 0); // 2Pi
+    float y[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+        y[i] = __builtin_fmaf(__builtin_fmaxf(u[i] + __builtin_fabsf(pr[i]), v[i] + __builtin_fabsf(pi[i])), 2.0f, ny[i]);
+#pragma unroll
+    for (int i = 0; i < 16; i += 2)
+        m = __builtin_fmaxf(__builtin_fmaxf(m, y[i]), y[i + 1]);
+    return m;
+}
+
+// The six-MFMA form for two range blocks sharing one domain tile (search_dft2<…, true>): the tile's
+// A fragments and row constants are read once for both blocks.
+__device__ inline void dft_tile_max6x2(const half8_t (&af)[5], const half8_t (&ba)[6], const half8_t (&bb)[6],
+                                       const floatx16_t& ny, float& ma, float& mb)
+{
+    const floatx16_t z = {};
+    const floatx16_t pa = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[0], ba[0], z, 0, 0, 0);
+    const floatx16_t pb = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[0], bb[0], z, 0, 0, 0);
+    const floatx16_t ka = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[2], ba[3], z, 0, 0, 0);
+    const floatx16_t kb = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[2], bb[3], z, 0, 0, 0);
+    const floatx16_t ua = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[1], ba[1], pa, 0, 0, 0);
+    const floatx16_t ub = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[1], bb[1], pb, 0, 0, 0);
+    const floatx16_t ra = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[3], ba[4], ka, 0, 0, 0);
+    const floatx16_t rb = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[3], bb[4], kb, 0, 0, 0);
+    const floatx16_t va = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[1], ba[2], pa, 0, 0, 0);
+    const floatx16_t vb = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[1], bb[2], pb, 0, 0, 0);
+    const floatx16_t ia = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[4], ba[5], ka, 0, 0, 0);
+    const floatx16_t ib = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[4], bb[5], kb, 0, 0, 0);
+    float ya[16], yb[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        ya[i] = __builtin_fmaf(__builtin_fmaxf(ua[i] + __builtin_fabsf(ra[i]), va[i] + __builtin_fabsf(ia[i])), 2.0f, ny[i]);
+        yb[i] = __builtin_fmaf(__builtin_fmaxf(ub[i] + __builtin_fabsf(rb[i]), vb[i] + __builtin_fabsf(ib[i])), 2.0f, ny[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < 16; i += 2) {
+        ma = __builtin_fmaxf(__builtin_fmaxf(ma, ya[i]), ya[i + 1]);
+        mb = __builtin_fmaxf(__builtin_fmaxf(mb, yb[i]), yb[i + 1]);
+    }
 }
 
 template <int VAR>
@@ -532,7 +617,11 @@ __device__ inline float dft_tile_max(const half8_t (&af)[DftForm<VAR>::KS], cons
     if constexpr (DftForm<VAR>::F5) {
         static_assert((VAR & 1) != 0, "the five-MFMA form has no guarded fast path");
         (void)fast;
-        return dft_tile_max5(af, bf, ny, m);
+        return dft_tile_max5<(VAR & kDftScalar) == 0>(af, bf, ny, m);
+    } else if constexpr (DftForm<VAR>::F6) {
+        static_assert((VAR & 1) != 0, "the six-MFMA form has no guarded fast path");
+        (void)fast;
+        return dft_tile_max6(af, bf, ny, m);
     } else {
         return dft_tile_max4<VAR>(af, bf, ny, fast, m);
     }
@@ -697,18 +786,20 @@ __global__ void __launch_bounds__(64 * WAVES) search_dft(DftArgs d)
 // constants are read from LDS once for both blocks, half the LDS bytes per (block, tile) pair.
 // 3 waves per SIMD (3 workgroups per CU) instead of 4.
 // ---------------------------------------------------------------------------
-template <bool HITS>
-__global__ void __launch_bounds__(256, 3) search_dft2(DftArgs d)
+// F6: the six-MFMA form (dft_tile_max6x2), 2 waves per SIMD
+template <bool HITS, bool F6 = false>
+__global__ void __launch_bounds__(256, F6 ? 2 : 3) search_dft2(DftArgs d)
 {
     const MfmaSearchArgs& a = d.m;
-    constexpr int KS = 4, VAR = 1 | kDftChain;
+    constexpr int VAR = 1 | kDftChain | (F6 ? kDft6 : 0);
+    constexpr int KS = DftForm<VAR>::KS, NBF = DftForm<VAR>::NBF;
     constexpr int STAGE = kTilesPerStage * KS * 64 + kTilesPerStage * 8;
     __shared__ uint4 lds0[STAGE];
     __shared__ uint4 lds1[STAGE];
     const uint4 wk = a.work[blockIdx.x];
     const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
     bool act[2];
-    half8_t bf[2][kDftRangeFrags];
+    half8_t bf[2][NBF];
     float hl[2] = {0.0f, 0.0f}, best[2];
     uint32_t btile[2] = {0u, 0u};
 #pragma unroll
@@ -717,21 +808,21 @@ __global__ void __launch_bounds__(256, 3) search_dft2(DftArgs d)
         act[k] = b < wk.y;
         const uint32_t blk = wk.x + (act[k] ? b : 0u);
 #pragma unroll
-        for (int f = 0; f < kDftRangeFrags; ++f)
-            bf[k][f] = __builtin_bit_cast(half8_t, a.rfrags[((size_t)blk * kDftRangeFrags + f) * 64 + lane]);
+        for (int f = 0; f < NBF; ++f)
+            bf[k][f] = __builtin_bit_cast(half8_t, a.rfrags[((size_t)blk * NBF + f) * 64 + lane]);
         if constexpr (HITS)
             hl[k] = (float)((int32_t)a.rconst[blk * 32 + (lane & 31u)] - (int32_t)a.hitH);
         best[k] = -__builtin_inff();
     }
     const uint32_t h = lane >> 5;
     auto compute = [&](const uint4* la, uint32_t nt, uint32_t tb) {
-        const uint4* lc = la + nt * 4u * 64u;
+        const uint4* lc = la + nt * (uint32_t)KS * 64u;
         float cm[2] = {-__builtin_inff(), -__builtin_inff()};
         for (uint32_t q = 0; q < nt; ++q) {
-            half8_t af[4];
+            half8_t af[KS];
 #pragma unroll
-            for (int s = 0; s < 4; ++s)
-                af[s] = __builtin_bit_cast(half8_t, la[(q * 4 + s) * 64 + lane]);
+            for (int s = 0; s < KS; ++s)
+                af[s] = __builtin_bit_cast(half8_t, la[(q * KS + s) * 64 + lane]);
             floatx16_t ny;
 #pragma unroll
             for (int c4 = 0; c4 < 4; ++c4) {
@@ -741,9 +832,13 @@ __global__ void __launch_bounds__(256, 3) search_dft2(DftArgs d)
                 ny[4 * c4 + 2] = __uint_as_float(v.z);
                 ny[4 * c4 + 3] = __uint_as_float(v.w);
             }
+            if constexpr (F6) {
+                dft_tile_max6x2(af, bf[0], bf[1], ny, cm[0], cm[1]);
+            } else {
 #pragma unroll
-            for (int k = 0; k < 2; ++k)
-                cm[k] = dft_tile_max<VAR>(af, bf[k], ny, false, cm[k]);
+                for (int k = 0; k < 2; ++k)
+                    cm[k] = dft_tile_max<VAR>(af, bf[k], ny, false, cm[k]);
+            }
         }
 #pragma unroll
         for (int k = 0; k < 2; ++k) {

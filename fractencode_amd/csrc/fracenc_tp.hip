@@ -96,7 +96,8 @@ __global__ void __launch_bounds__(256) tp_build_tiles(TpBuckets bk, const uint32
                                                       const uint32_t* __restrict__ spos, uint32_t ntiles,
                                                       int32_t* __restrict__ tile_pos, uint2* __restrict__ tile_sd,
                                                       uint32_t* __restrict__ row_of, uint4* __restrict__ dtiles,
-                                                      uint32_t* __restrict__ dconst, uint2* __restrict__ tguard)
+                                                      uint32_t* __restrict__ dconst, uint2* __restrict__ tguard,
+                                                      uint32_t ks)
 {
     const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
     if (gid >= ntiles * 32u)
@@ -112,11 +113,10 @@ __global__ void __launch_bounds__(256) tp_build_tiles(TpBuckets bk, const uint32
     if (valid) {
         row_of[p] = gid;
     } else {
-#pragma unroll
-        for (int st = 0; st < 4; ++st)
+        for (uint32_t st = 0; st < ks; ++st) // ks fragments per tile (the Fourier form's layout)
 #pragma unroll
             for (int h = 0; h < 2; ++h)
-                dtiles[((size_t)tile * 4 + st) * 64 + row + 32 * h] = make_uint4(0u, 0u, 0u, 0u);
+                dtiles[((size_t)tile * ks + st) * 64 + row + 32 * h] = make_uint4(0u, 0u, 0u, 0u);
         const uint32_t hh = (row >> 2) & 1u, i = (row & 3u) + 4u * (row >> 3);
         dconst[(size_t)tile * 32 + hh * 16 + i] = __float_as_uint(kDftPadY);
     }

@@ -265,7 +265,7 @@ DFT_CASES = [
 ]
 
 
-@pytest.mark.parametrize("dft", ["1", "0", "1/20"])
+@pytest.mark.parametrize("dft", ["1", "0", "1/20", "1/21", "1/23"])
 @pytest.mark.parametrize("case", range(len(DFT_CASES)))
 def test_mfma_fourier_and_direct_match_oracle(oracle, monkeypatch, case, dft):
     # "1/20": the five-MFMA Fourier form (FRAC_MFMA_VARIANT=20)
@@ -308,7 +308,7 @@ def _extreme_plane(rng, S, kind):
     return out.astype(np.uint8)
 
 
-@pytest.mark.parametrize("var", ["20"])
+@pytest.mark.parametrize("var", ["20", "21", "22", "23"])
 @pytest.mark.parametrize("kind", ["binary", "blocks8", "blocks2", "orbits"])
 def test_five_mfma_form_at_operand_extremes(monkeypatch, kind, var):
     """The five-MFMA Fourier form (FRAC_MFMA_VARIANT=20) has the tightest exactness margins (2Pr /
@@ -505,7 +505,7 @@ def test_encode_defaults_are_the_reference_cli_defaults():
     assert st["rejected_mappings"] == meta["rejected"]
 
 
-PRODUCT_VARIANTS = ("0", "1", "2", "3", "4", "5", "6", "7", "12", "20", "32", "64", "96", "98", "128", "130")
+PRODUCT_VARIANTS = ("0", "1", "2", "3", "4", "5", "6", "7", "12", "20", "21", "22", "23", "32", "64", "96", "98", "128", "130")
 
 
 @pytest.mark.parametrize("n,T,dft", [(8, 4, "0"), (4, 4, "0"), (8, 8, "0"), (8, 4, "1")])
