@@ -486,6 +486,20 @@ inline bool dft_four_wave(int var)
 constexpr int kTpVar = 1 | kDftChain | (kDftTpForm == 6 ? kDft6 : 0); // the SEA tiled form's search_dft
 constexpr uint32_t kTpKS = kDftTpForm == 4 ? 4u : 5u;                    // its domain fragments per tile
 inline int dft_form(int var) { return var == 20 || var == 22 ? 5 : var == 21 || var == 23 ? 6 : 4; }
+// The Fourier path's own variants: 1, 3 (4-wave exact / guarded), 5 (8-tile stages), 6 (pairwise-tree
+// row maximum), 12 (two range blocks per wave), 20 / 22 (five-MFMA form, packed / plain epilogue),
+// 21 / 23 (six-MFMA form, one / two range blocks per wave), 24 (the 8-MFMA exact form in 8-wave
+// workgroups) and the tuning ablations.  Every other value (the default, and the direct form's
+// schedule knobs) runs kDftDefaultVariant.
+constexpr int kDftDefaultVariant = 21; // the six-MFMA form: 13.71 vs 15.23 ms (24) at C3, 12-round A/B
+inline int dft_variant(int var)
+{
+    static const int own[] = {1, 3, 5, 6, 12, 20, 21, 22, 23, 24, 9, 17, 41, 65, 73, 105};
+    for (int v : own)
+        if (var == v)
+            return var;
+    return var >= 200 ? var : kDftDefaultVariant;
+}
 
 int prepare(frac_ctx* c)
 {
@@ -973,7 +987,7 @@ inline int mfma_variant(frac_ctx* c, int& var)
         return FRAC_OK;
     char* end = nullptr;
     const long x = strtol(v, &end, 10);
-    static const int exact[] = {0, 1, 2, 3, 4, 5, 6, 7, 12, 20, 21, 22, 23, 32, 64, 96, 98, 128, 130};
+    static const int exact[] = {0, 1, 2, 3, 4, 5, 6, 7, 12, 20, 21, 22, 23, 24, 32, 64, 96, 98, 128, 130};
     static const int ablation[] = {8, 9, 16, 17, 41, 65, 73, 105, 201, 202, 203, 204, 205, 206, 207};
     bool ok = end && *end == 0;
     bool known = false;
@@ -1048,6 +1062,7 @@ inline int launch_dft(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride)
     // values ≥ 9 = ablations of variant 1 (tuning only: wrong results)
     int var = 0;
     FRAC_TRY(mfma_variant(c, var));
+    var = dft_variant(var);
     const int form = dft_form(var);
     const bool f5 = form != 4; // five domain fragments per tile (forms 5 and 6)
     FRAC_HIP(c, c->d_m_dtiles.ensure(std::max<size_t>((size_t)c->ntiles * (f5 ? 5 : 4) * 64, 1)));

@@ -121,7 +121,7 @@ constexpr int kDftScalar = 4096; // with kDft5: the P ± M and the fma one row p
 constexpr int kDft6 = 8192;      // the six-MFMA form (dft_tile_max6)
 
 // the form the SEA engine's tiled search (fracenc_tp.hip) runs: 4 or 6
-constexpr int kDftTpForm = 4;
+constexpr int kDftTpForm = 6;
 
 template <int VAR>
 struct DftForm {

@@ -505,7 +505,7 @@ def test_encode_defaults_are_the_reference_cli_defaults():
     assert st["rejected_mappings"] == meta["rejected"]
 
 
-PRODUCT_VARIANTS = ("0", "1", "2", "3", "4", "5", "6", "7", "12", "20", "21", "22", "23", "32", "64", "96", "98", "128", "130")
+PRODUCT_VARIANTS = ("0", "1", "2", "3", "4", "5", "6", "7", "12", "20", "21", "22", "23", "24", "32", "64", "96", "98", "128", "130")
 
 
 @pytest.mark.parametrize("n,T,dft", [(8, 4, "0"), (4, 4, "0"), (8, 8, "0"), (8, 4, "1")])
