@@ -18,11 +18,16 @@
 //
 //   y = 8·max_t Z_t − Σb²  =  16Σa² − min_t S16                      (one GEMM per tile)
 //
-// Cost per (32 domains × 32 ranges): 8 MFMA 32x32x16 (U, U', Pr, Pi with K = 32) instead of
-// the direct T·n²/16 = 16, and 3 VALU per (range, domain) on the fast path (below) instead
-// of 4 transforms × 1.5.
+// Forms (the tile functions below; the default is the six-MFMA form, kDft6, dft_tile_max6):
+//   8-MFMA form  U, U', Pr, Pi as K = 32 GEMMs (8 MFMA 32x32x16 per 32 domains × 32 ranges);
+//   five-MFMA    the DFT's real bins P = U + U', M = U − U' (K = 16 each) and the complex bin by
+//                Gauss's three products, P ± M on the VALU (kDft5);
+//   six-MFMA     the same with M accumulated onto P inside the MFMA (2U, 2U'): 6 MFMA and the
+//                exact epilogue's 4.5 VALU per (range, domain) — against the direct form's
+//                T·n²/16 = 16 MFMA and 4 transforms × 1.5 VALU.
+// Their operand bounds are stated with kDft5 / kDft6; the 8-MFMA form's follow.
 //
-// Exactness (f16 operands, f32 accumulate, all values integers):
+// Exactness of the 8-MFMA form (f16 operands, f32 accumulate, all values integers):
 //   operands  |s_a|,|u_a| ≤ 256, |4s_a| ≤ 1024, |α|,|β| ≤ 255; |s_b|,|u_b| ≤ 1024,
 //             |γ|,|δ| ≤ 1020 — integers of magnitude ≤ 2048 are exact in f16;
 //   products  every partial sum of U, U' (32 terms ≤ 2^18) and Pr, Pi (32 terms ≤ 2^18) is
