@@ -63,7 +63,28 @@ def parse():
     ap.add_argument("--alt-steps", type=int, default=2,
                     help="steps of the VALU engine (north_star's no-MFMA formulation) reported beside (0 = skip)")
     ap.add_argument("--e2e-steps", type=int, default=-1, help="steps of the host-boundary leg (-1 = --steps)")
+    ap.add_argument("--ab", action="store_true",
+                    help="allow FRAC_LIB / A/B knobs in the environment (the line is then marked, not a headline)")
     return ap.parse_args()
+
+
+# environment knobs the library (or the package) reads that change which code runs: the headline
+# refuses them (an A/B run passes --ab and is marked as such); every FRAC_* variable in effect is
+# echoed into the line's config
+AB_KNOBS = ("FRAC_LIB", "FRAC_MFMA_VARIANT", "FRAC_MFMA_DFT", "FRAC_DFT_WGS", "FRAC_XCD_ORDER", "FRAC_SEA_TILED",
+            "FRAC_DECODE_UNFUSED")
+
+
+def frac_env() -> dict:
+    return {k: v for k, v in sorted(os.environ.items()) if k.startswith("FRAC_")}
+
+
+def check_headline_env(args) -> list:
+    knobs = [k for k in AB_KNOBS if k in os.environ]
+    if knobs and not args.ab:
+        raise SystemExit(f"bench.py: {', '.join(knobs)} set: the headline runs the product library with no A/B "
+                         "knob (pass --ab for an A/B run)")
+    return knobs
 
 
 def launch_ranks(args) -> int:
@@ -145,8 +166,10 @@ def load_traffic(form: str):
     e = d.get(form)
     if e is None:
         return None, f"no PMC entry for form {form}"
-    if e.get("source_id") != lib_sha16():
-        return None, f"PMC entry is from sources {e.get('source_id')}, not this build's"
+    import fractencode_amd as F
+
+    if e.get("source_id") != F.build_info()["build_id"]:
+        return None, f"PMC entry is from build {e.get('source_id')}, not this library's"
     return e.get("hbm_bytes_per_launch"), e.get("source")
 
 
@@ -158,6 +181,11 @@ def main(args):
     from fractencode_amd.distributed import TUPLE_BYTES, gather_tuples, plan_capacity, shard_plan
     from fractencode_amd.synth import value_noise
 
+    knobs = check_headline_env(args)
+    build = F.build_info()
+    if not build["matches_sources"] and not args.ab:
+        raise SystemExit(f"bench.py: the library was built from sources {build['build_id']}, these are "
+                         f"{F.source_id()}: rebuild (__graft_entry__.build())")
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -219,7 +247,8 @@ def main(args):
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     hist = eng.timing_history()  # per-run HIP events of the K timed steps (on the kernel's stream)
-    assert len(hist) == args.steps, (len(hist), args.steps)
+    # the library keeps the last 256 runs: with more steps the mean is over the last 256 of them
+    assert len(hist) == min(args.steps, 256), (len(hist), args.steps)
     _, st = eng.fetch()
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -273,12 +302,14 @@ def main(args):
         "data": "synthetic",
         "config": {"workload": f"C3: {S}x{S} S1 value-noise frame (seed 1234), 8x8 ranges ({nr_total}), "
                                f"16x16 domains stride 8 ({n_d}), T={args.transforms}, exhaustive, rms 0",
-                   "engine": engine_name, "ranges_per_gpu": len(mine), "parallelism": f"ranges/{world}"},
+                   "engine": engine_name, "ranges_per_gpu": len(mine), "parallelism": f"ranges/{world}",
+                   "env": frac_env(), "ab_run": bool(knobs)},
         "roofline": roof,
         "search_form": form,
         "phases_ms": {k: round(float(np.mean(hist["ms_" + k])), 3) for k in ("device", "prep", "search", "finish")},
         "fallback_ranges": st["fallback_ranges"],
         "source_id": lib_sha16(),
+        "build": build,  # the loaded library's compiled-in id (frac_build_id): the binary that ran
     }
 
     main_out, _ = eng.fetch()  # the timed steps' records (the SEA engine is checked against them)

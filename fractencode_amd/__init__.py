@@ -20,8 +20,11 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-# FRAC_LIB: an explicitly built alternative (tools/build_tuning.py's A/B library); the product is libfracenc.so
-LIB_PATH = os.environ.get("FRAC_LIB") or os.path.join(HERE, "libfracenc.so")
+# FRAC_LIB: an explicitly built alternative (tools/build_tuning.py's A/B library); the product is libfracenc.so.
+# build_info() reports which library was loaded and whether it is a tuning build; bench.py refuses the
+# headline with FRAC_LIB set.
+PRODUCT_LIB = os.path.join(HERE, "libfracenc.so")
+LIB_PATH = os.environ.get("FRAC_LIB") or PRODUCT_LIB
 
 GRID_ITEM = np.dtype([("x", "<u4"), ("y", "<u4"), ("w", "<u4"), ("h", "<u4"), ("category", "<i4")])
 ENCODE_ITEM = np.dtype([("x", "<u4"), ("y", "<u4"), ("w", "<u4"), ("h", "<u4"),
@@ -103,10 +106,16 @@ def lib() -> C.CDLL:
             import torch  # noqa: F401
         except ImportError:
             pass
+        if LIB_PATH != PRODUCT_LIB:
+            import warnings
+
+            warnings.warn(f"fractencode_amd: FRAC_LIB loads {LIB_PATH}, not the product library", stacklevel=2)
         L = C.CDLL(LIB_PATH)
         vp, u32, i32, sz = C.c_void_p, C.c_uint32, C.c_int, C.c_size_t
         sig = {
             "frac_abi_version": (i32, []),
+            "frac_build_id": (C.c_char_p, []),
+            "frac_build_flags": (i32, []),
             "frac_create": (vp, [i32, C.POINTER(FracParams)]),
             "frac_destroy": (None, [vp]),
             "frac_last_error": (C.c_char_p, [vp]),
@@ -148,6 +157,18 @@ def lib() -> C.CDLL:
             f.argtypes = args
         _lib = L
     return _lib
+
+
+BUILD_TUNING = 1
+
+
+def build_info() -> dict:
+    """The loaded library: its path, the source id compiled into it (frac_build_id), whether it is
+    a -DFRAC_TUNING build, and whether that id is the id of the sources next to it."""
+    L = lib()
+    bid = L.frac_build_id().decode()
+    return {"lib": os.path.relpath(LIB_PATH, os.path.dirname(HERE)), "build_id": bid,
+            "tuning": bool(L.frac_build_flags() & BUILD_TUNING), "matches_sources": bid == source_id()}
 
 
 def last_error(ctx=None) -> str:

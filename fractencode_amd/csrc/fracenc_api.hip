@@ -485,16 +485,17 @@ inline bool dft_four_wave(int var)
 // 6 (kDft6, variants 21, 23)
 constexpr int kTpVar = 1 | kDftChain | (kDftTpForm == 6 ? kDft6 : 0); // the SEA tiled form's search_dft
 constexpr uint32_t kTpKS = kDftTpForm == 4 ? 4u : 5u;                    // its domain fragments per tile
-inline int dft_form(int var) { return var == 20 || var == 22 ? 5 : var == 21 || var == 23 ? 6 : 4; }
+inline int dft_form(int var) { return var == 20 || var == 22 ? 5 : var == 21 || var == 23 || var == 26 ? 6 : 4; }
 // The Fourier path's own variants: 1, 3 (4-wave exact / guarded), 5 (8-tile stages), 6 (pairwise-tree
 // row maximum), 12 (two range blocks per wave), 20 / 22 (five-MFMA form, packed / plain epilogue),
 // 21 / 23 (six-MFMA form, one / two range blocks per wave), 24 (the 8-MFMA exact form in 8-wave
-// workgroups) and the tuning ablations.  Every other value (the default, and the direct form's
+// workgroups), 26 (the six-MFMA form with the guarded constant-folded epilogue, kDftFast6) and the
+// tuning ablations.  Every other value (the default, and the direct form's
 // schedule knobs) runs kDftDefaultVariant.
 constexpr int kDftDefaultVariant = 21; // the six-MFMA form: 13.71 vs 15.23 ms (24) at C3, 12-round A/B
 inline int dft_variant(int var)
 {
-    static const int own[] = {1, 3, 5, 6, 12, 20, 21, 22, 23, 24, 9, 17, 41, 65, 73, 105};
+    static const int own[] = {1, 3, 5, 6, 12, 20, 21, 22, 23, 24, 26, 9, 17, 41, 65, 73, 105};
     for (int v : own)
         if (var == v)
             return var;
@@ -987,8 +988,8 @@ inline int mfma_variant(frac_ctx* c, int& var)
         return FRAC_OK;
     char* end = nullptr;
     const long x = strtol(v, &end, 10);
-    static const int exact[] = {0, 1, 2, 3, 4, 5, 6, 7, 12, 20, 21, 22, 23, 24, 32, 64, 96, 98, 128, 130};
-    static const int ablation[] = {8, 9, 16, 17, 41, 65, 73, 105, 201, 202, 203, 204, 205, 206, 207};
+    static const int exact[] = {0, 1, 2, 3, 4, 5, 6, 7, 12, 20, 21, 22, 23, 24, 26, 32, 64, 96, 98, 128, 130};
+    static const int ablation[] = {8, 9, 16, 17, 41, 65, 73, 105, 201, 202, 203, 204, 205, 206, 207, 226, 227};
     bool ok = end && *end == 0;
     bool known = false;
     for (int e : exact)
@@ -1135,6 +1136,12 @@ inline int launch_dft(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride)
             case 204: search_dft<false, 521, W8><<<nwg, 64 * W8, 0, c->stream>>>(da); break; // MFMA-only, no barrier
             case 205: search_dft<false, 257, W8><<<nwg, 64 * W8, 0, c->stream>>>(da); break; // full, no DMA
             case 206: search_dft<false, 513, W8><<<nwg, 64 * W8, 0, c->stream>>>(da); break; // full, no barrier
+            case 226: // the guarded six-MFMA form (26), no barrier
+                search_dft<false, 1 | kDftChain | kDft6 | kDftFast6 | 512, W8><<<nwg, 64 * W8, 0, c->stream>>>(da);
+                break;
+            case 227: // the guarded six-MFMA form (26), no LDS-DMA / barrier after the first stages
+                search_dft<false, 1 | kDftChain | kDft6 | kDftFast6 | 64, W8><<<nwg, 64 * W8, 0, c->stream>>>(da);
+                break;
             default: search_dft<false, 65, W8><<<nwg, 64 * W8, 0, c->stream>>>(da); break;  // full, no DMA/bar
             }
 #endif
@@ -1143,6 +1150,11 @@ inline int launch_dft(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride)
                 search_dft2<true, true><<<nwg, 256, 0, c->stream>>>(da);
             else
                 search_dft2<false, true><<<nwg, 256, 0, c->stream>>>(da);
+        } else if (form == 6 && var == 26) { // the six-MFMA form, guarded constant-folded epilogue
+            if (hits)
+                search_dft<true, 1 | kDftChain | kDft6 | kDftFast6, W8><<<nwg, 64 * W8, 0, c->stream>>>(da);
+            else
+                search_dft<false, 1 | kDftChain | kDft6 | kDftFast6, W8><<<nwg, 64 * W8, 0, c->stream>>>(da);
         } else if (form == 6) { // the six-MFMA form
             if (hits)
                 search_dft<true, 1 | kDftChain | kDft6, W8><<<nwg, 64 * W8, 0, c->stream>>>(da);
@@ -1820,6 +1832,15 @@ int launch_all(frac_ctx* c)
 extern "C" {
 
 int frac_abi_version(void) { return FRAC_ABI_VERSION; }
+
+// The source id build() compiles in (-DFRAC_SOURCE_ID="…": the hash fractencode_amd.source_id()
+// computes over csrc/ and include/fracenc.h), so a result can name the binary that produced it.
+#ifndef FRAC_SOURCE_ID
+#define FRAC_SOURCE_ID "unknown"
+#endif
+const char* frac_build_id(void) { return FRAC_SOURCE_ID; }
+
+int frac_build_flags(void) { return kTuningBuild ? FRAC_BUILD_TUNING : 0; }
 
 const char* frac_last_error(const frac_ctx* ctx) { return ctx ? ctx->err.c_str() : g_last_error.c_str(); }
 

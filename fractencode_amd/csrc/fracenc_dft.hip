@@ -124,6 +124,25 @@ constexpr int kDftRangeFrags = 7;     // s, u, 4s, 4u, α, β, −α
 constexpr int kDft5 = 2048;
 constexpr int kDftScalar = 4096; // with kDft5: the P ± M and the fma one row per instruction
 constexpr int kDft6 = 8192;      // the six-MFMA form (dft_tile_max6)
+constexpr int kDftFast6 = 16384; // with kDft6: the guarded constant-folded epilogue (dft_tile_max6_fast)
+
+// The five- and six-MFMA forms track h = y/2 = 4·max_t Z_t − Σb²/2 instead of y: the row constant
+// (dconst) is −Σb²/2 — exact in f32 (Σb² ≤ 2^24, so a half-integer of magnitude ≤ 2^23) — and the
+// epilogue adds it instead of an fma by 2.  The entries keep y (= 2h, exact: a power-of-two scale),
+// so resolve_dft and the SEA tiled form read them unchanged.
+//
+// The guarded fast path of the six-MFMA form (kDftFast6) starts the P GEMM from C = −Σb²/2, so
+// both accumulators built on P carry the constant: u' = 2U − Σb²/2, v' = 2U' − Σb²/2, and
+//   h = max(u' + |2Pr|, v' + |2Pi|)      — 2 v_add + 1 v_max3 per candidate instead of 4.5 VALU.
+// Exactness: every partial sum of u', v' (C included, any accumulation order) is a half-integer of
+// magnitude ≤ Σb²/2 + Σ_o(|A0||B0| + |A2||B2|) ≤ Σb²/2 + R6·D6, with R6 = Σ_o(|s_a + u_a| + |s_a − u_a|)
+// per range and D6 = max_o max(|s_b + u_b|, |s_b − u_b|) per domain; f32 holds every half-integer
+// below 2^23, so the partial sums are exact whenever 2·R6·D6 + Σb² < 2^24.  The guard is taken per
+// (range block, domain tile) from the block's max R6 (rguard) and the tile's max 2·D6 and max Σb²
+// (tguard); a tile pair that fails it runs the exact epilogue.  2Pr, 2Pi are exact as in kDft5, and
+// u' + |2Pr| = 4·max(Z_0, Z_2) − Σb²/2 is one rounding of exact operands — the exact-form argument
+// (exact in the exact regime, monotone beyond it) holds unchanged.
+constexpr int64_t kFast6Limit = (1ll << 24) - 1; // 2·R6·D6 + Σb² ≤ this
 
 // the form the SEA engine's tiled search (fracenc_tp.hip) runs: 4 or 6
 constexpr int kDftTpForm = 6;
@@ -132,14 +151,18 @@ template <int VAR>
 struct DftForm {
     static constexpr bool F5 = (VAR & kDft5) != 0;
     static constexpr bool F6 = (VAR & kDft6) != 0;
+    static constexpr bool FAST6 = F6 && (VAR & kDftFast6) != 0;
+    static constexpr bool HALF = F5 || F6;                        // tracks h = y/2 (row constant −Σb²/2)
     static constexpr int KS = (F5 || F6) ? 5 : 4;                 // domain fragments per tile
     static constexpr int NBF = F6 ? 6 : F5 ? 5 : kDftRangeFrags; // range fragments per block
 };
 
 struct DftArgs {
     MfmaSearchArgs m;
-    uint32_t* rguard;     // [nblocks]  max over the block's ranges of R1 = Σ_o(|s_a| + |u_a|)
-    uint2* tguard;        // [ntiles]   {max 4·D∞, max Σb²} over the tile's valid rows
+    uint32_t* rguard;     // [nblocks]  max over the block's ranges of R1 = Σ_o(|s_a| + |u_a|) (six-MFMA
+                          //            form: R6 = Σ_o(|s_a + u_a| + |s_a − u_a|))
+    uint2* tguard;        // [ntiles]   {max 4·D∞, max Σb²} over the tile's valid rows (five- / six-MFMA
+                          //            layout: {max 2·D6, max Σb²})
     const uint32_t* choff; // CHUNKED: [work] first chunk entry of the work item (fracenc_tp.hip)
 };
 
@@ -260,7 +283,8 @@ __global__ void __launch_bounds__(256) dft_domain_build(MfmaDomainPrepArgs a, Df
     for (int o = 0; o < NO; ++o) {
         const int b0 = b[kOrb8.p[o][0]], b1 = b[kOrb8.p[o][1]], b2 = b[kOrb8.p[o][2]], b3 = b[kOrb8.p[o][3]];
         const int sb = b0 + b2, ub = b1 + b3, gb = b0 - b2, db = b1 - b3;
-        dinf = max(dinf, max(abs(sb), abs(ub)));
+        // guard term: D∞ = max(|s_b|, |u_b|) (8-MFMA form); D6 = max(|s_b + u_b|, |s_b − u_b|) (F5 layout)
+        dinf = F5 ? max(dinf, max(abs(sb + ub), abs(sb - ub))) : max(dinf, max(abs(sb), abs(ub)));
         if constexpr (F5) {
             comp[0][o] = (_Float16)(sb + ub);
             comp[1][o] = (_Float16)(sb - ub);
@@ -284,10 +308,12 @@ __global__ void __launch_bounds__(256) dft_domain_build(MfmaDomainPrepArgs a, Df
                 v8[j] = comp[st][8 * h + j];
             a.dtiles[((size_t)tile * KS + st) * 64 + row + 32 * h] = __builtin_bit_cast(uint4, v8);
         }
-    const float ny = p >= 0 ? -(float)sb2 : kDftPadY;
+    // the row constant: −Σb² (8-MFMA form, tracks y), −Σb²/2 (F5 layout: the five- and six-MFMA
+    // forms track h = y/2; exact, Σb² ≤ 2^24)
+    const float ny = p >= 0 ? (F5 ? -0.5f * (float)sb2 : -(float)sb2) : kDftPadY;
     const uint32_t h = (row >> 2) & 1u, i = (row & 3u) + 4u * (row >> 3);
     a.dconst[(size_t)tile * 32 + h * 16 + i] = __float_as_uint(ny);
-    uint32_t gx = p >= 0 ? (uint32_t)(4 * dinf) : 0u, gy = p >= 0 ? (uint32_t)sb2 : 0u;
+    uint32_t gx = p >= 0 ? (uint32_t)((F5 ? 2 : 4) * dinf) : 0u, gy = p >= 0 ? (uint32_t)sb2 : 0u;
     if constexpr (BYPOS) {
         atomicMax(&tguard[tile].x, gx);
         atomicMax(&tguard[tile].y, gy);
@@ -356,7 +382,8 @@ __global__ void __launch_bounds__(256) dft_range_prep(MfmaRangePrepArgs a, uint3
     for (int o = 0; o < NO; ++o) {
         const int a0 = av[kOrb8.p[o][0]], a1 = av[kOrb8.p[o][1]], a2 = av[kOrb8.p[o][2]], a3 = av[kOrb8.p[o][3]];
         const int sa = a0 + a2, ua = a1 + a3, al = a0 - a2, be = a1 - a3;
-        r1 += abs(sa) + abs(ua);
+        // guard term: R1 = Σ(|s_a| + |u_a|); the six-MFMA form's R6 = Σ(|s_a + u_a| + |s_a − u_a|)
+        r1 += FORM == 6 ? abs(sa + ua) + abs(sa - ua) : abs(sa) + abs(ua);
         if constexpr (FORM == 5) {
             comp[0][o] = (_Float16)(sa + ua);
             comp[1][o] = (_Float16)(sa - ua);
@@ -450,7 +477,7 @@ __device__ inline float dft_tile_max5(const half8_t (&af)[5], const half8_t (&bf
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
             const float X = p[i] + q[i], Xp = p[i] - q[i];
-            y[i] = __builtin_fmaf(__builtin_fmaxf(X + __builtin_fabsf(pr[i]), Xp + __builtin_fabsf(pi[i])), 2.0f, ny[i]);
+            y[i] = __builtin_fmaxf(X + __builtin_fabsf(pr[i]), Xp + __builtin_fabsf(pi[i])) + ny[i]; // h
         }
 #pragma unroll
         for (int i = 0; i < 16; i += 2)
@@ -465,7 +492,7 @@ __device__ inline float dft_tile_max5(const half8_t (&af)[5], const half8_t (&bf
         const float2v_t t = {__builtin_fmaxf(X.x + __builtin_fabsf(pr[i]), Xp.x + __builtin_fabsf(pi[i])),
                              __builtin_fmaxf(X.y + __builtin_fabsf(pr[i + 1]), Xp.y + __builtin_fabsf(pi[i + 1]))};
         const float2v_t N2 = {ny[i], ny[i + 1]};
-        const float2v_t yy = __builtin_elementwise_fma(t, (float2v_t){2.0f, 2.0f}, N2);
+        const float2v_t yy = t + N2; // h = y/2
         y[i] = yy.x;
         y[i + 1] = yy.y;
     }
@@ -481,7 +508,7 @@ __device__ inline float dft_tile_max5(const half8_t (&af)[5], const half8_t (&bf
 // accumulation order: with A0 = s_a + u_a, A2 = s_a − u_a (B0, B2 on the domain side),
 // |A0| + |A2| = 2·max(|s_a|, |u_a|) ≤ 512 and |B0|, |B2| ≤ 2048, so every partial sum of P ± M is
 // bounded by Σ_o (|A0·B0| + |A2·B2|) ≤ 16·2048·512 = 2^24.  Then the exact form's epilogue:
-//   y = fma(max(2U + |2Pr|, 2U' + |2Pi|), 2, −Σb²).
+//   h = max(2U + |2Pr|, 2U' + |2Pi|) − Σb²/2   (ny = −Σb²/2; y = 2h).
 __device__ inline float dft_tile_max6(const half8_t (&af)[5], const half8_t (&bf)[6], const floatx16_t& ny, float m)
 {
     const floatx16_t z = {};
@@ -494,10 +521,29 @@ __device__ inline float dft_tile_max6(const half8_t (&af)[5], const half8_t (&bf
     float y[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i)
-        y[i] = __builtin_fmaf(__builtin_fmaxf(u[i] + __builtin_fabsf(pr[i]), v[i] + __builtin_fabsf(pi[i])), 2.0f, ny[i]);
+        y[i] = __builtin_fmaxf(u[i] + __builtin_fabsf(pr[i]), v[i] + __builtin_fabsf(pi[i])) + ny[i];
 #pragma unroll
     for (int i = 0; i < 16; i += 2)
         m = __builtin_fmaxf(__builtin_fmaxf(m, y[i]), y[i + 1]);
+    return m;
+}
+
+// The guarded fast path (kDftFast6, exactness above kFast6Limit): P starts from C = −Σb²/2, so u' and
+// v' carry the row constant and a candidate costs u' + |2Pr|, v' + |2Pi| and one step of a v_max3
+// chain.  Only for tile pairs whose guard holds.
+__device__ inline float dft_tile_max6_fast(const half8_t (&af)[5], const half8_t (&bf)[6], const floatx16_t& ny,
+                                           float m)
+{
+    const floatx16_t z = {};
+    const floatx16_t k1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[2], bf[3], z, 0, 0, 0); // 2k1
+    const floatx16_t p = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[0], bf[0], ny, 0, 0, 0); // P − Σb²/2
+    const floatx16_t pr = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[3], bf[4], k1, 0, 0, 0); // 2Pr
+    const floatx16_t u = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[1], bf[1], p, 0, 0, 0);  // 2U − Σb²/2
+    const floatx16_t pi = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[4], bf[5], k1, 0, 0, 0); // 2Pi
+    const floatx16_t v = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[1], bf[2], p, 0, 0, 0);  // 2U' − Σb²/2
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+        m = __builtin_fmaxf(__builtin_fmaxf(m, u[i] + __builtin_fabsf(pr[i])), v[i] + __builtin_fabsf(pi[i]));
     return m;
 }
 
@@ -521,9 +567,9 @@ __device__ inline void dft_tile_max6x2(const half8_t (&af)[5], const half8_t (&b
     const floatx16_t ib = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[4], bb[5], kb, 0, 0, 0);
     float ya[16], yb[16];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        ya[i] = __builtin_fmaf(__builtin_fmaxf(ua[i] + __builtin_fabsf(ra[i]), va[i] + __builtin_fabsf(ia[i])), 2.0f, ny[i]);
-        yb[i] = __builtin_fmaf(__builtin_fmaxf(ub[i] + __builtin_fabsf(rb[i]), vb[i] + __builtin_fabsf(ib[i])), 2.0f, ny[i]);
+    for (int i = 0; i < 16; ++i) { // h = y/2 (ny = −Σb²/2)
+        ya[i] = __builtin_fmaxf(ua[i] + __builtin_fabsf(ra[i]), va[i] + __builtin_fabsf(ia[i])) + ny[i];
+        yb[i] = __builtin_fmaxf(ub[i] + __builtin_fabsf(rb[i]), vb[i] + __builtin_fabsf(ib[i])) + ny[i];
     }
 #pragma unroll
     for (int i = 0; i < 16; i += 2) {
@@ -624,7 +670,11 @@ __device__ inline float dft_tile_max(const half8_t (&af)[DftForm<VAR>::KS], cons
         (void)fast;
         return dft_tile_max5<(VAR & kDftScalar) == 0>(af, bf, ny, m);
     } else if constexpr (DftForm<VAR>::F6) {
-        static_assert((VAR & 1) != 0, "the six-MFMA form has no guarded fast path");
+        static_assert((VAR & 1) != 0, "the six-MFMA form's guarded path is kDftFast6");
+        if constexpr (DftForm<VAR>::FAST6) {
+            if (fast)
+                return dft_tile_max6_fast(af, bf, ny, m);
+        }
         (void)fast;
         return dft_tile_max6(af, bf, ny, m);
     } else {
@@ -634,11 +684,63 @@ __device__ inline float dft_tile_max(const half8_t (&af)[DftForm<VAR>::KS], cons
 
 // MASK (CHUNKED search): masks[0] gets the chunk tiles attaining the lane's maximum, masks[1]
 // (HITS) the tiles holding a hit (y ≥ hl), bit k for tile q0 + k
+__device__ inline floatx16_t lds_row_consts(const uint4* p)
+{
+    floatx16_t r;
+#pragma unroll
+    for (int c4 = 0; c4 < 4; ++c4) {
+        const uint4 v = p[c4];
+        r[4 * c4 + 0] = __uint_as_float(v.x);
+        r[4 * c4 + 1] = __uint_as_float(v.y);
+        r[4 * c4 + 2] = __uint_as_float(v.z);
+        r[4 * c4 + 3] = __uint_as_float(v.w);
+    }
+    return r;
+}
+
+// One tile pair of the six-MFMA form with the guarded fast path (kDftFast6).  Both paths issue
+// the same six MFMAs; only P's C operand differs — the tile's −Σb²/2 row constants when the guard
+// holds, the stage's zero block when it does not (a wave-uniform choice of address, so one MFMA
+// sequence and one register allocation serve both) — and the epilogue: the folded form
+// (2 VALU + one v_max3 step per candidate), or the exact one with the constants read after the
+// MFMAs.  lc: the tile's row constants ([2][16] lane-half layout), h: the lane half.
+__device__ inline float dft_tile_max6g(const half8_t (&af)[5], const half8_t (&bf)[6], const uint4* la, uint32_t ic,
+                                       uint32_t iz, uint32_t h, bool fast, float m)
+{
+    // one base pointer, a selected index: the compiler keeps the read's underlying LDS object and
+    // does not wait for the other stage buffer's pending LDS-DMA (a selected pointer made it)
+    const uint4* lc = la + ic;
+    const floatx16_t c = lds_row_consts(la + (fast ? ic : iz) + h * 4);
+    const floatx16_t z = {};
+    const floatx16_t k1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[2], bf[3], z, 0, 0, 0); // 2k1
+    const floatx16_t p = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[0], bf[0], c, 0, 0, 0);  // P (− Σb²/2)
+    const floatx16_t pr = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[3], bf[4], k1, 0, 0, 0); // 2Pr
+    const floatx16_t u = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[1], bf[1], p, 0, 0, 0);  // 2U (− Σb²/2)
+    const floatx16_t pi = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[4], bf[5], k1, 0, 0, 0); // 2Pi
+    const floatx16_t v = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[1], bf[2], p, 0, 0, 0);  // 2U' (− Σb²/2)
+    if (fast) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+            m = __builtin_fmaxf(__builtin_fmaxf(m, u[i] + __builtin_fabsf(pr[i])), v[i] + __builtin_fabsf(pi[i]));
+        return m;
+    }
+    const floatx16_t ny = lds_row_consts(lc + h * 4);
+    float y[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+        y[i] = __builtin_fmaxf(u[i] + __builtin_fabsf(pr[i]), v[i] + __builtin_fabsf(pi[i])) + ny[i];
+#pragma unroll
+    for (int i = 0; i < 16; i += 2)
+        m = __builtin_fmaxf(__builtin_fmaxf(m, y[i]), y[i + 1]);
+    return m;
+}
+
 template <int VAR, bool MASK = false, bool HITS = false>
 __device__ inline float dft_compute_stage(const uint4* __restrict__ la, uint32_t nt, uint32_t lane,
                                           const half8_t (&bf)[DftForm<VAR>::NBF], uint32_t tb,
                                           const uint2* __restrict__ tguard, uint32_t r1, uint32_t q0 = 0,
-                                          uint32_t q1 = ~0u, uint32_t* masks = nullptr, float hl = 0.0f)
+                                          uint32_t q1 = ~0u, uint32_t* masks = nullptr, float hl = 0.0f,
+                                          uint32_t iz = 0)
 {
     constexpr int KS = DftForm<VAR>::KS;
     const uint4* lc = la + nt * (uint32_t)KS * 64u;
@@ -646,12 +748,18 @@ __device__ inline float dft_compute_stage(const uint4* __restrict__ la, uint32_t
     float cm = -__builtin_inff();
     // the chunk's fast-path guards, loaded up front (wave-uniform scalar loads)
     uint32_t gfast = 0;
-    if constexpr ((VAR & 1) == 0) {
+    if constexpr ((VAR & 1) == 0 || DftForm<VAR>::FAST6) {
+        const uint64_t lim = DftForm<VAR>::FAST6 ? (uint64_t)kFast6Limit : (uint64_t)kExactLimit;
+        // the tile index is wave-uniform: readfirstlane makes these scalar loads, which the vmcnt
+        // waits of the stage's LDS-DMA do not serialise with
+        const uint32_t t0 = __builtin_amdgcn_readfirstlane(tb + q0), ne = __builtin_amdgcn_readfirstlane(min(q1, nt) - q0);
 #pragma unroll
         for (uint32_t k = 0; k < 4; ++k)
-            if (q0 + k < min(q1, nt)) {
-                const uint2 g = tguard[tb + q0 + k];
-                gfast |= ((uint64_t)r1 * g.x + g.y <= (uint64_t)kExactLimit) ? (1u << k) : 0u;
+            if (k < ne) {
+                const __attribute__((address_space(4))) uint32_t* gp =
+                    (const __attribute__((address_space(4))) uint32_t*)(uintptr_t)(tguard + t0 + k);
+                const uint32_t gx = gp[0], gy = gp[1];
+                gfast |= ((uint64_t)r1 * gx + gy <= lim) ? (1u << k) : 0u;
             }
     }
     auto tile = [&](uint32_t q) {
@@ -661,6 +769,10 @@ __device__ inline float dft_compute_stage(const uint4* __restrict__ la, uint32_t
 #pragma unroll
         for (int s = 0; s < KS; ++s)
             af[s] = __builtin_bit_cast(half8_t, la[(qq * KS + s) * 64 + lane]);
+        if constexpr (DftForm<VAR>::FAST6 && !MASK) {
+            cm = dft_tile_max6g(af, bf, la, nt * (uint32_t)KS * 64u + qq * 8, iz, h, (gfast >> (q - q0)) & 1u, cm);
+            return;
+        }
         floatx16_t ny;
 #pragma unroll
         for (int c4 = 0; c4 < 4; ++c4) {
@@ -703,8 +815,16 @@ __global__ void __launch_bounds__(64 * WAVES) search_dft(DftArgs d)
     constexpr int KS = DftForm<VAR>::KS, NBF = DftForm<VAR>::NBF;
     constexpr uint32_t kTilesPerStage = TPS; // LDS stage; chunks stay 4 tiles (resolve_dft)
     constexpr int STAGE = kTilesPerStage * KS * 64 + kTilesPerStage * 8;
-    __shared__ uint4 lds0[STAGE];
-    __shared__ uint4 lds1[STAGE];
+    // kDftFast6: each stage buffer ends in 8 zero uint4, the row constants of a tile pair that runs
+    // the exact epilogue (written here, published by the first stage barrier, never a DMA target).
+    // Inside the stage's own array, so the compiler still tells these reads from the other
+    // buffer's pending LDS-DMA (a separate array made it wait vmcnt(0) before every tile)
+    constexpr int ZTAIL = DftForm<VAR>::FAST6 ? 8 : 0;
+    __shared__ uint4 lds0[STAGE + ZTAIL];
+    __shared__ uint4 lds1[STAGE + ZTAIL];
+    if constexpr (DftForm<VAR>::FAST6)
+        if (threadIdx.x < 2 * ZTAIL)
+            (threadIdx.x < ZTAIL ? lds0 : lds1)[STAGE + (threadIdx.x % ZTAIL)] = make_uint4(0u, 0u, 0u, 0u);
     const uint4 wk = a.work[blockIdx.x];
     const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
     const bool active = wv < wk.y;
@@ -716,8 +836,13 @@ __global__ void __launch_bounds__(64 * WAVES) search_dft(DftArgs d)
     for (int f = 0; f < NBF; ++f)
         bf[f] = __builtin_bit_cast(half8_t, a.rfrags[((size_t)blk * NBF + f) * 64 + lane]);
     float hl = 0.0f;
-    if constexpr (HITS) // S16 ≤ H  ⇔  y ≥ 16Σa² − H  (exact integers below 2^24)
+    if constexpr (HITS) { // S16 ≤ H  ⇔  y ≥ 16Σa² − H  (exact integers below 2^24; halved exactly for h)
         hl = (float)((int32_t)a.rconst[blk * 32 + (lane & 31u)] - (int32_t)a.hitH);
+        if constexpr (DftForm<VAR>::HALF)
+            hl *= 0.5f;
+    }
+    // the forms that track h = y/2 store y = 2h (exact) in the entries
+    constexpr float kOut = DftForm<VAR>::HALF ? 2.0f : 1.0f;
 
     float best = -__builtin_inff();
     uint32_t btile = 0;
@@ -736,7 +861,7 @@ __global__ void __launch_bounds__(64 * WAVES) search_dft(DftArgs d)
                 }
             if (active)
                 a.entries[((size_t)(d.choff[blockIdx.x] + (tb - wk.z) / 4u) * WAVES + wv) * 64 + lane] =
-                    make_uint2(__float_as_uint(cm), tb | (msk << 28));
+                    make_uint2(__float_as_uint(cm * kOut), tb | (msk << 28));
             masks[0] = masks[1] = 0u;
             return;
         }
@@ -766,7 +891,7 @@ __global__ void __launch_bounds__(64 * WAVES) search_dft(DftArgs d)
                 stage_tiles<KS, 64 * WAVES>(lds1, a.dtiles, a.dconst, tb + kTilesPerStage, stage_nt(st + 1));
             for (uint32_t c0 = 0; c0 < stage_nt(st); c0 += 4)
                 finish_stage(dft_compute_stage<VAR, CHUNKED, HITS>(lds0, stage_nt(st), lane, bf, tb, d.tguard, r1, c0,
-                                                                   c0 + 4, masks, hl),
+                                                                   c0 + 4, masks, hl, STAGE),
                              tb + c0);
         }
         if (st + 1 < nstage) {
@@ -777,12 +902,12 @@ __global__ void __launch_bounds__(64 * WAVES) search_dft(DftArgs d)
                 stage_tiles<KS, 64 * WAVES>(lds0, a.dtiles, a.dconst, tb + kTilesPerStage, stage_nt(st + 2));
             for (uint32_t c0 = 0; c0 < stage_nt(st + 1); c0 += 4)
                 finish_stage(dft_compute_stage<VAR, CHUNKED, HITS>(lds1, stage_nt(st + 1), lane, bf, tb, d.tguard, r1,
-                                                                   c0, c0 + 4, masks, hl),
+                                                                   c0, c0 + 4, masks, hl, STAGE),
                              tb + c0);
         }
     }
     if (active && !CHUNKED)
-        a.entries[(size_t)(blockIdx.x * WAVES + wv) * 64 + lane] = make_uint2(__float_as_uint(best), btile);
+        a.entries[(size_t)(blockIdx.x * WAVES + wv) * 64 + lane] = make_uint2(__float_as_uint(best * kOut), btile);
 }
 
 // ---------------------------------------------------------------------------
@@ -816,7 +941,7 @@ __global__ void __launch_bounds__(256, F6 ? 2 : 3) search_dft2(DftArgs d)
         for (int f = 0; f < NBF; ++f)
             bf[k][f] = __builtin_bit_cast(half8_t, a.rfrags[((size_t)blk * NBF + f) * 64 + lane]);
         if constexpr (HITS)
-            hl[k] = (float)((int32_t)a.rconst[blk * 32 + (lane & 31u)] - (int32_t)a.hitH);
+            hl[k] = (float)((int32_t)a.rconst[blk * 32 + (lane & 31u)] - (int32_t)a.hitH) * (F6 ? 0.5f : 1.0f);
         best[k] = -__builtin_inff();
     }
     const uint32_t h = lane >> 5;
@@ -880,7 +1005,7 @@ __global__ void __launch_bounds__(256, F6 ? 2 : 3) search_dft2(DftArgs d)
     for (int k = 0; k < 2; ++k)
         if (act[k])
             a.entries[(size_t)(blockIdx.x * kDftBlocksPerWG + 2 * wv + k) * 64 + lane] =
-                make_uint2(__float_as_uint(best[k]), btile[k]);
+                make_uint2(__float_as_uint(best[k] * (F6 ? 2.0f : 1.0f)), btile[k]); // F6 tracks h = y/2
 }
 
 // ---------------------------------------------------------------------------

@@ -192,9 +192,14 @@ __device__ inline void stage_tiles(uint4* dst, const uint4* __restrict__ dtiles,
 // __syncthreads() alone is not enough: the compiler emits only lgkmcnt(0) before a barrier
 // whose preceding DMA it cannot match to a later ds_read (seen at the loop head of
 // search_dft: a stage could be read before all of its pieces had landed).
+// tests/test_lds_dma.py guards this statically (tools/lds_dma_check.py over the product code
+// object); FRAC_TEST_PLAIN_STAGE_BARRIER builds the hazard back in, only for that test's
+// negative control (a standalone kernel object, never the product library).
 __device__ inline void stage_barrier()
 {
+#ifndef FRAC_TEST_PLAIN_STAGE_BARRIER
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
     __syncthreads();
 }
 

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define FRAC_ABI_VERSION 4
+#define FRAC_ABI_VERSION 5
 
 /* error codes */
 #define FRAC_OK 0
@@ -121,6 +121,12 @@ typedef struct frac_stats {
 typedef struct frac_ctx frac_ctx;
 
 int frac_abi_version(void);
+/* The 16-hex-digit id of the sources this library was built from (compiled in by the build:
+ * a hash of csrc/ and this header), "unknown" for a build that did not pass one. */
+const char* frac_build_id(void);
+/* FRAC_BUILD_* bits of this library build. */
+#define FRAC_BUILD_TUNING 1 /* -DFRAC_TUNING: ablation variants (wrong results by design) compiled in */
+int frac_build_flags(void);
 /* NULL on failure (message via frac_last_error(NULL)). */
 frac_ctx* frac_create(int device, const frac_params* params);
 void frac_destroy(frac_ctx* ctx);

@@ -28,7 +28,15 @@ def test_library_exports_every_declared_symbol():
     assert len(names) >= 20
     missing = [n for n in names if not hasattr(lib, n)]
     assert not missing, missing
-    assert lib.frac_abi_version() == 4
+    assert lib.frac_abi_version() == 5
+
+
+def test_library_carries_the_source_id():
+    # build() compiles fractencode_amd.source_id() into the library (frac_build_id); a stale or
+    # foreign binary shows up here and in bench.py's line
+    info = F.build_info()
+    assert info["build_id"] == F.source_id(), info
+    assert info["matches_sources"] and not info["tuning"]
 
 
 def test_record_layouts_match_reference_structs(tmp_path):

@@ -4,6 +4,8 @@ Bar: bit-exact (domain, transform, distance, contrast, brightness) — the fit i
 exact in FP64 and the distance is the reference's fp32 value — plus the
 reference's rejected-mapping counts.  All calls go through the C ABI.
 """
+import zlib
+
 import numpy as np
 import pytest
 
@@ -315,7 +317,7 @@ def test_five_mfma_form_at_operand_extremes(monkeypatch, kind, var):
     2Pi partial sums up to 33.3M < 2^25, P up to 2^24): on 0/255 frames that drive every operand
     to its bound it returns the exhaustive VALU engine's records, with and without the
     classifier."""
-    rng = np.random.default_rng(hash(kind) & 0xffff)
+    rng = np.random.default_rng(zlib.crc32(kind.encode()))  # reproducible across processes
     S = 256
     p = _extreme_plane(rng, S, kind)
     doms, rngs = F.create_uniform_grid(S, S, 16, 8), F.create_uniform_grid(S, S, 8, 8)

@@ -12,6 +12,5 @@ sys.path.insert(0, ROOT)
 import __graft_entry__ as G  # noqa: E402
 
 out = os.path.join(ROOT, "fractencode_amd", "libfracenc_tuning.so")
-subprocess.check_call([G._hipcc(), *G.HIPCC_FLAGS, "-DFRAC_TUNING", "-o", out,
-                       os.path.join(G.CSRC, "fracenc_api.hip")], cwd=G.CSRC)
+subprocess.check_call(G.hipcc_cmd(out, "-DFRAC_TUNING"), cwd=G.CSRC)
 print(out)

@@ -1,0 +1,20 @@
+#!/bin/bash
+# round 3 session 2: counters of the six-MFMA form (21) and its guarded fast epilogue (26), and
+# tuning-build ablations of 26 (barrier / DMA) in one interleaved A/B
+set -euo pipefail
+R=$(pwd)
+O=$R/gpurun_out/r03_s2
+mkdir -p $O
+python3 -c "import torch"
+cd /tmp && export TMPDIR=/tmp
+for v in 21 26; do
+  for p in "GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA" \
+           "GRBM_GUI_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_VALU_MFMA_COEXEC_CYCLES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_INSTS_SALU SQ_INSTS_SMEM"; do
+    n=$(echo $p | md5sum | cut -c1-6)
+    FRAC_MFMA_VARIANT=$v timeout -s KILL 150 rocprofv3 --pmc $p -d $O/v${v}_$n -o pmc --output-format csv -- python3 $R/tools/c3_once.py mfma 4 > /dev/null
+  done
+  python3 $R/tools/pmc_summary.py $(find $O -path "*v${v}_*" -name '*counter_collection.csv') > $O/v${v}_pmc.txt
+done
+cd $R
+FRAC_LIB=$R/fractencode_amd/libfracenc_tuning.so timeout -k 10 500 python3 tools/ab_mfma.py d,d6f,dfB,df0 10 > $O/ab.log 2>&1
+echo ok
