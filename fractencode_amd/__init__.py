@@ -147,6 +147,7 @@ def lib() -> C.CDLL:
             "frac_rgb_to_yuv_device": (i32, [vp, vp, u32, u32, u32, vp, u32, vp, u32, vp, u32]),
             "frac_rgb_to_yuv": (i32, [vp, vp, u32, u32, u32, vp, vp, vp]),
             "frac_uniform_grid": (sz, [u32, u32, u32, u32, vp, sz]),
+            "frac_uniform_grid2": (sz, [u32, u32, u32, u32, u32, u32, vp, sz]),
             "frac_classify": (i32, [vp, u32, u32, u32, vp, sz]),
             "frac_transform_index": (i32, [u32, u32, u32]),
             "frac_hit_limit": (C.c_int64, [C.c_double, u32]),
@@ -178,12 +179,15 @@ def last_error(ctx=None) -> str:
 
 # ---- host helpers ----------------------------------------------------------------
 
-def create_uniform_grid(width: int, height: int, item_size: int, item_offset: int) -> np.ndarray:
-    """Frac2::createUniformGrid: row-major items, x fastest (categories -1)."""
-    n = lib().frac_uniform_grid(width, height, item_size, item_offset, None, 0)
+def create_uniform_grid(width: int, height: int, item_size, item_offset) -> np.ndarray:
+    """Frac2::createUniformGrid (image/partition2.hpp:109-135): row-major items, x fastest
+    (categories -1).  item_size / item_offset: an int, or (x, y) like the reference's Size32u."""
+    sw, sh = (item_size, item_size) if np.isscalar(item_size) else item_size
+    ox, oy = (item_offset, item_offset) if np.isscalar(item_offset) else item_offset
+    n = lib().frac_uniform_grid2(width, height, sw, sh, ox, oy, None, 0)
     out = np.zeros(n, dtype=GRID_ITEM)
     if n:
-        lib().frac_uniform_grid(width, height, item_size, item_offset, out.ctypes.data, n)
+        lib().frac_uniform_grid2(width, height, sw, sh, ox, oy, out.ctypes.data, n)
     return out
 
 

@@ -159,8 +159,9 @@ struct frac_ctx {
     bool dirty = true;
 
     // prepared state
-    int n = 0;
-    uint32_t S = 0;          // domain side
+    int n = 0;               // range side (0: rectangular ranges or domains, the sampled form)
+    uint32_t S = 0;          // domain side (width for rectangles)
+    uint32_t nw = 0, nh = 0, Sw = 0, Sh = 0; // range and domain width / height
     bool virt = false;       // sampled form (fracenc_gen.hip): one pool row per (domain, transform)
     bool generic = false;    // sampled form with a range size no templated engine covers (gen_search)
     uint32_t Teff = 4;       // transforms the engines search per pool row (1 in the sampled form)
@@ -214,6 +215,7 @@ struct frac_ctx {
     DBuf<DecodeState> d_dec_state;
     DecodeState* h_dec_state = nullptr;
     DBuf<uint2> d_dft_tguard;
+    DBuf<int32_t> d_dft_trmax; // the six-MFMA fast path's per-tile R6 threshold (kDftFast6)
     DBuf<uint32_t> d_dft_tpool; // pool rows in tile order (resolve_dft)
     DBuf<uint32_t> d_dft_rorb;  // range pixel pairs in orbit order, per slot (resolve_dft)
     DBuf<uint4> d_rstat;        // per range: the winner's sums (resolve_dft → fit_rstat)
@@ -443,7 +445,7 @@ int device_buckets(frac_ctx* c, int nb, uint32_t* dfirst, uint32_t* rfirst)
     const uint32_t tstride = c->same_plane ? c->d_sstride : c->d_tstride;
     size_t tb = c->bk_tmp_bytes;
     if (nd) { // a stored −1 is classified on the item's own plane (Classifier2::compare, Classifier2.cpp:70-81)
-        launch_bucket_keys(c->d_doms.ptr, nd, c->S, c->d_src.ptr, c->d_sstride, c->d_bk_keys.ptr, c->d_bk_iota.ptr,
+        launch_bucket_keys(c->d_doms.ptr, nd, c->Sh, c->d_src.ptr, c->d_sstride, c->d_bk_keys.ptr, c->d_bk_iota.ptr,
                            err, c->stream);
         FRAC_HIP(c, sort_pairs_u32(c->d_bk_tmp.ptr, tb, c->d_bk_keys.ptr, c->d_bk_keys2.ptr, c->d_bk_iota.ptr,
                                    c->d_porig.ptr, nd, 3, c->stream));
@@ -451,7 +453,7 @@ int device_buckets(frac_ctx* c, int nb, uint32_t* dfirst, uint32_t* rfirst)
     bucket_bounds<<<1, 64, 0, c->stream>>>(c->d_bk_keys2.ptr, nd, first);
     tb = c->bk_tmp_bytes;
     if (nr) {
-        launch_bucket_keys(c->d_ranges.ptr, nr, (uint32_t)c->n, tplane, tstride, c->d_rkey.ptr, c->d_bk_iota.ptr, err,
+        launch_bucket_keys(c->d_ranges.ptr, nr, c->nh, tplane, tstride, c->d_rkey.ptr, c->d_bk_iota.ptr, err,
                            c->stream);
         FRAC_HIP(c, sort_pairs_u32(c->d_bk_tmp.ptr, tb, c->d_rkey.ptr, c->d_bk_keys2.ptr, c->d_bk_iota.ptr,
                                    c->d_rord.ptr, nr, 3, c->stream));
@@ -502,6 +504,97 @@ inline int dft_variant(int var)
     return var >= 200 ? var : kDftDefaultVariant;
 }
 
+// Domain items as the search needs them: one size (Size32u, rectangles allowed), at least 2×2 (the
+// sampler reads 2×2 blocks, image/sampler.h:21-38), inside the source plane once one is set.
+// frac_set_domains runs it, so a reference-side engine rejects a bad grid in its constructor
+// (EncodingEngine2.cpp:22-29 catches there), and prepare() again against the current plane.
+int check_domains(frac_ctx* c, const frac_grid_item* d, size_t nd)
+{
+    if (!nd)
+        return FRAC_OK;
+    const uint32_t Sw = d[0].w, Sh = d[0].h;
+    if (Sw < 2 || Sh < 2)
+        return c->fail(FRAC_E_INVALID, "domain sides must be at least 2");
+    if ((uint64_t)nd >= (1u << 24))
+        return c->fail(FRAC_E_INVALID, "at most 2^24 - 1 domains");
+    for (size_t i = 0; i < nd; ++i) {
+        if (d[i].w != Sw || d[i].h != Sh)
+            return c->fail(FRAC_E_INVALID, "all domains must be of one size");
+        if (c->planes_set && ((uint64_t)d[i].x + d[i].w > c->src.w || (uint64_t)d[i].y + d[i].h > c->src.h))
+            return c->fail(FRAC_E_INVALID, "domain outside the source plane");
+        if (d[i].category < -1 || d[i].category > 5)
+            return c->fail(FRAC_E_INVALID, "domain category must be -1..5");
+    }
+    return FRAC_OK;
+}
+
+// Rectangular items: under a rotation a rectangle's samples leave its own patch
+// (image/transform.h:96-109 maps x' = y for Rotate_90 with the patch's own sizes), reading the plane
+// around it.  The reference reads whatever is there, inside the image; beyond the image it reads out
+// of bounds.  Every 2×2 block any transform samples — at the metric points (x·⌊Sw/nw⌋, y·⌊Sh/nh⌋) and
+// the fit points ((x·Sw)/nw, (y·Sh)/nh), after the sampler's edge clamp — must lie inside the source
+// plane for every domain; else the search is refused.
+struct SampleBox {
+    int x0 = INT32_MAX, x1 = INT32_MIN, y0 = INT32_MAX, y1 = INT32_MIN;
+};
+// the pixels (relative to the domain origin) that transform t's 2×2 samples of an Sw×Sh domain read
+// for an nw×nh range: the metric points and/or the fit points, after the sampler's edge clamp
+SampleBox sample_box(int t, int Sw, int Sh, int nw, int nh, bool metric, bool fit)
+{
+    static const int lutv[8][8] = {{1, 0, 0, 0, 0, 1, 0, 0},  {0, 1, 0, 0, -1, 0, 1, 0}, {-1, 0, 1, 0, 0, -1, 0, 1},
+                                   {0, -1, 0, 1, 1, 0, 0, 0}, {1, 0, 0, 0, 0, -1, 0, 1}, {0, 1, 0, 0, 1, 0, 0, 0},
+                                   {-1, 0, 1, 0, 0, 1, 0, 0}, {0, -1, 0, 1, -1, 0, 1, 0}};
+    SampleBox b;
+    const int* a = lutv[t];
+    auto add = [&](int lx, int ly) {
+        if (lx == Sw - 1)
+            --lx;
+        if (ly == Sh - 1)
+            --ly;
+        const int px = a[0] * lx + a[1] * ly + a[2] * (Sw - 1) + a[3] * (Sh - 1);
+        const int py = a[4] * lx + a[5] * ly + a[6] * (Sw - 1) + a[7] * (Sh - 1);
+        for (int k = 0; k < 4; ++k) {
+            const int qx = px + (k & 1 ? a[0] : 0) + (k & 2 ? a[1] : 0);
+            const int qy = py + (k & 1 ? a[4] : 0) + (k & 2 ? a[5] : 0);
+            b.x0 = std::min(b.x0, qx);
+            b.x1 = std::max(b.x1, qx);
+            b.y0 = std::min(b.y0, qy);
+            b.y1 = std::max(b.y1, qy);
+        }
+    };
+    for (int y = 0; y < nh; ++y)
+        for (int x = 0; x < nw; ++x) {
+            if (metric)
+                add(x * (Sw / nw), y * (Sh / nh));
+            if (fit)
+                add((x * Sw) / nw, (y * Sh) / nh);
+        }
+    return b;
+}
+
+bool box_inside(const SampleBox& b, uint32_t x, uint32_t y, uint32_t w, uint32_t h)
+{
+    return (int64_t)x + b.x0 >= 0 && (int64_t)x + b.x1 < (int64_t)w && (int64_t)y + b.y0 >= 0 &&
+           (int64_t)y + b.y1 < (int64_t)h;
+}
+
+int check_rect_samples(frac_ctx* c)
+{
+    SampleBox u;
+    for (uint32_t t = 0; t < c->p.transforms; ++t) {
+        const SampleBox b = sample_box((int)t, (int)c->Sw, (int)c->Sh, (int)c->nw, (int)c->nh, true, true);
+        u.x0 = std::min(u.x0, b.x0);
+        u.x1 = std::max(u.x1, b.x1);
+        u.y0 = std::min(u.y0, b.y0);
+        u.y1 = std::max(u.y1, b.y1);
+    }
+    for (const auto& d : c->doms)
+        if (!box_inside(u, d.x, d.y, c->src.w, c->src.h))
+            return c->fail(FRAC_E_INVALID, "a transform of a rectangular domain samples outside the source plane "
+                                           "(the reference reads out of bounds there)");
+    return FRAC_OK;
+}
+
 int prepare(frac_ctx* c)
 {
     HostTrace tr("prepare");
@@ -512,33 +605,43 @@ int prepare(frac_ctx* c)
     // and S×S domains, S > n (main.cpp:99 rejects target >= source).  S = 2n with n ∈ {2, 4, 8, 16}
     // is every engine's decimate-then-permute path; any other pair — the CLI default 16→4 among
     // them — runs the sampled form (fracenc_gen.hip): one pool row per (domain, transform).
-    int n = c->ranges_dev ? (int)c->n_dev : c->ranges.empty() ? 8 : (int)c->ranges[0].w;
+    // ranges: one size nw × nh (Size32u items, image/partition2.hpp:13-31: rectangles allowed)
+    const uint32_t nw = c->ranges_dev ? c->n_dev : c->ranges.empty() ? 8u : c->ranges[0].w;
+    const uint32_t nh = c->ranges_dev ? c->n_dev : c->ranges.empty() ? 8u : c->ranges[0].h;
     for (const auto& r : c->ranges) {
         if (c->ranges_dev)
             break; // built on the device from validated parents (frac_encode_quadtree)
-        if ((int)r.w != n || (int)r.h != n)
-            return c->fail(FRAC_E_INVALID, "all ranges must be square and of one size");
+        if (r.w != nw || r.h != nh)
+            return c->fail(FRAC_E_INVALID, "all ranges must be of one size");
         if ((uint64_t)r.x + r.w > c->tgt.w || (uint64_t)r.y + r.h > c->tgt.h)
             return c->fail(FRAC_E_INVALID, "range outside the target plane");
     }
-    if (n < 2 || n > (int)kGenMaxN)
-        return c->fail(FRAC_E_INVALID, "range size must be 2..32");
-    const uint32_t S = c->doms.empty() ? 2u * (uint32_t)n : c->doms[0].w;
-    for (size_t i = 0; !c->doms_trusted && i < c->doms.size(); ++i) {
-        const frac_grid_item& d = c->doms[i];
-        if (d.w != S || d.h != S)
-            return c->fail(FRAC_E_INVALID, "all domains must be square and of one size");
-        if ((uint64_t)d.x + d.w > c->src.w || (uint64_t)d.y + d.h > c->src.h)
-            return c->fail(FRAC_E_INVALID, "domain outside the source plane");
-    }
-    if (S <= (uint32_t)n)
-        return c->fail(FRAC_E_INVALID, "domains must be larger than the ranges (main.cpp:99)");
+    if (nw < 2 || nw > kGenMaxN || nh < 2 || nh > kGenMaxN)
+        return c->fail(FRAC_E_INVALID, "range sides must be 2..32");
+    // domains: validated by frac_set_domains (one size, inside the plane); re-checked against the
+    // current plane, which may have changed since
+    const uint32_t Sw = c->doms.empty() ? 2u * nw : c->doms[0].w;
+    const uint32_t Sh = c->doms.empty() ? 2u * nh : c->doms[0].h;
+    if (!c->doms_trusted)
+        FRAC_TRY(check_domains(c, c->doms.data(), c->doms.size()));
+    // RootMeanSquare's different-size branch (image/metrics.h:37-50) needs a domain wider than the
+    // range (its FRAC_ASSERT, :39; main.cpp:99 for the CLI's square items)
+    if (Sw <= nw)
+        return c->fail(FRAC_E_INVALID, "domains must be wider than the ranges (metrics.h:39, main.cpp:99)");
+    const bool square = nw == nh && Sw == Sh;
+    const int n = square ? (int)nw : 0;
     const bool pow2 = n == 2 || n == 4 || n == 8 || n == 16;
-    c->virt = !(pow2 && S == 2u * (uint32_t)n);
+    c->virt = !(pow2 && Sw == 2u * nw);
     c->generic = !pow2;
-    c->S = S;
+    c->S = Sw;
+    c->nw = nw;
+    c->nh = nh;
+    c->Sw = Sw;
+    c->Sh = Sh;
+    if (!square)
+        FRAC_TRY(check_rect_samples(c));
     c->Teff = c->virt ? 1u : T;
-    c->K2 = (uint32_t)(n * n + 1) / 2;
+    c->K2 = (nw * nh + 1) / 2;
     if ((uint64_t)c->doms.size() * (c->virt ? T : 1u) >= (1u << 24))
         return c->fail(FRAC_E_INVALID, "at most 2^24 - 1 domains (domains x transforms in the sampled form)");
     c->n = n;
@@ -624,7 +727,7 @@ int prepare(frac_ctx* c)
     c->eligible_pairs = 0;
     for (int b = 0; b < nb; ++b)
         c->eligible_pairs += (uint64_t)L.rcnt[b] * L.dcnt[b];
-    c->hitH = compute_hit_limit(c->p.rms_threshold, S * S); // the domain's area (image/metrics.h:49)
+    c->hitH = compute_hit_limit(c->p.rms_threshold, Sw * Sh); // the domain's area (image/metrics.h:49)
     c->all_fallback = c->hitH >= kExactLimit;
 
     // engine.  MFMA: exact for every templated n (n = 16 through search_mfma16's integer epilogue).
@@ -1054,6 +1157,7 @@ inline int launch_dft(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride)
     d.dtiles = c->d_m_dtiles.ptr;
     d.dconst = c->d_m_dconst.ptr;
     FRAC_HIP(c, c->d_dft_tguard.ensure(std::max<size_t>(c->ntiles, 1)));
+    FRAC_HIP(c, c->d_dft_trmax.ensure(std::max<size_t>(c->ntiles, 1)));
     FRAC_HIP(c, c->d_dft_tpool.ensure(std::max<size_t>((size_t)c->ntiles * 32 * 32, 1)));
     FRAC_HIP(c, c->d_dft_rguard.ensure(std::max<size_t>(c->nblocks, 1)));
     // FRAC_MFMA_VARIANT for this path (A/B knob): default = exact form in 8-wave workgroups
@@ -1078,7 +1182,8 @@ inline int launch_dft(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride)
     b.tpool = c->d_dft_tpool.ptr;
     if (c->ntiles) {
         if (f5)
-            dft_domain_build<false, true><<<(c->ntiles * 32 + 255) / 256, 256, 0, c->stream>>>(d, b, c->d_dft_tguard.ptr);
+            dft_domain_build<false, true><<<(c->ntiles * 32 + 255) / 256, 256, 0, c->stream>>>(d, b, c->d_dft_tguard.ptr,
+                                                                                              c->d_dft_trmax.ptr);
         else
             dft_domain_build<false><<<(c->ntiles * 32 + 255) / 256, 256, 0, c->stream>>>(d, b, c->d_dft_tguard.ptr);
     }
@@ -1124,6 +1229,7 @@ inline int launch_dft(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride)
         da.m = a;
         da.rguard = c->d_dft_rguard.ptr;
         da.tguard = c->d_dft_tguard.ptr;
+        da.trmax = c->d_dft_trmax.ptr;
         const unsigned nwg = (unsigned)work.size();
         const bool hits = c->hitH > 0;
         constexpr uint32_t W8 = kDftBlocksPerWG;
@@ -1437,6 +1543,7 @@ int launch_tp(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool timing)
     da.m = a;
     da.rguard = c->d_dft_rguard.ptr;
     da.tguard = c->d_dft_tguard.ptr;
+    da.trmax = nullptr; // kTpVar runs the exact epilogue only
     // seed: the Fourier search over one tile per group, one chunk entry per wave (choff = group)
     tp_seed_work<<<(ng + 255) / 256, 256, 0, c->stream>>>(c->d_tp_groups.ptr, ng, c->d_tp_blk_sr.ptr,
                                                           c->d_tp_tile_sd.ptr, c->d_m8_work.ptr);
@@ -1587,8 +1694,10 @@ GenArgs gen_args(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride)
     g.doms = c->d_doms.ptr;
     g.ranges = c->d_ranges.ptr;
     g.porig = c->d_porig.ptr;
-    g.n = (uint32_t)c->n;
-    g.S = c->S;
+    g.nw = c->nw;
+    g.nh = c->nh;
+    g.Sw = c->Sw;
+    g.Sh = c->Sh;
     g.T = c->p.transforms;
     g.K2 = c->K2;
     g.pool = c->d_pool.ptr;
@@ -1959,6 +2068,7 @@ void frac_destroy(frac_ctx* c)
     if (c->h_dec_state)
         (void)hipHostFree(c->h_dec_state);
     c->d_dft_tguard.release();
+    c->d_dft_trmax.release();
     c->d_dft_tpool.release();
     c->d_dft_rorb.release();
     c->d_rstat.release();
@@ -2086,6 +2196,7 @@ int frac_set_domains(frac_ctx* c, const frac_grid_item* d, size_t nd)
         return FRAC_E_INVALID;
     if (nd && !d)
         return c->fail(FRAC_E_INVALID, "domains is NULL");
+    FRAC_TRY(check_domains(c, d, nd));
     c->doms.assign(d, d + nd);
     c->doms_set = true;
     c->doms_uploaded = false;
@@ -2693,6 +2804,15 @@ int frac_decode(frac_ctx* c, const frac_encode_item* items, size_t n, uint32_t w
             e.match.score.transform > 7 ||
             (e.match.sw && ((uint64_t)e.match.x + e.match.sw > w || (uint64_t)e.match.y + e.match.sh > h)))
             return c->fail(FRAC_E_INVALID, "decode: item outside the plane or bad transform");
+        // a rectangular (or degenerate) domain: the transformed 2×2 samples (Frac::copy's fit points,
+        // DecodeUtils.hpp:9-25) may leave the patch; they must stay inside the plane
+        if (e.match.sw && (e.match.sw != e.match.sh || e.match.sw < 2) &&
+            (e.match.sw < 2 || e.match.sh < 2 || e.w == 0 || e.h == 0 ||
+             !box_inside(sample_box(e.match.score.transform, (int)e.match.sw, (int)e.match.sh, (int)e.w, (int)e.h,
+                                    false, true),
+                         e.match.x, e.match.y, w, h)))
+            return c->fail(FRAC_E_INVALID, "decode: a transformed sample of item " + std::to_string(i) +
+                                               " falls outside the plane");
     }
     FRAC_HIP(c, hipSetDevice(c->device));
     FRAC_HIP(c, c->d_dec_items.ensure(n));
@@ -2779,6 +2899,8 @@ int frac_pack_frc1(frac_ctx* c, uint32_t cbits, uint32_t bbits, uint8_t* out, si
                 return false;
         return true;
     };
+    if (n == 0)
+        return c->fail(FRAC_E_INVALID, "pack_frc1: the stream holds square items only");
     if (!same_grid(c->ranges, n, n))
         return c->fail(FRAC_E_INVALID, "pack_frc1: ranges are not the row-major range grid");
     if (!same_grid(c->doms, 2 * n, n))
@@ -2882,25 +3004,34 @@ int frac_copy_results_device(frac_ctx* c, void* d_dst)
     return FRAC_OK;
 }
 
-size_t frac_uniform_grid(uint32_t W, uint32_t H, uint32_t size, uint32_t offset, frac_grid_item* out, size_t cap)
+size_t frac_uniform_grid2(uint32_t W, uint32_t H, uint32_t size_w, uint32_t size_h, uint32_t off_x, uint32_t off_y,
+                          frac_grid_item* out, size_t cap)
 {
-    if (size == 0 || offset == 0 || W < size || H < size)
+    // createUniformGrid's loop (image/partition2.hpp:123-133): x advances by the offset's x, a row
+    // ends when the next item would cross the right edge, the grid when the next row would cross
+    // the bottom edge
+    if (size_w == 0 || size_h == 0 || off_x == 0 || off_y == 0 || W < size_w || H < size_h)
         return 0;
     size_t n = 0;
     uint32_t x = 0, y = 0;
     for (;;) {
         if (out && n < cap)
-            out[n] = frac_grid_item{x, y, size, size, -1};
+            out[n] = frac_grid_item{x, y, size_w, size_h, -1};
         ++n;
-        x += offset;
-        if (x + size > W) {
+        x += off_x;
+        if ((uint64_t)x + size_w > W) {
             x = 0;
-            y += offset;
-            if (y + size > H)
+            y += off_y;
+            if ((uint64_t)y + size_h > H)
                 break;
         }
     }
     return n;
+}
+
+size_t frac_uniform_grid(uint32_t W, uint32_t H, uint32_t size, uint32_t offset, frac_grid_item* out, size_t cap)
+{
+    return frac_uniform_grid2(W, H, size, size, offset, offset, out, cap);
 }
 
 int frac_classify(const uint8_t* plane, uint32_t w, uint32_t h, uint32_t stride, frac_grid_item* items, size_t n)

@@ -164,6 +164,8 @@ struct DftArgs {
     uint2* tguard;        // [ntiles]   {max 4·D∞, max Σb²} over the tile's valid rows (five- / six-MFMA
                           //            layout: {max 2·D6, max Σb²})
     const uint32_t* choff; // CHUNKED: [work] first chunk entry of the work item (fracenc_tp.hip)
+    const int32_t* trmax;  // kDftFast6: [ntiles] the largest block R6 whose guard holds against the
+                           // tile, (kFast6Limit − max Σb²) / max 2·D6 (−1: none)
 };
 
 // ---------------------------------------------------------------------------
@@ -203,7 +205,7 @@ __device__ inline uint32_t pair_sums(uint32_t w0, uint32_t w1)
 // F5: the five-MFMA form's fragments [s_b + u_b | s_b − u_b | γ | γ − δ | −δ − γ] (kDft5)
 template <bool BYPOS = false, bool F5 = false>
 __global__ void __launch_bounds__(256) dft_domain_build(MfmaDomainPrepArgs a, DftDomainBuildArgs s,
-                                                        uint2* __restrict__ tguard)
+                                                        uint2* __restrict__ tguard, int32_t* __restrict__ trmax = nullptr)
 {
     constexpr int NN = 64, NO = 16, KS = F5 ? 5 : 4;
     const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
@@ -326,8 +328,15 @@ __global__ void __launch_bounds__(256) dft_domain_build(MfmaDomainPrepArgs a, Df
         gx = max(gx, (uint32_t)__shfl_xor((int)gx, o, 64));
         gy = max(gy, (uint32_t)__shfl_xor((int)gy, o, 64));
     }
-    if (row == 0)
+    if (row == 0) {
         tguard[tile] = make_uint2(gx, gy);
+        // the six-MFMA fast path's guard as one threshold on the block's R6:
+        // R6·gx + gy ≤ kFast6Limit  ⇔  gy ≤ kFast6Limit and R6 ≤ ⌊(kFast6Limit − gy) / gx⌋
+        if (F5 && trmax)
+            trmax[tile] = (int64_t)gy > kFast6Limit ? -1
+                          : gx == 0                  ? INT32_MAX
+                                                     : (int32_t)min<int64_t>((kFast6Limit - gy) / gx, INT32_MAX);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -740,7 +749,7 @@ __device__ inline float dft_compute_stage(const uint4* __restrict__ la, uint32_t
                                           const half8_t (&bf)[DftForm<VAR>::NBF], uint32_t tb,
                                           const uint2* __restrict__ tguard, uint32_t r1, uint32_t q0 = 0,
                                           uint32_t q1 = ~0u, uint32_t* masks = nullptr, float hl = 0.0f,
-                                          uint32_t iz = 0)
+                                          uint32_t iz = 0, const int32_t* __restrict__ trmax = nullptr)
 {
     constexpr int KS = DftForm<VAR>::KS;
     const uint4* lc = la + nt * (uint32_t)KS * 64u;
@@ -748,18 +757,23 @@ __device__ inline float dft_compute_stage(const uint4* __restrict__ la, uint32_t
     float cm = -__builtin_inff();
     // the chunk's fast-path guards, loaded up front (wave-uniform scalar loads)
     uint32_t gfast = 0;
-    if constexpr ((VAR & 1) == 0 || DftForm<VAR>::FAST6) {
-        const uint64_t lim = DftForm<VAR>::FAST6 ? (uint64_t)kFast6Limit : (uint64_t)kExactLimit;
-        // the tile index is wave-uniform: readfirstlane makes these scalar loads, which the vmcnt
-        // waits of the stage's LDS-DMA do not serialise with
-        const uint32_t t0 = __builtin_amdgcn_readfirstlane(tb + q0), ne = __builtin_amdgcn_readfirstlane(min(q1, nt) - q0);
+    // the tile index is wave-uniform: readfirstlane + the constant address space make the guard
+    // loads scalar, which the vmcnt waits of the stage's LDS-DMA do not serialise with
+    const uint32_t t0 = __builtin_amdgcn_readfirstlane(tb + q0), ne = __builtin_amdgcn_readfirstlane(min(q1, nt) - q0);
+    if constexpr (DftForm<VAR>::FAST6) {
+        const __attribute__((address_space(4))) int32_t* rp =
+            (const __attribute__((address_space(4))) int32_t*)(uintptr_t)(trmax + t0);
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k)
+            if (k < ne)
+                gfast |= (int32_t)r1 <= rp[k] ? (1u << k) : 0u;
+    } else if constexpr ((VAR & 1) == 0) {
 #pragma unroll
         for (uint32_t k = 0; k < 4; ++k)
             if (k < ne) {
                 const __attribute__((address_space(4))) uint32_t* gp =
                     (const __attribute__((address_space(4))) uint32_t*)(uintptr_t)(tguard + t0 + k);
-                const uint32_t gx = gp[0], gy = gp[1];
-                gfast |= ((uint64_t)r1 * gx + gy <= lim) ? (1u << k) : 0u;
+                gfast |= ((uint64_t)r1 * gp[0] + gp[1] <= (uint64_t)kExactLimit) ? (1u << k) : 0u;
             }
     }
     auto tile = [&](uint32_t q) {
@@ -891,7 +905,7 @@ __global__ void __launch_bounds__(64 * WAVES) search_dft(DftArgs d)
                 stage_tiles<KS, 64 * WAVES>(lds1, a.dtiles, a.dconst, tb + kTilesPerStage, stage_nt(st + 1));
             for (uint32_t c0 = 0; c0 < stage_nt(st); c0 += 4)
                 finish_stage(dft_compute_stage<VAR, CHUNKED, HITS>(lds0, stage_nt(st), lane, bf, tb, d.tguard, r1, c0,
-                                                                   c0 + 4, masks, hl, STAGE),
+                                                                   c0 + 4, masks, hl, STAGE, d.trmax),
                              tb + c0);
         }
         if (st + 1 < nstage) {
@@ -902,7 +916,7 @@ __global__ void __launch_bounds__(64 * WAVES) search_dft(DftArgs d)
                 stage_tiles<KS, 64 * WAVES>(lds0, a.dtiles, a.dconst, tb + kTilesPerStage, stage_nt(st + 2));
             for (uint32_t c0 = 0; c0 < stage_nt(st + 1); c0 += 4)
                 finish_stage(dft_compute_stage<VAR, CHUNKED, HITS>(lds1, stage_nt(st + 1), lane, bf, tb, d.tguard, r1,
-                                                                   c0, c0 + 4, masks, hl, STAGE),
+                                                                   c0, c0 + 4, masks, hl, STAGE, d.trmax),
                              tb + c0);
         }
     }

@@ -8,7 +8,9 @@
 //   (x·⌊S/n⌋, y·⌊S/n⌋)                       (metrics.h:40-45)
 // while the fit samples it at
 //   ((x·S)/n, (y·S)/n)                       (transformmatcher.h:94-95; match_16to4: (4x, 4y))
-// — the same points whenever n divides S.  A sample is SamplerBilinear's 2×2 sum under the
+// — the same points whenever n divides S (per axis: ranges nw × nh and domains Sw × Sh may be
+// rectangles, as the reference's Size32u items allow, with the x and y ratios of metrics.h:40-41).
+// A sample is SamplerBilinear's 2×2 sum under the
 // transform (image/sampler.h:21-38, image/transform.h:96-109).  At ratio 2 the samples of every
 // transform are one permutation of the domain's 2×2-decimation; at any other ratio each transform
 // samples a different set of 2×2 blocks (at ratio 4 the flipped ones start at offset 2).
@@ -34,32 +36,35 @@ struct GenArgs {
     const frac_grid_item* doms;
     const frac_grid_item* ranges;
     const uint32_t* porig;  // pool position → domain index
-    uint32_t n, S, T, K2;   // range side, domain side, transforms, dwords per pool row
+    uint32_t nw, nh, Sw, Sh; // range width / height, domain width / height
+    uint32_t T, K2;          // transforms, dwords per pool row
     uint32_t* pool;         // [P·T][K2] metric samples, packed u16 pairs (zero padded)
     int32_t* negsd2;        // [P·T] −ΣM²
     uint32_t nrows;         // P·T
 };
 
-// SamplerBilinear::sample<·, t>'s integer 2×2 sum at patch-local (lx, ly) of an S×S domain at (dx, dy):
+// SamplerBilinear::sample<·, t>'s integer 2×2 sum at patch-local (lx, ly) of an Sw×Sh domain at (dx, dy):
 // the edge clamp of sampler.h:32-35, then the four offsets of Transform::generateSampleOffsets
-// (transform.h:96-109): T(lx, ly), T(lx+1, ly), T(lx, ly+1), T(lx+1, ly+1).
+// (transform.h:96-109): T(lx, ly), T(lx+1, ly), T(lx, ly+1), T(lx+1, ly+1).  For a rectangle the
+// rotations map parts of the patch outside it, as in the reference; prepare() checks that every such
+// read stays inside the plane (the reference reads out of bounds otherwise).
 __device__ inline int gen_sample(const uint8_t* __restrict__ img, uint32_t stride, uint32_t dx, uint32_t dy,
-                                 uint32_t S, int t, uint32_t lx, uint32_t ly)
+                                 uint32_t Sw, uint32_t Sh, int t, uint32_t lx, uint32_t ly)
 {
-    if (lx == S - 1)
+    if (lx == Sw - 1)
         --lx;
-    if (ly == S - 1)
+    if (ly == Sh - 1)
         --ly;
     const Aff a = lut(t);
-    const int px = (int)dx + a.a0 * (int)lx + a.a1 * (int)ly + (a.a2 + a.a3) * (int)(S - 1);
-    const int py = (int)dy + a.a4 * (int)lx + a.a5 * (int)ly + (a.a6 + a.a7) * (int)(S - 1);
+    const int px = (int)dx + a.a0 * (int)lx + a.a1 * (int)ly + a.a2 * (int)(Sw - 1) + a.a3 * (int)(Sh - 1);
+    const int py = (int)dy + a.a4 * (int)lx + a.a5 * (int)ly + a.a6 * (int)(Sw - 1) + a.a7 * (int)(Sh - 1);
     const ptrdiff_t s = (ptrdiff_t)stride;
     const uint8_t* p = img + (ptrdiff_t)py * s + px;
     return (int)p[0] + (int)p[a.a4 * s + a.a0] + (int)p[a.a5 * s + a.a1] + (int)p[(a.a4 + a.a5) * s + a.a0 + a.a1];
 }
 
-// One thread per virtual row v = p·T + (T−1−t): the n² metric samples of domain porig[p] under t at
-// (x·⌊S/n⌋, y·⌊S/n⌋) (image/metrics.h:40-45), as the pool row the engines read, and −ΣM².
+// One thread per virtual row v = p·T + (T−1−t): the nw·nh metric samples of domain porig[p] under t at
+// (x·⌊Sw/nw⌋, y·⌊Sh/nh⌋) (image/metrics.h:40-45), as the pool row the engines read, and −ΣM².
 __global__ void __launch_bounds__(256) gen_pool_build(GenArgs a)
 {
     const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
@@ -68,7 +73,7 @@ __global__ void __launch_bounds__(256) gen_pool_build(GenArgs a)
     const uint32_t p = v / a.T;
     const int t = (int)(a.T - 1 - v % a.T);
     const frac_grid_item d = a.doms[a.porig[p]];
-    const uint32_t ratio = a.S / a.n, NN = a.n * a.n;
+    const uint32_t rw = a.Sw / a.nw, rh = a.Sh / a.nh, NN = a.nw * a.nh;
     uint32_t* row = a.pool + (size_t)v * a.K2;
     int sq = 0;
     uint32_t x = 0, y = 0;
@@ -78,10 +83,10 @@ __global__ void __launch_bounds__(256) gen_pool_build(GenArgs a)
         for (int h = 0; h < 2; ++h) {
             const uint32_t q = 2 * k + h;
             if (q < NN) {
-                const int m = gen_sample(a.src, a.sstride, d.x, d.y, a.S, t, x * ratio, y * ratio);
+                const int m = gen_sample(a.src, a.sstride, d.x, d.y, a.Sw, a.Sh, t, x * rw, y * rh);
                 sq += m * m;
                 w |= (uint32_t)m << (16 * h);
-                if (++x == a.n) {
+                if (++x == a.nw) {
                     x = 0;
                     ++y;
                 }
@@ -97,7 +102,7 @@ __global__ void __launch_bounds__(256) gen_pool_build(GenArgs a)
 __device__ inline uint64_t gen_s16(const GenArgs& a, const frac_grid_item& rg, uint32_t v)
 {
     const uint32_t* row = a.pool + (size_t)v * a.K2;
-    const uint32_t NN = a.n * a.n;
+    const uint32_t NN = a.nw * a.nh;
     uint64_t s = 0;
     uint32_t x = 0, y = 0;
     for (uint32_t q = 0; q < NN; ++q) {
@@ -105,7 +110,7 @@ __device__ inline uint64_t gen_s16(const GenArgs& a, const frac_grid_item& rg, u
         const int m = (q & 1) ? (int)(w >> 16) : (int)(w & 0xffffu);
         const int e = 4 * (int)a.tgt[(size_t)(rg.y + y) * a.tstride + rg.x + x] - m;
         s += (uint64_t)(e * e);
-        if (++x == a.n) {
+        if (++x == a.nw) {
             x = 0;
             ++y;
         }
@@ -125,7 +130,7 @@ struct GenSearchArgs {
     unsigned long long* best_key;
 };
 
-constexpr uint32_t kGenMaxN = 32;
+constexpr uint32_t kGenMaxN = 32; // range sides (nw, nh ≤ 32: one wave's LDS copy of the range)
 
 __global__ void __launch_bounds__(256) gen_search(GenSearchArgs a)
 {
@@ -136,9 +141,9 @@ __global__ void __launch_bounds__(256) gen_search(GenSearchArgs a)
         return;
     const GenArgs& g = a.g;
     const frac_grid_item rg = g.ranges[r];
-    const uint32_t NN = g.n * g.n;
+    const uint32_t NN = g.nw * g.nh;
     for (uint32_t q = lane; q < NN; q += 64)
-        r4[wv][q] = (int16_t)(4 * (int)g.tgt[(size_t)(rg.y + q / g.n) * g.tstride + rg.x + q % g.n]);
+        r4[wv][q] = (int16_t)(4 * (int)g.tgt[(size_t)(rg.y + q / g.nw) * g.tstride + rg.x + q % g.nw]);
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     const uint2 seg = a.rbucket[r];
@@ -171,7 +176,7 @@ __global__ void __launch_bounds__(256) gen_search(GenSearchArgs a)
 // moves to the first transform of domain p whose error meets H (the chain's early exit,
 // transformmatcher.h:55,65; the search found the first domain holding a hit); a miss at or beyond
 // 2^24 goes to gen_fallback.  The fit is match_generic's (transformmatcher.h:89-108) with the
-// samples at ((x·S)/n, (y·S)/n); every sum is an exact integer in FP64.
+// samples at ((x·Sw)/nw, (y·Sh)/nh); every sum is an exact integer in FP64.
 struct GenFitArgs {
     GenArgs g;
     const unsigned long long* best_key;
@@ -188,19 +193,22 @@ struct GenFitArgs {
 __device__ inline void gen_write_fit(const GenArgs& g, frac_encode_item& o, const frac_grid_item& rg,
                                      const frac_grid_item& d, int t, uint64_t s16, double smax)
 {
-    const uint32_t n = g.n;
     long long sA = 0, sA2 = 0, sB = 0, sAB = 0;
-    for (uint32_t y = 0; y < n; ++y)
-        for (uint32_t x = 0; x < n; ++x) {
+    for (uint32_t y = 0; y < g.nh; ++y)
+        for (uint32_t x = 0; x < g.nw; ++x) {
             const long long rv = g.tgt[(size_t)(rg.y + y) * g.tstride + rg.x + x];
-            const long long b = gen_sample(g.src, g.sstride, d.x, d.y, g.S, t, (x * g.S) / n, (y * g.S) / n);
+            const long long b =
+                gen_sample(g.src, g.sstride, d.x, d.y, g.Sw, g.Sh, t, (x * g.Sw) / g.nw, (y * g.Sh) / g.nh);
             sA += rv;
             sA2 += rv * rv;
             sB += b;
             sAB += rv * b;
         }
     const double dist = ((double)s16 * 0.0625) / (double)(d.w * d.h);
-    const double N = (double)(n * n), sumA = (double)sA, sumA2 = (double)sA2;
+    // ΣA is ImageStatistics2::sum's: u16 arithmetic for ranges up to 16 wide (image/ImageStatistics.hpp:12-17,
+    // .cpp:14-51), which wraps for a tall rectangle (16×32: up to 130,560); squares never reach 2^16
+    const double N = (double)(g.nw * g.nh), sumA = g.nw <= 16 ? (double)(uint16_t)sA : (double)sA,
+                 sumA2 = (double)sA2;
     const double sumB = (double)sB * 0.25, sumAB = (double)sAB * 0.25;
     const double tmp = (N * sumA2 - (sumA - 1) * sumA);
     double s = fabs(tmp) < 0.00001 ? 0.0 : (N * sumAB - sumA * sumB) / tmp;
@@ -292,7 +300,7 @@ __global__ void __launch_bounds__(256) gen_fallback(GenFallbackArgs a)
     __shared__ float rpix[kGenMaxN * kGenMaxN];
     __shared__ unsigned long long red[256];
     const GenArgs& g = a.g;
-    const uint32_t NN = g.n * g.n, T = g.T;
+    const uint32_t NN = g.nw * g.nh, T = g.T;
     const uint32_t count = *a.fb_count;
     for (uint32_t e = blockIdx.x; e < count; e += gridDim.x) {
         const uint32_t r = a.fb_list[e];
@@ -301,9 +309,9 @@ __global__ void __launch_bounds__(256) gen_fallback(GenFallbackArgs a)
         const uint32_t p0 = seg.x / T; // the bucket's first pool position
         __syncthreads();
         for (uint32_t q = threadIdx.x; q < NN; q += blockDim.x)
-            rpix[q] = (float)(int16_t)g.tgt[(size_t)(rg.y + q / g.n) * g.tstride + rg.x + q % g.n];
+            rpix[q] = (float)(int16_t)g.tgt[(size_t)(rg.y + q / g.nw) * g.tstride + rg.x + q % g.nw];
         __syncthreads();
-        const double area = (double)(g.S * g.S);
+        const double area = (double)(g.Sw * g.Sh);
         unsigned long long best = kKeyNone;
         for (uint32_t v = seg.x + threadIdx.x; v < seg.y; v += blockDim.x) {
             const uint32_t* row = g.pool + (size_t)v * g.K2;

@@ -264,6 +264,11 @@ int frac_pack_frc1(frac_ctx* ctx, uint32_t contrast_bits, uint32_t brightness_bi
  * writes min(count, cap) items (categories -1). */
 size_t frac_uniform_grid(uint32_t width, uint32_t height, uint32_t item_size, uint32_t item_offset,
                          frac_grid_item* out, size_t cap);
+/* The same with createUniformGrid's Size32u item size and offset (partition2.hpp:110-113): items
+ * size_w × size_h, x stepping by off_x, rows by off_y (e.g. tests/OpenCLTest.cpp:76-78's 4×4 items
+ * at offset (4, 2)). */
+size_t frac_uniform_grid2(uint32_t width, uint32_t height, uint32_t size_w, uint32_t size_h, uint32_t off_x,
+                          uint32_t off_y, frac_grid_item* out, size_t cap);
 /* BrightnessBlocksClassifier2::preclassify over items (encode/Classifier2.cpp:64-68):
  * writes each item's category computed on `plane`. */
 int frac_classify(const uint8_t* plane, uint32_t w, uint32_t h, uint32_t stride, frac_grid_item* items, size_t n);

@@ -12,12 +12,19 @@
 //
 // It uses only the base class's public and protected interface — no change to the reference's
 // classes:
+//   * the constructor uploads the plane and the domain grid; the library validates the grid there
+//     (one item size, inside the plane, categories −1..5), so an unusable grid throws where
+//     EncodingEngine2.cpp:27-29 catches and logs "failed to create engine";
 //   * encode(item) (virtual, EncodingEngine2.hpp:63-66) only records the claimed item;
 //   * finalize() (run by the core on the engine's thread once the queue is empty,
 //     EncodingEngine2.hpp:144-145) searches every claimed item in ONE frac_search on the GPU,
 //     then hands each item to the base AbstractEncodingEngine2::encode, whose encode_impl call
 //     returns the precomputed record — so the base class's private result list and task counter
-//     fill exactly as for a CPU engine.
+//     fill exactly as for a CPU engine.  finalize() never lets an exception out: it runs on the
+//     core's worker thread with no handler (EncodingEngine2.hpp:144-145), where a throw would be
+//     std::terminate.  A failure (a HIP error, a range geometry the engine refuses) is kept, the
+//     claimed items produce no records, and rethrowIfFailed() rethrows it on the caller's thread
+//     after EncodingEngineCore2::encode returns (Encoder2.hpp:38) — see INTEGRATION.md.
 // The reference claims one range per mutex round trip (EncodingEngine2.hpp:131-140): batching it
 // on the device side is what makes a GPU engine pay off (the dormant OpenCL engine launched a
 // blocking kernel per item, gpu/opencl/OpenCLEncodingEngine.cpp:294-330).
@@ -30,6 +37,7 @@
 #include "fracenc.h"
 
 #include <cstddef>
+#include <exception>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -88,23 +96,42 @@ public:
     // a claim: recorded, searched in finalize()
     void encode(const UniformGridItem& targetItem) override { _pending.push_back(targetItem); }
 
-    // one batched search over every claimed range, then the base class records the results
-    void finalize() override
+    // one batched search over every claimed range, then the base class records the results; on
+    // the core's worker thread, so nothing may escape (see the header comment)
+    void finalize() noexcept override
     {
-        _records.resize(_pending.size());
-        frac_stats st{};
-        check(frac_search(_ctx, reinterpret_cast<const frac_grid_item*>(_pending.data()), _pending.size(),
-                          reinterpret_cast<frac_encode_item*>(_records.data()), &st));
-        _rejected += st.rejected_mappings;
-        _next = 0;
-        for (const auto& item : _pending)
-            AbstractEncodingEngine2::encode(item); // → encode_impl → _records[_next++]
+        try {
+            _records.resize(_pending.size());
+            frac_stats st{};
+            check(frac_search(_ctx, reinterpret_cast<const frac_grid_item*>(_pending.data()), _pending.size(),
+                              reinterpret_cast<frac_encode_item*>(_records.data()), &st));
+            _rejected += st.rejected_mappings;
+            _next = 0;
+            for (const auto& item : _pending)
+                AbstractEncodingEngine2::encode(item); // → encode_impl → _records[_next++]
+            _searched += _pending.size();
+        } catch (...) {
+            _failed = std::current_exception();
+            _lost += _pending.size();
+        }
         _pending.clear();
         _records.clear();
     }
 
+    // On the caller's thread after EncodingEngineCore2::encode: rethrows a failure of finalize()
+    // (whose claimed ranges then have no record in the core's result).
+    void rethrowIfFailed() const
+    {
+        if (_failed)
+            std::rethrow_exception(_failed);
+    }
+    bool failed() const noexcept { return _failed != nullptr; }
+
     // TransformEstimator2::rejectedMappings() of the ranges this engine searched
     uint64_t rejectedMappings() const noexcept { return _rejected; }
+    // ranges searched by this engine / claimed but lost to a failure
+    size_t searchedRanges() const noexcept { return _searched; }
+    size_t lostRanges() const noexcept { return _lost; }
 
 protected:
     encode_item_t encode_impl(const UniformGridItem& targetItem) const override
@@ -128,6 +155,8 @@ private:
     std::vector<encode_item_t> _records;
     mutable size_t _next = 0;
     uint64_t _rejected = 0;
+    size_t _searched = 0, _lost = 0;
+    std::exception_ptr _failed;
 };
 
 } // namespace Frac2

@@ -38,6 +38,8 @@ def lib():
         L.or_category.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32]
         L.or_uniform_grid.restype = C.c_size_t
         L.or_uniform_grid.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p, C.c_size_t]
+        L.or_uniform_grid2.restype = C.c_size_t
+        L.or_uniform_grid2.argtypes = [C.c_uint32] * 6 + [C.c_void_p, C.c_size_t]
         L.or_estimate.restype = C.c_int
         L.or_estimate.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32, C.c_void_p, C.c_size_t, C.c_void_p,
                                   C.c_size_t, C.c_int, C.c_double, C.c_double, C.c_int, C.c_int, C.c_void_p,
@@ -54,10 +56,13 @@ def category(plane: np.ndarray, x: int, y: int, w: int, h: int | None = None) ->
     return lib().or_category(plane.ctypes.data, plane.shape[1], x, y, w, w if h is None else h)
 
 
-def uniform_grid(W: int, H: int, size: int, offset: int) -> np.ndarray:
-    n = lib().or_uniform_grid(W, H, size, offset, None, 0)
+def uniform_grid(W: int, H: int, size, offset) -> np.ndarray:
+    """createUniformGrid; size / offset an int or (x, y) (the reference's Size32u)."""
+    sw, sh = (size, size) if np.isscalar(size) else size
+    ox, oy = (offset, offset) if np.isscalar(offset) else offset
+    n = lib().or_uniform_grid2(W, H, sw, sh, ox, oy, None, 0)
     out = np.zeros(n, dtype=ITEM_DTYPE)
-    lib().or_uniform_grid(W, H, size, offset, out.ctypes.data, n)
+    lib().or_uniform_grid2(W, H, sw, sh, ox, oy, out.ctypes.data, n)
     return out
 
 
@@ -141,6 +146,24 @@ def ref_lib():
                                   C.c_size_t, C.c_void_p, C.POINTER(C.c_uint64), C.c_double, C.POINTER(C.c_size_t)]
         _ref = L
     return _ref
+
+
+def ref_uniform_grid(W: int, H: int, size, offset):
+    """The REFERENCE's createUniformGrid (Size32u size / offset), or None when the build is absent.
+    The reference FRAC_ASSERTs an area that is not a multiple of the size and offset (exit 0): only
+    aligned arguments are passed here."""
+    L = ref_lib()
+    if L is None:
+        return None
+    sw, sh = (size, size) if np.isscalar(size) else size
+    ox, oy = (offset, offset) if np.isscalar(offset) else offset
+    assert W % sw == 0 and H % sh == 0 and W % ox == 0 and H % oy == 0, "unaligned: the reference exits"
+    L.fr_uniform_grid.restype = C.c_size_t
+    L.fr_uniform_grid.argtypes = [C.c_uint32] * 6 + [C.c_void_p, C.c_size_t]
+    n = L.fr_uniform_grid(W, H, sw, sh, ox, oy, None, 0)
+    out = np.zeros(n, dtype=ITEM_DTYPE)
+    L.fr_uniform_grid(W, H, sw, sh, ox, oy, out.ctypes.data, n)
+    return out
 
 
 def ref_quantize(vmin: float, vmax: float, bits: int, values: np.ndarray):

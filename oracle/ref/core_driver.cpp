@@ -1,6 +1,7 @@
 // core_driver.cpp — runs the REFERENCE's EncodingEngineCore2 (encode/EncodingEngine2.hpp:115-180,
 // EncodingEngine2.cpp:7-30, compiled unmodified from /root/reference) with the HIP engine of
-// integration/HipEncodingEngine2.hpp registered and the CPU engines off (--nocpu, main.cpp:83-84).
+// integration/HipEncodingEngine2.hpp registered — alone (--nocpu, main.cpp:83-84), or beside the
+// reference's hardware_concurrency CPU engines sharing the one claim queue (the default CLI).
 //
 // TEST INFRASTRUCTURE (tests/test_integration.py).  The reference registers accelerator engines
 // inside EncodingEngineCore2's constructor (EncodingEngine2.cpp:21-29, the commented OpenCL block);
@@ -9,9 +10,12 @@
 // instantiation access idiom (access checks do not apply to explicit instantiations,
 // [temp.spec.general]/6) — the registration itself, nothing else.
 //
-// usage: core_driver PLANE.u8 W H SRC TGT CLASSIFIER(0|1) RMS_THR SMAX OUT.bin
+// usage: core_driver PLANE.u8 W H SRC TGT CLASSIFIER(0|1) RMS_THR SMAX OUT.bin [CPU(0|1)]
 //   OUT.bin: the core's result().encoded (encode_item_t, 64 B each) in the core's order, then the
-//   HIP engine's rejected-mapping count (u64).
+//   rejected-mapping count of the whole search (u64: the CPU engines' estimator plus the HIP
+//   engine's) and the number of ranges the HIP engine searched (u64).
+//   Exit 6 (message on stderr) when the HIP engine's finalize() failed: rethrowIfFailed() on this
+//   thread, after the core's workers have joined — not std::terminate on a worker.
 #include "encode/EncodingEngine2.hpp"
 #include "encode/Classifier2.hpp"
 #include "encode/TransformEstimator2.hpp"
@@ -42,8 +46,8 @@ struct NullReporter : ProgressReporter2 {
 
 int main(int argc, char** argv)
 {
-    if (argc != 10) {
-        std::fprintf(stderr, "usage: %s PLANE W H SRC TGT CLS THR SMAX OUT\n", argv[0]);
+    if (argc != 10 && argc != 11) {
+        std::fprintf(stderr, "usage: %s PLANE W H SRC TGT CLS THR SMAX OUT [CPU]\n", argv[0]);
         return 2;
     }
     const uint32_t W = std::atoi(argv[2]), H = std::atoi(argv[3]);
@@ -53,7 +57,7 @@ int main(int argc, char** argv)
     params.noclassifier = std::atoi(argv[6]) == 0;
     params.rmsThreshold = std::atof(argv[7]);
     params.sMax = std::atof(argv[8]);
-    params.nocpu = true;
+    params.nocpu = argc == 11 ? std::atoi(argv[10]) == 0 : true;
     std::vector<uint8_t> buf(size_t(W) * H);
     {
         std::ifstream f(argv[1], std::ios::binary);
@@ -93,10 +97,19 @@ int main(int argc, char** argv)
         return 4;
     }
     core.encode(targetGrid);
-    rejected = hip->rejectedMappings();
+    try {
+        hip->rethrowIfFailed(); // the failure of finalize(), on this thread
+    } catch (const std::exception& exc) {
+        std::fprintf(stderr, "HIP engine failed: %s (%zu ranges without a record)\n", exc.what(), hip->lostRanges());
+        return 6;
+    }
+    // the CPU engines' rejected mappings accumulate in the shared estimator (TransformEstimator2.hpp:59)
+    rejected = estimator.rejectedMappings() + hip->rejectedMappings();
+    const uint64_t hip_ranges = hip->searchedRanges();
     const auto data = core.result();
     std::ofstream out(argv[9], std::ios::binary);
     out.write(reinterpret_cast<const char*>(data.encoded.data()), data.encoded.size() * sizeof(Frac::encode_item_t));
     out.write(reinterpret_cast<const char*>(&rejected), sizeof(rejected));
+    out.write(reinterpret_cast<const char*>(&hip_ranges), sizeof(hip_ranges));
     return out ? 0 : 5;
 }

@@ -175,6 +175,112 @@ int fr_estimate(const uint8_t* src, const uint8_t* tgt, uint32_t w, uint32_t h, 
     return 0;
 }
 
+// createUniformGrid (image/partition2.hpp:109-135) with the reference's Size32u item size and
+// offset (tests/OpenCLTest.cpp:76-78 uses 4×4 items at offset (4, 2)).  Returns the item count,
+// writes at most cap items {x, y, w, h, category = -1}.
+struct fr_item {
+    uint32_t x, y, w, h;
+    int32_t category;
+};
+
+size_t fr_uniform_grid(uint32_t w, uint32_t h, uint32_t sw, uint32_t sh, uint32_t ox, uint32_t oy, fr_item* out,
+                       size_t cap)
+{
+    const auto grid = createUniformGrid(Size32u(w, h), Size32u(sw, sh), Size32u(ox, oy));
+    const auto& items = grid.items();
+    for (size_t i = 0; i < items.size() && i < cap; ++i)
+        out[i] = fr_item{items[i].origin.x(), items[i].origin.y(), items[i].size.x(), items[i].size.y(),
+                         items[i].data.bb_classifierBin};
+    return items.size();
+}
+
+// BrightnessBlocksClassifier2::preclassify (encode/Classifier2.cpp:64-68) of arbitrary items on
+// `plane` (the grid-build callback of main.cpp:155-159 and tests/OpenCLTest.cpp:79-84).
+int fr_classify_items(const uint8_t* plane, uint32_t w, uint32_t h, uint32_t stride, fr_item* items, size_t n)
+{
+    auto img = make_plane(plane, w, h, stride);
+    BrightnessBlocksClassifier2 classifier(img, img);
+    for (size_t i = 0; i < n; ++i) {
+        UniformGridItem::ExtraData data;
+        classifier.preclassify(Point2du(items[i].x, items[i].y), Size32u(items[i].w, items[i].h), data);
+        items[i].category = data.bb_classifierBin;
+    }
+    return 0;
+}
+
+// TransformEstimator2::estimate (encode/TransformEstimator2.hpp:29-48) over caller-given domain and
+// range item lists — any item sizes the reference's types hold (Size32u: rectangles included) —
+// with the classifier categories preclassified on the source plane as main.cpp:155-161 does.
+// out[] and the reject count as fr_estimate; single-threaded.
+int fr_estimate_items(const uint8_t* src, const uint8_t* tgt, uint32_t w, uint32_t h, uint32_t stride,
+                      const fr_item* doms, size_t nd, const fr_item* rngs, size_t nr, int ntransforms, double thr,
+                      double smax, int use_classifier, fr_result* out, uint64_t* rejected)
+{
+    auto srcImg = make_plane(src, w, h, stride);
+    auto tgtImg = make_plane(tgt, w, h, stride);
+    std::unique_ptr<Classifier2> classifier;
+    if (use_classifier)
+        classifier = std::make_unique<BrightnessBlocksClassifier2>(srcImg, tgtImg);
+    else
+        classifier = std::make_unique<DummyClassifier>(srcImg, tgtImg);
+    UniformGrid sourceGrid = UniformGrid::createEmpty(0);
+    std::vector<UniformGridItem> ranges;
+    for (size_t i = 0; i < nd; ++i) {
+        UniformGridItem::ExtraData data;
+        classifier->preclassify(Point2du(doms[i].x, doms[i].y), Size32u(doms[i].w, doms[i].h), data);
+        sourceGrid.add(Point2du(doms[i].x, doms[i].y), Size32u(doms[i].w, doms[i].h), std::move(data));
+    }
+    for (size_t i = 0; i < nr; ++i) {
+        UniformGridItem::ExtraData data;
+        classifier->preclassify(Point2du(rngs[i].x, rngs[i].y), Size32u(rngs[i].w, rngs[i].h), data);
+        ranges.push_back(UniformGridItem(Point2du(rngs[i].x, rngs[i].y), Size32u(rngs[i].w, rngs[i].h), std::move(data)));
+    }
+    auto matcher = std::make_shared<TransformMatcher>(thr, smax);
+    const Classifier2* cls = classifier.get();
+    TransformEstimator2 estimator(srcImg, tgtImg, std::move(classifier), matcher, sourceGrid);
+    uint64_t rej8 = 0;
+    auto run8 = [&](const UniformGridItem& r) { // driver B (fr_estimate): estimate()'s loop, 8-transform chain
+        item_match_t result;
+        for (const auto& d : sourceGrid.items()) {
+            if (cls->compare(d, r)) {
+                auto score = matcher->matchTransformTypes<TransformType::Id, TransformType::Rotate_90,
+                    TransformType::Rotate_180, TransformType::Rotate_270, TransformType::Flip,
+                    TransformType::Flip_Rotate_90, TransformType::Flip_Rotate_180,
+                    TransformType::Flip_Rotate_270>(srcImg, d, tgtImg, r, transform_score_t{});
+                if (score.distance < result.score.distance) {
+                    result.score = score;
+                    result.x = d.origin.x();
+                    result.y = d.origin.y();
+                    result.sourceItemSize = d.size;
+                }
+                if (matcher->checkDistance(result.score.distance))
+                    break;
+            } else {
+                ++rej8;
+            }
+        }
+        return result;
+    };
+    for (size_t i = 0; i < nr; ++i) {
+        const item_match_t m = ntransforms == 8 ? run8(ranges[i]) : estimator.estimate(ranges[i]);
+        fr_result& o = out[i];
+        o.x = ranges[i].origin.x();
+        o.y = ranges[i].origin.y();
+        o.dx = m.x;
+        o.dy = m.y;
+        o.dw = m.sourceItemSize.x();
+        o.dh = m.sourceItemSize.y();
+        o.transform = static_cast<int32_t>(m.score.transform);
+        o.pad = 0;
+        o.distance = m.score.distance;
+        o.contrast = m.score.contrast;
+        o.brightness = m.score.brightness;
+    }
+    if (rejected)
+        *rejected = ntransforms == 8 ? rej8 : estimator.rejectedMappings();
+    return 0;
+}
+
 // Full reference decode (encode/Encoder2.hpp:67-99) of an encoding given as
 // fr_result records in range order; returns iterations, writes the plane.
 int fr_decode(const fr_result* recs, size_t n, uint32_t tgt_size, uint32_t w, uint32_t h,

@@ -68,10 +68,33 @@ def selection(meta: dict, n_ranges: int):
     raise ValueError(sel)
 
 
-# per-range search goldens (decode / quantizer / colour fixtures live beside them)
+def grid_specs(meta: dict, W: int, H: int):
+    """(domain spec, range spec) of a golden as createUniformGrid arguments (area W, H, item w, h,
+    offset x, y): the CLI's square grids (domains src at offset src/2, main.cpp:147) for an int
+    src/tgt, the stored Size32u specs of the rectangular goldens otherwise."""
+    src, tgt = meta["src"], meta["tgt"]
+    d = (W, H, src, src, src // 2, src // 2) if np.isscalar(src) else tuple(src)
+    r = (W, H, tgt, tgt, tgt, tgt) if np.isscalar(tgt) else tuple(tgt)
+    return d, r
+
+
+def make_grids(uniform_grid, classify, p: np.ndarray, meta: dict):
+    """The golden's domain and range grids by `uniform_grid(W, H, size, offset)` (the engine's or the
+    oracle's), preclassified on the plane when the golden has the classifier (main.cpp:155-162)."""
+    H, W = p.shape
+    d, r = grid_specs(meta, W, H)
+    doms = uniform_grid(d[0], d[1], (d[2], d[3]), (d[4], d[5]))
+    rngs = uniform_grid(r[0], r[1], (r[2], r[3]), (r[4], r[5]))
+    if meta["cls"]:
+        doms = classify(p, doms)
+        rngs = classify(p, rngs)
+    return doms, rngs
+
+
+# per-range search goldens (decode / quantizer / colour / classifier fixtures live beside them)
 GOLDEN_NAMES = sorted(f[:-4] for f in os.listdir(GOLD)
                       if f.endswith(".npz") and not f.endswith(("_decode.npz", "_quant.npz"))
-                      and not f.startswith("rgb_"))
+                      and not f.startswith(("rgb_", "opencl_")))
 
 
 _MAP = (("x", "x"), ("y", "y"), ("dx", "dx"), ("dy", "dy"), ("sw", "dw"), ("sh", "dh"), ("transform", "t"),

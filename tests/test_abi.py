@@ -73,6 +73,22 @@ def test_uniform_grid_matches_oracle(oracle, W, H, size, off):
         np.testing.assert_array_equal(g[k], o[k])
 
 
+@pytest.mark.parametrize("W,H,size,off", [(512, 512, (4, 4), (4, 2)), (64, 48, (16, 8), (8, 4)), (96, 64, (8, 4), (4, 2)),
+                                          (64, 64, (8, 16), (2, 4)), (48, 40, (12, 8), (6, 8))])
+def test_anisotropic_uniform_grid(oracle, W, H, size, off):
+    # createUniformGrid's Size32u item size and offset (image/partition2.hpp:110-113): the engine's grid
+    # equals the oracle's and — when the reference build is present — the reference's own
+    g = F.create_uniform_grid(W, H, size, off)
+    o = oracle.uniform_grid(W, H, size, off)
+    assert len(g) == len(o) > 0
+    for k in ("x", "y", "w", "h", "category"):
+        np.testing.assert_array_equal(g[k], o[k])
+    r = oracle.ref_uniform_grid(W, H, size, off)
+    if r is not None:
+        for k in ("x", "y", "w", "h", "category"):
+            np.testing.assert_array_equal(g[k], r[k])
+
+
 def test_preclassify_matches_oracle(oracle):
     from golden_util import plane
     y = plane("lenna_y")

