@@ -200,7 +200,8 @@ struct frac_ctx {
     uint32_t nblocks = 0, ntiles = 0;
     std::vector<uint4> m_work;             // per WG (4 range blocks: search_mfma)
     std::vector<uint32_t> m_blk_ptr, m_blk_ent;
-    std::vector<uint4> m8_work;            // per WG (8 range blocks: search_dft)
+    std::vector<uint4> m8_work;            // per WG (8 range blocks: search_dft; m8_bpw for the 16-wave forms)
+    uint32_t m8_bpw = 8;                   // range blocks per workgroup of m8_work
     std::vector<uint32_t> m8_blk_ptr, m8_blk_ent;
     DBuf<uint4> d_m8_work;
     DBuf<uint32_t> d_m8_blk_ptr, d_m8_blk_ent;
@@ -487,7 +488,13 @@ inline bool dft_four_wave(int var)
 // 6 (kDft6, variants 21, 23)
 constexpr int kTpVar = 1 | kDftChain | (kDftTpForm == 6 ? kDft6 : 0); // the SEA tiled form's search_dft
 constexpr uint32_t kTpKS = kDftTpForm == 4 ? 4u : 5u;                    // its domain fragments per tile
-inline int dft_form(int var) { return var == 20 || var == 22 ? 5 : var == 21 || var == 23 || var == 26 ? 6 : 4; }
+inline int dft_form(int var)
+{
+    return var == 20 || var == 22 ? 5 : var == 21 || var == 23 || var == 26 || var == 27 || var == 28 ? 6 : 4;
+}
+// range blocks (waves) per workgroup of the Fourier search: 16 for variants 27 / 28 (1024-thread
+// workgroups: each LDS stage serves twice the blocks, half the LDS-DMA per tile pair), else 8
+inline uint32_t dft_bpw(int var) { return var == 27 || var == 28 ? 16u : kDftBlocksPerWG; }
 // The Fourier path's own variants: 1, 3 (4-wave exact / guarded), 5 (8-tile stages), 6 (pairwise-tree
 // row maximum), 12 (two range blocks per wave), 20 / 22 (five-MFMA form, packed / plain epilogue),
 // 21 / 23 (six-MFMA form, one / two range blocks per wave), 24 (the 8-MFMA exact form in 8-wave
@@ -497,7 +504,7 @@ inline int dft_form(int var) { return var == 20 || var == 22 ? 5 : var == 21 || 
 constexpr int kDftDefaultVariant = 21; // the six-MFMA form: 13.71 vs 15.23 ms (24) at C3, 12-round A/B
 inline int dft_variant(int var)
 {
-    static const int own[] = {1, 3, 5, 6, 12, 20, 21, 22, 23, 24, 26, 9, 17, 41, 65, 73, 105};
+    static const int own[] = {1, 3, 5, 6, 12, 20, 21, 22, 23, 24, 26, 27, 28, 9, 17, 41, 65, 73, 105};
     for (int v : own)
         if (var == v)
             return var;
@@ -919,10 +926,11 @@ int prepare(frac_ctx* c)
         if (n == 8 && c->p.transforms == 4 && !c->virt) {
             // FRAC_DFT_WGS (tuning knob): target workgroup count of the Fourier search
             const char* tw = getenv("FRAC_DFT_WGS");
-            const size_t wgs = tw ? (size_t)std::max(1, atoi(tw)) : 8192 / kDftBlocksPerWG * 4;
+            c->m8_bpw = dft_bpw(dft_variant(var));
+            const size_t wgs = tw ? (size_t)std::max(1, atoi(tw)) : 8192 / c->m8_bpw * 4;
             // FRAC_XCD_ORDER (tuning knob): 0 = work items in (block group, split) order
             const char* xo = getenv("FRAC_XCD_ORDER");
-            build_work(kDftBlocksPerWG, wgs, c->m8_work, c->m8_blk_ptr, c->m8_blk_ent, xo ? atoi(xo) != 0 : true);
+            build_work(c->m8_bpw, wgs, c->m8_work, c->m8_blk_ptr, c->m8_blk_ent, xo ? atoi(xo) != 0 : true);
         }
         else {
             c->m8_work.clear();
@@ -1036,7 +1044,7 @@ int prepare(frac_ctx* c)
         FRAC_HIP(c, c->d_m_dconst.ensure((size_t)c->ntiles * 32));
         FRAC_HIP(c, c->d_m_dtiles.ensure((size_t)c->ntiles * KS * 64));
         FRAC_HIP(c, c->d_m_rfrags.ensure((size_t)c->nblocks * c->Teff * KS * 64));
-        FRAC_HIP(c, c->d_m_entries.ensure(std::max(c->m_work.size() * 4 * c->Teff, c->m8_work.size() * kDftBlocksPerWG) *
+        FRAC_HIP(c, c->d_m_entries.ensure(std::max(c->m_work.size() * 4 * c->Teff, c->m8_work.size() * c->m8_bpw) *
                                           64));
         if (!c->m8_blk_ptr.empty()) { // built for n = 8, T = 4 (search_dft); may have no work
             FRAC_HIP(c, c->d_m8_work.ensure(std::max<size_t>(c->m8_work.size(), 1)));
@@ -1091,7 +1099,7 @@ inline int mfma_variant(frac_ctx* c, int& var)
         return FRAC_OK;
     char* end = nullptr;
     const long x = strtol(v, &end, 10);
-    static const int exact[] = {0, 1, 2, 3, 4, 5, 6, 7, 12, 20, 21, 22, 23, 24, 26, 32, 64, 96, 98, 128, 130};
+    static const int exact[] = {0, 1, 2, 3, 4, 5, 6, 7, 12, 20, 21, 22, 23, 24, 26, 27, 28, 32, 64, 96, 98, 128, 130};
     static const int ablation[] = {8, 9, 16, 17, 41, 65, 73, 105, 201, 202, 203, 204, 205, 206, 207, 226, 227};
     bool ok = end && *end == 0;
     bool known = false;
@@ -1256,6 +1264,20 @@ inline int launch_dft(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride)
                 search_dft2<true, true><<<nwg, 256, 0, c->stream>>>(da);
             else
                 search_dft2<false, true><<<nwg, 256, 0, c->stream>>>(da);
+        } else if (form == 6 && (var == 27 || var == 28)) { // 16 range blocks per (1024-thread) workgroup
+            if (c->m8_bpw != 16)
+                return c->fail(FRAC_E_STATE, "search_dft: work lists built for another workgroup size");
+            if (var == 27) {
+                if (hits)
+                    search_dft<true, 1 | kDftChain | kDft6, 16><<<nwg, 1024, 0, c->stream>>>(da);
+                else
+                    search_dft<false, 1 | kDftChain | kDft6, 16><<<nwg, 1024, 0, c->stream>>>(da);
+            } else {
+                if (hits)
+                    search_dft<true, 1 | kDftChain | kDft6 | kDftFast6, 16><<<nwg, 1024, 0, c->stream>>>(da);
+                else
+                    search_dft<false, 1 | kDftChain | kDft6 | kDftFast6, 16><<<nwg, 1024, 0, c->stream>>>(da);
+            }
         } else if (form == 6 && var == 26) { // the six-MFMA form, guarded constant-folded epilogue
             if (hits)
                 search_dft<true, 1 | kDftChain | kDft6 | kDftFast6, W8><<<nwg, 64 * W8, 0, c->stream>>>(da);
