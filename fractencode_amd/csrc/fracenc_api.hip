@@ -490,7 +490,9 @@ constexpr int kTpVar = 1 | kDftChain | (kDftTpForm == 6 ? kDft6 : 0); // the SEA
 constexpr uint32_t kTpKS = kDftTpForm == 4 ? 4u : 5u;                    // its domain fragments per tile
 inline int dft_form(int var)
 {
-    return var == 20 || var == 22 ? 5 : var == 21 || var == 23 || var == 26 || var == 27 || var == 28 ? 6 : 4;
+    return var == 20 || var == 22                                                  ? 5
+           : var == 21 || var == 23 || (var >= 26 && var <= 28) || (var >= 33 && var <= 36) ? 6
+                                                                                          : 4;
 }
 // range blocks (waves) per workgroup of the Fourier search: 16 for variants 27 / 28 (1024-thread
 // workgroups: each LDS stage serves twice the blocks, half the LDS-DMA per tile pair), else 8
@@ -504,7 +506,7 @@ inline uint32_t dft_bpw(int var) { return var == 27 || var == 28 ? 16u : kDftBlo
 constexpr int kDftDefaultVariant = 21; // the six-MFMA form: 13.71 vs 15.23 ms (24) at C3, 12-round A/B
 inline int dft_variant(int var)
 {
-    static const int own[] = {1, 3, 5, 6, 12, 20, 21, 22, 23, 24, 26, 27, 28, 9, 17, 41, 65, 73, 105};
+    static const int own[] = {1, 3, 5, 6, 12, 20, 21, 22, 23, 24, 26, 27, 28, 33, 34, 35, 36, 9, 17, 41, 65, 73, 105};
     for (int v : own)
         if (var == v)
             return var;
@@ -1099,7 +1101,8 @@ inline int mfma_variant(frac_ctx* c, int& var)
         return FRAC_OK;
     char* end = nullptr;
     const long x = strtol(v, &end, 10);
-    static const int exact[] = {0, 1, 2, 3, 4, 5, 6, 7, 12, 20, 21, 22, 23, 24, 26, 27, 28, 32, 64, 96, 98, 128, 130};
+    static const int exact[] = {0,  1,  2,  3,  4,  5,  6,  7,  12, 20, 21, 22, 23, 24, 26,
+                                28, 27, 32, 33, 34, 35, 36, 64, 96, 98, 128, 130};
     static const int ablation[] = {8, 9, 16, 17, 41, 65, 73, 105, 201, 202, 203, 204, 205, 206, 207, 226, 227};
     bool ok = end && *end == 0;
     bool known = false;
@@ -1277,6 +1280,34 @@ inline int launch_dft(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride)
                     search_dft<true, 1 | kDftChain | kDft6 | kDftFast6, 16><<<nwg, 1024, 0, c->stream>>>(da);
                 else
                     search_dft<false, 1 | kDftChain | kDft6 | kDftFast6, 16><<<nwg, 1024, 0, c->stream>>>(da);
+            }
+        } else if (form == 6 && var >= 33 && var <= 36) { // 26 with the issue-cost knobs
+            constexpr int V = 1 | kDftChain | kDft6 | kDftFast6;
+            switch (var) {
+            case 33: // unrolled chunk
+                if (hits)
+                    search_dft<true, V | kDftUnroll, W8><<<nwg, 64 * W8, 0, c->stream>>>(da);
+                else
+                    search_dft<false, V | kDftUnroll, W8><<<nwg, 64 * W8, 0, c->stream>>>(da);
+                break;
+            case 34: // buffer_load … lds stages
+                if (hits)
+                    search_dft<true, V | kDftBufDma, W8><<<nwg, 64 * W8, 0, c->stream>>>(da);
+                else
+                    search_dft<false, V | kDftBufDma, W8><<<nwg, 64 * W8, 0, c->stream>>>(da);
+                break;
+            case 35: // both
+                if (hits)
+                    search_dft<true, V | kDftUnroll | kDftBufDma, W8><<<nwg, 64 * W8, 0, c->stream>>>(da);
+                else
+                    search_dft<false, V | kDftUnroll | kDftBufDma, W8><<<nwg, 64 * W8, 0, c->stream>>>(da);
+                break;
+            default: // both, second half of the waves at s_setprio 1
+                if (hits)
+                    search_dft<true, V | kDftUnroll | kDftBufDma | kDftPrio, W8><<<nwg, 64 * W8, 0, c->stream>>>(da);
+                else
+                    search_dft<false, V | kDftUnroll | kDftBufDma | kDftPrio, W8><<<nwg, 64 * W8, 0, c->stream>>>(da);
+                break;
             }
         } else if (form == 6 && var == 26) { // the six-MFMA form, guarded constant-folded epilogue
             if (hits)

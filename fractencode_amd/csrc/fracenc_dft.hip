@@ -125,6 +125,12 @@ constexpr int kDft5 = 2048;
 constexpr int kDftScalar = 4096; // with kDft5: the P ± M and the fma one row per instruction
 constexpr int kDft6 = 8192;      // the six-MFMA form (dft_tile_max6)
 constexpr int kDftFast6 = 16384; // with kDft6: the guarded constant-folded epilogue (dft_tile_max6_fast)
+// issue-cost knobs of the search loop (A/B): the 4-tile chunk unrolled (LDS reads at immediate
+// offsets from one base), the stage's LDS-DMA by buffer_load … lds (the stage base in an SGPR
+// soffset, per-thread offsets fixed: no VALU per piece), waves of the second half at s_setprio 1
+constexpr int kDftUnroll = 32768;
+constexpr int kDftBufDma = 65536;
+constexpr int kDftPrio = 131072;
 
 // The five- and six-MFMA forms track h = y/2 = 4·max_t Z_t − Σb²/2 instead of y: the row constant
 // (dconst) is −Σb²/2 — exact in f32 (Σb² ≤ 2^24, so a half-integer of magnitude ≤ 2^23) — and the
@@ -810,9 +816,35 @@ __device__ inline float dft_compute_stage(const uint4* __restrict__ la, uint32_t
         }
     };
     const uint32_t qe = min(q1, nt);
-    for (uint32_t q = q0; q < qe; ++q)
-        tile(q);
+    if constexpr ((VAR & kDftUnroll) != 0) {
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k)
+            if (q0 + k < qe)
+                tile(q0 + k);
+    } else {
+        for (uint32_t q = q0; q < qe; ++q)
+            tile(q);
+    }
     return cm;
+}
+
+// stage_tiles by buffer_load … lds: the same LDS image, the stage's base offset in the SGPR
+// soffset and each thread's piece offsets the same for every stage (no per-piece address VALU)
+template <int KS, uint32_t NTHREADS>
+__device__ inline void stage_tiles_buf(uint4* dst, __amdgpu_buffer_rsrc_t ra, __amdgpu_buffer_rsrc_t rc, uint32_t tb,
+                                       uint32_t nt)
+{
+    const uint32_t na = nt * KS * 64u, ntot = na + nt * 8u; // na is a whole number of waves' pieces
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t sa = __builtin_amdgcn_readfirstlane(tb * (uint32_t)KS * 64u * 16u);
+    const uint32_t sc = __builtin_amdgcn_readfirstlane(tb * 8u * 16u);
+    for (uint32_t i = threadIdx.x; i < ntot; i += NTHREADS) {
+        auto* l = (__attribute__((address_space(3))) void*)(dst + (i - lane));
+        if (i < na)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, l, 16, i * 16u, sa, 0, 0);
+        else
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rc, l, 16, (i - na) * 16u, sc, 0, 0);
+    }
 }
 
 constexpr uint32_t kDftBlocksPerWG = 8; // waves (range blocks) sharing one LDS domain stage
@@ -894,15 +926,26 @@ __global__ void __launch_bounds__(64 * WAVES) search_dft(DftArgs d)
     // stages; 256 no LDS-DMA (barriers kept); 512 no barrier (LDS-DMA kept)
     constexpr bool NODMA = (VAR & 64) != 0;
     constexpr bool SKIPDMA = NODMA || (VAR & 256) != 0, SKIPBAR = NODMA || (VAR & 512) != 0;
+    auto stage = [&](uint4* dst, uint32_t tb, uint32_t nt) {
+        if constexpr ((VAR & kDftBufDma) != 0) // raw buffers (no range check: the pieces are in bounds)
+            stage_tiles_buf<KS, 64 * WAVES>(
+                dst, __builtin_amdgcn_make_buffer_rsrc((void*)a.dtiles, 0, 0xffffffffu, 0x00020000),
+                __builtin_amdgcn_make_buffer_rsrc((void*)a.dconst, 0, 0xffffffffu, 0x00020000), tb, nt);
+        else
+            stage_tiles<KS, 64 * WAVES>(dst, a.dtiles, a.dconst, tb, nt);
+    };
+    if constexpr ((VAR & kDftPrio) != 0)
+        if (wv >= WAVES / 2)
+            __builtin_amdgcn_s_setprio(1);
     if (nstage)
-        stage_tiles<KS, 64 * WAVES>(lds0, a.dtiles, a.dconst, wk.z, stage_nt(0));
+        stage(lds0, wk.z, stage_nt(0));
     for (uint32_t st = 0; st < nstage; st += 2) {
         {
             const uint32_t tb = wk.z + st * kTilesPerStage;
             if (!SKIPBAR || st < 2)
                 stage_barrier();
             if (st + 1 < nstage && (!SKIPDMA || st == 0))
-                stage_tiles<KS, 64 * WAVES>(lds1, a.dtiles, a.dconst, tb + kTilesPerStage, stage_nt(st + 1));
+                stage(lds1, tb + kTilesPerStage, stage_nt(st + 1));
             for (uint32_t c0 = 0; c0 < stage_nt(st); c0 += 4)
                 finish_stage(dft_compute_stage<VAR, CHUNKED, HITS>(lds0, stage_nt(st), lane, bf, tb, d.tguard, r1, c0,
                                                                    c0 + 4, masks, hl, STAGE, d.trmax),
@@ -913,7 +956,7 @@ __global__ void __launch_bounds__(64 * WAVES) search_dft(DftArgs d)
             if (!SKIPBAR || st < 2)
                 stage_barrier();
             if (st + 2 < nstage && !SKIPDMA)
-                stage_tiles<KS, 64 * WAVES>(lds0, a.dtiles, a.dconst, tb + kTilesPerStage, stage_nt(st + 2));
+                stage(lds0, tb + kTilesPerStage, stage_nt(st + 2));
             for (uint32_t c0 = 0; c0 < stage_nt(st + 1); c0 += 4)
                 finish_stage(dft_compute_stage<VAR, CHUNKED, HITS>(lds1, stage_nt(st + 1), lane, bf, tb, d.tguard, r1,
                                                                    c0, c0 + 4, masks, hl, STAGE, d.trmax),

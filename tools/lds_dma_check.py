@@ -23,7 +23,13 @@ LLVM = "/opt/rocm/lib/llvm/bin"
 FUNC = re.compile(r"^([0-9a-f]+) <(.+)>:$")
 INSN = re.compile(r"^\s+(\S+)\s*(.*?)\s*//\s*([0-9A-Fa-f]+):")
 TARGET = re.compile(r"<(.+?)\+0x([0-9a-f]+)>")
-DMA = re.compile(r"^(global_load_lds_|buffer_load_.*lds|global_load_lds)")
+DMA_OP = re.compile(r"^(global_load_lds|buffer_load_)")
+
+
+def is_dma(op: str, line: str) -> bool:
+    """An LDS-DMA load: global_load_lds_*, or a buffer_load_* with the lds modifier."""
+    m = DMA_OP.match(op)
+    return bool(m) and (op.startswith("global_load_lds") or re.search(r"\blds\b", line.split("//")[0]) is not None)
 
 
 def code_object(path: str, workdir: str) -> str:
@@ -95,7 +101,7 @@ def violations(insns: list[tuple[int, str, str]]) -> list[str]:
         _, op, line = insns[i]
         if op == "s_barrier" and p:
             bad.add(i)
-        if DMA.match(op):
+        if is_dma(op, line):
             p = True
         elif op == "s_waitcnt" and re.search(r"\bvmcnt\(0\)", line):
             p = False
@@ -114,7 +120,7 @@ def check(path: str, kernel_regex: str = ".*") -> tuple[dict[str, list[str]], li
     rx = re.compile(kernel_regex)
     res, checked = {}, []
     for name, insns in funcs.items():
-        if not rx.search(name) or not any(DMA.match(op) for _, op, _ in insns):
+        if not rx.search(name) or not any(is_dma(op, line) for _, op, line in insns):
             continue
         checked.append(name)
         v = violations(insns)
