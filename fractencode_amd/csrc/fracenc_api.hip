@@ -491,7 +491,7 @@ constexpr uint32_t kTpKS = kDftTpForm == 4 ? 4u : 5u;                    // its 
 inline int dft_form(int var)
 {
     return var == 20 || var == 22                                                  ? 5
-           : var == 21 || var == 23 || (var >= 26 && var <= 28) || (var >= 33 && var <= 36) ? 6
+           : var == 21 || var == 23 || (var >= 26 && var <= 28) || (var >= 33 && var <= 37) ? 6
                                                                                           : 4;
 }
 // range blocks (waves) per workgroup of the Fourier search: 16 for variants 27 / 28 (1024-thread
@@ -506,7 +506,7 @@ inline uint32_t dft_bpw(int var) { return var == 27 || var == 28 ? 16u : kDftBlo
 constexpr int kDftDefaultVariant = 21; // the six-MFMA form: 13.71 vs 15.23 ms (24) at C3, 12-round A/B
 inline int dft_variant(int var)
 {
-    static const int own[] = {1, 3, 5, 6, 12, 20, 21, 22, 23, 24, 26, 27, 28, 33, 34, 35, 36, 9, 17, 41, 65, 73, 105};
+    static const int own[] = {1, 3, 5, 6, 12, 20, 21, 22, 23, 24, 26, 27, 28, 33, 34, 35, 36, 37, 9, 17, 41, 65, 73, 105};
     for (int v : own)
         if (var == v)
             return var;
@@ -996,7 +996,7 @@ int prepare(frac_ctx* c)
         FRAC_HIP(c, c->d_m_range_slot.ensure(std::max<size_t>(nr, 1)));
         FRAC_HIP(c, c->d_m_tile_pos.ensure(std::max<size_t>(nt * 32, 1)));
         FRAC_HIP(c, c->d_m_dtiles.ensure(std::max<size_t>(nt * kTpKS * 64, 1)));
-        FRAC_HIP(c, c->d_m_dconst.ensure(std::max<size_t>(nt * 32, 1)));
+        FRAC_HIP(c, c->d_m_dconst.ensure((size_t)nt * kDftCS * 4 + 256)); // Fourier layout + one DMA piece of slack
         FRAC_HIP(c, c->d_m_rfrags.ensure(std::max<size_t>(nbk * 7 * 64, 1)));
         FRAC_HIP(c, c->d_m_rconst.ensure(std::max<size_t>(nbk * 32, 1)));
         FRAC_HIP(c, c->d_dft_tguard.ensure(std::max<size_t>(nt, 1)));
@@ -1043,7 +1043,8 @@ int prepare(frac_ctx* c)
         FRAC_HIP(c, c->d_m_blk_ptr.ensure(c->m_blk_ptr.size()));
         FRAC_HIP(c, c->d_m_blk_ent.ensure(c->m_blk_ent.size()));
         FRAC_HIP(c, c->d_m_rconst.ensure((size_t)c->nblocks * 32));
-        FRAC_HIP(c, c->d_m_dconst.ensure((size_t)c->ntiles * 32));
+        // the direct form's [tile][8] uint4 and the Fourier form's [tile][kDftCS] (+ one LDS-DMA piece of slack)
+        FRAC_HIP(c, c->d_m_dconst.ensure((size_t)c->ntiles * kDftCS * 4 + 256));
         FRAC_HIP(c, c->d_m_dtiles.ensure((size_t)c->ntiles * KS * 64));
         FRAC_HIP(c, c->d_m_rfrags.ensure((size_t)c->nblocks * c->Teff * KS * 64));
         FRAC_HIP(c, c->d_m_entries.ensure(std::max(c->m_work.size() * 4 * c->Teff, c->m8_work.size() * c->m8_bpw) *
@@ -1102,7 +1103,7 @@ inline int mfma_variant(frac_ctx* c, int& var)
     char* end = nullptr;
     const long x = strtol(v, &end, 10);
     static const int exact[] = {0,  1,  2,  3,  4,  5,  6,  7,  12, 20, 21, 22, 23, 24, 26,
-                                28, 27, 32, 33, 34, 35, 36, 64, 96, 98, 128, 130};
+                                28, 27, 32, 33, 34, 35, 36, 37, 64, 96, 98, 128, 130};
     static const int ablation[] = {8, 9, 16, 17, 41, 65, 73, 105, 201, 202, 203, 204, 205, 206, 207, 226, 227};
     bool ok = end && *end == 0;
     bool known = false;
@@ -1168,7 +1169,7 @@ inline int launch_dft(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride)
     d.dtiles = c->d_m_dtiles.ptr;
     d.dconst = c->d_m_dconst.ptr;
     FRAC_HIP(c, c->d_dft_tguard.ensure(std::max<size_t>(c->ntiles, 1)));
-    FRAC_HIP(c, c->d_dft_trmax.ensure(std::max<size_t>(c->ntiles, 1)));
+    FRAC_HIP(c, c->d_dft_trmax.ensure((size_t)c->ntiles + 4)); // + 4: a chunk's thresholds are one scalar load
     FRAC_HIP(c, c->d_dft_tpool.ensure(std::max<size_t>((size_t)c->ntiles * 32 * 32, 1)));
     FRAC_HIP(c, c->d_dft_rguard.ensure(std::max<size_t>(c->nblocks, 1)));
     // FRAC_MFMA_VARIANT for this path (A/B knob): default = exact form in 8-wave workgroups
@@ -1281,7 +1282,7 @@ inline int launch_dft(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride)
                 else
                     search_dft<false, 1 | kDftChain | kDft6 | kDftFast6, 16><<<nwg, 1024, 0, c->stream>>>(da);
             }
-        } else if (form == 6 && var >= 33 && var <= 36) { // 26 with the issue-cost knobs
+        } else if (form == 6 && var >= 33 && var <= 37) { // 26 with the issue-cost knobs
             constexpr int V = 1 | kDftChain | kDft6 | kDftFast6;
             switch (var) {
             case 33: // unrolled chunk
@@ -1301,6 +1302,14 @@ inline int launch_dft(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride)
                     search_dft<true, V | kDftUnroll | kDftBufDma, W8><<<nwg, 64 * W8, 0, c->stream>>>(da);
                 else
                     search_dft<false, V | kDftUnroll | kDftBufDma, W8><<<nwg, 64 * W8, 0, c->stream>>>(da);
+                break;
+            case 37: // 36 with the stage's guard thresholds loaded before its barrier
+                if (hits)
+                    search_dft<true, V | kDftUnroll | kDftBufDma | kDftPrio | kDftGpre, W8><<<nwg, 64 * W8, 0, c->stream>>>(
+                        da);
+                else
+                    search_dft<false, V | kDftUnroll | kDftBufDma | kDftPrio | kDftGpre, W8><<<nwg, 64 * W8, 0,
+                                                                                                c->stream>>>(da);
                 break;
             default: // both, second half of the waves at s_setprio 1
                 if (hits)
@@ -2470,8 +2479,10 @@ int frac_encode_quadtree(frac_ctx* c, const frac_quadtree_params* qp, frac_encod
     }
     // every level's domain grid (geometry only) stays on the host and the device across frames: the
     // level swaps them in (no copy, no upload, no re-validation) and back out afterwards
+    // the caller's domain-list state comes back afterwards; the range list is consumed (cleared, unset)
     struct LevelGrid {
         frac_ctx* c;
+        bool doms_set_before;
         int lv = -1;
         void in(int level)
         {
@@ -2499,8 +2510,10 @@ int frac_encode_quadtree(frac_ctx* c, const frac_quadtree_params* qp, frac_encod
         {
             out();
             c->ranges_dev = false;
+            c->doms_set = doms_set_before;
+            c->ranges_set = false;
         }
-    } level{c};
+    } level{c, c->doms_set};
     // the level-to-level step runs on the device (qt_flags, scan, qt_scatter): each level's leaves are
     // appended to d_qt_leaves and its split ranges' quadrants become the next level's device range list;
     // the host reads one count per level and the leaves once at the end
@@ -2563,7 +2576,8 @@ int frac_encode_quadtree(frac_ctx* c, const frac_quadtree_params* qp, frac_encod
         size_t tb = c->qt_tmp_bytes;
         FRAC_HIP(c, hipcub::DeviceScan::ExclusiveSum(c->d_qt_tmp.ptr, tb, c->d_qt_flags.ptr, c->d_qt_offs.ptr, (int)nr,
                                                      c->stream));
-        FRAC_HIP(c, c->d_qt_next.ensure(std::max<size_t>(4 * (size_t)nr, 1)));
+        // d_qt_next holds max_leaves items already: the 4·nsplit quadrants tile part of the plane at
+        // ≥ min_size each, and the last level (n == min_size) splits nothing
         qt_scatter<<<(nr + 255) / 256, 256, 0, c->stream>>>(c->d_out.ptr, c->d_ranges.ptr, nr, c->d_qt_flags.ptr,
                                                            c->d_qt_offs.ptr, c->d_qt_leaves.ptr, n_leaves,
                                                            c->d_qt_next.ptr, c->d_qt_count.ptr);

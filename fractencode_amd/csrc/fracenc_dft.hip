@@ -128,9 +128,13 @@ constexpr int kDftFast6 = 16384; // with kDft6: the guarded constant-folded epil
 // issue-cost knobs of the search loop (A/B): the 4-tile chunk unrolled (LDS reads at immediate
 // offsets from one base), the stage's LDS-DMA by buffer_load … lds (the stage base in an SGPR
 // soffset, per-thread offsets fixed: no VALU per piece), waves of the second half at s_setprio 1
+// Row constants of a Fourier tile: [2][16] f32 = 8 uint4, padded to kDftCS = 16 uint4 per tile in
+// memory and in the LDS stage, so a 4-tile stage's constants are exactly one 1 KiB LDS-DMA piece
+constexpr uint32_t kDftCS = 16;
 constexpr int kDftUnroll = 32768;
 constexpr int kDftBufDma = 65536;
 constexpr int kDftPrio = 131072;
+constexpr int kDftGpre = 262144; // kDftFast6: the stage's guard bits loaded before its barrier
 
 // The five- and six-MFMA forms track h = y/2 = 4·max_t Z_t − Σb²/2 instead of y: the row constant
 // (dconst) is −Σb²/2 — exact in f32 (Σb² ≤ 2^24, so a half-integer of magnitude ≤ 2^23) — and the
@@ -320,7 +324,7 @@ __global__ void __launch_bounds__(256) dft_domain_build(MfmaDomainPrepArgs a, Df
     // forms track h = y/2; exact, Σb² ≤ 2^24)
     const float ny = p >= 0 ? (F5 ? -0.5f * (float)sb2 : -(float)sb2) : kDftPadY;
     const uint32_t h = (row >> 2) & 1u, i = (row & 3u) + 4u * (row >> 3);
-    a.dconst[(size_t)tile * 32 + h * 16 + i] = __float_as_uint(ny);
+    a.dconst[(size_t)tile * (kDftCS * 4) + h * 16 + i] = __float_as_uint(ny);
     uint32_t gx = p >= 0 ? (uint32_t)((F5 ? 2 : 4) * dinf) : 0u, gy = p >= 0 ? (uint32_t)sb2 : 0u;
     if constexpr (BYPOS) {
         atomicMax(&tguard[tile].x, gx);
@@ -750,12 +754,25 @@ __device__ inline float dft_tile_max6g(const half8_t (&af)[5], const half8_t (&b
     return m;
 }
 
+// kDftFast6 guard bits of a 4-tile chunk: bit k set iff the block's R6 ≤ tile t0 + k's threshold
+// (one scalar load of four thresholds; trmax is padded by 4 entries), masked to the chunk's ne tiles
+__device__ inline uint32_t dft_guard_bits(const int32_t* __restrict__ trmax, uint32_t t0, uint32_t ne, uint32_t r1)
+{
+    t0 = __builtin_amdgcn_readfirstlane(t0);
+    const __attribute__((address_space(4))) int32_t* rp =
+        (const __attribute__((address_space(4))) int32_t*)(uintptr_t)(trmax + t0);
+    const int32_t g0 = rp[0], g1 = rp[1], g2 = rp[2], g3 = rp[3], ri = (int32_t)r1;
+    const uint32_t g = ((ri <= g0) ? 1u : 0u) | ((ri <= g1) ? 2u : 0u) | ((ri <= g2) ? 4u : 0u) | ((ri <= g3) ? 8u : 0u);
+    return g & ((1u << ne) - 1u);
+}
+
 template <int VAR, bool MASK = false, bool HITS = false>
 __device__ inline float dft_compute_stage(const uint4* __restrict__ la, uint32_t nt, uint32_t lane,
                                           const half8_t (&bf)[DftForm<VAR>::NBF], uint32_t tb,
                                           const uint2* __restrict__ tguard, uint32_t r1, uint32_t q0 = 0,
                                           uint32_t q1 = ~0u, uint32_t* masks = nullptr, float hl = 0.0f,
-                                          uint32_t iz = 0, const int32_t* __restrict__ trmax = nullptr)
+                                          uint32_t iz = 0, const int32_t* __restrict__ trmax = nullptr,
+                                          uint32_t gpre = 0)
 {
     constexpr int KS = DftForm<VAR>::KS;
     const uint4* lc = la + nt * (uint32_t)KS * 64u;
@@ -766,13 +783,12 @@ __device__ inline float dft_compute_stage(const uint4* __restrict__ la, uint32_t
     // the tile index is wave-uniform: readfirstlane + the constant address space make the guard
     // loads scalar, which the vmcnt waits of the stage's LDS-DMA do not serialise with
     const uint32_t t0 = __builtin_amdgcn_readfirstlane(tb + q0), ne = __builtin_amdgcn_readfirstlane(min(q1, nt) - q0);
-    if constexpr (DftForm<VAR>::FAST6) {
-        const __attribute__((address_space(4))) int32_t* rp =
-            (const __attribute__((address_space(4))) int32_t*)(uintptr_t)(trmax + t0);
-#pragma unroll
-        for (uint32_t k = 0; k < 4; ++k)
-            if (k < ne)
-                gfast |= (int32_t)r1 <= rp[k] ? (1u << k) : 0u;
+    if constexpr (DftForm<VAR>::FAST6 && (VAR & kDftGpre) != 0) {
+        gfast = gpre; // dft_guard_bits, issued by the caller ahead of the stage barrier
+        (void)t0;
+        (void)ne;
+    } else if constexpr (DftForm<VAR>::FAST6) {
+        gfast = dft_guard_bits(trmax, t0, ne, r1);
     } else if constexpr ((VAR & 1) == 0) {
 #pragma unroll
         for (uint32_t k = 0; k < 4; ++k)
@@ -790,13 +806,13 @@ __device__ inline float dft_compute_stage(const uint4* __restrict__ la, uint32_t
         for (int s = 0; s < KS; ++s)
             af[s] = __builtin_bit_cast(half8_t, la[(qq * KS + s) * 64 + lane]);
         if constexpr (DftForm<VAR>::FAST6 && !MASK) {
-            cm = dft_tile_max6g(af, bf, la, nt * (uint32_t)KS * 64u + qq * 8, iz, h, (gfast >> (q - q0)) & 1u, cm);
+            cm = dft_tile_max6g(af, bf, la, nt * (uint32_t)KS * 64u + qq * kDftCS, iz, h, (gfast >> (q - q0)) & 1u, cm);
             return;
         }
         floatx16_t ny;
 #pragma unroll
         for (int c4 = 0; c4 < 4; ++c4) {
-            const uint4 v = lc[qq * 8 + h * 4 + c4];
+            const uint4 v = lc[qq * kDftCS + h * 4 + c4];
             ny[4 * c4 + 0] = __uint_as_float(v.x);
             ny[4 * c4 + 1] = __uint_as_float(v.y);
             ny[4 * c4 + 2] = __uint_as_float(v.z);
@@ -828,22 +844,24 @@ __device__ inline float dft_compute_stage(const uint4* __restrict__ la, uint32_t
     return cm;
 }
 
-// stage_tiles by buffer_load … lds: the same LDS image, the stage's base offset in the SGPR
-// soffset and each thread's piece offsets the same for every stage (no per-piece address VALU)
-template <int KS, uint32_t NTHREADS>
+// stage_tiles by buffer_load … lds in whole-wave pieces (1 KiB each): the stage's nt·KS A-fragment
+// pieces and its one constants piece (kDftCS = 16 uint4 per tile: 4 tiles are one piece; a shorter
+// last stage reads the next tiles' constants or the allocation's 1 KiB of slack, never used).  The
+// loop, the LDS destination (M0) and the source offset (soffset) are wave-uniform: every piece costs
+// scalar instructions only, the lane's voffset (lane·16) is fixed.
+template <int KS, uint32_t WAVES>
 __device__ inline void stage_tiles_buf(uint4* dst, __amdgpu_buffer_rsrc_t ra, __amdgpu_buffer_rsrc_t rc, uint32_t tb,
                                        uint32_t nt)
 {
-    const uint32_t na = nt * KS * 64u, ntot = na + nt * 8u; // na is a whole number of waves' pieces
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t sa = __builtin_amdgcn_readfirstlane(tb * (uint32_t)KS * 64u * 16u);
-    const uint32_t sc = __builtin_amdgcn_readfirstlane(tb * 8u * 16u);
-    for (uint32_t i = threadIdx.x; i < ntot; i += NTHREADS) {
-        auto* l = (__attribute__((address_space(3))) void*)(dst + (i - lane));
-        if (i < na)
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, l, 16, i * 16u, sa, 0, 0);
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t voff = (threadIdx.x & 63u) * 16u;
+    const uint32_t tbu = __builtin_amdgcn_readfirstlane(tb), npa = __builtin_amdgcn_readfirstlane(nt * (uint32_t)KS);
+    for (uint32_t p = wv; p <= npa; p += WAVES) {
+        auto* l = (__attribute__((address_space(3))) void*)(dst + p * 64u);
+        if (p < npa)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, l, 16, voff, (tbu * (uint32_t)KS + p) * 1024u, 0, 0);
         else
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rc, l, 16, (i - na) * 16u, sc, 0, 0);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rc, l, 16, voff, tbu * kDftCS * 16u, 0, 0);
     }
 }
 
@@ -860,7 +878,7 @@ __global__ void __launch_bounds__(64 * WAVES) search_dft(DftArgs d)
     const MfmaSearchArgs& a = d.m;
     constexpr int KS = DftForm<VAR>::KS, NBF = DftForm<VAR>::NBF;
     constexpr uint32_t kTilesPerStage = TPS; // LDS stage; chunks stay 4 tiles (resolve_dft)
-    constexpr int STAGE = kTilesPerStage * KS * 64 + kTilesPerStage * 8;
+    constexpr int STAGE = kTilesPerStage * KS * 64 + kTilesPerStage * kDftCS;
     // kDftFast6: each stage buffer ends in 8 zero uint4, the row constants of a tile pair that runs
     // the exact epilogue (written here, published by the first stage barrier, never a DMA target).
     // Inside the stage's own array, so the compiler still tells these reads from the other
@@ -928,11 +946,22 @@ __global__ void __launch_bounds__(64 * WAVES) search_dft(DftArgs d)
     constexpr bool SKIPDMA = NODMA || (VAR & 256) != 0, SKIPBAR = NODMA || (VAR & 512) != 0;
     auto stage = [&](uint4* dst, uint32_t tb, uint32_t nt) {
         if constexpr ((VAR & kDftBufDma) != 0) // raw buffers (no range check: the pieces are in bounds)
-            stage_tiles_buf<KS, 64 * WAVES>(
+            stage_tiles_buf<KS, WAVES>(
                 dst, __builtin_amdgcn_make_buffer_rsrc((void*)a.dtiles, 0, 0xffffffffu, 0x00020000),
                 __builtin_amdgcn_make_buffer_rsrc((void*)a.dconst, 0, 0xffffffffu, 0x00020000), tb, nt);
         else
-            stage_tiles<KS, 64 * WAVES>(dst, a.dtiles, a.dconst, tb, nt);
+            stage_tiles<KS, 64 * WAVES, kDftCS>(dst, a.dtiles, a.dconst, tb, nt);
+    };
+    // kDftGpre (4-tile stages = one chunk): the stage's guard bits, loaded before its barrier so the
+    // scalar load's latency hides in the barrier wait instead of the first tile's
+    auto guards = [&](uint32_t tb, uint32_t nt) -> uint32_t {
+        if constexpr (DftForm<VAR>::FAST6 && (VAR & kDftGpre) != 0) {
+            static_assert(TPS == 4, "one chunk per stage");
+            return dft_guard_bits(d.trmax, tb, min(nt, 4u), r1);
+        }
+        (void)tb;
+        (void)nt;
+        return 0u;
     };
     if constexpr ((VAR & kDftPrio) != 0)
         if (wv >= WAVES / 2)
@@ -942,24 +971,26 @@ __global__ void __launch_bounds__(64 * WAVES) search_dft(DftArgs d)
     for (uint32_t st = 0; st < nstage; st += 2) {
         {
             const uint32_t tb = wk.z + st * kTilesPerStage;
+            const uint32_t gb = guards(tb, stage_nt(st));
             if (!SKIPBAR || st < 2)
                 stage_barrier();
             if (st + 1 < nstage && (!SKIPDMA || st == 0))
                 stage(lds1, tb + kTilesPerStage, stage_nt(st + 1));
             for (uint32_t c0 = 0; c0 < stage_nt(st); c0 += 4)
                 finish_stage(dft_compute_stage<VAR, CHUNKED, HITS>(lds0, stage_nt(st), lane, bf, tb, d.tguard, r1, c0,
-                                                                   c0 + 4, masks, hl, STAGE, d.trmax),
+                                                                   c0 + 4, masks, hl, STAGE, d.trmax, gb),
                              tb + c0);
         }
         if (st + 1 < nstage) {
             const uint32_t tb = wk.z + (st + 1) * kTilesPerStage;
+            const uint32_t gb = guards(tb, stage_nt(st + 1));
             if (!SKIPBAR || st < 2)
                 stage_barrier();
             if (st + 2 < nstage && !SKIPDMA)
                 stage(lds0, tb + kTilesPerStage, stage_nt(st + 2));
             for (uint32_t c0 = 0; c0 < stage_nt(st + 1); c0 += 4)
                 finish_stage(dft_compute_stage<VAR, CHUNKED, HITS>(lds1, stage_nt(st + 1), lane, bf, tb, d.tguard, r1,
-                                                                   c0, c0 + 4, masks, hl, STAGE, d.trmax),
+                                                                   c0, c0 + 4, masks, hl, STAGE, d.trmax, gb),
                              tb + c0);
         }
     }
@@ -980,7 +1011,7 @@ __global__ void __launch_bounds__(256, F6 ? 2 : 3) search_dft2(DftArgs d)
     const MfmaSearchArgs& a = d.m;
     constexpr int VAR = 1 | kDftChain | (F6 ? kDft6 : 0);
     constexpr int KS = DftForm<VAR>::KS, NBF = DftForm<VAR>::NBF;
-    constexpr int STAGE = kTilesPerStage * KS * 64 + kTilesPerStage * 8;
+    constexpr int STAGE = kTilesPerStage * KS * 64 + kTilesPerStage * kDftCS;
     __shared__ uint4 lds0[STAGE];
     __shared__ uint4 lds1[STAGE];
     const uint4 wk = a.work[blockIdx.x];
@@ -1013,7 +1044,7 @@ __global__ void __launch_bounds__(256, F6 ? 2 : 3) search_dft2(DftArgs d)
             floatx16_t ny;
 #pragma unroll
             for (int c4 = 0; c4 < 4; ++c4) {
-                const uint4 v = lc[q * 8 + h * 4 + c4];
+                const uint4 v = lc[q * kDftCS + h * 4 + c4];
                 ny[4 * c4 + 0] = __uint_as_float(v.x);
                 ny[4 * c4 + 1] = __uint_as_float(v.y);
                 ny[4 * c4 + 2] = __uint_as_float(v.z);
@@ -1041,20 +1072,20 @@ __global__ void __launch_bounds__(256, F6 ? 2 : 3) search_dft2(DftArgs d)
     const uint32_t nstage = (wk.w - wk.z + kTilesPerStage - 1) / kTilesPerStage;
     auto stage_nt = [&](uint32_t st) { return min((uint32_t)kTilesPerStage, wk.w - (wk.z + st * kTilesPerStage)); };
     if (nstage)
-        stage_tiles<KS, 256>(lds0, a.dtiles, a.dconst, wk.z, stage_nt(0));
+        stage_tiles<KS, 256, kDftCS>(lds0, a.dtiles, a.dconst, wk.z, stage_nt(0));
     for (uint32_t st = 0; st < nstage; st += 2) {
         {
             const uint32_t tb = wk.z + st * kTilesPerStage;
             stage_barrier();
             if (st + 1 < nstage)
-                stage_tiles<KS, 256>(lds1, a.dtiles, a.dconst, tb + kTilesPerStage, stage_nt(st + 1));
+                stage_tiles<KS, 256, kDftCS>(lds1, a.dtiles, a.dconst, tb + kTilesPerStage, stage_nt(st + 1));
             compute(lds0, stage_nt(st), tb);
         }
         if (st + 1 < nstage) {
             const uint32_t tb = wk.z + (st + 1) * kTilesPerStage;
             stage_barrier();
             if (st + 2 < nstage)
-                stage_tiles<KS, 256>(lds0, a.dtiles, a.dconst, tb + kTilesPerStage, stage_nt(st + 2));
+                stage_tiles<KS, 256, kDftCS>(lds0, a.dtiles, a.dconst, tb + kTilesPerStage, stage_nt(st + 2));
             compute(lds1, stage_nt(st + 1), tb);
         }
     }

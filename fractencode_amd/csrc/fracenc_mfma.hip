@@ -163,7 +163,7 @@ __global__ void __launch_bounds__(256) mfma_range_prep(MfmaRangePrepArgs a)
 // ---------------------------------------------------------------------------
 struct MfmaSearchArgs {
     const uint4* dtiles;
-    const uint4* dconst;   // [ntiles][8] (= [2][16] u32)
+    const uint4* dconst;   // [ntiles][8] (= [2][16] u32); the Fourier forms pad a tile to kDftCS = 16
     const uint4* rfrags;
     const uint32_t* rconst;
     const uint4* work;     // per WG: {first block, number of blocks (1..4), tile_begin, tile_end}
@@ -172,16 +172,18 @@ struct MfmaSearchArgs {
     uint2* entries;        // [nwork*4][T][64] {min v (0 = hit), tile}
 };
 
-template <int KS, uint32_t NTHREADS = 256>
+// CS: uint4 of epilogue constants per tile (8 = [2][16] u32; the Fourier search pads them to 16, one
+// LDS-DMA piece per 4-tile stage, fracenc_dft.hip kDftCS)
+template <int KS, uint32_t NTHREADS = 256, uint32_t CS = 8>
 __device__ inline void stage_tiles(uint4* dst, const uint4* __restrict__ dtiles, const uint4* __restrict__ dconst,
                                    uint32_t tb, uint32_t nt)
 {
     // LDS-DMA (global_load_lds_dwordx4): the LDS image is lane-linear per wave, which is
     // exactly this [A fragments | epilogue constants] stage layout.
-    const uint32_t na = nt * KS * 64u, ntot = na + nt * 8u;
+    const uint32_t na = nt * KS * 64u, ntot = na + nt * CS;
     const uint32_t lane = threadIdx.x & 63u;
     for (uint32_t i = threadIdx.x; i < ntot; i += NTHREADS) {
-        const uint4* src = i < na ? dtiles + (size_t)tb * KS * 64 + i : dconst + (size_t)tb * 8 + (i - na);
+        const uint4* src = i < na ? dtiles + (size_t)tb * KS * 64 + i : dconst + (size_t)tb * CS + (i - na);
         __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)src,
                                          (__attribute__((address_space(3))) void*)(dst + (i - lane)), 16, 0, 0);
     }

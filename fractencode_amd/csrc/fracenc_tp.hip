@@ -118,7 +118,7 @@ __global__ void __launch_bounds__(256) tp_build_tiles(TpBuckets bk, const uint32
             for (int h = 0; h < 2; ++h)
                 dtiles[((size_t)tile * ks + st) * 64 + row + 32 * h] = make_uint4(0u, 0u, 0u, 0u);
         const uint32_t hh = (row >> 2) & 1u, i = (row & 3u) + 4u * (row >> 3);
-        dconst[(size_t)tile * 32 + hh * 16 + i] = __float_as_uint(kDftPadY);
+        dconst[(size_t)tile * (kDftCS * 4) + hh * 16 + i] = __float_as_uint(kDftPadY);
     }
     if (row == 0)
         tguard[tile] = make_uint2(0u, 0u);

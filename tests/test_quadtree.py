@@ -104,3 +104,27 @@ def test_gpu_quadtree_stats_are_the_levels_stats(cls, thr):
             assert st[k] == want[k], k
             assert st2[k] == want[k], k
         np.testing.assert_array_equal(items, np.concatenate(leaves))
+
+
+@pytest.mark.gpu
+def test_gpu_quadtree_restores_the_list_state():
+    # the quadtree swaps its level grids in and out: the caller's domain list (set or not) comes
+    # back, and the consumed range list is unset, so a later run without set_ranges is a state error
+    p = plane("crop64")
+    with F.Engine(0, 4) as e:
+        e.set_frame(p)
+        e.encode_quadtree(16, 4, 2.0)
+        with pytest.raises(RuntimeError):
+            e.run()  # no domains were ever set
+        doms = F.create_uniform_grid(64, 64, 8, 4)
+        e.set_domains(doms)
+        e.encode_quadtree(16, 4, 2.0)
+        with pytest.raises(RuntimeError):
+            e.run()  # the ranges were consumed
+        rngs = F.create_uniform_grid(64, 64, 4, 4)
+        out, _ = e.search(rngs)  # the caller's own domain list is back
+        with F.Engine(0, 4) as f:
+            f.set_frame(p)
+            f.set_domains(doms)
+            want, _ = f.search(rngs)
+        np.testing.assert_array_equal(out, want)
