@@ -490,9 +490,11 @@ constexpr int kTpVar = 1 | kDftChain | (kDftTpForm == 6 ? kDft6 : 0); // the SEA
 constexpr uint32_t kTpKS = kDftTpForm == 4 ? 4u : 5u;                    // its domain fragments per tile
 inline int dft_form(int var)
 {
-    return var == 20 || var == 22                                                  ? 5
-           : var == 21 || var == 23 || (var >= 26 && var <= 28) || (var >= 33 && var <= 37) ? 6
-                                                                                          : 4;
+    if (var == 20 || var == 22)
+        return 5;
+    const bool six = var == 21 || var == 23 || (var >= 26 && var <= 28) || (var >= 33 && var <= 39) ||
+                     var == 226 || var == 227 || (var >= 240 && var <= 243);
+    return six ? 6 : 4;
 }
 // range blocks (waves) per workgroup of the Fourier search: 16 for variants 27 / 28 (1024-thread
 // workgroups: each LDS stage serves twice the blocks, half the LDS-DMA per tile pair), else 8
@@ -506,7 +508,7 @@ inline uint32_t dft_bpw(int var) { return var == 27 || var == 28 ? 16u : kDftBlo
 constexpr int kDftDefaultVariant = 21; // the six-MFMA form: 13.71 vs 15.23 ms (24) at C3, 12-round A/B
 inline int dft_variant(int var)
 {
-    static const int own[] = {1, 3, 5, 6, 12, 20, 21, 22, 23, 24, 26, 27, 28, 33, 34, 35, 36, 37, 9, 17, 41, 65, 73, 105};
+    static const int own[] = {1, 3, 5, 6, 12, 20, 21, 22, 23, 24, 26, 27, 28, 33, 34, 35, 36, 37, 38, 39, 9, 17, 41, 65, 73, 105};
     for (int v : own)
         if (var == v)
             return var;
@@ -1103,8 +1105,8 @@ inline int mfma_variant(frac_ctx* c, int& var)
     char* end = nullptr;
     const long x = strtol(v, &end, 10);
     static const int exact[] = {0,  1,  2,  3,  4,  5,  6,  7,  12, 20, 21, 22, 23, 24, 26,
-                                28, 27, 32, 33, 34, 35, 36, 37, 64, 96, 98, 128, 130};
-    static const int ablation[] = {8, 9, 16, 17, 41, 65, 73, 105, 201, 202, 203, 204, 205, 206, 207, 226, 227};
+                                28, 27, 32, 33, 34, 35, 36, 37, 38, 39, 64, 96, 98, 128, 130};
+    static const int ablation[] = {8, 9, 16, 17, 41, 65, 73, 105, 201, 202, 203, 204, 205, 206, 207, 226, 227, 240, 241, 242, 243};
     bool ok = end && *end == 0;
     bool known = false;
     for (int e : exact)
@@ -1260,6 +1262,22 @@ inline int launch_dft(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride)
             case 227: // the guarded six-MFMA form (26), no LDS-DMA / barrier after the first stages
                 search_dft<false, 1 | kDftChain | kDft6 | kDftFast6 | 64, W8><<<nwg, 64 * W8, 0, c->stream>>>(da);
                 break;
+            case 240: // variant 35, MFMAs with a one-value epilogue
+                search_dft<false, 1 | kDftChain | kDft6 | kDftFast6 | kDftUnroll | kDftBufDma | 8, W8><<<nwg, 64 * W8, 0,
+                                                                                                    c->stream>>>(da);
+                break;
+            case 241: // variant 35, the fast epilogue without MFMAs
+                search_dft<false, 1 | kDftChain | kDft6 | kDftFast6 | kDftUnroll | kDftBufDma | 16, W8><<<nwg, 64 * W8, 0,
+                                                                                                     c->stream>>>(da);
+                break;
+            case 242: // variant 35, no barrier
+                search_dft<false, 1 | kDftChain | kDft6 | kDftFast6 | kDftUnroll | kDftBufDma | 512, W8><<<nwg, 64 * W8,
+                                                                                                      0, c->stream>>>(da);
+                break;
+            case 243: // variant 35, no LDS-DMA / barrier after the first stages
+                search_dft<false, 1 | kDftChain | kDft6 | kDftFast6 | kDftUnroll | kDftBufDma | 64, W8><<<nwg, 64 * W8, 0,
+                                                                                                     c->stream>>>(da);
+                break;
             default: search_dft<false, 65, W8><<<nwg, 64 * W8, 0, c->stream>>>(da); break;  // full, no DMA/bar
             }
 #endif
@@ -1282,7 +1300,7 @@ inline int launch_dft(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride)
                 else
                     search_dft<false, 1 | kDftChain | kDft6 | kDftFast6, 16><<<nwg, 1024, 0, c->stream>>>(da);
             }
-        } else if (form == 6 && var >= 33 && var <= 37) { // 26 with the issue-cost knobs
+        } else if (form == 6 && var >= 33 && var <= 39) { // 26 with the issue-cost knobs
             constexpr int V = 1 | kDftChain | kDft6 | kDftFast6;
             switch (var) {
             case 33: // unrolled chunk
@@ -1310,6 +1328,20 @@ inline int launch_dft(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride)
                 else
                     search_dft<false, V | kDftUnroll | kDftBufDma | kDftPrio | kDftGpre, W8><<<nwg, 64 * W8, 0,
                                                                                                 c->stream>>>(da);
+                break;
+            case 38: // 35 + guards before the barrier + s_setprio 1 around each tile's MFMAs
+                if (hits)
+                    search_dft<true, V | kDftUnroll | kDftBufDma | kDftGpre | kDftTilePrio, W8><<<nwg, 64 * W8, 0,
+                                                                                                 c->stream>>>(da);
+                else
+                    search_dft<false, V | kDftUnroll | kDftBufDma | kDftGpre | kDftTilePrio, W8><<<nwg, 64 * W8, 0,
+                                                                                                  c->stream>>>(da);
+                break;
+            case 39: // 35 + guards before the barrier
+                if (hits)
+                    search_dft<true, V | kDftUnroll | kDftBufDma | kDftGpre, W8><<<nwg, 64 * W8, 0, c->stream>>>(da);
+                else
+                    search_dft<false, V | kDftUnroll | kDftBufDma | kDftGpre, W8><<<nwg, 64 * W8, 0, c->stream>>>(da);
                 break;
             default: // both, second half of the waves at s_setprio 1
                 if (hits)

@@ -135,6 +135,7 @@ constexpr int kDftUnroll = 32768;
 constexpr int kDftBufDma = 65536;
 constexpr int kDftPrio = 131072;
 constexpr int kDftGpre = 262144; // kDftFast6: the stage's guard bits loaded before its barrier
+constexpr int kDftTilePrio = 524288; // kDftFast6: s_setprio 1 around each tile's MFMA issue
 
 // The five- and six-MFMA forms track h = y/2 = 4·max_t Z_t − Σb²/2 instead of y: the row constant
 // (dconst) is −Σb²/2 — exact in f32 (Σb² ≤ 2^24, so a half-integer of magnitude ≤ 2^23) — and the
@@ -723,20 +724,43 @@ __device__ inline floatx16_t lds_row_consts(const uint4* p)
 // sequence and one register allocation serve both) — and the epilogue: the folded form
 // (2 VALU + one v_max3 step per candidate), or the exact one with the constants read after the
 // MFMAs.  lc: the tile's row constants ([2][16] lane-half layout), h: the lane half.
+template <bool PRIO = false, int ABL = 0>
 __device__ inline float dft_tile_max6g(const half8_t (&af)[5], const half8_t (&bf)[6], const uint4* la, uint32_t ic,
                                        uint32_t iz, uint32_t h, bool fast, float m)
 {
+    if constexpr (ABL == 16) {
+        // ABLATION (tuning only, wrong results): the fast epilogue on the fragments' bits, no MFMA
+        const floatx16_t c = lds_row_consts(la + (fast ? ic : iz) + h * 4);
+        auto bits = [&](const half8_t& x, int i) { return __builtin_bit_cast(uint4, x)[i & 3]; };
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const float u = c[i] + __uint_as_float(bits(af[i >> 2], i)), pr = __uint_as_float(bits(bf[i >> 2], i));
+            const float v = __uint_as_float(bits(af[(i >> 2) + 1], i)), pi = __uint_as_float(bits(bf[(i >> 2) + 2], i));
+            m = __builtin_fmaxf(__builtin_fmaxf(m, u + __builtin_fabsf(pr)), v + __builtin_fabsf(pi));
+        }
+        return m;
+    }
     // one base pointer, a selected index: the compiler keeps the read's underlying LDS object and
     // does not wait for the other stage buffer's pending LDS-DMA (a selected pointer made it)
     const uint4* lc = la + ic;
     const floatx16_t c = lds_row_consts(la + (fast ? ic : iz) + h * 4);
     const floatx16_t z = {};
+    if constexpr (PRIO) { // the MFMA issue ahead of the other waves' epilogues on this SIMD
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_setprio(1);
+    }
     const floatx16_t k1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[2], bf[3], z, 0, 0, 0); // 2k1
     const floatx16_t p = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[0], bf[0], c, 0, 0, 0);  // P (− Σb²/2)
     const floatx16_t pr = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[3], bf[4], k1, 0, 0, 0); // 2Pr
     const floatx16_t u = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[1], bf[1], p, 0, 0, 0);  // 2U (− Σb²/2)
     const floatx16_t pi = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[4], bf[5], k1, 0, 0, 0); // 2Pi
     const floatx16_t v = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[1], bf[2], p, 0, 0, 0);  // 2U' (− Σb²/2)
+    if constexpr (PRIO) {
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_setprio(0);
+    }
+    if constexpr (ABL == 8) // ABLATION (tuning only, wrong results): the MFMAs with a one-value epilogue
+        return __builtin_fmaxf(m, (u[0] + pr[0]) + (v[0] + pi[0]));
     if (fast) {
 #pragma unroll
         for (int i = 0; i < 16; ++i)
@@ -806,7 +830,8 @@ __device__ inline float dft_compute_stage(const uint4* __restrict__ la, uint32_t
         for (int s = 0; s < KS; ++s)
             af[s] = __builtin_bit_cast(half8_t, la[(qq * KS + s) * 64 + lane]);
         if constexpr (DftForm<VAR>::FAST6 && !MASK) {
-            cm = dft_tile_max6g(af, bf, la, nt * (uint32_t)KS * 64u + qq * kDftCS, iz, h, (gfast >> (q - q0)) & 1u, cm);
+            cm = dft_tile_max6g<(VAR & kDftTilePrio) != 0, VAR & (8 | 16)>(af, bf, la, nt * (uint32_t)KS * 64u + qq * kDftCS, iz, h,
+                                                          (gfast >> (q - q0)) & 1u, cm);
             return;
         }
         floatx16_t ny;
