@@ -492,7 +492,7 @@ inline int dft_form(int var)
 {
     if (var == 20 || var == 22)
         return 5;
-    const bool six = var == 21 || var == 23 || (var >= 26 && var <= 28) || (var >= 33 && var <= 39) ||
+    const bool six = var == 21 || var == 23 || (var >= 26 && var <= 28) || (var >= 33 && var <= 36) ||
                      var == 226 || var == 227 || (var >= 240 && var <= 243);
     return six ? 6 : 4;
 }
@@ -505,10 +505,14 @@ inline uint32_t dft_bpw(int var) { return var == 27 || var == 28 ? 16u : kDftBlo
 // workgroups), 26 (the six-MFMA form with the guarded constant-folded epilogue, kDftFast6) and the
 // tuning ablations.  Every other value (the default, and the direct form's
 // schedule knobs) runs kDftDefaultVariant.
-constexpr int kDftDefaultVariant = 21; // the six-MFMA form: 13.71 vs 15.23 ms (24) at C3, 12-round A/B
+// the six-MFMA form with the guarded constant-folded epilogue, the chunk unrolled and wave-uniform
+// buffer_load … lds stages (variant 35): 12.09 / 12.02 vs 13.85 / 13.65 ms for the exact six-MFMA
+// form (21) at C3 in two 8-round interleaved A/Bs on two boxes (profiles/r03/session3/r03_ab5.log,
+// r03_ab6.log); 21 was 13.71 vs 15.23 ms for the 8-MFMA form (24) in round 2
+constexpr int kDftDefaultVariant = 35;
 inline int dft_variant(int var)
 {
-    static const int own[] = {1, 3, 5, 6, 12, 20, 21, 22, 23, 24, 26, 27, 28, 33, 34, 35, 36, 37, 38, 39, 9, 17, 41, 65, 73, 105};
+    static const int own[] = {1, 3, 5, 6, 12, 20, 21, 22, 23, 24, 26, 27, 28, 33, 34, 35, 36, 9, 17, 41, 65, 73, 105};
     for (int v : own)
         if (var == v)
             return var;
@@ -1105,7 +1109,7 @@ inline int mfma_variant(frac_ctx* c, int& var)
     char* end = nullptr;
     const long x = strtol(v, &end, 10);
     static const int exact[] = {0,  1,  2,  3,  4,  5,  6,  7,  12, 20, 21, 22, 23, 24, 26,
-                                28, 27, 32, 33, 34, 35, 36, 37, 38, 39, 64, 96, 98, 128, 130};
+                                28, 27, 32, 33, 34, 35, 36, 64, 96, 98, 128, 130};
     static const int ablation[] = {8, 9, 16, 17, 41, 65, 73, 105, 201, 202, 203, 204, 205, 206, 207, 226, 227, 240, 241, 242, 243};
     bool ok = end && *end == 0;
     bool known = false;
@@ -1300,7 +1304,7 @@ inline int launch_dft(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride)
                 else
                     search_dft<false, 1 | kDftChain | kDft6 | kDftFast6, 16><<<nwg, 1024, 0, c->stream>>>(da);
             }
-        } else if (form == 6 && var >= 33 && var <= 39) { // 26 with the issue-cost knobs
+        } else if (form == 6 && var >= 33 && var <= 36) { // 26 with the issue-cost knobs
             constexpr int V = 1 | kDftChain | kDft6 | kDftFast6;
             switch (var) {
             case 33: // unrolled chunk
@@ -1320,28 +1324,6 @@ inline int launch_dft(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride)
                     search_dft<true, V | kDftUnroll | kDftBufDma, W8><<<nwg, 64 * W8, 0, c->stream>>>(da);
                 else
                     search_dft<false, V | kDftUnroll | kDftBufDma, W8><<<nwg, 64 * W8, 0, c->stream>>>(da);
-                break;
-            case 37: // 36 with the stage's guard thresholds loaded before its barrier
-                if (hits)
-                    search_dft<true, V | kDftUnroll | kDftBufDma | kDftPrio | kDftGpre, W8><<<nwg, 64 * W8, 0, c->stream>>>(
-                        da);
-                else
-                    search_dft<false, V | kDftUnroll | kDftBufDma | kDftPrio | kDftGpre, W8><<<nwg, 64 * W8, 0,
-                                                                                                c->stream>>>(da);
-                break;
-            case 38: // 35 + guards before the barrier + s_setprio 1 around each tile's MFMAs
-                if (hits)
-                    search_dft<true, V | kDftUnroll | kDftBufDma | kDftGpre | kDftTilePrio, W8><<<nwg, 64 * W8, 0,
-                                                                                                 c->stream>>>(da);
-                else
-                    search_dft<false, V | kDftUnroll | kDftBufDma | kDftGpre | kDftTilePrio, W8><<<nwg, 64 * W8, 0,
-                                                                                                  c->stream>>>(da);
-                break;
-            case 39: // 35 + guards before the barrier
-                if (hits)
-                    search_dft<true, V | kDftUnroll | kDftBufDma | kDftGpre, W8><<<nwg, 64 * W8, 0, c->stream>>>(da);
-                else
-                    search_dft<false, V | kDftUnroll | kDftBufDma | kDftGpre, W8><<<nwg, 64 * W8, 0, c->stream>>>(da);
                 break;
             default: // both, second half of the waves at s_setprio 1
                 if (hits)

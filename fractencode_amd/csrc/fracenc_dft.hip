@@ -134,8 +134,6 @@ constexpr uint32_t kDftCS = 16;
 constexpr int kDftUnroll = 32768;
 constexpr int kDftBufDma = 65536;
 constexpr int kDftPrio = 131072;
-constexpr int kDftGpre = 262144; // kDftFast6: the stage's guard bits loaded before its barrier
-constexpr int kDftTilePrio = 524288; // kDftFast6: s_setprio 1 around each tile's MFMA issue
 
 // The five- and six-MFMA forms track h = y/2 = 4·max_t Z_t − Σb²/2 instead of y: the row constant
 // (dconst) is −Σb²/2 — exact in f32 (Σb² ≤ 2^24, so a half-integer of magnitude ≤ 2^23) — and the
@@ -724,7 +722,7 @@ __device__ inline floatx16_t lds_row_consts(const uint4* p)
 // sequence and one register allocation serve both) — and the epilogue: the folded form
 // (2 VALU + one v_max3 step per candidate), or the exact one with the constants read after the
 // MFMAs.  lc: the tile's row constants ([2][16] lane-half layout), h: the lane half.
-template <bool PRIO = false, int ABL = 0>
+template <int ABL = 0>
 __device__ inline float dft_tile_max6g(const half8_t (&af)[5], const half8_t (&bf)[6], const uint4* la, uint32_t ic,
                                        uint32_t iz, uint32_t h, bool fast, float m)
 {
@@ -745,20 +743,12 @@ __device__ inline float dft_tile_max6g(const half8_t (&af)[5], const half8_t (&b
     const uint4* lc = la + ic;
     const floatx16_t c = lds_row_consts(la + (fast ? ic : iz) + h * 4);
     const floatx16_t z = {};
-    if constexpr (PRIO) { // the MFMA issue ahead of the other waves' epilogues on this SIMD
-        __builtin_amdgcn_sched_barrier(0);
-        __builtin_amdgcn_s_setprio(1);
-    }
     const floatx16_t k1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[2], bf[3], z, 0, 0, 0); // 2k1
     const floatx16_t p = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[0], bf[0], c, 0, 0, 0);  // P (− Σb²/2)
     const floatx16_t pr = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[3], bf[4], k1, 0, 0, 0); // 2Pr
     const floatx16_t u = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[1], bf[1], p, 0, 0, 0);  // 2U (− Σb²/2)
     const floatx16_t pi = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[4], bf[5], k1, 0, 0, 0); // 2Pi
     const floatx16_t v = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[1], bf[2], p, 0, 0, 0);  // 2U' (− Σb²/2)
-    if constexpr (PRIO) {
-        __builtin_amdgcn_sched_barrier(0);
-        __builtin_amdgcn_s_setprio(0);
-    }
     if constexpr (ABL == 8) // ABLATION (tuning only, wrong results): the MFMAs with a one-value epilogue
         return __builtin_fmaxf(m, (u[0] + pr[0]) + (v[0] + pi[0]));
     if (fast) {
@@ -795,8 +785,7 @@ __device__ inline float dft_compute_stage(const uint4* __restrict__ la, uint32_t
                                           const half8_t (&bf)[DftForm<VAR>::NBF], uint32_t tb,
                                           const uint2* __restrict__ tguard, uint32_t r1, uint32_t q0 = 0,
                                           uint32_t q1 = ~0u, uint32_t* masks = nullptr, float hl = 0.0f,
-                                          uint32_t iz = 0, const int32_t* __restrict__ trmax = nullptr,
-                                          uint32_t gpre = 0)
+                                          uint32_t iz = 0, const int32_t* __restrict__ trmax = nullptr)
 {
     constexpr int KS = DftForm<VAR>::KS;
     const uint4* lc = la + nt * (uint32_t)KS * 64u;
@@ -807,11 +796,7 @@ __device__ inline float dft_compute_stage(const uint4* __restrict__ la, uint32_t
     // the tile index is wave-uniform: readfirstlane + the constant address space make the guard
     // loads scalar, which the vmcnt waits of the stage's LDS-DMA do not serialise with
     const uint32_t t0 = __builtin_amdgcn_readfirstlane(tb + q0), ne = __builtin_amdgcn_readfirstlane(min(q1, nt) - q0);
-    if constexpr (DftForm<VAR>::FAST6 && (VAR & kDftGpre) != 0) {
-        gfast = gpre; // dft_guard_bits, issued by the caller ahead of the stage barrier
-        (void)t0;
-        (void)ne;
-    } else if constexpr (DftForm<VAR>::FAST6) {
+    if constexpr (DftForm<VAR>::FAST6) {
         gfast = dft_guard_bits(trmax, t0, ne, r1);
     } else if constexpr ((VAR & 1) == 0) {
 #pragma unroll
@@ -830,7 +815,7 @@ __device__ inline float dft_compute_stage(const uint4* __restrict__ la, uint32_t
         for (int s = 0; s < KS; ++s)
             af[s] = __builtin_bit_cast(half8_t, la[(qq * KS + s) * 64 + lane]);
         if constexpr (DftForm<VAR>::FAST6 && !MASK) {
-            cm = dft_tile_max6g<(VAR & kDftTilePrio) != 0, VAR & (8 | 16)>(af, bf, la, nt * (uint32_t)KS * 64u + qq * kDftCS, iz, h,
+            cm = dft_tile_max6g<VAR & (8 | 16)>(af, bf, la, nt * (uint32_t)KS * 64u + qq * kDftCS, iz, h,
                                                           (gfast >> (q - q0)) & 1u, cm);
             return;
         }
@@ -977,17 +962,6 @@ __global__ void __launch_bounds__(64 * WAVES) search_dft(DftArgs d)
         else
             stage_tiles<KS, 64 * WAVES, kDftCS>(dst, a.dtiles, a.dconst, tb, nt);
     };
-    // kDftGpre (4-tile stages = one chunk): the stage's guard bits, loaded before its barrier so the
-    // scalar load's latency hides in the barrier wait instead of the first tile's
-    auto guards = [&](uint32_t tb, uint32_t nt) -> uint32_t {
-        if constexpr (DftForm<VAR>::FAST6 && (VAR & kDftGpre) != 0) {
-            static_assert(TPS == 4, "one chunk per stage");
-            return dft_guard_bits(d.trmax, tb, min(nt, 4u), r1);
-        }
-        (void)tb;
-        (void)nt;
-        return 0u;
-    };
     if constexpr ((VAR & kDftPrio) != 0)
         if (wv >= WAVES / 2)
             __builtin_amdgcn_s_setprio(1);
@@ -996,26 +970,24 @@ __global__ void __launch_bounds__(64 * WAVES) search_dft(DftArgs d)
     for (uint32_t st = 0; st < nstage; st += 2) {
         {
             const uint32_t tb = wk.z + st * kTilesPerStage;
-            const uint32_t gb = guards(tb, stage_nt(st));
             if (!SKIPBAR || st < 2)
                 stage_barrier();
             if (st + 1 < nstage && (!SKIPDMA || st == 0))
                 stage(lds1, tb + kTilesPerStage, stage_nt(st + 1));
             for (uint32_t c0 = 0; c0 < stage_nt(st); c0 += 4)
                 finish_stage(dft_compute_stage<VAR, CHUNKED, HITS>(lds0, stage_nt(st), lane, bf, tb, d.tguard, r1, c0,
-                                                                   c0 + 4, masks, hl, STAGE, d.trmax, gb),
+                                                                   c0 + 4, masks, hl, STAGE, d.trmax),
                              tb + c0);
         }
         if (st + 1 < nstage) {
             const uint32_t tb = wk.z + (st + 1) * kTilesPerStage;
-            const uint32_t gb = guards(tb, stage_nt(st + 1));
             if (!SKIPBAR || st < 2)
                 stage_barrier();
             if (st + 2 < nstage && !SKIPDMA)
                 stage(lds0, tb + kTilesPerStage, stage_nt(st + 2));
             for (uint32_t c0 = 0; c0 < stage_nt(st + 1); c0 += 4)
                 finish_stage(dft_compute_stage<VAR, CHUNKED, HITS>(lds1, stage_nt(st + 1), lane, bf, tb, d.tguard, r1,
-                                                                   c0, c0 + 4, masks, hl, STAGE, d.trmax, gb),
+                                                                   c0, c0 + 4, masks, hl, STAGE, d.trmax),
                              tb + c0);
         }
     }

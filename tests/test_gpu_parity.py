@@ -259,7 +259,7 @@ DFT_CASES = [
 ]
 
 
-@pytest.mark.parametrize("dft", ["1", "0", "1/20", "1/21", "1/23"])
+@pytest.mark.parametrize("dft", ["1", "0", "1/20", "1/21", "1/23", "1/26"])
 @pytest.mark.parametrize("case", range(len(DFT_CASES)))
 def test_mfma_fourier_and_direct_match_oracle(oracle, monkeypatch, case, dft):
     # "1/20": the five-MFMA Fourier form (FRAC_MFMA_VARIANT=20)
@@ -302,13 +302,14 @@ def _extreme_plane(rng, S, kind):
     return out.astype(np.uint8)
 
 
-@pytest.mark.parametrize("var", ["20", "21", "22", "23"])
+@pytest.mark.parametrize("var", ["20", "21", "22", "23", "26", "35"])
 @pytest.mark.parametrize("kind", ["binary", "blocks8", "blocks2", "orbits"])
 def test_five_mfma_form_at_operand_extremes(monkeypatch, kind, var):
     """The five-MFMA Fourier form (FRAC_MFMA_VARIANT=20) has the tightest exactness margins (2Pr /
-    2Pi partial sums up to 33.3M < 2^25, P up to 2^24): on 0/255 frames that drive every operand
-    to its bound it returns the exhaustive VALU engine's records, with and without the
-    classifier."""
+    2Pi partial sums up to 33.3M < 2^25, P up to 2^24), the six-MFMA forms' guarded fast path
+    (26, 35: P from −Σb²/2 where 2·R6·D6 + Σb² < 2^24) the tightest guard: on 0/255 frames that
+    drive every operand to its bound they return the exhaustive VALU engine's records, with and
+    without the classifier."""
     rng = np.random.default_rng(zlib.crc32(kind.encode()))  # reproducible across processes
     S = 256
     p = _extreme_plane(rng, S, kind)
@@ -499,7 +500,8 @@ def test_encode_defaults_are_the_reference_cli_defaults():
     assert st["rejected_mappings"] == meta["rejected"]
 
 
-PRODUCT_VARIANTS = ("0", "1", "2", "3", "4", "5", "6", "7", "12", "20", "21", "22", "23", "24", "32", "64", "96", "98", "128", "130")
+PRODUCT_VARIANTS = ("0", "1", "2", "3", "4", "5", "6", "7", "12", "20", "21", "22", "23", "24", "26", "27", "28", "32",
+                    "33", "34", "35", "36", "64", "96", "98", "128", "130")
 
 
 @pytest.mark.parametrize("n,T,dft", [(8, 4, "0"), (4, 4, "0"), (8, 8, "0"), (8, 4, "1")])
