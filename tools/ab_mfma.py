@@ -19,6 +19,7 @@ from fractencode_amd.synth import value_noise  # noqa: E402
 variants = sys.argv[1].split(",") if len(sys.argv) > 1 else ["d", "2"]
 rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 5
 S = int(os.environ.get("AB_SIZE", "4096"))
+REPS = int(os.environ.get("AB_REPS", "1"))
 p = value_noise(S, S, 1234)
 ref = None
 with F.Engine(0, 4, False, 0.0, -1.0, F.ENGINE_MFMA, timing=True) as e:
@@ -33,7 +34,8 @@ with F.Engine(0, 4, False, 0.0, -1.0, F.ENGINE_MFMA, timing=True) as e:
             os.environ["FRAC_MFMA_VARIANT"] = {"d": "2", "e": "1", "g": "3", "p": "4", "d8": "5", "dt": "6", "d2": "12", "d5": "20", "d5s": "22", "d6": "21", "d62": "23", "d6f": "26", "d6w": "27", "d6fw": "28", "fu": "33", "fb": "34", "fub": "35", "fubp": "36", "d4": "24", "dm": "201", "dm0": "202", "dmD": "203", "dmB": "204", "dD": "205", "dB": "206",
                                               "d0": "207", "dfB": "226", "df0": "227", "fM": "240", "fV": "241", "fB": "242", "f0": "243", "em": "9", "ev": "17", "emL": "41", "emB": "73",
                                               "em0": "105", "eB": "65"}.get(v, v)
-            e.run()
+            for _ in range(REPS):  # back-to-back runs: the last one is timed (the clock settles under load)
+                e.run()
             out, st = e.fetch()
             if ref is None:
                 ref = out.tobytes()
