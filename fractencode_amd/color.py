@@ -4,8 +4,10 @@ The reference loads a PNG, converts it with ImageIO::rgb2yuv (image/ImageIO.cpp:
 and encodes the three planes independently, each with its own grids and classifier
 (main.cpp:184-196 → encode_image2, main.cpp:142-180).  Here the RGB frame is uploaded
 once, converted on the device (frac_rgb_to_yuv_device), and the Y, U and V searches
-are enqueued on three engines with their own HIP streams so the small chroma searches
-overlap the luma search instead of running after it.
+are enqueued on three engines that share one HIP stream, so the searches run in turn: the luma
+search alone fills the GPU, and letting the small chroma searches overlap it on streams of their
+own measured slower (C5: 12.73 vs 12.54 ms per frame for the three searches, 13.32 vs 12.69 ms with
+the conversion; profiles/r03/session5/paths.jsonl).  streams="own" keeps one stream per engine.
 """
 from __future__ import annotations
 
@@ -21,12 +23,21 @@ class ColorEncoder:
 
     def __init__(self, device: int = 0, range_size: int = 8, domain_size: int | None = None, transforms: int = 4,
                  use_classifier: bool = False, rms_threshold: float = 0.0, s_max: float = -1.0,
-                 engine: int = ENGINE_AUTO, timing: bool = False):
+                 engine: int = ENGINE_AUTO, timing: bool = False, streams: str = "shared"):
+        if streams not in ("shared", "own"):
+            raise ValueError(f"streams must be 'shared' or 'own', not {streams!r}")
         self.device = device
         self.range_size = range_size
         self.domain_size = domain_size or 2 * range_size
         self.use_classifier = use_classifier
         self.engines = [Engine(device, transforms, use_classifier, rms_threshold, s_max, engine, timing) for _ in PLANES]
+        self._stream = None
+        if streams == "shared":
+            import torch
+
+            self._stream = torch.cuda.Stream(torch.device("cuda", device))
+            for e in self.engines:
+                e.set_stream(self._stream.cuda_stream)
         self.planes = None
         self.ranges = None
 
@@ -72,7 +83,7 @@ class ColorEncoder:
         self._geom = geom
 
     def run(self) -> None:
-        """Enqueue the three searches (asynchronous; each engine on its own stream)."""
+        """Enqueue the three searches (asynchronous; on the shared stream, or each engine's own)."""
         for e in self.engines:
             e.run()
 

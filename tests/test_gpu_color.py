@@ -89,6 +89,25 @@ def test_color_encoder_matches_reference_planes(oracle, engine):
         assert codec.psnr(p, dec) > 25.0
 
 
+def test_color_encoder_streams_give_the_same_records():
+    # the default runs the three plane searches in turn on one shared stream; streams="own" overlaps
+    # them on one stream per engine: the same records either way, frame after frame
+    from fractencode_amd.color import ColorEncoder
+
+    rgb = plane("lenna_rgb")
+    res = {}
+    for streams in ("shared", "own"):
+        with ColorEncoder(0, 8, 16, 4, streams=streams) as enc:
+            for _ in range(2):
+                enc.load(rgb)
+                enc.run()
+            enc.sync()
+            res[streams] = [out.tobytes() for out, _ in enc.fetch()]
+    assert res["shared"] == res["own"]
+    with pytest.raises(ValueError):
+        ColorEncoder(0, streams="two")
+
+
 def test_color_encoder_with_classifier(oracle):
     # Y against the reference's classifier golden; U and V against the oracle (the engine
     # classifies every plane's grids on the device)

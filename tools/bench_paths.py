@@ -96,21 +96,25 @@ def main():
                           "peak_gbs": 8000.0, "frac": round(nbytes / ms / 1e6 / 8000.0, 4)}), flush=True)
 
     if want("c5"):
-        with ColorEncoder(0, 8, 16, 4, timing=True) as enc:
-            def step():
-                enc.load(rgb)
-                enc.run()
+        # the three plane searches on three streams (concurrent) or on one (in turn)
+        for streams in ("own", "shared"):
+            with ColorEncoder(0, 8, 16, 4, timing=True, streams=streams) as enc:
 
-            sec = timed(step, args.steps, args.warmup, enc.sync)
-            res = enc.fetch()
-            nr = sum(len(r) for r in enc.ranges)
-            sec_run = timed(enc.run, args.steps, args.warmup, enc.sync)
-        print(json.dumps({"path": "c5", "workload": "C5: S1 RGB 4096² (seeds 1234/1235/1236) → Y 4096², U/V 2048², "
-                                                    "8x8 ranges, T=4, exhaustive",
-                          "ranges": nr, "ms_per_frame_incl_load": round(sec * 1e3, 3),
-                          "ms_per_frame_search": round(sec_run * 1e3, 3),
-                          "range_blocks_per_s": round(nr / sec_run, 1),
-                          "plane_search_ms": [round(st["ms_search"], 3) for _, st in res]}), flush=True)
+                def step():
+                    enc.load(rgb)
+                    enc.run()
+
+                sec = timed(step, args.steps, args.warmup, enc.sync)
+                res = enc.fetch()
+                nr = sum(len(r) for r in enc.ranges)
+                sec_run = timed(enc.run, args.steps, args.warmup, enc.sync)
+            print(json.dumps({"path": "c5", "streams": streams,
+                              "workload": "C5: S1 RGB 4096² (seeds 1234/1235/1236) → Y 4096², U/V 2048², "
+                                          "8x8 ranges, T=4, exhaustive",
+                              "ranges": nr, "ms_per_frame_incl_load": round(sec * 1e3, 3),
+                              "ms_per_frame_search": round(sec_run * 1e3, 3),
+                              "range_blocks_per_s": round(nr / sec_run, 1),
+                              "plane_search_ms": [round(st["ms_search"], 3) for _, st in res]}), flush=True)
 
     if want("c4"):
         frame = value_noise(4096, 4096, 1234)[:2048, :2048].copy()
