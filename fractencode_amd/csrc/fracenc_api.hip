@@ -202,6 +202,11 @@ struct frac_ctx {
     std::vector<uint32_t> m_blk_ptr, m_blk_ent;
     std::vector<uint4> m8_work;            // per WG (8 range blocks: search_dft; m8_bpw for the 16-wave forms)
     uint32_t m8_bpw = 8;                   // range blocks per workgroup of m8_work
+    // T = 8 on the Fourier path (n = 8, ratio 2): Flip_Rotate_k = Flip ∘ Rotate_k (image/transform.h:32-41),
+    // so the flip half is the rotation search of each range read through Flip — a second copy of every
+    // range block (blocks nblocks .. 2·nblocks − 1, same bucket), resolved together with the original
+    // (resolve_dft: Rotate-group index t' of the flipped copy = transform 4 + (−t' mod 4))
+    uint32_t dft_copies = 1;
     std::vector<uint32_t> m8_blk_ptr, m8_blk_ent;
     DBuf<uint4> d_m8_work;
     DBuf<uint32_t> d_m8_blk_ptr, d_m8_blk_ent;
@@ -798,6 +803,7 @@ int prepare(frac_ctx* c)
             }
         }
     }
+    c->dft_copies = 1;
     if (c->engine == FRAC_ENGINE_MFMA) {
         // range blocks of 32 slots per bucket; domain tiles of 32 engine pool rows per bucket (the
         // maps themselves are filled on the device below)
@@ -826,11 +832,12 @@ int prepare(frac_ctx* c)
             size_t groups = 0;
             for (int b = 0; b < nb; ++b)
                 if (tile_count[b])
-                    groups += (blk_count[b] + bpw - 1) / bpw;
+                    groups += (blk_count[b] + bpw - 1) / bpw * c->dft_copies;
             // every block of bucket b gets one entry per domain split of b: the CSR map is
             // sized by a count pass, then filled in work order (no per-block lists)
+            const uint32_t ncp = c->dft_copies, nbt = c->nblocks * ncp; // T = 8 Fourier: flipped copies
             std::vector<uint32_t> nsplit(nb, 0);
-            blk_ptr.assign(c->nblocks + 1, 0);
+            blk_ptr.assign(nbt + 1, 0);
             for (int b = 0; b < nb; ++b) {
                 if (!tile_count[b] || !blk_count[b])
                     continue;
@@ -840,33 +847,36 @@ int prepare(frac_ctx* c)
                 for (size_t sp = 0; sp < splits; ++sp)
                     ns += (uint64_t)tile_count[b] * (sp + 1) / splits > (uint64_t)tile_count[b] * sp / splits;
                 nsplit[b] = (uint32_t)splits;
-                for (uint32_t k = 0; k < blk_count[b]; ++k)
-                    blk_ptr[blk_first[b] + k + 1] = ns;
+                for (uint32_t cp = 0; cp < ncp; ++cp)
+                    for (uint32_t k = 0; k < blk_count[b]; ++k)
+                        blk_ptr[cp * c->nblocks + blk_first[b] + k + 1] = ns;
             }
-            for (uint32_t b = 0; b < c->nblocks; ++b)
+            for (uint32_t b = 0; b < nbt; ++b)
                 blk_ptr[b + 1] += blk_ptr[b];
-            blk_ent.assign(blk_ptr[c->nblocks], 0);
+            blk_ent.assign(blk_ptr[nbt], 0);
             std::vector<uint32_t> cur(blk_ptr.begin(), blk_ptr.end() - 1);
             work.clear();
-            for (int b = 0; b < nb; ++b) {
-                if (!nsplit[b])
-                    continue;
-                const size_t splits = nsplit[b];
-                for (uint32_t g = 0; g < blk_count[b]; g += bpw) {
-                    const uint32_t nbk = std::min(bpw, blk_count[b] - g);
-                    for (size_t sp = 0; sp < splits; ++sp) {
-                        const uint32_t t0 = tile_first[b] + (uint32_t)((uint64_t)tile_count[b] * sp / splits);
-                        const uint32_t t1 = tile_first[b] + (uint32_t)((uint64_t)tile_count[b] * (sp + 1) / splits);
-                        if (t1 <= t0)
-                            continue;
-                        const uint32_t w = (uint32_t)work.size();
-                        work.push_back(make_uint4(blk_first[b] + g, nbk, t0, t1));
-                        split_of.push_back((uint32_t)sp);
-                        for (uint32_t k = 0; k < nbk; ++k)
-                            blk_ent[cur[blk_first[b] + g + k]++] = w * bpw + k;
+            for (uint32_t cp = 0; cp < ncp; ++cp)
+                for (int b = 0; b < nb; ++b) {
+                    if (!nsplit[b])
+                        continue;
+                    const size_t splits = nsplit[b];
+                    const uint32_t bf = cp * c->nblocks + blk_first[b];
+                    for (uint32_t g = 0; g < blk_count[b]; g += bpw) {
+                        const uint32_t nbk = std::min(bpw, blk_count[b] - g);
+                        for (size_t sp = 0; sp < splits; ++sp) {
+                            const uint32_t t0 = tile_first[b] + (uint32_t)((uint64_t)tile_count[b] * sp / splits);
+                            const uint32_t t1 = tile_first[b] + (uint32_t)((uint64_t)tile_count[b] * (sp + 1) / splits);
+                            if (t1 <= t0)
+                                continue;
+                            const uint32_t w = (uint32_t)work.size();
+                            work.push_back(make_uint4(bf + g, nbk, t0, t1));
+                            split_of.push_back((uint32_t)sp);
+                            for (uint32_t k = 0; k < nbk; ++k)
+                                blk_ent[cur[bf + g + k]++] = w * bpw + k;
+                        }
                     }
                 }
-            }
             if (xcd_order && !work.empty()) {
                 // XCD-aware order: workgroup n runs on XCD n % 8 (dispatch round-robin), so the
                 // items of one domain split go to the same XCDs and their in-flight workgroups
@@ -918,7 +928,8 @@ int prepare(frac_ctx* c)
                     e = inv[e / bpw] * bpw + e % bpw;
             }
         };
-        const bool fourier = n == 8 && c->p.transforms == 4 && !c->virt && mfma_dft_enabled();
+        const bool fourier = n == 8 && (T == 4 || T == 8) && !c->virt && mfma_dft_enabled();
+        c->dft_copies = fourier && T == 8 ? 2u : 1u;
         int var = 0;
         FRAC_TRY(mfma_variant(c, var));
         const bool four_wave = dft_four_wave(var);
@@ -931,7 +942,7 @@ int prepare(frac_ctx* c)
             c->m_blk_ptr.assign(c->nblocks + 1, 0);
             c->m_blk_ent.clear();
         }
-        if (n == 8 && c->p.transforms == 4 && !c->virt) {
+        if (n == 8 && !c->virt && (T == 4 || c->dft_copies == 2)) {
             // FRAC_DFT_WGS (tuning knob): target workgroup count of the Fourier search
             const char* tw = getenv("FRAC_DFT_WGS");
             c->m8_bpw = dft_bpw(dft_variant(var));
@@ -1042,17 +1053,18 @@ int prepare(frac_ctx* c)
     }
     if (c->engine == FRAC_ENGINE_MFMA) {
         const int KS = (n * n + 15) / 16;
-        FRAC_HIP(c, c->d_m_slot_range.ensure((size_t)c->nblocks * 32));
+        // (T = 8 Fourier: the flipped copies' slots map to the same ranges, second half)
+        FRAC_HIP(c, c->d_m_slot_range.ensure((size_t)c->nblocks * 32 * c->dft_copies));
         FRAC_HIP(c, c->d_m_range_slot.ensure(nr));
         FRAC_HIP(c, c->d_m_tile_pos.ensure((size_t)c->ntiles * 32));
         FRAC_HIP(c, c->d_m_work.ensure(c->m_work.size()));
         FRAC_HIP(c, c->d_m_blk_ptr.ensure(c->m_blk_ptr.size()));
         FRAC_HIP(c, c->d_m_blk_ent.ensure(c->m_blk_ent.size()));
-        FRAC_HIP(c, c->d_m_rconst.ensure((size_t)c->nblocks * 32));
+        FRAC_HIP(c, c->d_m_rconst.ensure((size_t)c->nblocks * 32 * c->dft_copies));
         // the direct form's [tile][8] uint4 and the Fourier form's [tile][kDftCS] (+ one LDS-DMA piece of slack)
         FRAC_HIP(c, c->d_m_dconst.ensure((size_t)c->ntiles * kDftCS * 4 + 256));
         FRAC_HIP(c, c->d_m_dtiles.ensure((size_t)c->ntiles * KS * 64));
-        FRAC_HIP(c, c->d_m_rfrags.ensure((size_t)c->nblocks * c->Teff * KS * 64));
+        FRAC_HIP(c, c->d_m_rfrags.ensure((size_t)c->nblocks * std::max(c->Teff * KS, 6u * c->dft_copies) * 64));
         FRAC_HIP(c, c->d_m_entries.ensure(std::max(c->m_work.size() * 4 * c->Teff, c->m8_work.size() * c->m8_bpw) *
                                           64));
         if (!c->m8_blk_ptr.empty()) { // built for n = 8, T = 4 (search_dft); may have no work
@@ -1063,9 +1075,14 @@ int prepare(frac_ctx* c)
             FRAC_TRY(up(c->d_m8_blk_ptr.ptr, c->m8_blk_ptr.data(), c->m8_blk_ptr.size() * sizeof(uint32_t)));
             FRAC_TRY(up(c->d_m8_blk_ent.ptr, c->m8_blk_ent.data(), c->m8_blk_ent.size() * sizeof(uint32_t)));
         }
-        if (c->nblocks)
+        if (c->nblocks) {
             fill_range_slots<<<(c->nblocks * 32 + 255) / 256, 256, 0, c->stream>>>(
                 c->mlayout, c->d_rord.ptr, c->nblocks * 32, c->d_m_slot_range.ptr, c->d_m_range_slot.ptr);
+            if (c->dft_copies == 2)
+                FRAC_HIP(c, hipMemcpyAsync(c->d_m_slot_range.ptr + (size_t)c->nblocks * 32, c->d_m_slot_range.ptr,
+                                           (size_t)c->nblocks * 32 * sizeof(int32_t), hipMemcpyDeviceToDevice,
+                                           c->stream));
+        }
         if (c->ntiles)
             fill_tile_pos<<<(c->ntiles * 32 + 255) / 256, 256, 0, c->stream>>>(c->mlayout, c->ntiles * 32,
                                                                               c->d_m_tile_pos.ptr);
@@ -1177,7 +1194,8 @@ inline int launch_dft(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride)
     FRAC_HIP(c, c->d_dft_tguard.ensure(std::max<size_t>(c->ntiles, 1)));
     FRAC_HIP(c, c->d_dft_trmax.ensure((size_t)c->ntiles + 4)); // + 4: a chunk's thresholds are one scalar load
     FRAC_HIP(c, c->d_dft_tpool.ensure(std::max<size_t>((size_t)c->ntiles * 32 * 32, 1)));
-    FRAC_HIP(c, c->d_dft_rguard.ensure(std::max<size_t>(c->nblocks, 1)));
+    const uint32_t nbk = c->nblocks * c->dft_copies; // range blocks incl. T = 8's flipped copies
+    FRAC_HIP(c, c->d_dft_rguard.ensure(std::max<size_t>(nbk, 1)));
     // FRAC_MFMA_VARIANT for this path (A/B knob): default = exact form in 8-wave workgroups
     // with the v_max3-chain row maximum; 20 = the five-MFMA form (kDft5) in the same
     // workgroups; 6 = the pairwise-tree row maximum; 5 = 8-tile stages; 12 = two range blocks
@@ -1210,14 +1228,15 @@ inline int launch_dft(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride)
     r.tstride = tstride;
     r.ranges = c->d_ranges.ptr;
     r.slot_range = c->d_m_slot_range.ptr;
-    r.nblocks = c->nblocks;
+    r.nblocks = nbk;
     r.T = 4;
     r.rfrags = c->d_m_rfrags.ptr;
     r.rconst = c->d_m_rconst.ptr;
+    r.flip_from = c->dft_copies == 2 ? c->nblocks : ~0u;
     FRAC_HIP(c, c->d_dft_rorb.ensure(std::max<size_t>((size_t)r.nblocks * 32 * 32, 1)));
     r.rorb = c->d_dft_rorb.ptr;
-    if (c->nblocks) {
-        const unsigned g = (c->nblocks * 32 + 255) / 256;
+    if (nbk) {
+        const unsigned g = (nbk * 32 + 255) / 256;
         if (form == 5)
             dft_range_prep<5><<<g, 256, 0, c->stream>>>(r, c->d_dft_rguard.ptr);
         else if (form == 6)
@@ -1414,11 +1433,12 @@ inline int launch_dft(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride)
         v.pool = c->d_pool.ptr;
         v.negsd2 = c->d_negsd2.ptr;
         v.nr = nr;
-        v.T = 4;
+        v.T = c->dft_copies == 2 ? 8u : 4u;
         v.hitH = c->hitH;
         v.best_key = c->d_best_key.ptr;
         v.slot_range = c->d_m_slot_range.ptr;
         v.nslots = c->nblocks * 32u;
+        v.flip_slots = c->dft_copies == 2 ? c->nblocks * 32u : 0u;
         v.tpool = c->d_dft_tpool.ptr;
         v.rorb = c->d_dft_rorb.ptr;
         FRAC_HIP(c, c->d_rstat.ensure(std::max<size_t>(nr, 1)));
@@ -1437,7 +1457,7 @@ int launch_mfma(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride)
     // T = the transforms per pool row: 1 in the sampled form (one row per domain and transform)
     const uint32_t nr = (uint32_t)nranges(c), T = c->Teff;
     if constexpr (N == 8) {
-        if (T == 4 && !c->virt && mfma_dft_enabled())
+        if ((T == 4 || c->dft_copies == 2) && !c->virt && mfma_dft_enabled())
             return launch_dft(c, dtgt, tstride);
     }
     if (c->ntiles) {
@@ -1890,7 +1910,7 @@ int launch_all(frac_ctx* c)
     // the Fourier path and the SEA engine's tiled form build the pool in their fused domain pass
     // (dft_domain_build)
     const bool fused_pool = N == 8 && !c->virt &&
-                            ((use_mfma && c->p.transforms == 4 && mfma_dft_enabled()) ||
+                            ((use_mfma && (c->p.transforms == 4 || c->dft_copies == 2) && mfma_dft_enabled()) ||
                              (c->engine == FRAC_ENGINE_SEA && !c->all_fallback && c->tp));
     const GenArgs g = gen_args(c, dtgt, tstride);
     if (P && c->virt) // the sampled form: one row per (domain, transform), fracenc_gen.hip

@@ -102,6 +102,21 @@ constexpr bool orbits4_valid()
 }
 
 static_assert(orbits4_valid<8>(), "the reference's rotations must be the powers of Rotate_90 with 4-orbits");
+
+// T = 8 on the Fourier path: Flip_Rotate_k = Flip ∘ Rotate_k and Flip ∘ Rotate_k ∘ Flip = Rotate_{−k}
+template <int N>
+constexpr bool flips_valid()
+{
+    for (int k = 0; k < 4; ++k)
+        for (int p = 0; p < N * N; ++p) {
+            if (fwd_index<N>(4 + k, p) != fwd_index<N>(4, fwd_index<N>(k, p)))
+                return false;
+            if (fwd_index<N>(4, fwd_index<N>(k, fwd_index<N>(4, p))) != fwd_index<N>((4 - k) & 3, p))
+                return false;
+        }
+    return true;
+}
+static_assert(flips_valid<8>(), "the flip half of T = 8 is the rotation search of the flipped range");
 constexpr Orbits4<8> kOrb8 = make_orbits4<8>();
 constexpr float kDftPadY = -1.0e30f; // −Σb² of padding rows: y ≈ −1e30 never wins
 constexpr int kDftRangeFrags = 7;     // s, u, 4s, 4u, α, β, −α
@@ -389,6 +404,18 @@ __global__ void __launch_bounds__(256) dft_range_prep(MfmaRangePrepArgs a, uint3
 #pragma unroll
         for (int q = 0; q < NN; ++q)
             sa2 += av[q] * av[q];
+        if (b >= a.flip_from) {
+            // T = 8: the block's flipped copy, a'(q) = a(Flip q).  Flip_Rotate_k = Flip ∘ Rotate_k
+            // (fwd(4 + k, p) = fwd(4, fwd(k, p)), image/transform.h:32-41) and Flip ∘ g^k ∘ Flip = g^−k, so
+            // Σ_p a(p)·b(fwd(4 + k, p)) = Σ_q a'(q)·b(g^{−k} q): the copy's rotation t' is transform 4 + (−t' mod 4)
+            int fv[NN];
+#pragma unroll
+            for (int q = 0; q < NN; ++q)
+                fv[q] = av[fwd_index<N>(4, q)];
+#pragma unroll
+            for (int q = 0; q < NN; ++q)
+                av[q] = fv[q];
+        }
     } else {
 #pragma unroll
         for (int q = 0; q < NN; ++q)
@@ -1103,14 +1130,23 @@ __global__ void __launch_bounds__(256, F6 ? 2 : 3) search_dft2(DftArgs d)
 // ---------------------------------------------------------------------------
 // SORTED (tiles in ΣD4 order, fracenc_tp.hip): rows and tiles are not in domain order, so the
 // least key over every matching row of every tile of the chunk is taken (no first-row shortcut).
+// One slot's least key and the winner's sums (bestk = kKeyNone: padding slot, or no eligible domain).
+// FLIP: the slot holds a T = 8 range's flipped copy (dft_range_prep flip_from), whose rotation t' is the
+// reference's transform 4 + (−t' mod 4); the keys carry the reference's transform and a.T.
+struct DftResolved {
+    unsigned long long bestk = kKeyNone;
+    uint32_t bx = 0, bs1 = 0, bs2 = 0, sr1 = 0, sr2 = 0;
+};
+
 template <bool SORTED>
-__device__ inline void resolve_dft_slot(const MfmaResolveArgs& a, uint32_t slot, int lane)
+__device__ inline DftResolved resolve_dft_eval(const MfmaResolveArgs& a, uint32_t slot, int lane, bool flip)
 {
-    constexpr int PG = 16, T = 4;
+    constexpr int PG = 16, T = 4; // T: the rotations evaluated per slot
+    const uint32_t TK = a.T;      // the transforms of the keys (4, or 8 with the flipped copies)
+    DftResolved res;
     const int ri = a.slot_range[slot];
     if (ri < 0)
-        return;
-    const uint32_t r = (uint32_t)ri;
+        return res;
     const uint32_t blk = slot >> 5, col = slot & 31u;
     const int i = lane >> 2, g = lane & 3;
     // lane (i, g) holds orbits 4g..4g+3 of the range as pixel pairs (dft_range_prep) and meets
@@ -1149,7 +1185,7 @@ __device__ inline void resolve_dft_slot(const MfmaResolveArgs& a, uint32_t slot,
     for (int o = 32; o > 0; o >>= 1)
         vmax = __builtin_fmaxf(vmax, __uint_as_float(lane_xor(__float_as_uint(vmax), lane, o)));
     if (!(vmax > -1.0e29f))
-        return; // only padding rows: no eligible domain, best_key stays "none"
+        return res; // only padding rows: no eligible domain, best_key stays "none"
     const int64_t sa16 = (int64_t)a.rconst[slot];
     const bool sentinel = vmax == __builtin_inff();
     const bool exact = sentinel || vmax > (float)(sa16 - kExactLimit);
@@ -1230,10 +1266,11 @@ __device__ inline void resolve_dft_slot(const MfmaResolveArgs& a, uint32_t slot,
                     // S16 = 16Σr² − 8X + ΣD4² ≤ 64·1020² < 2^31: exact in int32
                     const int64_t s16 = p >= 0 ? (int64_t)(16 * sr2 - 8 * (int32_t)X - nsd2) : 0;
                     const bool ok = p >= 0 && g == 0 && (hit ? (s16 <= a.hitH) : (s16 == target));
+                    const uint32_t tr = flip ? 4u + ((4u - (uint32_t)t) & 3u) : (uint32_t)t; // the reference's transform
                     if constexpr (SORTED) {
                         // lane-local least key; one wave reduction per range at the end
                         const unsigned long long k =
-                            ok ? (hit ? key_hit((uint32_t)p, t) : key_miss((uint64_t)target, (uint32_t)p, T - 1 - t))
+                            ok ? (hit ? key_hit((uint32_t)p, tr) : key_miss((uint64_t)target, (uint32_t)p, TK - 1 - tr))
                                : kKeyNone;
                         if (k < tk) {
                             tk = k;
@@ -1244,8 +1281,8 @@ __device__ inline void resolve_dft_slot(const MfmaResolveArgs& a, uint32_t slot,
                         if (mask) {
                             const int first = __ffsll((long long)mask) - 1;
                             const int pf = __builtin_amdgcn_readlane(p, first);
-                            const unsigned long long k = hit ? key_hit((uint32_t)pf, t)
-                                                             : key_miss((uint64_t)target, (uint32_t)pf, T - 1 - t);
+                            const unsigned long long k = hit ? key_hit((uint32_t)pf, tr)
+                                                             : key_miss((uint64_t)target, (uint32_t)pf, TK - 1 - tr);
                             const uint32_t xf = (uint32_t)__builtin_amdgcn_readlane((int)X, first);
                             const uint32_t s1f = (uint32_t)__builtin_amdgcn_readlane((int)sd1, first);
                             const uint32_t s2f = (uint32_t)__builtin_amdgcn_readlane((int)sd2, first);
@@ -1283,13 +1320,45 @@ __device__ inline void resolve_dft_slot(const MfmaResolveArgs& a, uint32_t slot,
                                            lane_xor((uint32_t)bestk, lane, o);
             bestk = ok2 < bestk ? ok2 : bestk;
         }
+        // the winner's sums: from the lane that evaluated it (keys are unique per (domain, transform)),
+        // broadcast through a ballot
+        const unsigned long long own = __ballot(mine == bestk && bestk != kKeyNone);
+        if (own) {
+            const int src = __ffsll((long long)own) - 1;
+            bx = (uint32_t)__builtin_amdgcn_readlane((int)bx, src);
+            bs1 = (uint32_t)__builtin_amdgcn_readlane((int)bs1, src);
+            bs2 = (uint32_t)__builtin_amdgcn_readlane((int)bs2, src);
+        }
     }
-    if (lane == 0)
-        a.best_key[r] = bestk;
-    // the winner's sums for fit_rstat, from the lane that evaluated it (keys are unique per
-    // (domain, transform); without SORTED every lane holds the same)
-    if (a.rstat && bestk != kKeyNone && (SORTED ? mine == bestk : lane == 0))
-        a.rstat[r] = make_uint4(bx, bs1 | (sr1 << 16), bs2, (uint32_t)sr2);
+    res.bestk = bestk;
+    res.bx = bx;
+    res.bs1 = bs1;
+    res.bs2 = bs2;
+    res.sr1 = sr1;
+    res.sr2 = (uint32_t)sr2;
+    return res;
+}
+
+// the slot's range record: its least key (with T = 8's flipped copy, the lesser of the two) and the
+// winner's sums for fit_rstat (every lane holds the same after resolve_dft_eval)
+template <bool SORTED>
+__device__ inline void resolve_dft_slot(const MfmaResolveArgs& a, uint32_t slot, int lane)
+{
+    const int ri = a.slot_range[slot];
+    if (ri < 0)
+        return;
+    DftResolved w = resolve_dft_eval<SORTED>(a, slot, lane, false);
+    if (!SORTED && a.flip_slots) {
+        const DftResolved f = resolve_dft_eval<SORTED>(a, slot + a.flip_slots, lane, true);
+        if (f.bestk < w.bestk)
+            w = f;
+    }
+    const uint32_t r = (uint32_t)ri;
+    if (lane == 0) {
+        a.best_key[r] = w.bestk;
+        if (a.rstat && w.bestk != kKeyNone)
+            a.rstat[r] = make_uint4(w.bx, w.bs1 | (w.sr1 << 16), w.bs2, w.sr2);
+    }
 }
 
 // One wave per slot, in slot order (the 32 ranges of a block read the same entry lines back to

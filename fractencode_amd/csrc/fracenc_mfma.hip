@@ -113,6 +113,7 @@ struct MfmaRangePrepArgs {
     uint4* rfrags;             // [nblocks][T][KS][64]
     uint32_t* rconst;          // [nblocks*32]
     uint32_t* rorb = nullptr;  // dft_range_prep: [nblocks*32][32] pixel pairs in orbit order (resolve_dft)
+    uint32_t flip_from = ~0u;  // dft_range_prep: blocks from here on hold their range read through Flip (T = 8)
 };
 
 template <int N>
@@ -551,6 +552,7 @@ struct MfmaResolveArgs {
     const uint32_t* tpool;      // [ntiles*32][32] D4 pairs in orbit order (dft_domain_build)
     const uint32_t* rorb;       // [nslots][32] range pixel pairs in orbit order (dft_range_prep)
     uint4* rstat = nullptr;     // [nr] the winner's {X_t, ΣD4 | Σr << 16, ΣD4², Σr²} (fit_rstat)
+    uint32_t flip_slots = 0;    // T = 8 Fourier: slot s's flipped copy is slot s + flip_slots (0: none)
     int merged = 0;             // resolve_mfma: entries hold the minimum over every transform (search_mfma VAR 128)
 };
 

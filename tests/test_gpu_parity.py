@@ -330,6 +330,35 @@ def test_five_mfma_form_at_operand_extremes(monkeypatch, kind, var):
         assert st["rejected_mappings"] == wst["rejected_mappings"]
 
 
+@pytest.mark.parametrize("kind", ["binary", "blocks8", "orbits", "noise"])
+def test_t8_fourier_flipped_copies_at_operand_extremes(monkeypatch, kind):
+    """T = 8 on the Fourier path: each range block runs a second time read through Flip
+    (Flip_Rotate_k = Flip ∘ Rotate_k, dft_range_prep flip_from) and resolve_dft keeps the lesser key of
+    the two copies, with the copy's rotation t' as transform 4 + (−t' mod 4).  On the operand-extreme
+    frames and on noise, with and without the classifier and with a hit threshold (the first hit in
+    (domain, transform) order, image/metrics.h + TransformEstimator2.hpp:34-41), the records equal the
+    exhaustive VALU engine's and the direct MFMA form's."""
+    rng = np.random.default_rng(zlib.crc32(("t8" + kind).encode()))
+    S = 256
+    p = rng.integers(0, 256, (S, S), dtype=np.uint8) if kind == "noise" else _extreme_plane(rng, S, kind)
+    doms, rngs = F.create_uniform_grid(S, S, 16, 8), F.create_uniform_grid(S, S, 8, 8)
+    for cls, thr in ((False, 0.0), (True, 0.0), (False, 40.0)):
+        outs = {}
+        for name, eng, dft in (("valu", F.ENGINE_VALU, "1"), ("direct", F.ENGINE_MFMA, "0"),
+                               ("fourier", F.ENGINE_MFMA, "1")):
+            monkeypatch.setenv("FRAC_MFMA_DFT", dft)
+            with F.Engine(0, 8, cls, thr, -1.0, eng) as e:
+                e.set_frame(p)
+                e.set_domains(doms)
+                outs[name], st = e.search(rngs)
+            if name == "fourier":
+                assert st["search_form"] == F.FORM_FOURIER
+        for name in ("direct", "fourier"):
+            assert outs[name].tobytes() == outs["valu"].tobytes(), f"{kind} cls={cls} thr={thr}: {name}"
+        if kind in ("binary", "noise") and thr == 0.0:  # exact copies (blocks8) are hits: transform 0 first
+            assert (outs["fourier"]["transform"] >= 4).any(), "the flipped copies win somewhere"
+
+
 def test_fourier_direct_and_valu_agree_on_stress_frame(monkeypatch):
     """n = 8, T = 4 on a uniform-noise 1024² frame: C4-Fourier MFMA, direct MFMA and VALU
     engines give identical records."""
@@ -504,7 +533,7 @@ PRODUCT_VARIANTS = ("0", "1", "2", "3", "4", "5", "6", "7", "12", "20", "21", "2
                     "33", "34", "35", "36", "64", "96", "98", "128", "130")
 
 
-@pytest.mark.parametrize("n,T,dft", [(8, 4, "0"), (4, 4, "0"), (8, 8, "0"), (8, 4, "1")])
+@pytest.mark.parametrize("n,T,dft", [(8, 4, "0"), (4, 4, "0"), (8, 8, "0"), (8, 4, "1"), (8, 8, "1")])
 def test_every_product_variant_gives_the_same_records(monkeypatch, n, T, dft):
     # FRAC_MFMA_VARIANT is an A/B knob: every value a product build accepts must give the records of
     # the exhaustive VALU engine (the launch switch and the resolve's entry layout must agree)

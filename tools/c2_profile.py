@@ -24,3 +24,22 @@ for T in (8, 4):
         a = np.median(np.array(ms[2:]), axis=0)
         print(f"T={T}: device {a[0]:.3f} ms (prep {a[1]:.3f}, search {a[2]:.3f}, finish {a[3]:.3f}), "
               f"{4096 / a[0] * 1e3 / 1e6:.2f} M range-blocks/s", flush=True)
+
+if len(sys.argv) > 1 and sys.argv[1] == "c3t8":
+    # the C3 frame with all 8 transforms (BASELINE configs[1]'s transform set at configs[2]'s size)
+    from fractencode_amd.synth import value_noise  # noqa: E402
+
+    S = 4096
+    q = value_noise(S, S, 1234)
+    with F.Engine(0, 8, False, 0.0, -1.0, F.ENGINE_AUTO, timing=True) as e:
+        e.set_frame(q)
+        e.set_domains(F.create_uniform_grid(S, S, 16, 8))
+        e.set_ranges(F.create_uniform_grid(S, S, 8, 8))
+        ms = []
+        for _ in range(4):
+            e.run()
+            _, st = e.fetch()
+            ms.append((st["ms_device"], st["ms_prep"], st["ms_search"], st["ms_finish"]))
+        a = np.median(np.array(ms[1:]), axis=0)
+        print(f"C3 T=8: device {a[0]:.3f} ms (prep {a[1]:.3f}, search {a[2]:.3f}, finish {a[3]:.3f}), "
+              f"{262144 / a[0] * 1e3 / 1e6:.2f} M range-blocks/s, form {st['search_form']}", flush=True)
