@@ -32,8 +32,11 @@ typedef float f4v __attribute__((ext_vector_type(4)));
 constexpr int NT = 8; // 32-domain tiles resident in LDS
 
 // k32: LDS = NT × (5 A pieces of 1 KiB) + NT × 16 uint4 of constants
-__global__ void __launch_bounds__(512, 4) k32(const uint4* __restrict__ src, const uint4* __restrict__ rf, int iters,
-                                            float* out)
+// F5: the five-MFMA form with the folded constant (P from C = −Σb²/2, M separate; 2U − Σb²/2 = P + M and
+// 2U' − Σb²/2 = P − M on the VALU): 5 MFMA and 5 VALU per candidate instead of 6 and 3
+template <int WPE, bool F5 = false>
+__global__ void __launch_bounds__(512, WPE) k32(const uint4* __restrict__ src, const uint4* __restrict__ rf, int iters,
+                                              float* out)
 {
     constexpr int A = NT * 5 * 64, C = NT * 16;
     __shared__ uint4 lds[A + C];
@@ -65,12 +68,21 @@ __global__ void __launch_bounds__(512, 4) k32(const uint4* __restrict__ src, con
             const f16v k1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[2], bf[3], z, 0, 0, 0);
             const f16v p = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[0], bf[0], c, 0, 0, 0);
             const f16v pr = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[3], bf[4], k1, 0, 0, 0);
-            const f16v u = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[1], bf[1], p, 0, 0, 0);
-            const f16v pi = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[4], bf[5], k1, 0, 0, 0);
-            const f16v v = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[1], bf[2], p, 0, 0, 0);
+            if constexpr (F5) {
+                const f16v mm = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[1], bf[1], z, 0, 0, 0);
+                const f16v pi = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[4], bf[5], k1, 0, 0, 0);
 #pragma unroll
-            for (int i = 0; i < 16; ++i)
-                m = __builtin_fmaxf(__builtin_fmaxf(m, u[i] + __builtin_fabsf(pr[i])), v[i] + __builtin_fabsf(pi[i]));
+                for (int i = 0; i < 16; ++i)
+                    m = __builtin_fmaxf(__builtin_fmaxf(m, (p[i] + mm[i]) + __builtin_fabsf(pr[i])),
+                                        (p[i] - mm[i]) + __builtin_fabsf(pi[i]));
+            } else {
+                const f16v u = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[1], bf[1], p, 0, 0, 0);
+                const f16v pi = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[4], bf[5], k1, 0, 0, 0);
+                const f16v v = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[1], bf[2], p, 0, 0, 0);
+#pragma unroll
+                for (int i = 0; i < 16; ++i)
+                    m = __builtin_fmaxf(__builtin_fmaxf(m, u[i] + __builtin_fabsf(pr[i])), v[i] + __builtin_fabsf(pi[i]));
+            }
         }
     }
     out[blockIdx.x * 512 + threadIdx.x] = m;
@@ -178,9 +190,12 @@ int main(int argc, char** argv)
     };
     // pairs per launch: waves × iters × NT tiles × (32×32 | 16×16·2) pairs
     const double waves = (double)nwg * 8;
-    run("k32", [&]() { k32<<<nwg, 512>>>(ds, dr, iters, dout); }, waves * iters * NT * 1024.0);
+    run("k32", [&]() { k32<4><<<nwg, 512>>>(ds, dr, iters, dout); }, waves * iters * NT * 1024.0);
+    run("k32/w5", [&]() { k32<5><<<nwg, 512>>>(ds, dr, iters, dout); }, waves * iters * NT * 1024.0);
+    run("k32/w3", [&]() { k32<3><<<nwg, 512>>>(ds, dr, iters, dout); }, waves * iters * NT * 1024.0);
+    run("k32f5", [&]() { k32<4, true><<<nwg, 512>>>(ds, dr, iters, dout); }, waves * iters * NT * 1024.0);
     run("k16/w8", [&]() { k16<8><<<nwg, 512>>>(d16, dr, iters, dout); }, waves * iters * NT * 512.0);
     run("k16/w4", [&]() { k16<4><<<nwg, 512>>>(d16, dr, iters, dout); }, waves * iters * NT * 512.0);
-    run("k32", [&]() { k32<<<nwg, 512>>>(ds, dr, iters, dout); }, waves * iters * NT * 1024.0);
+    run("k32", [&]() { k32<4><<<nwg, 512>>>(ds, dr, iters, dout); }, waves * iters * NT * 1024.0);
     return 0;
 }
