@@ -123,6 +123,54 @@ __global__ void __launch_bounds__(512, WPE) k16(const uint4* __restrict__ src, c
     out[blockIdx.x * 512 + threadIdx.x] = m;
 }
 
+// kl: the six-MFMA loop with five B fragments (the negated one moved to the domain side: 2U' = P − M from
+// a sixth A fragment −(s_b − u_b) against s_a − u_a), WAVES waves per workgroup, at least WPE waves per SIMD
+// (10-wave workgroups at WPE 5: 20 waves per CU = 5 per SIMD)
+template <int WAVES, int WPE>
+__global__ void __launch_bounds__(64 * WAVES, WPE) kl(const uint4* __restrict__ src, const uint4* __restrict__ rf,
+                                                       int iters, float* out)
+{
+    constexpr int A = NT * 6 * 64, C = NT * 16;
+    __shared__ uint4 lds[A + C];
+    for (int i = threadIdx.x; i < A + C; i += 64 * WAVES)
+        lds[i] = src[i % (NT * 5 * 64 + NT * 16)];
+    __syncthreads();
+    const int lane = threadIdx.x & 63, h = lane >> 5;
+    half8 bf[5];
+    for (int f = 0; f < 5; ++f)
+        bf[f] = __builtin_bit_cast(half8, rf[((blockIdx.x * WAVES + (threadIdx.x >> 6)) % 64 * 6 + f) * 64 + lane]);
+    float m = -__builtin_inff();
+    for (int it = 0; it < iters; ++it) {
+#pragma unroll 1
+        for (int q = 0; q < NT; ++q) {
+            half8 af[6];
+#pragma unroll
+            for (int s = 0; s < 6; ++s)
+                af[s] = __builtin_bit_cast(half8, lds[(q * 6 + s) * 64 + lane]);
+            f16v c;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint4 v = lds[A + q * 16 + h * 4 + k];
+                c[4 * k] = __uint_as_float(v.x);
+                c[4 * k + 1] = __uint_as_float(v.y);
+                c[4 * k + 2] = __uint_as_float(v.z);
+                c[4 * k + 3] = __uint_as_float(v.w);
+            }
+            const f16v z = {};
+            const f16v k1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[2], bf[2], z, 0, 0, 0);
+            const f16v p = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[0], bf[0], c, 0, 0, 0);
+            const f16v pr = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[3], bf[3], k1, 0, 0, 0);
+            const f16v u = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[1], bf[1], p, 0, 0, 0);
+            const f16v pi = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[4], bf[4], k1, 0, 0, 0);
+            const f16v v = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[5], bf[1], p, 0, 0, 0);
+#pragma unroll
+            for (int i = 0; i < 16; ++i)
+                m = __builtin_fmaxf(__builtin_fmaxf(m, u[i] + __builtin_fabsf(pr[i])), v[i] + __builtin_fabsf(pi[i]));
+        }
+    }
+    out[blockIdx.x * 64 * WAVES + threadIdx.x] = m;
+}
+
 static uint4 rand_frag(std::mt19937& g, int lo, int hi)
 {
     std::uniform_int_distribution<int> d(lo, hi);
@@ -194,6 +242,11 @@ int main(int argc, char** argv)
     run("k32/w5", [&]() { k32<5><<<nwg, 512>>>(ds, dr, iters, dout); }, waves * iters * NT * 1024.0);
     run("k32/w3", [&]() { k32<3><<<nwg, 512>>>(ds, dr, iters, dout); }, waves * iters * NT * 1024.0);
     run("k32f5", [&]() { k32<4, true><<<nwg, 512>>>(ds, dr, iters, dout); }, waves * iters * NT * 1024.0);
+    run("kl8/w4", [&]() { kl<8, 4><<<nwg, 512>>>(ds, dr, iters, dout); }, waves * iters * NT * 1024.0);
+    {
+        const int nwg10 = nwg * 8 / 10; // the same waves in 10-wave workgroups
+        run("kl10/w5", [&]() { kl<10, 5><<<nwg10, 640>>>(ds, dr, iters, dout); }, (double)nwg10 * 10 * iters * NT * 1024.0);
+    }
     run("k16/w8", [&]() { k16<8><<<nwg, 512>>>(d16, dr, iters, dout); }, waves * iters * NT * 512.0);
     run("k16/w4", [&]() { k16<4><<<nwg, 512>>>(d16, dr, iters, dout); }, waves * iters * NT * 512.0);
     run("k32", [&]() { k32<4><<<nwg, 512>>>(ds, dr, iters, dout); }, waves * iters * NT * 1024.0);
