@@ -42,14 +42,15 @@ def _as_oracle(items):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("cls", [False, True])
-@pytest.mark.parametrize("split", [1.0, 8.0])
-def test_gpu_quadtree_matches_oracle(oracle, cls, split):
+@pytest.mark.parametrize("cls,split,T", [(False, 1.0, 4), (False, 8.0, 4), (True, 1.0, 4), (True, 8.0, 4),
+                                         (True, 8.0, 8), (False, 1.0, 8)])
+def test_gpu_quadtree_matches_oracle(oracle, cls, split, T):
+    # T = 8: the n = 8 level runs the Fourier form with the flipped range copies
     p = plane("lenna_y")
-    with F.Engine(0, 4, cls) as e:
+    with F.Engine(0, T, cls) as e:
         e.set_frame(p)
         items, st = e.encode_quadtree(16, 4, split)
-        want, sizes = oracle.quadtree(p, 16, 4, split, use_classifier=cls)
+        want, sizes = oracle.quadtree(p, 16, 4, split, T=T, use_classifier=cls)
         got = _as_oracle(items)
         for k in want.dtype.names:
             if k != "pad":
