@@ -314,14 +314,23 @@ inline size_t nranges(const frac_ctx* c) { return c->ranges_dev ? c->nr_dev : c-
 namespace {
 constexpr uint32_t kHistRuns = 256;
 
-// Boundary k of the current run (0 start, 1 search begins, 2 search ends, 3 finish ends): the
-// last-run event (frac_stats) and the run's slot in the timing history (frac_timing_history)
+// Boundary k of the current run (0 start, 1 search begins, 2 search ends, 3 finish ends), one
+// event each: the run's slot in the timing history (frac_timing_history), which frac_stats reads
+// for the last run (last_event).  Every record is a marker packet the GPU waits on, so a second
+// record per boundary cost C2 (Lenna 512², T = 8) ≈ 17 µs per frame.
 int mark_event(frac_ctx* c, int k)
 {
-    FRAC_HIP(c, hipEventRecord(c->ev[k], c->stream));
-    if (!c->hist.empty())
-        FRAC_HIP(c, hipEventRecord(c->hist[(size_t)(c->hist_runs % kHistRuns) * 4 + k], c->stream));
+    hipEvent_t e = c->hist.empty() ? c->ev[k] : c->hist[(size_t)(c->hist_runs % kHistRuns) * 4 + k];
+    FRAC_HIP(c, hipEventRecord(e, c->stream));
     return FRAC_OK;
+}
+
+// boundary k of the last completed launch (after launch_all / launch_generic counted it)
+hipEvent_t last_event(const frac_ctx* c, int k)
+{
+    if (c->hist.empty() || c->hist_runs == 0)
+        return c->ev[k];
+    return c->hist[(size_t)((c->hist_runs - 1) % kHistRuns) * 4 + k];
 }
 } // namespace
 
@@ -1180,8 +1189,16 @@ inline bool mfma_dft_enabled()
     return v ? atoi(v) != 0 : true;
 }
 
-// n = 8, T = 4: the C4-Fourier search (6 MFMAs per 32×32 tile pair instead of 16)
-inline int launch_dft(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride)
+// whether launch_mfma<8> takes the Fourier path (launch_dft); launch_all leaves the run's
+// best_key / fb_count resets to it then
+inline bool dft_route(const frac_ctx* c)
+{
+    return (c->Teff == 4 || c->dft_copies == 2) && !c->virt && mfma_dft_enabled();
+}
+
+// n = 8, T = 4: the C4-Fourier search (6 MFMAs per 32×32 tile pair instead of 16).  inits: reset
+// best_key and fb_count in the preparation kernel (launch_all skipped its memsets)
+inline int launch_dft(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool inits)
 {
     const uint32_t nr = (uint32_t)nranges(c);
     MfmaDomainPrepArgs d;
@@ -1216,13 +1233,6 @@ inline int launch_dft(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride)
     b.pool = c->d_pool.ptr;
     b.negsd2 = c->d_negsd2.ptr;
     b.tpool = c->d_dft_tpool.ptr;
-    if (c->ntiles) {
-        if (f5)
-            dft_domain_build<false, true><<<(c->ntiles * 32 + 255) / 256, 256, 0, c->stream>>>(d, b, c->d_dft_tguard.ptr,
-                                                                                              c->d_dft_trmax.ptr);
-        else
-            dft_domain_build<false><<<(c->ntiles * 32 + 255) / 256, 256, 0, c->stream>>>(d, b, c->d_dft_tguard.ptr);
-    }
     MfmaRangePrepArgs r;
     r.tgt = dtgt;
     r.tstride = tstride;
@@ -1235,14 +1245,25 @@ inline int launch_dft(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride)
     r.flip_from = c->dft_copies == 2 ? c->nblocks : ~0u;
     FRAC_HIP(c, c->d_dft_rorb.ensure(std::max<size_t>((size_t)r.nblocks * 32 * 32, 1)));
     r.rorb = c->d_dft_rorb.ptr;
-    if (nbk) {
-        const unsigned g = (nbk * 32 + 255) / 256;
+    // one launch: domain tiles, range blocks and (inits) the run's resets
+    DftPrepInit in;
+    if (inits) {
+        in.best_key = c->d_best_key.ptr;
+        in.nr = nr;
+        in.fb_count = c->d_fb_count.ptr;
+        in.fbc = 0; // the Fourier path never runs with all_fallback
+    }
+    in.dblocks = (c->ntiles * 32 + 255) / 256;
+    const unsigned pg = in.dblocks + (nbk * 32 + 255) / 256;
+    if (pg || inits) {
+        int32_t* trmax = f5 ? c->d_dft_trmax.ptr : nullptr;
+        const dim3 grid(std::max(pg, 1u));
         if (form == 5)
-            dft_range_prep<5><<<g, 256, 0, c->stream>>>(r, c->d_dft_rguard.ptr);
+            dft_prep<5><<<grid, 256, 0, c->stream>>>(d, b, c->d_dft_tguard.ptr, trmax, r, c->d_dft_rguard.ptr, in);
         else if (form == 6)
-            dft_range_prep<6><<<g, 256, 0, c->stream>>>(r, c->d_dft_rguard.ptr);
+            dft_prep<6><<<grid, 256, 0, c->stream>>>(d, b, c->d_dft_tguard.ptr, trmax, r, c->d_dft_rguard.ptr, in);
         else
-            dft_range_prep<4><<<g, 256, 0, c->stream>>>(r, c->d_dft_rguard.ptr);
+            dft_prep<4><<<grid, 256, 0, c->stream>>>(d, b, c->d_dft_tguard.ptr, trmax, r, c->d_dft_rguard.ptr, in);
     }
     if (c->p.flags & FRAC_FLAG_TIMING)
         FRAC_TRY(mark_event(c, 1));
@@ -1452,13 +1473,13 @@ inline int launch_dft(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride)
 }
 
 template <int N>
-int launch_mfma(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride)
+int launch_mfma(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool inits = false)
 {
     // T = the transforms per pool row: 1 in the sampled form (one row per domain and transform)
     const uint32_t nr = (uint32_t)nranges(c), T = c->Teff;
     if constexpr (N == 8) {
-        if ((T == 4 || c->dft_copies == 2) && !c->virt && mfma_dft_enabled())
-            return launch_dft(c, dtgt, tstride);
+        if (dft_route(c))
+            return launch_dft(c, dtgt, tstride, inits);
     }
     if (c->ntiles) {
         MfmaDomainPrepArgs d;
@@ -1899,14 +1920,18 @@ int launch_all(frac_ctx* c)
     }
     if (timing)
         FRAC_TRY(mark_event(c, 0));
-    if (nr)
-        FRAC_HIP(c, hipMemsetAsync(c->d_best_key.ptr, 0xff, nr * sizeof(unsigned long long), c->stream));
-    const uint32_t fbc = c->all_fallback ? nr : 0u;
-    // a device-side fill, not an H2D copy from pageable host memory (which serialises the host
-    // with the stream)
-    FRAC_HIP(c, hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(c->d_fb_count.ptr), (int)fbc, 1, c->stream));
     c->fit_rstat = false;
     const bool use_mfma = c->engine == FRAC_ENGINE_MFMA && !c->all_fallback;
+    // the Fourier path resets best_key and fb_count in its preparation kernel (dft_prep)
+    const bool dft_inits = N == 8 && use_mfma && nr && dft_route(c);
+    if (!dft_inits) {
+        if (nr)
+            FRAC_HIP(c, hipMemsetAsync(c->d_best_key.ptr, 0xff, nr * sizeof(unsigned long long), c->stream));
+        const uint32_t fbc = c->all_fallback ? nr : 0u;
+        // a device-side fill, not an H2D copy from pageable host memory (which serialises the host
+        // with the stream)
+        FRAC_HIP(c, hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(c->d_fb_count.ptr), (int)fbc, 1, c->stream));
+    }
     // the Fourier path and the SEA engine's tiled form build the pool in their fused domain pass
     // (dft_domain_build)
     const bool fused_pool = N == 8 && !c->virt &&
@@ -1923,7 +1948,7 @@ int launch_all(frac_ctx* c)
     const bool use_sea = c->engine == FRAC_ENGINE_SEA && !c->all_fallback;
     tr.mark("memsets + pool");
     if (use_mfma)
-        FRAC_TRY(launch_mfma<N>(c, dtgt, tstride));
+        FRAC_TRY(launch_mfma<N>(c, dtgt, tstride, dft_inits));
     if constexpr (N <= 8) {
         if (use_sea)
             FRAC_TRY(launch_sea<N>(c, dtgt, tstride, timing));
@@ -2418,13 +2443,13 @@ int frac_fetch(frac_ctx* c, frac_encode_item* out, frac_stats* stats)
         }
         if (c->p.flags & FRAC_FLAG_TIMING) {
             float ms = 0.f;
-            if (hipEventElapsedTime(&ms, c->ev[0], c->ev[3]) == hipSuccess)
+            if (hipEventElapsedTime(&ms, last_event(c, 0), last_event(c, 3)) == hipSuccess)
                 stats->ms_device = ms;
-            if (hipEventElapsedTime(&ms, c->ev[0], c->ev[1]) == hipSuccess)
+            if (hipEventElapsedTime(&ms, last_event(c, 0), last_event(c, 1)) == hipSuccess)
                 stats->ms_prep = ms;
-            if (hipEventElapsedTime(&ms, c->ev[1], c->ev[2]) == hipSuccess)
+            if (hipEventElapsedTime(&ms, last_event(c, 1), last_event(c, 2)) == hipSuccess)
                 stats->ms_search = ms;
-            if (hipEventElapsedTime(&ms, c->ev[2], c->ev[3]) == hipSuccess)
+            if (hipEventElapsedTime(&ms, last_event(c, 2), last_event(c, 3)) == hipSuccess)
                 stats->ms_finish = ms;
         }
     }
@@ -2620,13 +2645,13 @@ int frac_encode_quadtree(frac_ctx* c, const frac_quadtree_params* qp, frac_encod
         FRAC_HIP(c, hipStreamSynchronize(c->stream));
         if (stats && (c->p.flags & FRAC_FLAG_TIMING)) { // the level's run has completed
             float ms = 0.f;
-            if (hipEventElapsedTime(&ms, c->ev[0], c->ev[3]) == hipSuccess)
+            if (hipEventElapsedTime(&ms, last_event(c, 0), last_event(c, 3)) == hipSuccess)
                 total.ms_device += ms;
-            if (hipEventElapsedTime(&ms, c->ev[0], c->ev[1]) == hipSuccess)
+            if (hipEventElapsedTime(&ms, last_event(c, 0), last_event(c, 1)) == hipSuccess)
                 total.ms_prep += ms;
-            if (hipEventElapsedTime(&ms, c->ev[1], c->ev[2]) == hipSuccess)
+            if (hipEventElapsedTime(&ms, last_event(c, 1), last_event(c, 2)) == hipSuccess)
                 total.ms_search += ms;
-            if (hipEventElapsedTime(&ms, c->ev[2], c->ev[3]) == hipSuccess)
+            if (hipEventElapsedTime(&ms, last_event(c, 2), last_event(c, 3)) == hipSuccess)
                 total.ms_finish += ms;
         }
         n_leaves += nr - nsplit;

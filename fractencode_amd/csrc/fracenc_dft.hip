@@ -228,11 +228,10 @@ __device__ inline uint32_t pair_sums(uint32_t w0, uint32_t w1)
 // zeroes the tile guards, which are then raised with atomics.
 // F5: the five-MFMA form's fragments [s_b + u_b | s_b − u_b | γ | γ − δ | −δ − γ] (kDft5)
 template <bool BYPOS = false, bool F5 = false>
-__global__ void __launch_bounds__(256) dft_domain_build(MfmaDomainPrepArgs a, DftDomainBuildArgs s,
-                                                        uint2* __restrict__ tguard, int32_t* __restrict__ trmax = nullptr)
+__device__ __forceinline__ void dft_domain_build_at(uint32_t tid, const MfmaDomainPrepArgs& a, const DftDomainBuildArgs& s,
+                                                    uint2* __restrict__ tguard, int32_t* __restrict__ trmax)
 {
     constexpr int NN = 64, NO = 16, KS = F5 ? 5 : 4;
-    const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
     if (tid >= (BYPOS ? s.npos : a.ntiles * 32u))
         return;
     const uint32_t gid = BYPOS ? s.row_of[tid] : tid;
@@ -363,6 +362,13 @@ __global__ void __launch_bounds__(256) dft_domain_build(MfmaDomainPrepArgs a, Df
     }
 }
 
+template <bool BYPOS = false, bool F5 = false>
+__global__ void __launch_bounds__(256) dft_domain_build(MfmaDomainPrepArgs a, DftDomainBuildArgs s,
+                                                        uint2* __restrict__ tguard, int32_t* __restrict__ trmax = nullptr)
+{
+    dft_domain_build_at<BYPOS, F5>(blockIdx.x * blockDim.x + threadIdx.x, a, s, tguard, trmax);
+}
+
 // ---------------------------------------------------------------------------
 // dft_range_prep: per range block the seven distinct B fragments
 //   f0 = s_a, f1 = u_a, f2 = 4s_a, f3 = 4u_a, f4 = α, f5 = β, f6 = −α
@@ -374,10 +380,9 @@ __global__ void __launch_bounds__(256) dft_domain_build(MfmaDomainPrepArgs a, Df
 // FORM 5: the five-MFMA form's fragments [s_a + u_a | s_a − u_a | 2(α + β) | −2β | 2α] (kDft5);
 // FORM 6: the six-MFMA form's [s_a + u_a | s_a − u_a | u_a − s_a | 2(α + β) | −2β | 2α] (kDft6)
 template <int FORM = 4>
-__global__ void __launch_bounds__(256) dft_range_prep(MfmaRangePrepArgs a, uint32_t* __restrict__ rguard)
+__device__ __forceinline__ void dft_range_prep_at(uint32_t gid, const MfmaRangePrepArgs& a, uint32_t* __restrict__ rguard)
 {
     constexpr int N = 8, NN = 64, NO = 16, NBF = FORM == 6 ? 6 : FORM == 5 ? 5 : kDftRangeFrags;
-    const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
     if (gid >= a.nblocks * 32u)
         return;
     const uint32_t b = gid >> 5, col = gid & 31u;
@@ -484,6 +489,43 @@ __global__ void __launch_bounds__(256) dft_range_prep(MfmaRangePrepArgs a, uint3
         g1 = max(g1, (uint32_t)__shfl_xor((int)g1, o, 64));
     if (col == 0)
         rguard[b] = g1;
+}
+
+template <int FORM = 4>
+__global__ void __launch_bounds__(256) dft_range_prep(MfmaRangePrepArgs a, uint32_t* __restrict__ rguard)
+{
+    dft_range_prep_at<FORM>(blockIdx.x * blockDim.x + threadIdx.x, a, rguard);
+}
+
+// ---------------------------------------------------------------------------
+// dft_prep: the Fourier path's preparation in one launch.  Blocks [0, dblocks) build the domain
+// tiles (dft_domain_build), the rest prepare the range blocks (dft_range_prep), so the two run
+// side by side instead of one after the other.  Every thread also takes a grid-stride share of
+// the run's best_key reset, and thread 0 sets the fallback count: the two hipMemsetAsync of
+// launch_all, whose launches cost more than their bytes on small frames.
+// ---------------------------------------------------------------------------
+struct DftPrepInit {
+    unsigned long long* best_key = nullptr; // nr entries set to ~0 (no candidate yet)
+    uint32_t nr = 0;
+    uint32_t* fb_count = nullptr; // set to fbc when not null
+    uint32_t fbc = 0;
+    uint32_t dblocks = 0; // blocks of the domain build
+};
+
+template <int FORM>
+__global__ void __launch_bounds__(256) dft_prep(MfmaDomainPrepArgs d, DftDomainBuildArgs s, uint2* __restrict__ tguard,
+                                                int32_t* __restrict__ trmax, MfmaRangePrepArgs r,
+                                                uint32_t* __restrict__ rguard, DftPrepInit in)
+{
+    const uint32_t gt = blockIdx.x * blockDim.x + threadIdx.x;
+    for (uint32_t i = gt; i < in.nr; i += gridDim.x * blockDim.x)
+        in.best_key[i] = ~0ull;
+    if (gt == 0 && in.fb_count)
+        *in.fb_count = in.fbc;
+    if (blockIdx.x < in.dblocks)
+        dft_domain_build_at<false, FORM != 4>(gt, d, s, tguard, trmax);
+    else
+        dft_range_prep_at<FORM>((blockIdx.x - in.dblocks) * blockDim.x + threadIdx.x, r, rguard);
 }
 
 // ---------------------------------------------------------------------------
