@@ -422,16 +422,19 @@ def test_unaligned_origins(oracle, engine, n):
 
 @pytest.mark.parametrize("engine", ENGINES)
 @pytest.mark.parametrize("cls", [False, True])
-def test_new_frame_same_geometry(engine, cls):
+@pytest.mark.parametrize("T,thr", [(4, 0.0), (8, 0.0), (4, 2.0), (8, 2.0)])
+def test_new_frame_same_geometry(engine, cls, T, thr):
     """A second frame of the same geometry into a prepared context (the video case: the
     classifier-off path keeps the prepared structures, the classifier-on path re-prepares)
-    gives the records a fresh context gives for that frame."""
+    gives the records a fresh context gives for that frame. Each run resets its winners
+    (on the Fourier path inside dft_prep, not by a memset), with and without flipped copies
+    and hit thresholds."""
     rng = np.random.default_rng(21)
     a = rng.integers(0, 256, (128, 128), dtype=np.uint8)
     b = np.ascontiguousarray(np.rot90(a)) // 2 + rng.integers(0, 100, (128, 128), dtype=np.uint8)
     doms = F.create_uniform_grid(128, 128, 16, 8)
     rngs = F.create_uniform_grid(128, 128, 8, 8)
-    with F.Engine(0, 4, cls, 0.0, -1.0, engine) as e:
+    with F.Engine(0, T, cls, thr, -1.0, engine) as e:
         e.set_frame(a)
         e.set_domains(doms)
         e.set_ranges(rngs)
@@ -440,7 +443,7 @@ def test_new_frame_same_geometry(engine, cls):
         e.set_frame(b)
         e.run()
         second, _ = e.fetch()
-    with F.Engine(0, 4, cls, 0.0, -1.0, engine) as e:
+    with F.Engine(0, T, cls, thr, -1.0, engine) as e:
         e.set_frame(b)
         e.set_domains(doms)
         want, _ = e.search(rngs)
