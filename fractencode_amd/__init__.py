@@ -44,6 +44,9 @@ FORM_DOT2, FORM_DIRECT, FORM_FOURIER, FORM_SEA, FORM_SEA_MFMA, FORM_SAMPLED = 0,
 FORM_NAMES = {FORM_DOT2: "dot2", FORM_DIRECT: "direct", FORM_FOURIER: "fourier", FORM_SEA: "sea",
               FORM_SEA_MFMA: "sea_mfma", FORM_SAMPLED: "sampled"}
 FLAG_TIMING = 1
+# alternative exact forms (ABI 6; the product build refuses the old FRAC_MFMA_DFT / FRAC_SEA_TILED /
+# FRAC_DECODE_UNFUSED environment knobs)
+FLAG_DIRECT_FORM, FLAG_SEA_PER_RANGE, FLAG_DECODE_STEPWISE = 2, 4, 8
 
 # Frac::TransformType (image/transform.h:16-25)
 TRANSFORM_NAMES = ("Id", "Rotate_90", "Rotate_180", "Rotate_270", "Flip", "Flip_Rotate_90", "Flip_Rotate_180",
@@ -77,18 +80,40 @@ class FracError(RuntimeError):
 _lib = None
 
 
+# The product compile line (__graft_entry__.build): part of the source id, so a change of flags or
+# of the ROCm toolchain rebuilds the library and re-keys the PMC measurements like a source change.
+# -amdgpu-mfma-vgpr-form: MFMA accumulators in VGPRs (gfx950 has one unified register file), so the
+# integer epilogue reads them without v_accvgpr_read copies.
+HIPCC_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-Wall",
+               "-mllvm", "-amdgpu-mfma-vgpr-form"]
+SOURCE_EXTS = (".hip", ".h", ".cuh")
+
+
+def _rocm_version() -> str:
+    try:
+        with open("/opt/rocm/.info/version") as f:
+            return f.read().strip()
+    except OSError:
+        return "unknown"
+
+
 def source_id() -> str:
-    """16 hex digits identifying the library's sources (csrc/, include/fracenc.h): the key under
-    which profiles/ records PMC measurements, so a measurement of another build is never reused."""
+    """16 hex digits identifying the library's sources (the .hip / .h files of csrc/ and
+    include/fracenc.h), its compile flags and the ROCm version: the key under which profiles/ records
+    PMC measurements, so a measurement of another build is never reused."""
     import hashlib
 
     h = hashlib.sha256()
     csrc = os.path.join(HERE, "csrc")
     for name in sorted(os.listdir(csrc)):
-        with open(os.path.join(csrc, name), "rb") as f:
+        path = os.path.join(csrc, name)
+        if not (os.path.isfile(path) and name.endswith(SOURCE_EXTS)):
+            continue
+        with open(path, "rb") as f:
             h.update(name.encode() + b"\0" + f.read())
     with open(os.path.join(os.path.dirname(HERE), "include", "fracenc.h"), "rb") as f:
         h.update(f.read())
+    h.update(("\0".join(HIPCC_FLAGS) + "\0rocm " + _rocm_version()).encode())
     return h.hexdigest()[:16]
 
 
@@ -221,9 +246,12 @@ class Engine:
     """
 
     def __init__(self, device: int = 0, transforms: int = 4, use_classifier: bool = False,
-                 rms_threshold: float = 0.0, s_max: float = -1.0, engine: int = ENGINE_AUTO, timing: bool = False):
+                 rms_threshold: float = 0.0, s_max: float = -1.0, engine: int = ENGINE_AUTO, timing: bool = False,
+                 flags: int = 0):
+        """flags: FLAG_DIRECT_FORM / FLAG_SEA_PER_RANGE / FLAG_DECODE_STEPWISE select an alternative
+        exact form (the same records from other kernels: cross-checks)."""
         self._p = FracParams(transforms, int(use_classifier), rms_threshold, s_max, engine,
-                             FLAG_TIMING if timing else 0)
+                             (FLAG_TIMING if timing else 0) | flags)
         self._ctx = lib().frac_create(device, C.byref(self._p))
         if not self._ctx:
             raise FracError("frac_create failed: " + last_error())
@@ -252,7 +280,8 @@ class Engine:
         if rc != 0:
             raise FracError(f"rc={rc}: {last_error(self._ctx)}")
 
-    def set_params(self, transforms=None, use_classifier=None, rms_threshold=None, s_max=None, engine=None):
+    def set_params(self, transforms=None, use_classifier=None, rms_threshold=None, s_max=None, engine=None,
+                   flags=None):
         if transforms is not None:
             self._p.transforms = transforms
         if use_classifier is not None:
@@ -263,6 +292,8 @@ class Engine:
             self._p.s_max = s_max
         if engine is not None:
             self._p.engine = engine
+        if flags is not None:
+            self._p.flags = (self._p.flags & FLAG_TIMING) | flags
         self._check(lib().frac_set_params(self._ctx, C.byref(self._p)))
 
     def set_frame(self, plane) -> None:

@@ -350,6 +350,35 @@ int check_params(const frac_params* p, std::string& msg)
         msg = "unknown engine";
         return FRAC_E_INVALID;
     }
+    if (p->flags & ~(FRAC_FLAG_TIMING | FRAC_FLAG_DIRECT_FORM | FRAC_FLAG_SEA_PER_RANGE | FRAC_FLAG_DECODE_STEPWISE)) {
+        msg = "unknown flag bits";
+        return FRAC_E_INVALID;
+    }
+    return FRAC_OK;
+}
+
+// The A/B knobs of the tuning build.  A product build compiles only the shipped forms (the
+// alternative exact forms are frac_params flags), so it refuses a run with any of these set rather
+// than silently running the default: encode(), the C++ EncodingEngineCore and the reference-side
+// binding cannot be steered into an A/B form by the environment.
+constexpr const char* kAbKnobs[] = {"FRAC_MFMA_VARIANT", "FRAC_MFMA_DFT", "FRAC_DFT_WGS", "FRAC_XCD_ORDER",
+                                    "FRAC_SEA_TILED", "FRAC_DECODE_UNFUSED"};
+
+// the knob's value in a tuning build; nullptr in a product build (check_ab_knobs refused it)
+inline const char* ab_knob(const char* name) { return kTuningBuild ? getenv(name) : nullptr; }
+
+int check_ab_knobs(std::string& msg)
+{
+    if (kTuningBuild)
+        return FRAC_OK;
+    for (const char* k : kAbKnobs) {
+        const char* v = getenv(k);
+        if (v && *v) {
+            msg = std::string(k) + "=" + v + ": A/B knobs exist only in a -DFRAC_TUNING build (tools/build_tuning.py); "
+                                             "the alternative exact forms are frac_params flags";
+            return FRAC_E_INVALID;
+        }
+    }
     return FRAC_OK;
 }
 
@@ -489,7 +518,7 @@ int device_buckets(frac_ctx* c, int nb, uint32_t* dfirst, uint32_t* rfirst)
 }
 
 inline int mfma_variant(frac_ctx* c, int& var);
-inline bool mfma_dft_enabled();
+inline bool mfma_dft_enabled(const frac_ctx* c);
 // the Fourier search variants that run 4-wave workgroups (and read m_work): 1, 3 and the odd
 // ablations below 200; every other variant runs 8-wave workgroups on m8_work
 // the variants that run search_dft in 4-wave workgroups over the 4-block work lists: 1, 3 and the
@@ -570,11 +599,11 @@ struct SampleBox {
 // for an nw×nh range: the metric points and/or the fit points, after the sampler's edge clamp
 SampleBox sample_box(int t, int Sw, int Sh, int nw, int nh, bool metric, bool fit)
 {
-    static const int lutv[8][8] = {{1, 0, 0, 0, 0, 1, 0, 0},  {0, 1, 0, 0, -1, 0, 1, 0}, {-1, 0, 1, 0, 0, -1, 0, 1},
-                                   {0, -1, 0, 1, 1, 0, 0, 0}, {1, 0, 0, 0, 0, -1, 0, 1}, {0, 1, 0, 0, 1, 0, 0, 0},
-                                   {-1, 0, 1, 0, 0, 1, 0, 0}, {0, -1, 0, 1, -1, 0, 1, 0}};
+    // the sampler's own table (fracenc_common.h lut(), which gen_sample reads), so the refusal and
+    // the decode check cannot drift from the samples the kernels take
+    const Aff L = lut(t);
+    const int a[8] = {L.a0, L.a1, L.a2, L.a3, L.a4, L.a5, L.a6, L.a7};
     SampleBox b;
-    const int* a = lutv[t];
     auto add = [&](int lx, int ly) {
         if (lx == Sw - 1)
             --lx;
@@ -767,10 +796,12 @@ int prepare(frac_ctx* c)
                 : c->p.engine == FRAC_ENGINE_VALU          ? FRAC_ENGINE_VALU
                 : c->p.engine == FRAC_ENGINE_SEA && n <= 8 ? FRAC_ENGINE_SEA
                                                            : FRAC_ENGINE_MFMA;
-    // SEA, n = 8, T = 4: the tiled form (FRAC_SEA_TILED=0 keeps the per-range form, A/B knob)
+    // SEA, n = 8, T = 4: the tiled form (FRAC_FLAG_SEA_PER_RANGE keeps the per-range form; in a
+    // tuning build also FRAC_SEA_TILED=0)
     {
-        const char* st = getenv("FRAC_SEA_TILED");
-        c->tp = c->engine == FRAC_ENGINE_SEA && !c->virt && n == 8 && T == 4 && (st ? atoi(st) != 0 : true);
+        const char* st = ab_knob("FRAC_SEA_TILED");
+        c->tp = c->engine == FRAC_ENGINE_SEA && !c->virt && n == 8 && T == 4 &&
+                !(c->p.flags & FRAC_FLAG_SEA_PER_RANGE) && (st ? atoi(st) != 0 : true);
     }
     if (c->tp) {
         if (nb > kTpMaxBuckets)
@@ -937,7 +968,7 @@ int prepare(frac_ctx* c)
                     e = inv[e / bpw] * bpw + e % bpw;
             }
         };
-        const bool fourier = n == 8 && (T == 4 || T == 8) && !c->virt && mfma_dft_enabled();
+        const bool fourier = n == 8 && (T == 4 || T == 8) && !c->virt && mfma_dft_enabled(c);
         c->dft_copies = fourier && T == 8 ? 2u : 1u;
         int var = 0;
         FRAC_TRY(mfma_variant(c, var));
@@ -953,11 +984,11 @@ int prepare(frac_ctx* c)
         }
         if (n == 8 && !c->virt && (T == 4 || c->dft_copies == 2)) {
             // FRAC_DFT_WGS (tuning knob): target workgroup count of the Fourier search
-            const char* tw = getenv("FRAC_DFT_WGS");
+            const char* tw = ab_knob("FRAC_DFT_WGS");
             c->m8_bpw = dft_bpw(dft_variant(var));
             const size_t wgs = tw ? (size_t)std::max(1, atoi(tw)) : 8192 / c->m8_bpw * 4;
             // FRAC_XCD_ORDER (tuning knob): 0 = work items in (block group, split) order
-            const char* xo = getenv("FRAC_XCD_ORDER");
+            const char* xo = ab_knob("FRAC_XCD_ORDER");
             build_work(c->m8_bpw, wgs, c->m8_work, c->m8_blk_ptr, c->m8_blk_ent, xo ? atoi(xo) != 0 : true);
         }
         else {
@@ -1128,7 +1159,7 @@ void launch_search_mfma_v(frac_ctx* c, const MfmaSearchArgs& a)
 //                ablations 9, 17, 41, 73, 105, 65 (four-wave) and 201..207 (eight-wave)
 inline int mfma_variant(frac_ctx* c, int& var)
 {
-    const char* v = getenv("FRAC_MFMA_VARIANT");
+    const char* v = ab_knob("FRAC_MFMA_VARIANT");
     var = kDefaultMfmaVariant;
     if (!v || !*v)
         return FRAC_OK;
@@ -1157,6 +1188,10 @@ int launch_search_mfma(frac_ctx* c, const MfmaSearchArgs& a)
 {
     int var = 0;
     FRAC_TRY(mfma_variant(c, var));
+#ifndef FRAC_TUNING
+    (void)var; // the product build: the shipped schedule only
+    launch_search_mfma_v<N, T, kDefaultMfmaVariant>(c, a);
+#else
     switch (var) {
     case 0: launch_search_mfma_v<N, T, 0>(c, a); break;
     case 1: launch_search_mfma_v<N, T, 1>(c, a); break;
@@ -1172,20 +1207,21 @@ int launch_search_mfma(frac_ctx* c, const MfmaSearchArgs& a)
     case 98: launch_search_mfma_v<N, T, 98>(c, a); break;
     case 128: launch_search_mfma_v<N, T, 128>(c, a); break; // minimum over transforms first
     case 130: launch_search_mfma_v<N, T, 130>(c, a); break;
-#ifdef FRAC_TUNING
     case 8: launch_search_mfma_v<N, T, 8>(c, a); break;   // ablation: 1-value epilogue
     case 16: launch_search_mfma_v<N, T, 16>(c, a); break; // ablation: no MFMA
-#endif
     default: launch_search_mfma_v<N, T, kDefaultMfmaVariant>(c, a); break;
     }
+#endif
     return FRAC_OK;
 }
 
-// FRAC_MFMA_DFT (tuning knob, read per run): 0 selects the direct n=8, T=4 MFMA search
-// instead of the rotation-group Fourier form (fracenc_dft.hip)
-inline bool mfma_dft_enabled()
+// FRAC_FLAG_DIRECT_FORM (and, in a tuning build, FRAC_MFMA_DFT=0): the direct MFMA search for
+// ratio-2 n = 8 instead of the rotation-group Fourier form (fracenc_dft.hip)
+inline bool mfma_dft_enabled(const frac_ctx* c)
 {
-    const char* v = getenv("FRAC_MFMA_DFT");
+    if (c->p.flags & FRAC_FLAG_DIRECT_FORM)
+        return false;
+    const char* v = ab_knob("FRAC_MFMA_DFT");
     return v ? atoi(v) != 0 : true;
 }
 
@@ -1193,7 +1229,7 @@ inline bool mfma_dft_enabled()
 // best_key / fb_count resets to it then
 inline bool dft_route(const frac_ctx* c)
 {
-    return (c->Teff == 4 || c->dft_copies == 2) && !c->virt && mfma_dft_enabled();
+    return (c->Teff == 4 || c->dft_copies == 2) && !c->virt && mfma_dft_enabled(c);
 }
 
 // n = 8, T = 4: the C4-Fourier search (6 MFMAs per 32×32 tile pair instead of 16).  inits: reset
@@ -1291,8 +1327,19 @@ inline int launch_dft(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool i
         const unsigned nwg = (unsigned)work.size();
         const bool hits = c->hitH > 0;
         constexpr uint32_t W8 = kDftBlocksPerWG;
+#ifndef FRAC_TUNING
+        // the product build: the shipped form only (variant 35, kDftDefaultVariant) — the six-MFMA
+        // form with the guarded constant-folded epilogue, the unrolled chunk and buffer_load … lds stages
+        static_assert(kDftDefaultVariant == 35, "the product build's Fourier search is variant 35");
+        (void)four;
+        constexpr int V35 = 1 | kDftChain | kDft6 | kDftFast6 | kDftUnroll | kDftBufDma;
+        if (hits)
+            search_dft<true, V35, W8><<<nwg, 64 * W8, 0, c->stream>>>(da);
+        else
+            search_dft<false, V35, W8><<<nwg, 64 * W8, 0, c->stream>>>(da);
+#else // the tuning build: every A/B variant and ablation
         if (!four && var >= 200) {
-#ifdef FRAC_TUNING // ablations of the 8-wave exact form (wrong results by design)
+            // ablations of the 8-wave exact form (wrong results by design)
             switch (var) {
             case 201: search_dft<false, 9, W8><<<nwg, 64 * W8, 0, c->stream>>>(da); break;   // MFMA-only
             case 202: search_dft<false, 73, W8><<<nwg, 64 * W8, 0, c->stream>>>(da); break;  // MFMA-only, no DMA/bar
@@ -1324,7 +1371,6 @@ inline int launch_dft(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool i
                 break;
             default: search_dft<false, 65, W8><<<nwg, 64 * W8, 0, c->stream>>>(da); break;  // full, no DMA/bar
             }
-#endif
         } else if (form == 6 && var == 23) { // the six-MFMA form, two range blocks per wave (search_dft2)
             if (hits)
                 search_dft2<true, true><<<nwg, 256, 0, c->stream>>>(da);
@@ -1424,7 +1470,7 @@ inline int launch_dft(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool i
             else
                 search_dft<false, 0><<<nwg, 256, 0, c->stream>>>(da);
         } else {
-#ifdef FRAC_TUNING // ablations of the 4-wave exact form (wrong results by design)
+            // ablations of the 4-wave exact form (wrong results by design)
             switch (var) {
             case 9: search_dft<false, 9><<<nwg, 256, 0, c->stream>>>(da); break;     // MFMA-only
             case 17: search_dft<false, 17><<<nwg, 256, 0, c->stream>>>(da); break;   // VALU-only
@@ -1434,8 +1480,8 @@ inline int launch_dft(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool i
             case 65: search_dft<false, 65><<<nwg, 256, 0, c->stream>>>(da); break;   // full, no DMA/barrier
             default: search_dft<false, 1><<<nwg, 256, 0, c->stream>>>(da); break;
             }
-#endif
         }
+#endif
     }
     if (c->p.flags & FRAC_FLAG_TIMING)
         FRAC_TRY(mark_event(c, 2));
@@ -1738,6 +1784,11 @@ int launch_tp(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool timing)
     FRAC_HIP(c, c->d_rstat.ensure(std::max<size_t>(nr, 1)));
     v.rstat = c->d_rstat.ptr;
     c->fit_rstat = true;
+    // resolve_dft<true> (SORTED) keeps every tie of the ΣD4-ordered chunks but does not merge T = 8's
+    // flipped copies (that is the !SORTED path): the tiled form exists for T = 4 only (prepare)
+    v.flip_slots = 0;
+    if (c->dft_copies != 1 || c->p.transforms != 4)
+        return c->fail(FRAC_E_STATE, "SEA tiled form: T = 4 only (resolve_dft<true> has no flipped copies)");
     resolve_dft<true><<<std::max(1u, (v.nslots + 3) / 4), 256, 0, c->stream>>>(v);
     return FRAC_OK;
 }
@@ -1935,7 +1986,7 @@ int launch_all(frac_ctx* c)
     // the Fourier path and the SEA engine's tiled form build the pool in their fused domain pass
     // (dft_domain_build)
     const bool fused_pool = N == 8 && !c->virt &&
-                            ((use_mfma && (c->p.transforms == 4 || c->dft_copies == 2) && mfma_dft_enabled()) ||
+                            ((use_mfma && (c->p.transforms == 4 || c->dft_copies == 2) && mfma_dft_enabled(c)) ||
                              (c->engine == FRAC_ENGINE_SEA && !c->all_fallback && c->tp));
     const GenArgs g = gen_args(c, dtgt, tstride);
     if (P && c->virt) // the sampled form: one row per (domain, transform), fracenc_gen.hip
@@ -2346,10 +2397,15 @@ int frac_run(frac_ctx* c)
         return FRAC_E_INVALID;
     FRAC_HIP(c, hipSetDevice(c->device));
     {
+        std::string msg;
+        if (check_ab_knobs(msg) != FRAC_OK)
+            return c->fail(FRAC_E_INVALID, msg);
+    }
+    {
         // the work lists prepare() builds depend on the A/B knobs: a change re-prepares
         int var = 0;
         FRAC_TRY(mfma_variant(c, var));
-        const int knobs = var * 2 + (mfma_dft_enabled() ? 1 : 0);
+        const int knobs = var * 2 + (mfma_dft_enabled(c) ? 1 : 0);
         if (knobs != c->prep_knobs)
             c->dirty = true;
         c->prep_knobs = knobs;
@@ -2869,7 +2925,12 @@ static int decode_impl(frac_ctx* c, const frac_encode_item* d_items, size_t n, u
 {
     if (!plane || w == 0 || h == 0)
         return c->fail(FRAC_E_INVALID, "decode: invalid plane");
-    if (fused && getenv("FRAC_DECODE_UNFUSED") == nullptr)
+    {
+        std::string msg;
+        if (check_ab_knobs(msg) != FRAC_OK)
+            return c->fail(FRAC_E_INVALID, msg);
+    }
+    if (fused &&!(c->p.flags & FRAC_FLAG_DECODE_STEPWISE) && ab_knob("FRAC_DECODE_UNFUSED") == nullptr)
         return decode_fused_impl(c, d_items, n, w, h, max_iter < 0 ? 300 : max_iter, eps, plane, iterations, rms);
     const uint32_t stride = (w + 63u) & ~63u;
     const size_t bytes = (size_t)stride * (h + 1);

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define FRAC_ABI_VERSION 5
+#define FRAC_ABI_VERSION 6
 
 /* error codes */
 #define FRAC_OK 0
@@ -49,6 +49,13 @@ extern "C" {
 
 /* flags (frac_params.flags) */
 #define FRAC_FLAG_TIMING 1u     /* record per-kernel device time with HIP events         */
+/* Alternative exact forms (same records, other kernels; for cross-checks, ABI 6).  They replace
+ * the FRAC_MFMA_DFT / FRAC_SEA_TILED / FRAC_DECODE_UNFUSED environment knobs of ABI 5, which a
+ * product build now refuses (FRAC_E_INVALID) like every other A/B knob. */
+#define FRAC_FLAG_DIRECT_FORM 2u    /* MFMA engine, ratio-2 n = 8 and 16: the direct form (T GEMMs of K = n²)  */
+                                    /* instead of the rotation-group Fourier form                               */
+#define FRAC_FLAG_SEA_PER_RANGE 4u  /* SEA engine, n = 8, T = 4: the per-range form instead of the tiled one   */
+#define FRAC_FLAG_DECODE_STEPWISE 8u /* decoder: one apply + one rms launch per iteration (no fused loop)       */
 
 /* == Frac2::UniformGridItem (image/partition2.hpp:93-99): GridItemBase{origin, size}
  *    + GridItemData{bb_classifierBin}; 20 bytes. category -1 = not classified

@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol():
     assert len(names) >= 20
     missing = [n for n in names if not hasattr(lib, n)]
     assert not missing, missing
-    assert lib.frac_abi_version() == 5
+    assert lib.frac_abi_version() == 6
 
 
 def test_library_carries_the_source_id():
@@ -157,3 +157,9 @@ def test_product_library_has_no_ablation_kernels():
     assert dft and mfma
     assert all(int(v) & (8 | 16 | 32 | 64 | 256 | 512) == 0 for v in dft), sorted(set(dft))
     assert all(int(v) & (8 | 16) == 0 for v in mfma), sorted(set(mfma))
+    # and no A/B variant either (round 4): the Fourier search as shipped (variant 35 =
+    # 1|kDftChain|kDft6|kDftFast6|kDftUnroll|kDftBufDma) and the SEA tiled form's exact six-MFMA
+    # tile (1|kDftChain|kDft6); the direct form's shipped schedule (130)
+    assert set(map(int, dft)) == {123905, 9217}, sorted(set(dft))
+    assert set(map(int, mfma)) == {130}, sorted(set(mfma))
+    assert not _kernel_instances(r"fracenc::(search_dft2)<"), "the two-block A/B form is tuning-only"

@@ -130,7 +130,7 @@ def test_decode_rejects_bad_items():
 
 
 @pytest.mark.parametrize("name", ["lenna_t4", "lenna_n4", "crop64_n2_t8"])
-def test_fused_and_stepwise_decoders_agree(monkeypatch, name):
+def test_fused_and_stepwise_decoders_agree(name):
     # the fused decoder (exact coverage: rms accumulated while writing, buffer swap, device-side
     # convergence test) against the step-by-step form, including bounded iteration counts
     rec, meta = golden(name)
@@ -138,12 +138,8 @@ def test_fused_and_stepwise_decoders_agree(monkeypatch, name):
     H, W = p.shape
     items = encode_items(rec, meta["tgt"])
     outs = []
-    for unfused in ("", "1"):
-        if unfused:
-            monkeypatch.setenv("FRAC_DECODE_UNFUSED", "1")
-        else:
-            monkeypatch.delenv("FRAC_DECODE_UNFUSED", raising=False)
-        with F.Engine(0, 4) as e:
+    for fl in (0, F.FLAG_DECODE_STEPWISE):
+        with F.Engine(0, 4, flags=fl) as e:
             outs.append([e.decode(items, W, H, max_iter=m) for m in (-1, 0, 1, 2, 9)])
     for (a, ia, ra), (b, ib, rb) in zip(*outs):
         assert (ia, ra) == (ib, rb)

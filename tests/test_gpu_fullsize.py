@@ -200,7 +200,7 @@ def test_c5_rgb_4096_three_planes_quantized_decode(oracle):
 C5_DECODE_ITERS = 20
 
 
-def _engines_identical(p, tag, T=4, monkeypatch=None):
+def _engines_identical(p, tag, T=4):
     """The VALU engine (v_dot2, integer — the north-star formulation) and the MFMA engine (f16 Fourier
     form) are independent implementations of the same search: their records must be byte-identical
     for every range of the frame (the SEA engine's too: its bound only skips candidates; at T = 8 the
@@ -210,11 +210,9 @@ def _engines_identical(p, tag, T=4, monkeypatch=None):
     rngs = F.create_uniform_grid(W, H, 8, 8)
     outs = {}
     forms = {}
-    third = ("sea", F.ENGINE_SEA, "1") if T == 4 else ("direct", F.ENGINE_MFMA, "0")
-    for name, eng, dft in (("mfma", F.ENGINE_MFMA, "1"), ("valu", F.ENGINE_VALU, "1"), third):
-        if monkeypatch is not None:
-            monkeypatch.setenv("FRAC_MFMA_DFT", dft)
-        with F.Engine(0, T, False, 0.0, -1.0, eng) as e:
+    third = ("sea", F.ENGINE_SEA, 0) if T == 4 else ("direct", F.ENGINE_MFMA, F.FLAG_DIRECT_FORM)
+    for name, eng, fl in (("mfma", F.ENGINE_MFMA, 0), ("valu", F.ENGINE_VALU, 0), third):
+        with F.Engine(0, T, False, 0.0, -1.0, eng, flags=fl) as e:
             e.set_frame(p)
             e.set_domains(doms)
             outs[name], st = e.search(rngs)
@@ -234,7 +232,7 @@ def test_c5_y_all_ranges_valu_equals_mfma():
     _engines_identical(plane("c5_y"), "C5 Y")
 
 
-def test_c3_t8_all_ranges_valu_equals_mfma(monkeypatch):
+def test_c3_t8_all_ranges_valu_equals_mfma():
     # all 8 transforms at C3 size: the Fourier form with the flipped range copies, the exhaustive VALU
     # engine and the direct MFMA form agree on every one of the 262,144 records
-    _engines_identical(plane("s1_4096"), "C3 T=8", T=8, monkeypatch=monkeypatch)
+    _engines_identical(plane("s1_4096"), "C3 T=8", T=8)

@@ -24,11 +24,11 @@ def as_oracle_fields(out):
             "t": out["transform"], "dist": out["distance"], "s": out["contrast"], "o": out["brightness"]}
 
 
-def run_engine(p, meta, engine, tgt=None, ranges_idx=None):
+def run_engine(p, meta, engine, tgt=None, ranges_idx=None, flags=0):
     doms, rngs = make_grids(F.create_uniform_grid, F.preclassify, p, meta)
     if ranges_idx is not None:
         rngs = rngs[ranges_idx]
-    with F.Engine(0, meta["T"], meta["cls"], meta["thr"], meta["smax"], engine) as e:
+    with F.Engine(0, meta["T"], meta["cls"], meta["thr"], meta["smax"], engine, flags=flags) as e:
         e.set_frame(p)
         e.set_domains(doms)
         return e.search(rngs)
@@ -259,26 +259,25 @@ DFT_CASES = [
 ]
 
 
-@pytest.mark.parametrize("dft", ["1", "0", "1/20", "1/21", "1/23", "1/26"])
+@pytest.mark.parametrize("form", ["fourier", "direct"])
 @pytest.mark.parametrize("case", range(len(DFT_CASES)))
-def test_mfma_fourier_and_direct_match_oracle(oracle, monkeypatch, case, dft):
-    # "1/20": the five-MFMA Fourier form (FRAC_MFMA_VARIANT=20)
-    dft, _, var = dft.partition("/")
-    monkeypatch.setenv("FRAC_MFMA_DFT", dft)
-    if var:
-        monkeypatch.setenv("FRAC_MFMA_VARIANT", var)
+def test_mfma_fourier_and_direct_match_oracle(oracle, case, form):
+    # the shipped Fourier form (six MFMAs, guarded constant-folded epilogue) and the direct form
+    # (FRAC_FLAG_DIRECT_FORM); the A/B variants of the tuning build are not in the product library
+    flags = F.FLAG_DIRECT_FORM if form == "direct" else 0
     W, H, cls, thr, smax, kind = DFT_CASES[case]
     rng = np.random.default_rng(2000 + case)
     p = _random_plane(rng, W, H, kind)
     meta = dict(src=16, tgt=8, T=4, cls=cls, thr=thr, smax=smax)
-    out, st = run_engine(p, meta, F.ENGINE_MFMA)
+    out, st = run_engine(p, meta, F.ENGINE_MFMA, flags=flags)
+    assert st["search_form"] == (F.FORM_DIRECT if flags else F.FORM_FOURIER)
     doms = oracle.uniform_grid(W, H, 16, 8)
     rngs = oracle.uniform_grid(W, H, 8, 8)
     if cls:
         doms = oracle.classify(p, doms)
         rngs = oracle.classify(p, rngs)
     want, rej, _ = oracle.estimate(p, doms, rngs, T=4, thr=thr, smax=smax, use_classifier=cls)
-    assert_same(out, {k: want[k] for k in FIELDS}, f"dft={dft} case {DFT_CASES[case]}")
+    assert_same(out, {k: want[k] for k in FIELDS}, f"{form} case {DFT_CASES[case]}")
     assert st["rejected_mappings"] == rej
 
 
@@ -302,14 +301,14 @@ def _extreme_plane(rng, S, kind):
     return out.astype(np.uint8)
 
 
-@pytest.mark.parametrize("var", ["20", "21", "22", "23", "26", "35"])
+@pytest.mark.parametrize("form", ["fourier", "direct"])
 @pytest.mark.parametrize("kind", ["binary", "blocks8", "blocks2", "orbits"])
-def test_five_mfma_form_at_operand_extremes(monkeypatch, kind, var):
-    """The five-MFMA Fourier form (FRAC_MFMA_VARIANT=20) has the tightest exactness margins (2Pr /
-    2Pi partial sums up to 33.3M < 2^25, P up to 2^24), the six-MFMA forms' guarded fast path
-    (26, 35: P from −Σb²/2 where 2·R6·D6 + Σb² < 2^24) the tightest guard: on 0/255 frames that
-    drive every operand to its bound they return the exhaustive VALU engine's records, with and
-    without the classifier."""
+def test_mfma_forms_at_operand_extremes(kind, form):
+    """The six-MFMA Fourier form's guarded fast path (P from −Σb²/2 where 2·R6·D6 + Σb² < 2^24) has
+    the tightest exactness margin, 2Pr / 2Pi the next (partial sums up to 33.3M < 2^25): on 0/255
+    frames that drive every operand to its bound the shipped form and the direct form
+    (FRAC_FLAG_DIRECT_FORM) return the exhaustive VALU engine's records, with and without the
+    classifier."""
     rng = np.random.default_rng(zlib.crc32(kind.encode()))  # reproducible across processes
     S = 256
     p = _extreme_plane(rng, S, kind)
@@ -319,19 +318,17 @@ def test_five_mfma_form_at_operand_extremes(monkeypatch, kind, var):
             e.set_frame(p)
             e.set_domains(doms)
             want, wst = e.search(rngs)
-        monkeypatch.setenv("FRAC_MFMA_DFT", "1")
-        monkeypatch.setenv("FRAC_MFMA_VARIANT", var)
-        with F.Engine(0, 4, cls, 0.0, -1.0, F.ENGINE_MFMA) as e:
+        with F.Engine(0, 4, cls, 0.0, -1.0, F.ENGINE_MFMA,
+                      flags=F.FLAG_DIRECT_FORM if form == "direct" else 0) as e:
             e.set_frame(p)
             e.set_domains(doms)
             out, st = e.search(rngs)
-        monkeypatch.delenv("FRAC_MFMA_VARIANT")
         assert out.tobytes() == want.tobytes(), f"{kind} cls={cls}"
         assert st["rejected_mappings"] == wst["rejected_mappings"]
 
 
 @pytest.mark.parametrize("kind", ["binary", "blocks8", "orbits", "noise"])
-def test_t8_fourier_flipped_copies_at_operand_extremes(monkeypatch, kind):
+def test_t8_fourier_flipped_copies_at_operand_extremes(kind):
     """T = 8 on the Fourier path: each range block runs a second time read through Flip
     (Flip_Rotate_k = Flip ∘ Rotate_k, dft_range_prep flip_from) and resolve_dft keeps the lesser key of
     the two copies, with the copy's rotation t' as transform 4 + (−t' mod 4).  On the operand-extreme
@@ -344,10 +341,9 @@ def test_t8_fourier_flipped_copies_at_operand_extremes(monkeypatch, kind):
     doms, rngs = F.create_uniform_grid(S, S, 16, 8), F.create_uniform_grid(S, S, 8, 8)
     for cls, thr in ((False, 0.0), (True, 0.0), (False, 40.0)):
         outs = {}
-        for name, eng, dft in (("valu", F.ENGINE_VALU, "1"), ("direct", F.ENGINE_MFMA, "0"),
-                               ("fourier", F.ENGINE_MFMA, "1")):
-            monkeypatch.setenv("FRAC_MFMA_DFT", dft)
-            with F.Engine(0, 8, cls, thr, -1.0, eng) as e:
+        for name, eng, fl in (("valu", F.ENGINE_VALU, 0), ("direct", F.ENGINE_MFMA, F.FLAG_DIRECT_FORM),
+                              ("fourier", F.ENGINE_MFMA, 0)):
+            with F.Engine(0, 8, cls, thr, -1.0, eng, flags=fl) as e:
                 e.set_frame(p)
                 e.set_domains(doms)
                 outs[name], st = e.search(rngs)
@@ -359,15 +355,14 @@ def test_t8_fourier_flipped_copies_at_operand_extremes(monkeypatch, kind):
             assert (outs["fourier"]["transform"] >= 4).any(), "the flipped copies win somewhere"
 
 
-def test_fourier_direct_and_valu_agree_on_stress_frame(monkeypatch):
+def test_fourier_direct_and_valu_agree_on_stress_frame():
     """n = 8, T = 4 on a uniform-noise 1024² frame: C4-Fourier MFMA, direct MFMA and VALU
     engines give identical records."""
     from fractencode_amd.synth import uniform_noise
     p = uniform_noise(1024, 1024, 43)
     outs = []
-    for eng, dft in ((F.ENGINE_VALU, "1"), (F.ENGINE_MFMA, "0"), (F.ENGINE_MFMA, "1"), (F.ENGINE_SEA, "1")):
-        monkeypatch.setenv("FRAC_MFMA_DFT", dft)
-        with F.Engine(0, 4, False, 0.0, -1.0, eng) as e:
+    for eng, fl in ((F.ENGINE_VALU, 0), (F.ENGINE_MFMA, F.FLAG_DIRECT_FORM), (F.ENGINE_MFMA, 0), (F.ENGINE_SEA, 0)):
+        with F.Engine(0, 4, False, 0.0, -1.0, eng, flags=fl) as e:
             e.set_frame(p)
             e.set_domains(F.create_uniform_grid(1024, 1024, 16, 8))
             out, st = e.search(F.create_uniform_grid(1024, 1024, 8, 8))
@@ -532,14 +527,11 @@ def test_encode_defaults_are_the_reference_cli_defaults():
     assert st["rejected_mappings"] == meta["rejected"]
 
 
-PRODUCT_VARIANTS = ("0", "1", "2", "3", "4", "5", "6", "7", "12", "20", "21", "22", "23", "24", "26", "27", "28", "32",
-                    "33", "34", "35", "36", "64", "96", "98", "128", "130")
-
-
-@pytest.mark.parametrize("n,T,dft", [(8, 4, "0"), (4, 4, "0"), (8, 8, "0"), (8, 4, "1"), (8, 8, "1")])
-def test_every_product_variant_gives_the_same_records(monkeypatch, n, T, dft):
-    # FRAC_MFMA_VARIANT is an A/B knob: every value a product build accepts must give the records of
-    # the exhaustive VALU engine (the launch switch and the resolve's entry layout must agree)
+@pytest.mark.parametrize("n,T", [(8, 4), (4, 4), (8, 8), (16, 4)])
+def test_every_product_form_gives_the_same_records(monkeypatch, n, T):
+    # the product library holds the shipped forms only: the default (Fourier for ratio-2 n = 8) and
+    # FRAC_FLAG_DIRECT_FORM must give the records of the exhaustive VALU engine, and an A/B knob of
+    # the tuning build fails the run instead of selecting anything
     from fractencode_amd.synth import value_noise
     S = 256
     p = value_noise(S, S, 77)
@@ -548,14 +540,20 @@ def test_every_product_variant_gives_the_same_records(monkeypatch, n, T, dft):
         e.set_frame(p)
         e.set_domains(doms)
         want, _ = e.search(rngs)
-    monkeypatch.setenv("FRAC_MFMA_DFT", dft)
-    for v in PRODUCT_VARIANTS:
-        monkeypatch.setenv("FRAC_MFMA_VARIANT", v)
-        with F.Engine(0, T, False, 0.0, -1.0, F.ENGINE_MFMA) as e:
+    for fl in (0, F.FLAG_DIRECT_FORM):
+        with F.Engine(0, T, False, 0.0, -1.0, F.ENGINE_MFMA, flags=fl) as e:
             e.set_frame(p)
             e.set_domains(doms)
             out, _ = e.search(rngs)
-        assert out.tobytes() == want.tobytes(), f"variant {v} (n={n}, T={T}, dft={dft})"
+        assert out.tobytes() == want.tobytes(), f"flags {fl} (n={n}, T={T})"
+    for knob, val in (("FRAC_MFMA_VARIANT", "21"), ("FRAC_MFMA_DFT", "0"), ("FRAC_DFT_WGS", "2048")):
+        monkeypatch.setenv(knob, val)
+        with F.Engine(0, T, False, 0.0, -1.0, F.ENGINE_MFMA) as e:
+            e.set_frame(p)
+            e.set_domains(doms)
+            with pytest.raises(F.FracError, match="FRAC_TUNING"):
+                e.search(rngs)
+        monkeypatch.delenv(knob)
 
 
 # --- rectangular items (Size32u grids) and grid validation ---------------------------------------

@@ -22,13 +22,17 @@ sys.path.insert(0, os.path.join(ROOT, "tools"))
 import lds_dma_check  # noqa: E402
 
 CSRC = os.path.join(ROOT, "fractencode_amd", "csrc")
-FAMILIES = ("search_dft<", "search_dft2<", "search_mfma<", "search_mfma16<")
-# one instance per family, as the product library instantiates them (the shipped C3 search first)
+FAMILIES = ("search_dft<", "search_mfma<", "search_mfma16<")
+# one instance per family, as the product library instantiates them: the shipped C3 search first
+# (variant 35 = 1|kDftChain|kDft6|kDftFast6|kDftUnroll|kDftBufDma: buffer_load … lds stages and the
+# zero-tail reads of the guarded epilogue), then the SEA tiled form's exact six-MFMA tile (9217,
+# global_load_lds stages) and the direct form's shipped schedule (130)
 INSTANCES = {
-    "search_dft": "template __global__ void fracenc::search_dft<false, 9217, 8u, 4u, false>(fracenc::DftArgs);",
-    "search_dft_hits": "template __global__ void fracenc::search_dft<true, 9217, 8u, 4u, false>(fracenc::DftArgs);",
-    "search_dft2": "template __global__ void fracenc::search_dft2<false, true>(fracenc::DftArgs);",
-    "search_mfma": "template __global__ void fracenc::search_mfma<4, 4, false, 2>(fracenc::MfmaSearchArgs);",
+    "search_dft35": "template __global__ void fracenc::search_dft<false, 123905, 8u, 4u, false>(fracenc::DftArgs);",
+    "search_dft35_hits": "template __global__ void fracenc::search_dft<true, 123905, 8u, 4u, false>(fracenc::DftArgs);",
+    "search_dft": "template __global__ void fracenc::search_dft<false, 9217, 8u, 4u, true>(fracenc::DftArgs);",
+    "search_dft_hits": "template __global__ void fracenc::search_dft<true, 9217, 8u, 4u, true>(fracenc::DftArgs);",
+    "search_mfma": "template __global__ void fracenc::search_mfma<4, 4, false, 130>(fracenc::MfmaSearchArgs);",
     "search_mfma16": "template __global__ void fracenc::search_mfma16<4, false>(fracenc::MfmaSearchArgs);",
 }
 
@@ -42,7 +46,7 @@ def test_product_search_kernels_wait_for_their_dma_before_every_barrier():
 
 def test_every_lds_dma_kernel_in_the_library_is_guarded():
     bad, checked = lds_dma_check.check(F.PRODUCT_LIB)
-    assert len(checked) >= 100
+    assert len(checked) >= 20
     assert not bad, sorted(bad)[:5]
 
 
@@ -61,9 +65,17 @@ def _compile(tmp_path, name, plain):
 
 
 @pytest.mark.skipif(not os.path.exists("/opt/rocm/bin/hipcc"), reason="hipcc not present")
-@pytest.mark.parametrize("name", ["search_dft", "search_dft_hits", "search_mfma"])
-def test_check_flags_a_plain_barrier(tmp_path, name):
+@pytest.mark.parametrize("name", sorted(INSTANCES))
+def test_each_instance_is_guarded_compiled_alone(tmp_path, name):
     good, checked = lds_dma_check.check(_compile(tmp_path, name, plain=False))
     assert checked and not good
+
+
+# The negative control: with the barrier reduced to a plain __syncthreads() the check must flag the
+# hazard.  (The SEA tiled form's instance is left out: its chunk-entry stores before each barrier
+# happen to make the compiler emit vmcnt(0) even there, so it shows no hazard to detect.)
+@pytest.mark.skipif(not os.path.exists("/opt/rocm/bin/hipcc"), reason="hipcc not present")
+@pytest.mark.parametrize("name", ["search_dft35", "search_dft35_hits", "search_mfma"])
+def test_check_flags_a_plain_barrier(tmp_path, name):
     bad, checked = lds_dma_check.check(_compile(tmp_path, name, plain=True))
     assert checked and bad, f"{name}: the check did not see the hazard of a plain __syncthreads() stage barrier"
