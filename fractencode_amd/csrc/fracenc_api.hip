@@ -260,6 +260,14 @@ struct frac_ctx {
     DBuf<frac_encode_item> d_qt_leaves;   // the frame's leaves, in output order
     DBuf<uint32_t> d_qt_flags, d_qt_offs, d_qt_count;
     DBuf<unsigned long long> d_qt_stats; // quadtree: the levels' frac_stats counters (qt_level_stats)
+    // device-planned quadtree levels (frac_encode_quadtree, MFMA engine): the levels' plans (+1 for
+    // the count after the last), their bucket bounds, and the first level's range grid
+    DBuf<DevPlan> d_qt_plan;
+    DBuf<uint32_t> d_qt_first;
+    DBuf<frac_grid_item> d_qt_r0;
+    uint32_t qt_r0_key[3] = {0, 0, 0};
+    const DevPlan* qplan = nullptr; // set while a device-planned level launches (launch_all in plan mode)
+    uint32_t qp_nwork_cap = 0;      // its work-item bound: the search grid
     DBuf<uint8_t> d_qt_tmp;
     size_t qt_tmp_bytes = 0;
     bool qt_dvalid[5] = {false, false, false, false, false};
@@ -1143,9 +1151,9 @@ void launch_search_mfma_v(frac_ctx* c, const MfmaSearchArgs& a)
     // H = 0 (the default threshold): a hit is S16 = 0, the smallest possible error, so
     // the plain first-minimum search already finds the first hit
     if (c->hitH > 0)
-        search_mfma<N, T, true, VAR><<<(unsigned)c->m_work.size(), 256, 0, c->stream>>>(a);
+        search_mfma<N, T, true, VAR><<<a.nwork, 256, 0, c->stream>>>(a);
     else
-        search_mfma<N, T, false, VAR><<<(unsigned)c->m_work.size(), 256, 0, c->stream>>>(a);
+        search_mfma<N, T, false, VAR><<<a.nwork, 256, 0, c->stream>>>(a);
 }
 
 // FRAC_MFMA_VARIANT (A/B knob, read per run): schedule variant of the MFMA searches. Every
@@ -1232,6 +1240,13 @@ inline bool dft_route(const frac_ctx* c)
     return (c->Teff == 4 || c->dft_copies == 2) && !c->virt && mfma_dft_enabled(c);
 }
 
+// work items a search launch covers: the host-built list, or a device-planned level's bound (its
+// workgroups past DevPlan::nwork leave at once)
+inline uint32_t launch_nwork(const frac_ctx* c, const std::vector<uint4>& w)
+{
+    return c->qplan ? c->qp_nwork_cap : (uint32_t)w.size();
+}
+
 // n = 8, T = 4: the C4-Fourier search (6 MFMAs per 32×32 tile pair instead of 16).  inits: reset
 // best_key and fb_count in the preparation kernel (launch_all skipped its memsets)
 inline int launch_dft(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool inits)
@@ -1244,6 +1259,7 @@ inline int launch_dft(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool i
     d.ntiles = c->ntiles;
     d.dtiles = c->d_m_dtiles.ptr;
     d.dconst = c->d_m_dconst.ptr;
+    d.plan = c->qplan;
     FRAC_HIP(c, c->d_dft_tguard.ensure(std::max<size_t>(c->ntiles, 1)));
     FRAC_HIP(c, c->d_dft_trmax.ensure((size_t)c->ntiles + 4)); // + 4: a chunk's thresholds are one scalar load
     FRAC_HIP(c, c->d_dft_tpool.ensure(std::max<size_t>((size_t)c->ntiles * 32 * 32, 1)));
@@ -1279,6 +1295,7 @@ inline int launch_dft(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool i
     r.rfrags = c->d_m_rfrags.ptr;
     r.rconst = c->d_m_rconst.ptr;
     r.flip_from = c->dft_copies == 2 ? c->nblocks : ~0u;
+    r.plan = c->qplan;
     FRAC_HIP(c, c->d_dft_rorb.ensure(std::max<size_t>((size_t)r.nblocks * 32 * 32, 1)));
     r.rorb = c->d_dft_rorb.ptr;
     // one launch: domain tiles, range blocks and (inits) the run's resets
@@ -1290,6 +1307,8 @@ inline int launch_dft(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool i
         in.fbc = 0; // the Fourier path never runs with all_fallback
     }
     in.dblocks = (c->ntiles * 32 + 255) / 256;
+    in.plan = c->qplan;
+    in.copies = c->dft_copies;
     const unsigned pg = in.dblocks + (nbk * 32 + 255) / 256;
     if (pg || inits) {
         int32_t* trmax = f5 ? c->d_dft_trmax.ptr : nullptr;
@@ -1309,22 +1328,24 @@ inline int launch_dft(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool i
     c->flops_ran = 0;
     for (const uint4& w : work) // 8 (forms 5 / 6: 5 / 6) MFMA 32x32x16 (32768 flops each) per (block, tile)
         c->flops_ran += (uint64_t)w.y * (w.w - w.z) * (form == 5 ? 5ull : form == 6 ? 6ull : 8ull) * 32768ull;
-    if (!work.empty()) {
+    const uint32_t nwork = launch_nwork(c, work);
+    if (nwork) {
         MfmaSearchArgs a;
         a.dtiles = c->d_m_dtiles.ptr;
         a.dconst = reinterpret_cast<const uint4*>(c->d_m_dconst.ptr);
         a.rfrags = c->d_m_rfrags.ptr;
         a.rconst = c->d_m_rconst.ptr;
         a.work = four ? c->d_m_work.ptr : c->d_m8_work.ptr;
-        a.nwork = (uint32_t)work.size();
+        a.nwork = nwork;
         a.hitH = (uint32_t)std::max<int64_t>(c->hitH, 0);
         a.entries = c->d_m_entries.ptr;
+        a.plan = c->qplan;
         DftArgs da;
         da.m = a;
         da.rguard = c->d_dft_rguard.ptr;
         da.tguard = c->d_dft_tguard.ptr;
         da.trmax = c->d_dft_trmax.ptr;
-        const unsigned nwg = (unsigned)work.size();
+        const unsigned nwg = nwork;
         const bool hits = c->hitH > 0;
         constexpr uint32_t W8 = kDftBlocksPerWG;
 #ifndef FRAC_TUNING
@@ -1508,6 +1529,7 @@ inline int launch_dft(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool i
         v.flip_slots = c->dft_copies == 2 ? c->nblocks * 32u : 0u;
         v.tpool = c->d_dft_tpool.ptr;
         v.rorb = c->d_dft_rorb.ptr;
+        v.plan = c->qplan;
         FRAC_HIP(c, c->d_rstat.ensure(std::max<size_t>(nr, 1)));
         v.rstat = c->d_rstat.ptr;
         c->fit_rstat = true;
@@ -1535,6 +1557,7 @@ int launch_mfma(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool inits =
         d.ntiles = c->ntiles;
         d.dtiles = c->d_m_dtiles.ptr;
         d.dconst = c->d_m_dconst.ptr;
+        d.plan = c->qplan;
         mfma_domain_prep<N><<<(c->ntiles * 32 + 255) / 256, 256, 0, c->stream>>>(d);
     }
     if (c->nblocks) {
@@ -1547,9 +1570,12 @@ int launch_mfma(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool inits =
         r.T = T;
         r.rfrags = c->d_m_rfrags.ptr;
         r.rconst = c->d_m_rconst.ptr;
+        r.plan = c->qplan;
         const size_t threads = (size_t)c->nblocks * T * MfmaGeom<N>::KS * 64;
-        // rconst is a sum of per-pixel terms, accumulated by the transform-0 threads
-        FRAC_HIP(c, hipMemsetAsync(c->d_m_rconst.ptr, 0, (size_t)c->nblocks * 32 * sizeof(uint32_t), c->stream));
+        // rconst is a sum of per-pixel terms, accumulated by the transform-0 threads (a planned level's
+        // qt_fill_maps zeroed it)
+        if (!c->qplan)
+            FRAC_HIP(c, hipMemsetAsync(c->d_m_rconst.ptr, 0, (size_t)c->nblocks * 32 * sizeof(uint32_t), c->stream));
         mfma_range_prep<N><<<(unsigned)((threads + 255) / 256), 256, 0, c->stream>>>(r);
     }
     if (c->p.flags & FRAC_FLAG_TIMING)
@@ -1558,18 +1584,20 @@ int launch_mfma(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool inits =
     c->flops_ran = 0;
     for (const uint4& w : c->m_work) // T·KS MFMA 32x32x16 per (range block, domain tile)
         c->flops_ran += (uint64_t)w.y * (w.w - w.z) * T * MfmaGeom<N>::KS * 32768ull;
-    if (!c->m_work.empty()) {
+    const uint32_t nwork = launch_nwork(c, c->m_work);
+    if (nwork) {
         MfmaSearchArgs a;
         a.dtiles = c->d_m_dtiles.ptr;
         a.dconst = reinterpret_cast<const uint4*>(c->d_m_dconst.ptr);
         a.rfrags = c->d_m_rfrags.ptr;
         a.rconst = c->d_m_rconst.ptr;
         a.work = c->d_m_work.ptr;
-        a.nwork = (uint32_t)c->m_work.size();
+        a.nwork = nwork;
         a.hitH = (uint32_t)std::max<int64_t>(c->hitH, 0);
         a.entries = c->d_m_entries.ptr;
+        a.plan = c->qplan;
         if constexpr (N == 16) { // one range block × its T transforms per workgroup
-            const unsigned nwg = (unsigned)c->m_work.size();
+            const unsigned nwg = nwork;
             const bool hits = c->hitH > 0;
             if (T == 8) {
                 if (hits)
@@ -1615,6 +1643,7 @@ int launch_mfma(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool inits =
         v.hitH = c->hitH;
         v.best_key = c->d_best_key.ptr;
         v.merged = (N != 16 && T > 1 && (c->mfma_var_ran & 128)) ? 1 : 0; // search_mfma's entries merged over t
+        v.plan = c->qplan;
         resolve_mfma<N><<<(nr + 3) / 4, 256, 0, c->stream>>>(v);
     }
     return FRAC_OK;
@@ -1975,7 +2004,7 @@ int launch_all(frac_ctx* c)
     const bool use_mfma = c->engine == FRAC_ENGINE_MFMA && !c->all_fallback;
     // the Fourier path resets best_key and fb_count in its preparation kernel (dft_prep)
     const bool dft_inits = N == 8 && use_mfma && nr && dft_route(c);
-    if (!dft_inits) {
+    if (!dft_inits && !c->qplan) { // (a planned level's qt_fill_maps did both)
         if (nr)
             FRAC_HIP(c, hipMemsetAsync(c->d_best_key.ptr, 0xff, nr * sizeof(unsigned long long), c->stream));
         const uint32_t fbc = c->all_fallback ? nr : 0u;
@@ -2068,6 +2097,7 @@ int launch_all(frac_ctx* c)
         f.aux = c->d_aux.ptr;
         f.fb_count = c->d_fb_count.ptr;
         f.fb_list = c->d_fb_list.ptr;
+        f.plan = c->qplan;
         if (c->fit_rstat)
             fit_rstat<N><<<(nr + 255) / 256, 256, 0, c->stream>>>(f, c->d_rstat.ptr);
         else
@@ -2108,6 +2138,326 @@ int launch_all(frac_ctx* c)
     return FRAC_OK;
 }
 
+// every level's domain grid (geometry only) stays on the host and the device across frames: the
+// level swaps them in (no copy, no upload, no re-validation) and back out afterwards
+// the caller's domain-list state comes back afterwards; the range list is consumed (cleared, unset)
+struct LevelGrid {
+    frac_ctx* c;
+    bool doms_set_before;
+    int lv = -1;
+    void in(int level)
+    {
+        lv = level;
+        std::swap(c->doms, c->qt_doms[lv]);
+        std::swap(c->d_doms, c->qt_ddoms[lv]);
+        c->doms_set = true;
+        c->doms_uploaded = c->qt_dvalid[lv];
+        c->doms_trusted = true;
+        c->dirty = true;
+    }
+    void out()
+    {
+        if (lv < 0)
+            return;
+        c->qt_dvalid[lv] = c->doms_uploaded;
+        std::swap(c->doms, c->qt_doms[lv]);
+        std::swap(c->d_doms, c->qt_ddoms[lv]);
+        c->doms_uploaded = false;
+        c->doms_trusted = false;
+        c->dirty = true;
+        lv = -1;
+    }
+    ~LevelGrid()
+    {
+        out();
+        c->ranges_dev = false;
+        c->doms_set = doms_set_before;
+        c->ranges_set = false;
+    }
+};
+
+// Whether a quadtree frame runs device-planned (qt_encode_dev): the MFMA engine at every level (AUTO
+// or MFMA requested; the VALU and SEA engines keep the host-planned levels below), and no level in
+// the all-fallback regime (a threshold that can be met in the inexact regime).
+bool qt_device_planned(const frac_ctx* c, const frac_quadtree_params* qp)
+{
+    if (c->p.engine != FRAC_ENGINE_AUTO && c->p.engine != FRAC_ENGINE_MFMA)
+        return false;
+    for (uint32_t n = qp->max_size; n >= qp->min_size; n /= 2)
+        if (compute_hit_limit(c->p.rms_threshold, 4 * n * n) >= kExactLimit)
+            return false;
+    return true;
+}
+
+// A quadtree frame with every level laid out on the device (fracenc_bucket.hip qt_plan): per level the
+// domain and range bucket keys, sorts and bounds, the planner (layout, work lists, CSR map, counts
+// into the level's DevPlan), qt_fill_maps, the level's search (launch_all in plan mode: worst-case
+// grids whose surplus workgroups leave at once) and the level transition (qt_flags, scan, qt_scatter,
+// which writes the next level's count into the next DevPlan).  Nothing comes back to the host until
+// the frame is done: one synchronisation for the leaf count and the counters, one for the leaves —
+// where the host-planned path synchronised twice per level (bucket counts, split count).  Records,
+// leaves and counters are those of the host-planned path.
+int qt_encode_dev(frac_ctx* c, const frac_quadtree_params* qp, LevelGrid& level, frac_encode_item* out, size_t cap,
+                  size_t* n_out, frac_stats* stats)
+{
+    const uint32_t W = c->src.w, H = c->src.h, T = c->p.transforms;
+    const int nb = c->p.use_classifier ? 7 : 1;
+    const bool timing = (c->p.flags & FRAC_FLAG_TIMING) != 0;
+    const uint8_t* tplane = c->same_plane ? c->d_src.ptr : c->d_tgt.ptr;
+    const uint32_t tstride = c->same_plane ? c->d_sstride : c->d_tstride;
+    HostTrace tr("quadtree (device-planned)");
+    const size_t max_leaves = (size_t)(W / qp->min_size) * (H / qp->min_size);
+    constexpr uint32_t kFirst = 2 * (kMaxBuckets + 1); // bucket bounds per level: domains, ranges
+    FRAC_HIP(c, c->d_qt_leaves.ensure(std::max<size_t>(max_leaves, 1)));
+    FRAC_HIP(c, c->d_ranges.ensure(std::max<size_t>(max_leaves, 1)));
+    FRAC_HIP(c, c->d_qt_next.ensure(std::max<size_t>(max_leaves, 1)));
+    FRAC_HIP(c, c->d_qt_plan.ensure(6));
+    FRAC_HIP(c, c->d_qt_first.ensure(5 * kFirst));
+    FRAC_HIP(c, c->d_qt_stats.ensure(9));
+    FRAC_HIP(c, c->d_bk_first.ensure(2 * (kMaxBuckets + 1) + 1));
+    FRAC_HIP(c, hipMemsetAsync(c->d_qt_stats.ptr, 0, 9 * sizeof(unsigned long long), c->stream));
+    // the first level's ranges: createUniformGrid(W, H, max, max), generated on the device
+    const uint32_t nr0 = (uint32_t)frac_uniform_grid(W, H, qp->max_size, qp->max_size, nullptr, 0);
+    if (nr0)
+        qt_uniform_grid<<<(nr0 + 255) / 256, 256, 0, c->stream>>>((W - qp->max_size) / qp->max_size + 1, nr0,
+                                                                  qp->max_size, qp->max_size, c->d_ranges.ptr);
+    uint32_t nr_bound = nr0; // the level's worst-case range count
+    int lvi = 0;             // level index (plans 0..4; plan lvi + 1 receives the next count)
+    std::vector<uint64_t> runs; // the levels' timing-history runs
+    for (uint32_t n = qp->max_size; n >= qp->min_size && nr_bound; n /= 2, ++lvi) {
+        const int lv = __builtin_ctz(n);
+        if (c->qt_doms[lv].empty()) {
+            c->qt_doms[lv].resize(frac_uniform_grid(W, H, 2 * n, n, nullptr, 0));
+            if (!c->qt_doms[lv].empty())
+                frac_uniform_grid(W, H, 2 * n, n, c->qt_doms[lv].data(), c->qt_doms[lv].size());
+        }
+        level.in(lv);
+        const uint32_t nd = (uint32_t)c->doms.size(), nr_max = nr_bound;
+        FRAC_HIP(c, c->d_doms.ensure(std::max<uint32_t>(nd, 1)));
+        if (!c->doms_uploaded && nd) {
+            FRAC_HIP(c, hipMemcpyAsync(c->d_doms.ptr, c->doms.data(), nd * sizeof(frac_grid_item),
+                                       hipMemcpyHostToDevice, c->stream));
+            c->doms_uploaded = true;
+        }
+        // the level's geometry (prepare()'s fields for a ratio-2 square level on the MFMA engine)
+        c->n = (int)n;
+        c->S = c->Sw = c->Sh = 2 * n;
+        c->nw = c->nh = n;
+        c->virt = c->generic = false;
+        c->Teff = T;
+        c->K2 = n * n / 2;
+        c->G = n == 16 ? 1u : (n <= 4 ? T : 4u);
+        c->NG = T / c->G;
+        c->npos = nd;
+        c->engine = FRAC_ENGINE_MFMA;
+        c->tp = false;
+        c->hitH = compute_hit_limit(c->p.rms_threshold, 4 * n * n);
+        c->all_fallback = false;
+        const bool fourier = n == 8 && mfma_dft_enabled(c);
+        c->dft_copies = fourier && T == 8 ? 2u : 1u;
+        const uint32_t cp = c->dft_copies, KS = (n * n + 15) / 16;
+        const uint32_t bpw = n == 16 ? 1u : fourier ? kDftBlocksPerWG : 4u;
+        const uint32_t target = n == 16 ? 4096u : fourier ? 8192u / kDftBlocksPerWG * 4u : 8192u;
+        const uint32_t nblocks_cap = (nr_max + 31) / 32 + (uint32_t)nb;
+        const uint32_t ntiles_cap = (nd + 31) / 32 + (uint32_t)nb;
+        const uint32_t groups_cap = (nblocks_cap * cp + bpw - 1) / bpw + (uint32_t)nb * cp;
+        const uint32_t nwork_cap = target + groups_cap, nent_cap = bpw * nwork_cap;
+        // buffers at the level's bounds (kept across frames: ensure() reallocates only to grow)
+        const size_t mx = std::max<size_t>(std::max<size_t>(nd, nr_max), 1);
+        FRAC_HIP(c, c->d_porig.ensure(std::max<uint32_t>(nd, 1)));
+        FRAC_HIP(c, c->d_pool.ensure((size_t)std::max<uint32_t>(nd, 1) * c->K2));
+        FRAC_HIP(c, c->d_negsd2.ensure(std::max<uint32_t>(nd, 1)));
+        for (auto* b : {&c->d_rord, &c->d_rkey, &c->d_fb_list, &c->d_m_range_slot, &c->d_qt_flags, &c->d_qt_offs})
+            FRAC_HIP(c, b->ensure(std::max<uint32_t>(nr_max, 1)));
+        FRAC_HIP(c, c->d_rbucket.ensure(std::max<uint32_t>(nr_max, 1)));
+        FRAC_HIP(c, c->d_best_key.ensure(std::max<uint32_t>(nr_max, 1)));
+        FRAC_HIP(c, c->d_out.ensure(std::max<uint32_t>(nr_max, 1)));
+        FRAC_HIP(c, c->d_aux.ensure(std::max<uint32_t>(nr_max, 1)));
+        FRAC_HIP(c, c->d_fb_count.ensure(1));
+        FRAC_HIP(c, c->d_bk_keys.ensure(mx));
+        FRAC_HIP(c, c->d_bk_keys2.ensure(mx));
+        FRAC_HIP(c, c->d_bk_iota.ensure(mx));
+        FRAC_HIP(c, c->d_m_slot_range.ensure((size_t)nblocks_cap * 32 * cp));
+        FRAC_HIP(c, c->d_m_rconst.ensure((size_t)nblocks_cap * 32 * cp));
+        FRAC_HIP(c, c->d_m_tile_pos.ensure((size_t)ntiles_cap * 32));
+        FRAC_HIP(c, c->d_m_dconst.ensure((size_t)ntiles_cap * kDftCS * 4 + 256));
+        FRAC_HIP(c, c->d_m_dtiles.ensure((size_t)ntiles_cap * std::max(KS, 5u) * 64));
+        FRAC_HIP(c, c->d_m_rfrags.ensure((size_t)nblocks_cap * std::max(T * KS, 6u * cp) * 64));
+        DBuf<uint4>& dwork = fourier ? c->d_m8_work : c->d_m_work;
+        DBuf<uint32_t>& dptr = fourier ? c->d_m8_blk_ptr : c->d_m_blk_ptr;
+        DBuf<uint32_t>& dent = fourier ? c->d_m8_blk_ent : c->d_m_blk_ent;
+        FRAC_HIP(c, dwork.ensure(nwork_cap));
+        FRAC_HIP(c, dptr.ensure((size_t)nblocks_cap * cp + 1));
+        FRAC_HIP(c, dent.ensure(std::max<uint32_t>(nent_cap, 1)));
+        FRAC_HIP(c, c->d_m_entries.ensure((size_t)nwork_cap * (fourier ? kDftBlocksPerWG : 4u * T) * 64));
+        size_t need = 0, sneed = 0;
+        FRAC_HIP(c, sort_pairs_u32(nullptr, need, c->d_bk_keys.ptr, c->d_bk_keys2.ptr, c->d_bk_iota.ptr, c->d_porig.ptr,
+                                   (uint32_t)mx, 3, c->stream));
+        if (need > c->bk_tmp_bytes) {
+            FRAC_HIP(c, c->d_bk_tmp.ensure(need));
+            c->bk_tmp_bytes = need;
+        }
+        FRAC_HIP(c, hipcub::DeviceScan::ExclusiveSum(nullptr, sneed, c->d_qt_flags.ptr, c->d_qt_offs.ptr,
+                                                     (int)std::max<uint32_t>(nr_max, 1), c->stream));
+        if (sneed > c->qt_tmp_bytes) {
+            FRAC_HIP(c, c->d_qt_tmp.ensure(sneed));
+            c->qt_tmp_bytes = sneed;
+        }
+        tr.mark("level buffers");
+        DevPlan* plan = c->d_qt_plan.ptr + lvi;
+        const uint32_t* dn = lvi ? &plan->nr : nullptr; // the first level's count is the host's
+        uint32_t* first = c->d_qt_first.ptr + (size_t)lv * kFirst;
+        uint32_t* err = c->d_bk_first.ptr + 2 * (kMaxBuckets + 1);
+        if (nb > 1) {
+            // domains: keys + stable sort by bucket (the pool order porig) + bounds; ranges: the same over
+            // the worst case, the items past the level's count keyed kPadKey (last)
+            size_t tb = c->bk_tmp_bytes;
+            FRAC_HIP(c, hipMemsetAsync(err, 0, sizeof(uint32_t), c->stream));
+            launch_bucket_keys(c->d_doms.ptr, nd, 2 * n, c->d_src.ptr, c->d_sstride, c->d_bk_keys.ptr, c->d_bk_iota.ptr,
+                               err, c->stream);
+            FRAC_HIP(c, sort_pairs_u32(c->d_bk_tmp.ptr, tb, c->d_bk_keys.ptr, c->d_bk_keys2.ptr, c->d_bk_iota.ptr,
+                                       c->d_porig.ptr, nd, 3, c->stream));
+            bucket_bounds<<<1, 64, 0, c->stream>>>(c->d_bk_keys2.ptr, nd, first);
+            tb = c->bk_tmp_bytes;
+            launch_bucket_keys(c->d_ranges.ptr, nr_max, n, tplane, tstride, c->d_rkey.ptr, c->d_bk_iota.ptr, err,
+                               c->stream, dn);
+            FRAC_HIP(c, sort_pairs_u32(c->d_bk_tmp.ptr, tb, c->d_rkey.ptr, c->d_bk_keys2.ptr, c->d_bk_iota.ptr,
+                                       c->d_rord.ptr, nr_max, 3, c->stream));
+            bucket_bounds<<<1, 64, 0, c->stream>>>(c->d_bk_keys2.ptr, nr_max, first + kMaxBuckets + 1);
+        } else {
+            if (nd)
+                fill_iota<<<(nd + 255) / 256, 256, 0, c->stream>>>(c->d_porig.ptr, nd);
+            fill_iota<<<(nr_max + 255) / 256, 256, 0, c->stream>>>(c->d_rord.ptr, nr_max);
+            FRAC_HIP(c, hipMemsetAsync(c->d_rkey.ptr, 0, nr_max * sizeof(uint32_t), c->stream));
+        }
+        QtPlanArgs pa;
+        pa.plan = plan;
+        pa.dfirst = nb > 1 ? first : nullptr;
+        pa.rfirst = nb > 1 ? first + kMaxBuckets + 1 : nullptr;
+        pa.nb = (uint32_t)nb;
+        pa.nd = nd;
+        pa.nr_init = lvi ? ~0u : nr0;
+        pa.bpw = bpw;
+        pa.target = target;
+        pa.copies = cp;
+        pa.mfma_per_pair = fourier ? 6u : T * KS;
+        pa.nwork_cap = nwork_cap;
+        pa.nent_cap = nent_cap;
+        pa.nblocks_cap = nblocks_cap;
+        pa.ntiles_cap = ntiles_cap;
+        pa.work = dwork.ptr;
+        pa.blk_ptr = dptr.ptr;
+        pa.blk_ent = dent.ptr;
+        pa.acc = c->d_qt_stats.ptr;
+        qt_plan<<<8, 256, 0, c->stream>>>(pa);
+        QtFillArgs fa;
+        fa.plan = plan;
+        fa.rord = c->d_rord.ptr;
+        fa.rkey = c->d_rkey.ptr;
+        fa.copies = cp;
+        fa.nthreads = std::max(std::max(nblocks_cap * 32 * cp, ntiles_cap * 32), nr_max);
+        fa.slot_range = c->d_m_slot_range.ptr;
+        fa.range_slot = c->d_m_range_slot.ptr;
+        fa.tile_pos = c->d_m_tile_pos.ptr;
+        fa.rbucket = c->d_rbucket.ptr;
+        fa.rconst = fourier ? nullptr : c->d_m_rconst.ptr;
+        fa.best_key = c->d_best_key.ptr;
+        fa.fb_count = c->d_fb_count.ptr;
+        qt_fill_maps<<<(fa.nthreads + 255) / 256, 256, 0, c->stream>>>(fa);
+        // the level's search, on the bounds: launch_all in plan mode
+        c->m_work.clear();
+        c->m8_work.clear();
+        c->ranges_dev = true;
+        c->nr_dev = nr_max;
+        c->n_dev = n;
+        c->ntiles = ntiles_cap;
+        c->nblocks = nblocks_cap;
+        c->m8_bpw = kDftBlocksPerWG;
+        c->qplan = plan;
+        c->qp_nwork_cap = nwork_cap;
+        int rc;
+        switch (n) {
+        case 2: rc = launch_all<2>(c); break;
+        case 4: rc = launch_all<4>(c); break;
+        case 16: rc = launch_all<16>(c); break;
+        default: rc = launch_all<8>(c); break;
+        }
+        c->qplan = nullptr;
+        FRAC_TRY(rc);
+        if (timing)
+            runs.push_back(c->hist_runs - 1);
+        tr.mark("level launch");
+        if (stats)
+            qt_level_stats<<<(nr_max + 255) / 256, 256, 0, c->stream>>>(
+                c->d_aux.ptr, c->d_rkey.ptr, c->d_porig.ptr, nr_max, (uint64_t)nd, c->p.use_classifier ? 1 : 0,
+                QtBuckets{}, nullptr, c->d_qt_stats.ptr, plan);
+        level.out();
+        qt_flags<<<(nr_max + 255) / 256, 256, 0, c->stream>>>(c->d_out.ptr, nr_max, n > qp->min_size ? 1 : 0,
+                                                             qp->split_distance, c->d_qt_flags.ptr, plan);
+        size_t tb = c->qt_tmp_bytes;
+        FRAC_HIP(c, hipcub::DeviceScan::ExclusiveSum(c->d_qt_tmp.ptr, tb, c->d_qt_flags.ptr, c->d_qt_offs.ptr,
+                                                     (int)nr_max, c->stream));
+        qt_scatter<<<(nr_max + 255) / 256, 256, 0, c->stream>>>(c->d_out.ptr, c->d_ranges.ptr, nr_max,
+                                                               c->d_qt_flags.ptr, c->d_qt_offs.ptr,
+                                                               c->d_qt_leaves.ptr, 0, c->d_qt_next.ptr, nullptr,
+                                                               plan, plan + 1);
+        std::swap(c->d_ranges, c->d_qt_next);
+        // the next level: at most four quadrants per range, at most the full grid of its size
+        const uint32_t full = n > 2 ? (uint32_t)frac_uniform_grid(W, H, n / 2, n / 2, nullptr, 0) : 0u;
+        nr_bound = n > qp->min_size ? std::min<uint32_t>(4 * nr_max, full) : 0u;
+        tr.mark("split (device)");
+    }
+    c->ranges_dev = false;
+    c->ranges.clear();
+    c->ranges_set = false;
+    c->dirty = true;
+    c->ran = false;
+    // the frame's one round trip for the counts: leaves (after the last level run), counters
+    struct {
+        DevPlan last;
+        unsigned long long acc[9];
+    } h{};
+    FRAC_HIP(c, hipMemcpyAsync(&h.last, c->d_qt_plan.ptr + lvi, sizeof(DevPlan), hipMemcpyDeviceToHost, c->stream));
+    FRAC_HIP(c, hipMemcpyAsync(h.acc, c->d_qt_stats.ptr, sizeof(h.acc), hipMemcpyDeviceToHost, c->stream));
+    FRAC_HIP(c, hipStreamSynchronize(c->stream));
+    if (lvi == 0)
+        h.last.leaf_base = 0;
+    if (h.acc[8])
+        return c->fail(FRAC_E_STATE, "quadtree: a level's layout exceeded its planned bounds");
+    const uint32_t n_leaves = h.last.leaf_base;
+    *n_out = n_leaves;
+    if (out && n_leaves)
+        FRAC_HIP(c, hipMemcpy(out, c->d_qt_leaves.ptr, std::min<size_t>(cap, n_leaves) * sizeof(frac_encode_item),
+                              hipMemcpyDeviceToHost));
+    tr.mark("leaves D2H");
+    if (stats) {
+        frac_stats total{};
+        total.rejected_mappings = h.acc[0];
+        total.hit_ranges = (uint32_t)h.acc[1];
+        total.fallback_ranges = (uint32_t)h.acc[2];
+        total.empty_ranges = (uint32_t)h.acc[3];
+        total.total_mappings = h.acc[5];
+        total.evaluated_mappings = h.acc[6];
+        total.matrix_flops = h.acc[7];
+        total.engine = FRAC_ENGINE_MFMA;
+        total.search_form = c->form_ran;
+        if (timing)
+            for (uint64_t r : runs) {
+                hipEvent_t* e = &c->hist[(size_t)(r % kHistRuns) * 4];
+                float ms = 0.f;
+                if (hipEventElapsedTime(&ms, e[0], e[3]) == hipSuccess)
+                    total.ms_device += ms;
+                if (hipEventElapsedTime(&ms, e[0], e[1]) == hipSuccess)
+                    total.ms_prep += ms;
+                if (hipEventElapsedTime(&ms, e[1], e[2]) == hipSuccess)
+                    total.ms_search += ms;
+                if (hipEventElapsedTime(&ms, e[2], e[3]) == hipSuccess)
+                    total.ms_finish += ms;
+            }
+        *stats = total;
+    }
+    return FRAC_OK;
+}
 } // namespace
 
 extern "C" {
@@ -2592,43 +2942,9 @@ int frac_encode_quadtree(frac_ctx* c, const frac_quadtree_params* qp, frac_encod
         c->qt_w = W;
         c->qt_h = H;
     }
-    // every level's domain grid (geometry only) stays on the host and the device across frames: the
-    // level swaps them in (no copy, no upload, no re-validation) and back out afterwards
-    // the caller's domain-list state comes back afterwards; the range list is consumed (cleared, unset)
-    struct LevelGrid {
-        frac_ctx* c;
-        bool doms_set_before;
-        int lv = -1;
-        void in(int level)
-        {
-            lv = level;
-            std::swap(c->doms, c->qt_doms[lv]);
-            std::swap(c->d_doms, c->qt_ddoms[lv]);
-            c->doms_set = true;
-            c->doms_uploaded = c->qt_dvalid[lv];
-            c->doms_trusted = true;
-            c->dirty = true;
-        }
-        void out()
-        {
-            if (lv < 0)
-                return;
-            c->qt_dvalid[lv] = c->doms_uploaded;
-            std::swap(c->doms, c->qt_doms[lv]);
-            std::swap(c->d_doms, c->qt_ddoms[lv]);
-            c->doms_uploaded = false;
-            c->doms_trusted = false;
-            c->dirty = true;
-            lv = -1;
-        }
-        ~LevelGrid()
-        {
-            out();
-            c->ranges_dev = false;
-            c->doms_set = doms_set_before;
-            c->ranges_set = false;
-        }
-    } level{c, c->doms_set};
+    LevelGrid level{c, c->doms_set};
+    if (qt_device_planned(c, qp))
+        return qt_encode_dev(c, qp, level, out, cap, n_out, stats);
     // the level-to-level step runs on the device (qt_flags, scan, qt_scatter): each level's leaves are
     // appended to d_qt_leaves and its split ranges' quadrants become the next level's device range list;
     // the host reads one count per level and the leaves once at the end

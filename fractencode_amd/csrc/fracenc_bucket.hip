@@ -16,20 +16,6 @@
 
 namespace fracenc {
 
-constexpr int kMaxBuckets = 8; // 7 classifier buckets (categories −1..5); 1 without the classifier
-
-// per-bucket layout, passed by value to the fill kernels
-struct BucketLayout {
-    uint32_t nb;
-    uint32_t VT;                        // engine pool rows per pool position (T in the sampled form, else 1)
-    uint32_t dbeg[kMaxBuckets];         // first pool position of the bucket
-    uint32_t dcnt[kMaxBuckets];         // pool positions (domains) in the bucket
-    uint32_t rbeg[kMaxBuckets];         // first bucket-sorted range of the bucket
-    uint32_t rcnt[kMaxBuckets];         // ranges in the bucket
-    uint32_t slot_first[kMaxBuckets];   // first slot of the bucket's ranges (blocks padded to `pad` slots)
-    uint32_t tile_first[kMaxBuckets];   // first 32-row tile of the bucket's engine pool rows
-};
-
 // key = category + 1 of item i; a stored −1 is classified on `plane` (classify_items' arithmetic:
 // quadrant sums, u16 for quadrants ≤ 16 wide).  A stored category outside −1..5 raises *err.
 // One wave per item (blockDim 256).
@@ -77,15 +63,29 @@ __global__ void __launch_bounds__(256) bucket_keys(const frac_grid_item* __restr
 // a power of two), lane j sums the two halves of row j (dword loads and v_dot4 when the row
 // and the half width are 4-byte aligned, else bytes), and the group reduces the quadrants.
 // 64/L items per wave instead of one.
+// dn (device-planned quadtree levels): the item count is *dn ≤ n, known only on the device; the
+// items [*dn, n) of the worst-case grid get the padding key kPadKey, which sorts after every bucket.
+constexpr uint32_t kPadKey = 7; // categories −1..5 are keys 0..6; the 3-bit radix sort keeps 7 last
+
 template <uint32_t L>
 __global__ void __launch_bounds__(256) bucket_keys_rows(const frac_grid_item* __restrict__ items, uint32_t n,
                                                         const uint8_t* __restrict__ plane, uint32_t stride,
                                                         uint32_t* __restrict__ key, uint32_t* __restrict__ iota,
-                                                        uint32_t* __restrict__ err)
+                                                        uint32_t* __restrict__ err, const uint32_t* __restrict__ dn)
 {
     static_assert(L >= 1 && L <= 64 && (L & (L - 1)) == 0, "lanes per item: a power of two up to 64");
     const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t k = gid / L, j = gid % L;
+    if (dn) {
+        const uint32_t nd = min(*dn, n);
+        if (k >= nd) {
+            if (k < n && j == 0) {
+                key[k] = kPadKey;
+                iota[k] = k;
+            }
+            return; // whole item groups leave together: the shuffles below see only live lanes
+        }
+    }
     frac_grid_item it{0, 0, 0, 0, 0};
     if (k < n)
         it = items[k];
@@ -129,14 +129,17 @@ __global__ void __launch_bounds__(256) bucket_keys_rows(const frac_grid_item* __
     iota[k] = k;
 }
 
-// bucket keys of `cnt` items of height h (every item of a grid has the size of the first)
+// bucket keys of `cnt` items of height h (every item of a grid has the size of the first); dn: the
+// device-side count of a worst-case grid of cnt items (items ≤ 64 rows high only)
 inline void launch_bucket_keys(const frac_grid_item* items, uint32_t cnt, uint32_t h, const uint8_t* plane,
-                               uint32_t stride, uint32_t* key, uint32_t* iota, uint32_t* err, hipStream_t s)
+                               uint32_t stride, uint32_t* key, uint32_t* iota, uint32_t* err, hipStream_t s,
+                               const uint32_t* dn = nullptr)
 {
     auto rows = [&](auto lanes) {
         constexpr uint32_t L = decltype(lanes)::value;
         const uint64_t threads = (uint64_t)cnt * L;
-        bucket_keys_rows<L><<<(unsigned)((threads + 255) / 256), 256, 0, s>>>(items, cnt, plane, stride, key, iota, err);
+        bucket_keys_rows<L><<<(unsigned)((threads + 255) / 256), 256, 0, s>>>(items, cnt, plane, stride, key, iota, err,
+                                                                             dn);
     };
     if (h <= 2)
         rows(std::integral_constant<uint32_t, 2>());
@@ -237,12 +240,16 @@ __global__ void __launch_bounds__(256) fill_rbucket(BucketLayout L, const uint32
 // threshold; the level's leaves are appended, in search order, to the frame's leaf list, and the
 // split ranges' four quadrants (top-left, top-right, bottom-left, bottom-right) become the next
 // level's ranges in their parents' order.  offs = exclusive scan of the flags.
+// plan (device-planned levels): the level's range count is plan->nr ≤ n, the grid and the scan
+// cover the worst case n, and the items past plan->nr get flag 0.
 __global__ void __launch_bounds__(256) qt_flags(const frac_encode_item* __restrict__ out, uint32_t n, int can_split,
-                                                double split, uint32_t* __restrict__ flags)
+                                                double split, uint32_t* __restrict__ flags,
+                                                const DevPlan* __restrict__ plan = nullptr)
 {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t nl = plan ? min(plan->nr, n) : n;
     if (i < n)
-        flags[i] = (can_split && out[i].match.score.distance > split) ? 1u : 0u;
+        flags[i] = (i < nl && can_split && out[i].match.score.distance > split) ? 1u : 0u;
 }
 
 // A level's frac_stats counters, added on the device into acc = {rejected, hit, fallback, empty,
@@ -260,9 +267,18 @@ __global__ void __launch_bounds__(256) qt_level_stats(const RangeAux* __restrict
                                                       const uint32_t* __restrict__ porig, uint32_t nr, uint64_t nd,
                                                       int classifier, QtBuckets B,
                                                       const unsigned long long* __restrict__ sea_count,
-                                                      unsigned long long* __restrict__ acc)
+                                                      unsigned long long* __restrict__ acc,
+                                                      const DevPlan* __restrict__ plan = nullptr)
 {
     const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (plan) { // the buckets as the planner laid them out
+        nr = plan->nr;
+        B.nb = plan->L.nb;
+        for (uint32_t b = 0; b < (uint32_t)kMaxBuckets; ++b) {
+            B.beg[b] = plan->L.dbeg[b];
+            B.end[b] = plan->L.dbeg[b] + plan->L.dcnt[b];
+        }
+    }
     unsigned long long v[4] = {0ull, 0ull, 0ull, 0ull}; // rejected, hit, fallback, empty
     if (r < nr) {
         const RangeAux ax = aux[r];
@@ -293,13 +309,25 @@ __global__ void __launch_bounds__(256) qt_level_stats(const RangeAux* __restrict
         atomicAdd(&acc[4], *sea_count);
 }
 
+// plan / next (device-planned levels): the level's count and leaf base come from plan, and the
+// next level's (4·nsplit ranges, leaves so far) go to next — the host never reads them per level.
 __global__ void __launch_bounds__(256) qt_scatter(const frac_encode_item* __restrict__ out,
                                                   const frac_grid_item* __restrict__ ranges, uint32_t n,
                                                   const uint32_t* __restrict__ flags, const uint32_t* __restrict__ offs,
                                                   frac_encode_item* __restrict__ leaves, uint32_t leaf_base,
-                                                  frac_grid_item* __restrict__ next, uint32_t* __restrict__ nsplit)
+                                                  frac_grid_item* __restrict__ next, uint32_t* __restrict__ nsplit,
+                                                  const DevPlan* __restrict__ plan = nullptr,
+                                                  DevPlan* __restrict__ next_plan = nullptr)
 {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (plan) {
+        n = min(plan->nr, n);
+        leaf_base = plan->leaf_base;
+        if (n == 0 && i == 0) { // an empty level: nothing splits, nothing is emitted
+            next_plan->nr = 0;
+            next_plan->leaf_base = leaf_base;
+        }
+    }
     if (i >= n)
         return;
     const uint32_t o = offs[i];
@@ -313,8 +341,231 @@ __global__ void __launch_bounds__(256) qt_scatter(const frac_encode_item* __rest
     } else {
         leaves[leaf_base + (i - o)] = out[i];
     }
-    if (i == n - 1)
-        *nsplit = o + flags[i];
+    if (i == n - 1) {
+        const uint32_t ns = o + flags[i];
+        if (nsplit)
+            *nsplit = ns;
+        if (next_plan) {
+            next_plan->nr = 4 * ns;
+            next_plan->leaf_base = leaf_base + n - ns;
+        }
+    }
+}
+
+// ---- the device planner of a quadtree level (prepare()'s layout and work lists, restated) ----
+// From the bucket bounds of the level's domains and ranges (bucket_bounds over the sorted keys)
+// it lays out the MFMA engine's 32-slot range blocks and 32-row domain tiles per bucket, and writes
+// the search's work items {first block, blocks, tile begin, tile end} — groups of `bpw` blocks of one
+// bucket × splits of the bucket's tiles, splits = ⌈target / groups⌉ capped at tiles / 4, in
+// prepare()'s (copy, bucket, group, split) order — and the CSR map block → entries (work·bpw + k)
+// the resolve kernels read.  Every count goes to the DevPlan; the launches that follow use
+// worst-case grids.  The frame's counters get the level's total / eligible pairs and the MFMA
+// flops the search issues.  Every block recomputes the (at most 7-bucket) header; block 0 writes it.
+struct QtPlanArgs {
+    DevPlan* plan;
+    const uint32_t* dfirst;  // [kMaxBuckets + 1] first pool position per bucket (nullptr: one bucket)
+    const uint32_t* rfirst;  // [kMaxBuckets + 1] first bucket-sorted range per bucket
+    uint32_t nb;             // buckets: 7 with the classifier, 1 without
+    uint32_t nd;             // domains of the level
+    uint32_t nr_init;        // the first level: its range count (host-known); ~0u: plan->nr (qt_scatter)
+    uint32_t bpw;            // range blocks per work item (search_dft 8, search_mfma 4, search_mfma16 1)
+    uint32_t target;         // target work items (workgroups)
+    uint32_t copies;         // T = 8 Fourier: 2 (flipped copies), else 1
+    uint32_t mfma_per_pair;  // MFMA 32x32x16 per (range block, domain tile) pair: flops accounting
+    uint32_t nwork_cap, nent_cap, nblocks_cap, ntiles_cap; // buffer capacities
+    uint4* work;
+    uint32_t* blk_ptr;       // [nblocks·copies + 1]
+    uint32_t* blk_ent;
+    unsigned long long* acc; // frame counters: [5] total mappings, [6] eligible pairs, [7] flops, [8] overflow
+};
+
+struct QtPlanHeader {
+    BucketLayout L;
+    uint32_t blk_first[kMaxBuckets], blk_count[kMaxBuckets], tile_count[kMaxBuckets], ns[kMaxBuckets];
+    uint32_t wbase[2 * kMaxBuckets + 1]; // first work item of (copy, bucket), in that order
+    uint32_t ebase[2 * kMaxBuckets + 1]; // first CSR entry of (copy, bucket)
+    uint32_t nr, nblocks, ntiles, nwork, nent;
+    bool ok;
+};
+
+__device__ inline void qt_plan_header(const QtPlanArgs& a, QtPlanHeader& h)
+{
+    const uint32_t nr = a.nr_init != ~0u ? a.nr_init : a.plan->nr;
+    h.nr = nr;
+    BucketLayout& L = h.L;
+    L.nb = a.nb;
+    L.VT = 1;
+    uint32_t nbk = 0, nt = 0;
+    for (uint32_t b = 0; b < (uint32_t)kMaxBuckets; ++b) {
+        const bool in = b < a.nb;
+        L.dbeg[b] = in ? (a.dfirst ? a.dfirst[b] : 0u) : 0u;
+        L.dcnt[b] = in ? (a.dfirst ? a.dfirst[b + 1] - a.dfirst[b] : a.nd) : 0u;
+        // the last bucket ends where the padding keys begin (first[kPadKey] = the level's count)
+        L.rbeg[b] = in ? (a.rfirst ? a.rfirst[b] : 0u) : 0u;
+        L.rcnt[b] = in ? (a.rfirst ? min(a.rfirst[b + 1], nr) - min(a.rfirst[b], nr) : nr) : 0u;
+        h.blk_first[b] = nbk;
+        h.blk_count[b] = (L.rcnt[b] + 31) / 32;
+        nbk += h.blk_count[b];
+        L.tile_first[b] = nt;
+        h.tile_count[b] = (L.dcnt[b] + 31) / 32;
+        nt += h.tile_count[b];
+        L.slot_first[b] = 32 * h.blk_first[b];
+    }
+    h.nblocks = nbk;
+    h.ntiles = nt;
+    uint64_t groups = 0;
+    for (uint32_t b = 0; b < a.nb; ++b)
+        if (h.tile_count[b])
+            groups += (uint64_t)(h.blk_count[b] + a.bpw - 1) / a.bpw * a.copies;
+    uint32_t w = 0, e = 0;
+    for (uint32_t cp = 0; cp < 2; ++cp) // every (copy, bucket) entry is written: the work loop scans them
+        for (uint32_t b = 0; b < (uint32_t)kMaxBuckets; ++b) {
+            const uint32_t tc = h.tile_count[b], bc = cp < a.copies ? h.blk_count[b] : 0u;
+            uint32_t ns = 0;
+            if (b < a.nb && tc && bc) {
+                uint64_t sp = groups ? (a.target + groups - 1) / groups : 1;
+                sp = max<uint64_t>(1, min<uint64_t>(sp, max(1u, tc / 4u)));
+                ns = (uint32_t)sp; // sp ≤ tc: every split holds at least one tile
+            }
+            if (cp == 0)
+                h.ns[b] = ns;
+            h.wbase[cp * kMaxBuckets + b] = w;
+            h.ebase[cp * kMaxBuckets + b] = e;
+            w += (bc + a.bpw - 1) / a.bpw * ns;
+            e += bc * ns;
+        }
+    h.wbase[2 * kMaxBuckets] = w;
+    h.ebase[2 * kMaxBuckets] = e;
+    h.nwork = w;
+    h.nent = e;
+    h.ok = w <= a.nwork_cap && e <= a.nent_cap && nbk <= a.nblocks_cap && nt <= a.ntiles_cap;
+}
+
+__global__ void __launch_bounds__(256) qt_plan(QtPlanArgs a)
+{
+    __shared__ QtPlanHeader h;
+    if (threadIdx.x == 0)
+        qt_plan_header(a, h);
+    __syncthreads();
+    const uint32_t gt = blockIdx.x * blockDim.x + threadIdx.x, gs = gridDim.x * blockDim.x;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        DevPlan& p = *a.plan;
+        p.L = h.L;
+        p.nr = h.nr;
+        if (a.nr_init != ~0u)
+            p.leaf_base = 0;
+        p.nblocks = h.ok ? h.nblocks : 0u;
+        p.ntiles = h.ok ? h.ntiles : 0u;
+        p.nwork = h.ok ? h.nwork : 0u;
+        p.nslots = h.ok ? h.nblocks * 32u : 0u; // resolve_dft's slots: one wave takes both copies of a slot
+        p.flip_slots = a.copies == 2 ? h.nblocks * 32u : 0u;
+        uint64_t elig = 0, flops = 0;
+        for (uint32_t b = 0; b < a.nb; ++b) {
+            elig += (uint64_t)h.L.rcnt[b] * h.L.dcnt[b];
+            flops += (uint64_t)h.blk_count[b] * h.tile_count[b] * a.copies * a.mfma_per_pair * 32768ull;
+        }
+        atomicAdd(&a.acc[5], (unsigned long long)a.nd * h.nr);
+        atomicAdd(&a.acc[6], (unsigned long long)elig);
+        atomicAdd(&a.acc[7], (unsigned long long)flops);
+        if (!h.ok)
+            atomicAdd(&a.acc[8], 1ull); // the host fails the frame (a bound was wrong: never expected)
+    }
+    if (!h.ok)
+        return;
+    // work items, in (copy, bucket, group, split) order
+    for (uint32_t w = gt; w < h.nwork; w += gs) {
+        uint32_t q = 0;
+        while (q + 1 < 2 * (uint32_t)kMaxBuckets && h.wbase[q + 1] <= w)
+            ++q;
+        const uint32_t cp = q / kMaxBuckets, b = q % kMaxBuckets, ns = h.ns[b], loc = w - h.wbase[q];
+        const uint32_t g = (loc / ns) * a.bpw, sp = loc % ns, tc = h.tile_count[b];
+        const uint32_t bf = cp * h.nblocks + h.blk_first[b];
+        const uint32_t t0 = h.L.tile_first[b] + (uint32_t)((uint64_t)tc * sp / ns);
+        const uint32_t t1 = h.L.tile_first[b] + (uint32_t)((uint64_t)tc * (sp + 1) / ns);
+        a.work[w] = make_uint4(bf + g, min(a.bpw, h.blk_count[b] - g), t0, t1);
+    }
+    // the CSR map: block (copy, bucket, k) holds one entry per split of its bucket
+    const uint32_t nbt = h.nblocks * a.copies;
+    for (uint32_t i = gt; i <= nbt; i += gs) {
+        if (i == nbt) {
+            a.blk_ptr[i] = h.nent;
+            continue;
+        }
+        const uint32_t cp = i / h.nblocks, loc = i % h.nblocks;
+        uint32_t b = 0;
+        for (uint32_t k = 1; k < a.nb; ++k)
+            b = loc >= h.blk_first[k] ? k : b;
+        const uint32_t k = loc - h.blk_first[b], ns = h.ns[b], q = cp * kMaxBuckets + b;
+        const uint32_t base = h.ebase[q] + k * ns;
+        a.blk_ptr[i] = base;
+        for (uint32_t sp = 0; sp < ns; ++sp)
+            a.blk_ent[base + sp] = (h.wbase[q] + (k / a.bpw) * ns + sp) * a.bpw + k % a.bpw;
+    }
+}
+
+// The per-item maps of a planned level (fill_range_slots, fill_tile_pos and fill_rbucket in one
+// launch over the worst case), and the run's resets: best_key (none yet), the direct form's
+// zeroed rconst words (mfma_range_prep accumulates into them), the fallback count.
+struct QtFillArgs {
+    const DevPlan* plan;
+    const uint32_t* rord;     // bucket-sorted range order
+    const uint32_t* rkey;     // per range: its bucket
+    uint32_t copies;          // T = 8 Fourier: slot s ≥ nblocks·32 is the flipped copy of s − nblocks·32
+    uint32_t nthreads;        // the grid's bound: max(slots, tile rows, ranges)
+    int32_t* slot_range;
+    uint32_t* range_slot;
+    int32_t* tile_pos;
+    uint2* rbucket;
+    uint32_t* rconst;         // zeroed per slot when not null (the direct form)
+    unsigned long long* best_key;
+    uint32_t* fb_count;
+};
+
+__global__ void __launch_bounds__(256) qt_fill_maps(QtFillArgs a)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.nthreads)
+        return;
+    const DevPlan& p = *a.plan;
+    const BucketLayout& L = p.L;
+    const uint32_t nslots = p.nblocks * 32u;
+    if (i < nslots * a.copies) {
+        const uint32_t s = i % nslots, b = layout_bucket_of_slot(L, s), k = s - L.slot_first[b];
+        int32_t r = -1;
+        if (k < L.rcnt[b]) {
+            r = (int32_t)a.rord[L.rbeg[b] + k];
+            if (i < nslots)
+                a.range_slot[r] = s;
+        }
+        a.slot_range[i] = r;
+        if (a.rconst)
+            a.rconst[i] = 0u;
+    }
+    if (i < p.ntiles * 32u) {
+        const uint32_t tile = i >> 5;
+        uint32_t b = 0;
+        for (uint32_t k = 1; k < L.nb; ++k)
+            b = tile >= L.tile_first[k] ? k : b;
+        const uint32_t j = i - 32u * L.tile_first[b];
+        a.tile_pos[i] = j < L.dcnt[b] ? (int32_t)(L.dbeg[b] + j) : -1;
+    }
+    if (i < p.nr) {
+        const uint32_t b = a.rkey[i];
+        a.rbucket[i] = make_uint2(L.dbeg[b], L.dbeg[b] + L.dcnt[b]);
+        a.best_key[i] = ~0ull;
+    }
+    if (i == 0)
+        *a.fb_count = 0u;
+}
+
+// createUniformGrid(W, H, size, off) on the device (image/partition2.hpp:123-133, frac_uniform_grid2):
+// the first quadtree level's ranges, kept on the device across frames like the domain grids
+__global__ void __launch_bounds__(256) qt_uniform_grid(uint32_t nx, uint32_t n, uint32_t size, uint32_t off,
+                                                       frac_grid_item* __restrict__ out)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n)
+        out[i] = frac_grid_item{(i % nx) * off, (i / nx) * off, size, size, -1};
 }
 
 } // namespace fracenc

@@ -120,6 +120,36 @@ struct RangeAux {
     uint32_t flags; // AuxFlags
 };
 
+constexpr int kMaxBuckets = 8; // 7 classifier buckets (categories −1..5); 1 without the classifier
+
+// per-bucket layout, passed by value to the fill kernels (or read from a DevPlan)
+struct BucketLayout {
+    uint32_t nb;
+    uint32_t VT;                        // engine pool rows per pool position (T in the sampled form, else 1)
+    uint32_t dbeg[kMaxBuckets];         // first pool position of the bucket
+    uint32_t dcnt[kMaxBuckets];         // pool positions (domains) in the bucket
+    uint32_t rbeg[kMaxBuckets];         // first bucket-sorted range of the bucket
+    uint32_t rcnt[kMaxBuckets];         // ranges in the bucket
+    uint32_t slot_first[kMaxBuckets];   // first slot of the bucket's ranges (blocks padded to `pad` slots)
+    uint32_t tile_first[kMaxBuckets];   // first 32-row tile of the bucket's engine pool rows
+};
+
+// A search's layout when the device plans it (the quadtree levels, fracenc_bucket.hip qt_plan):
+// the bucket counts never come back to the host, so every count the host would have passed as a
+// kernel argument lives here, and the kernels (launched on worst-case grids) read it when their
+// args carry a plan pointer.  nr and leaf_base of level k + 1 are written by level k's qt_scatter.
+struct DevPlan {
+    BucketLayout L;      // the MFMA engine's layout (slot_first = 32 · first block, tile_first)
+    uint32_t nr;         // ranges of the level
+    uint32_t leaf_base;  // leaves the previous levels emitted
+    uint32_t nblocks;    // 32-slot range blocks (without T = 8's flipped copies)
+    uint32_t ntiles;     // 32-row domain tiles
+    uint32_t nwork;      // search work items (workgroups that do work)
+    uint32_t nslots;     // range slots, 32 per block (resolve_dft: without the flipped copies)
+    uint32_t flip_slots; // T = 8 Fourier: slot s's flipped copy is s + flip_slots (0: none)
+    uint32_t pad_;
+};
+
 struct SearchArgs {
     const uint8_t* tgt;
     uint32_t tstride;

@@ -510,6 +510,8 @@ struct DftPrepInit {
     uint32_t* fb_count = nullptr; // set to fbc when not null
     uint32_t fbc = 0;
     uint32_t dblocks = 0; // blocks of the domain build
+    const DevPlan* plan = nullptr; // device-planned search: tile / block / range counts from the plan
+    uint32_t copies = 1;           // with a plan: range blocks per planned block (T = 8 Fourier: 2)
 };
 
 template <int FORM>
@@ -518,6 +520,11 @@ __global__ void __launch_bounds__(256) dft_prep(MfmaDomainPrepArgs d, DftDomainB
                                                 uint32_t* __restrict__ rguard, DftPrepInit in)
 {
     const uint32_t gt = blockIdx.x * blockDim.x + threadIdx.x;
+    if (in.plan) {
+        d.ntiles = in.plan->ntiles;
+        apply_plan(r, in.copies);
+        in.nr = in.plan->nr;
+    }
     for (uint32_t i = gt; i < in.nr; i += gridDim.x * blockDim.x)
         in.best_key[i] = ~0ull;
     if (gt == 0 && in.fb_count)
@@ -954,6 +961,8 @@ __global__ void __launch_bounds__(64 * WAVES) search_dft(DftArgs d)
 {
     static_assert(kTuningBuild || (VAR & (8 | 16 | 32 | 64 | 256 | 512)) == 0,
                   "search_dft ablations exist only in FRAC_TUNING builds");
+    if (past_plan(d.m))
+        return;
     const MfmaSearchArgs& a = d.m;
     constexpr int KS = DftForm<VAR>::KS, NBF = DftForm<VAR>::NBF;
     constexpr uint32_t kTilesPerStage = TPS; // LDS stage; chunks stay 4 tiles (resolve_dft)
@@ -1410,6 +1419,7 @@ __device__ inline void resolve_dft_slot(const MfmaResolveArgs& a, uint32_t slot,
 template <bool SORTED = false>
 __global__ void __launch_bounds__(256) resolve_dft(MfmaResolveArgs a)
 {
+    apply_plan(a);
     // the slot is wave-uniform: readfirstlane lets its loads go through the scalar unit
     const uint32_t slot = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
     if (slot < a.nslots)

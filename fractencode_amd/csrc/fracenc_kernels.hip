@@ -248,6 +248,7 @@ struct FitArgs {
     RangeAux* aux;
     uint32_t* fb_count;
     uint32_t* fb_list;
+    const DevPlan* plan = nullptr; // device-planned search: nr from the plan (the grid is a bound)
 };
 
 __device__ inline void write_fit(frac_encode_item& o, const frac_grid_item& rg, const frac_grid_item& d, int t,
@@ -406,6 +407,8 @@ template <int N>
 __global__ void __launch_bounds__(256) fit_rstat(FitArgs a, const uint4* __restrict__ rstat)
 {
     constexpr int NN = N * N;
+    if (a.plan)
+        a.nr = a.plan->nr;
     const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= a.nr)
         return;
@@ -441,6 +444,8 @@ template <int N>
 __global__ void __launch_bounds__(256) fit_winner(FitArgs a)
 {
     constexpr int L = fit_lanes<N>(), RPW = 64 / L;
+    if (a.plan)
+        a.nr = a.plan->nr;
     const int lane = threadIdx.x & 63;
     const uint32_t w = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
     fit_range<N>(a, w * RPW + (uint32_t)(lane / L), lane % L);

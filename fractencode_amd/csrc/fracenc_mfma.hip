@@ -57,12 +57,15 @@ struct MfmaDomainPrepArgs {
     uint32_t ntiles;
     uint4* dtiles;              // [ntiles][KS][64] 16 B
     uint32_t* dconst;           // [ntiles][2][16]
+    const DevPlan* plan = nullptr; // device-planned search: ntiles from the plan (the grid is a bound)
 };
 
 template <int N>
 __global__ void __launch_bounds__(256) mfma_domain_prep(MfmaDomainPrepArgs a)
 {
     constexpr int NN = N * N, KS = MfmaGeom<N>::KS;
+    if (a.plan)
+        a.ntiles = a.plan->ntiles;
     const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
     if (gid >= a.ntiles * 32u)
         return;
@@ -114,12 +117,24 @@ struct MfmaRangePrepArgs {
     uint32_t* rconst;          // [nblocks*32]
     uint32_t* rorb = nullptr;  // dft_range_prep: [nblocks*32][32] pixel pairs in orbit order (resolve_dft)
     uint32_t flip_from = ~0u;  // dft_range_prep: blocks from here on hold their range read through Flip (T = 8)
+    const DevPlan* plan = nullptr; // device-planned search: the block count (and flip_from) from the plan
 };
+
+// the range-block count of a device-planned search (T = 8 Fourier: the originals and their copies)
+__device__ inline void apply_plan(MfmaRangePrepArgs& a, uint32_t copies)
+{
+    if (!a.plan)
+        return;
+    a.nblocks = a.plan->nblocks * copies;
+    if (a.flip_from != ~0u)
+        a.flip_from = a.plan->nblocks;
+}
 
 template <int N>
 __global__ void __launch_bounds__(256) mfma_range_prep(MfmaRangePrepArgs a)
 {
     constexpr int NN = N * N, KS = MfmaGeom<N>::KS;
+    apply_plan(a, 1);
     const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t per_block = a.T * KS * 64u;
     if (gid >= a.nblocks * per_block)
@@ -171,7 +186,14 @@ struct MfmaSearchArgs {
     uint32_t nwork;
     uint32_t hitH;         // valid when HITS
     uint2* entries;        // [nwork*4][T][64] {min v (0 = hit), tile}
+    const DevPlan* plan = nullptr; // device-planned search: workgroups past plan->nwork leave at once
 };
+
+// a workgroup of a device-planned search's worst-case grid with no work item
+__device__ inline bool past_plan(const MfmaSearchArgs& a)
+{
+    return a.plan && blockIdx.x >= a.plan->nwork;
+}
 
 // CS: uint4 of epilogue constants per tile (8 = [2][16] u32; the Fourier search pads them to 16, one
 // LDS-DMA piece per 4-tile stage, fracenc_dft.hip kDftCS)
@@ -354,6 +376,8 @@ template <int N, int T, bool HITS, int VAR>
 __global__ void __launch_bounds__(256) search_mfma(MfmaSearchArgs a)
 {
     static_assert(kTuningBuild || (VAR & (8 | 16)) == 0, "search_mfma ablations exist only in FRAC_TUNING builds");
+    if (past_plan(a))
+        return;
     constexpr int KS = MfmaGeom<N>::KS;
     constexpr int STAGE = kTilesPerStage * KS * 64 + kTilesPerStage * 8; // uint4 per stage
     // two distinct LDS objects: the stage loop is unrolled by two so the LDS-DMA into
@@ -456,6 +480,8 @@ __global__ void __launch_bounds__(64 * T) search_mfma16(MfmaSearchArgs a)
 {
     constexpr int KS = MfmaGeom<16>::KS; // 16
     constexpr int STAGE = kTilesPerStage16 * KS * 64 + kTilesPerStage16 * 8;
+    if (past_plan(a))
+        return;
     __shared__ uint4 lds0[STAGE];
     __shared__ uint4 lds1[STAGE];
     const uint4 wk = a.work[blockIdx.x];
@@ -554,7 +580,18 @@ struct MfmaResolveArgs {
     uint4* rstat = nullptr;     // [nr] the winner's {X_t, ΣD4 | Σr << 16, ΣD4², Σr²} (fit_rstat)
     uint32_t flip_slots = 0;    // T = 8 Fourier: slot s's flipped copy is slot s + flip_slots (0: none)
     int merged = 0;             // resolve_mfma: entries hold the minimum over every transform (search_mfma VAR 128)
+    const DevPlan* plan = nullptr; // device-planned search: nr, ntiles, nslots, flip_slots from the plan
 };
+
+__device__ inline void apply_plan(MfmaResolveArgs& a)
+{
+    if (!a.plan)
+        return;
+    a.nr = a.plan->nr;
+    a.ntiles = a.plan->ntiles;
+    a.nslots = a.plan->nslots;
+    a.flip_slots = a.plan->flip_slots;
+}
 
 __device__ inline int fwd_rt(const Aff& a, int N, int q)
 {
@@ -584,6 +621,7 @@ template <int N>
 __global__ void __launch_bounds__(256) resolve_mfma(MfmaResolveArgs a)
 {
     constexpr int NN = N * N, K2 = NN / 2, WPL = K2 >= 4 ? K2 / 4 : 1; // pool words per lane slice
+    apply_plan(a);
     const uint32_t r = blockIdx.x * 4u + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     if (r >= a.nr)

@@ -79,7 +79,10 @@ def test_gpu_quadtree_stats_are_the_levels_stats(cls, thr):
         assert np.shares_memory(items, buf)
         items2, st2 = e.encode_quadtree(16, 4, split)
         np.testing.assert_array_equal(items, items2)
-        keys = ("rejected_mappings", "total_mappings", "hit_ranges", "fallback_ranges", "empty_ranges")
+        # (round 4: the device-planned levels count total / evaluated pairs and the search's MFMA flops
+        # on the device, from their own layout: they must equal the host-planned searches' counts)
+        keys = ("rejected_mappings", "total_mappings", "hit_ranges", "fallback_ranges", "empty_ranges",
+                "evaluated_mappings", "matrix_flops")
         want = dict.fromkeys(keys, 0)
         ranges = F.create_uniform_grid(512, 512, 16, 16)
         leaves = []
@@ -129,3 +132,47 @@ def test_gpu_quadtree_restores_the_list_state():
             f.set_domains(doms)
             want, _ = f.search(rngs)
         np.testing.assert_array_equal(out, want)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sizes", [(16, 4), (16, 2), (8, 2), (16, 16), (4, 2)])
+@pytest.mark.parametrize("cls,T,thr,split", [(True, 4, 0.0, 8.0), (False, 8, 2.0, 1.0), (True, 8, 0.0, 1e9),
+                                             (True, 4, 0.0, 0.0), (False, 4, 0.0, 20.0)])
+def test_gpu_quadtree_device_planned_equals_host_planned(sizes, cls, T, thr, split):
+    """The MFMA engine's quadtree levels are laid out on the device (qt_plan: bucket bounds, work lists,
+    CSR map and every count stay in HBM; worst-case grids; one round trip per frame).  The VALU engine
+    keeps the host-planned levels (bucket counts and split counts read back per level).  Both must give
+    the same leaves and the same summed counters, for every level-size range, with and without the
+    classifier, T = 4 / 8 (the n = 8 level's Fourier form with flipped copies), a hit threshold, a
+    split that empties the later levels (1e9) and one that splits every inexact range (0)."""
+    p = plane("lenna_y")
+    res = {}
+    for eng in (F.ENGINE_VALU, F.ENGINE_AUTO):
+        with F.Engine(0, T, cls, thr, -1.0, eng, timing=True) as e:
+            e.set_frame(p)
+            res[eng] = e.encode_quadtree(*sizes, split)
+    (a, sa), (b, sb) = res[F.ENGINE_VALU], res[F.ENGINE_AUTO]
+    np.testing.assert_array_equal(a, b)
+    for k in ("rejected_mappings", "total_mappings", "hit_ranges", "fallback_ranges", "empty_ranges",
+              "evaluated_mappings"):
+        assert sa[k] == sb[k], k
+    assert sb["engine"] == F.ENGINE_MFMA and sb["matrix_flops"] > 0
+    assert sb["ms_device"] > 0 and sb["ms_search"] > 0
+    assert (_coverage(b, b["w"], 512, 512, sizes[0]) == 1).all()
+
+
+@pytest.mark.gpu
+def test_gpu_quadtree_device_planned_across_frames():
+    # one engine, frames of different content and size in turn (the cached level grids, the plans and
+    # the buffers sized by the first frame are reused or regrown): each equals a fresh engine's frame
+    lenna = plane("lenna_y")
+    frames = [lenna, lenna[::-1, ::-1].copy(), plane("crop64"), lenna[:256, :384].copy(), lenna]
+    with F.Engine(0, 4, True) as e:
+        for i, p in enumerate(frames):
+            e.set_frame(p)
+            got, sg = e.encode_quadtree(16, 4, 4.0)
+            with F.Engine(0, 4, True, 0.0, -1.0, F.ENGINE_VALU) as f:
+                f.set_frame(p)
+                want, sw = f.encode_quadtree(16, 4, 4.0)
+            np.testing.assert_array_equal(got, want, err_msg=f"frame {i}")
+            assert sg["rejected_mappings"] == sw["rejected_mappings"], i
