@@ -683,7 +683,7 @@ int prepare(frac_ctx* c)
             return c->fail(FRAC_E_INVALID, "range outside the target plane");
     }
     if (nw < 2 || nw > kGenMaxN || nh < 2 || nh > kGenMaxN)
-        return c->fail(FRAC_E_INVALID, "range sides must be 2..32");
+        return c->fail(FRAC_E_INVALID, "range sides must be 2..256");
     // domains: validated by frac_set_domains (one size, inside the plane); re-checked against the
     // current plane, which may have changed since
     const uint32_t Sw = c->doms.empty() ? 2u * nw : c->doms[0].w;

@@ -22,7 +22,7 @@
 // error with ties to the earliest domain and then to the later transform (the reference's order,
 // encode/TransformEstimator2.hpp:34, transformmatcher.h:57,67), and gen_fit turns v back into
 // (domain, transform), moves a hit to the first transform of its domain that meets the threshold,
-// and fits with the fit-point samples.  Range sizes other than 2, 4, 8, 16 (any n ≤ 32) search
+// and fits with the fit-point samples.  Range sizes other than 2, 4, 8, 16 (any side up to 256) search
 // with gen_search.  The fp32 fallback (gen_fallback) replays the reference's sequential fp32 sum.
 #include "fracenc_common.h"
 
@@ -130,11 +130,16 @@ struct GenSearchArgs {
     unsigned long long* best_key;
 };
 
-constexpr uint32_t kGenMaxN = 32; // range sides (nw, nh ≤ 32: one wave's LDS copy of the range)
+// Range sides up to 256 (match_generic takes any size, transformmatcher.h:80-111; the CLI any
+// 2 ≤ target < source, main.cpp:99): the largest S16 of a 256×256 range, 65,536 · 1020², stays below
+// 2^36, the key's error field (fracenc_common.h key_miss).
+constexpr uint32_t kGenMaxN = 256;
+// gen_search holds the range in LDS (as 4r) in chunks of kGenChunk pixels per wave
+constexpr uint32_t kGenChunk = 4096;
 
 __global__ void __launch_bounds__(256) gen_search(GenSearchArgs a)
 {
-    __shared__ int16_t r4[4][kGenMaxN * kGenMaxN];
+    __shared__ int16_t r4[4][kGenChunk];
     const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
     const uint32_t r = blockIdx.x * 4u + wv;
     if (r >= a.nr)
@@ -142,26 +147,44 @@ __global__ void __launch_bounds__(256) gen_search(GenSearchArgs a)
     const GenArgs& g = a.g;
     const frac_grid_item rg = g.ranges[r];
     const uint32_t NN = g.nw * g.nh;
-    for (uint32_t q = lane; q < NN; q += 64)
-        r4[wv][q] = (int16_t)(4 * (int)g.tgt[(size_t)(rg.y + q / g.nw) * g.tstride + rg.x + q % g.nw]);
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    auto load_chunk = [&](uint32_t c0) {
+        __builtin_amdgcn_wave_barrier(); // the previous chunk's reads are done (the wave runs in lockstep)
+        for (uint32_t q = lane; q < kGenChunk && c0 + q < NN; q += 64) {
+            const uint32_t qq = c0 + q;
+            r4[wv][q] = (int16_t)(4 * (int)g.tgt[(size_t)(rg.y + qq / g.nw) * g.tstride + rg.x + qq % g.nw]);
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    };
     const uint2 seg = a.rbucket[r];
     unsigned long long best = kKeyNone;
-    for (uint32_t v = seg.x + lane; v < seg.y; v += 64) {
-        const uint32_t* row = g.pool + (size_t)v * g.K2;
+    const bool one_chunk = NN <= kGenChunk;
+    if (one_chunk)
+        load_chunk(0);
+    // rows in groups of 64, one per lane; a range larger than one chunk streams its chunks per group
+    for (uint32_t v0 = seg.x; v0 < seg.y; v0 += 64) {
+        const uint32_t v = v0 + lane;
+        const uint32_t* row = g.pool + (size_t)min(v, seg.y - 1) * g.K2;
         uint64_t s = 0;
-        for (uint32_t k = 0; k < g.K2; ++k) {
-            const uint32_t w = row[k];
-            const int e0 = (int)r4[wv][2 * k] - (int)(w & 0xffffu);
-            s += (uint64_t)(e0 * e0);
-            if (2 * k + 1 < NN) {
-                const int e1 = (int)r4[wv][2 * k + 1] - (int)(w >> 16);
-                s += (uint64_t)(e1 * e1);
+        for (uint32_t c0 = 0; c0 < NN; c0 += kGenChunk) {
+            if (!one_chunk)
+                load_chunk(c0);
+            const uint32_t ce = min(NN, c0 + kGenChunk);
+            for (uint32_t q = c0; q < ce; q += 2) {
+                const uint32_t w = row[q >> 1];
+                const int e0 = (int)r4[wv][q - c0] - (int)(w & 0xffffu);
+                s += (uint64_t)(e0 * e0);
+                if (q + 1 < ce) {
+                    const int e1 = (int)r4[wv][q + 1 - c0] - (int)(w >> 16);
+                    s += (uint64_t)(e1 * e1);
+                }
             }
         }
-        const unsigned long long key = (a.hitH >= 0 && (int64_t)s <= a.hitH) ? key_hit(v, 0) : key_miss(s, v, 0);
-        best = key < best ? key : best;
+        if (v < seg.y) {
+            const unsigned long long key =
+                (a.hitH >= 0 && (int64_t)s <= a.hitH) ? key_hit(v, 0) : key_miss(s, v, 0);
+            best = key < best ? key : best;
+        }
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
@@ -295,21 +318,30 @@ struct GenFallbackArgs {
     RangeAux* aux;
 };
 
+// the range's pixels as int16 in LDS (the fp32 value of each is exact): up to 128×128; a larger
+// range reads them from the plane (a wave-uniform address per step)
+constexpr uint32_t kGenFbLds = 128 * 128;
+
 __global__ void __launch_bounds__(256) gen_fallback(GenFallbackArgs a)
 {
-    __shared__ float rpix[kGenMaxN * kGenMaxN];
+    __shared__ int16_t rpx[kGenFbLds];
     __shared__ unsigned long long red[256];
     const GenArgs& g = a.g;
     const uint32_t NN = g.nw * g.nh, T = g.T;
+    const bool in_lds = NN <= kGenFbLds;
+    frac_grid_item rg{};
+    auto rpix = [&](uint32_t q) -> float {
+        return in_lds ? (float)rpx[q] : (float)(int16_t)g.tgt[(size_t)(rg.y + q / g.nw) * g.tstride + rg.x + q % g.nw];
+    };
     const uint32_t count = *a.fb_count;
     for (uint32_t e = blockIdx.x; e < count; e += gridDim.x) {
         const uint32_t r = a.fb_list[e];
-        const frac_grid_item rg = g.ranges[r];
+        rg = g.ranges[r];
         const uint2 seg = a.rbucket[r];
         const uint32_t p0 = seg.x / T; // the bucket's first pool position
         __syncthreads();
-        for (uint32_t q = threadIdx.x; q < NN; q += blockDim.x)
-            rpix[q] = (float)(int16_t)g.tgt[(size_t)(rg.y + q / g.nw) * g.tstride + rg.x + q % g.nw];
+        for (uint32_t q = threadIdx.x; in_lds && q < NN; q += blockDim.x)
+            rpx[q] = (int16_t)g.tgt[(size_t)(rg.y + q / g.nw) * g.tstride + rg.x + q % g.nw];
         __syncthreads();
         const double area = (double)(g.Sw * g.Sh);
         unsigned long long best = kKeyNone;
@@ -319,7 +351,7 @@ __global__ void __launch_bounds__(256) gen_fallback(GenFallbackArgs a)
             for (uint32_t q = 0; q < NN; ++q) {
                 const uint32_t w = row[q >> 1];
                 const float smp = (float)((q & 1) ? (w >> 16) : (w & 0xffffu)) / 4.0f;
-                const float val = __fsub_rn(rpix[q], smp);
+                const float val = __fsub_rn(rpix(q), smp);
                 F = __fadd_rn(F, __fmul_rn(val, val));
             }
             const uint32_t pl = v / T - p0, tc = v % T; // tc = T − 1 − t
@@ -352,7 +384,7 @@ __global__ void __launch_bounds__(256) gen_fallback(GenFallbackArgs a)
                 for (uint32_t q = 0; q < NN; ++q) {
                     const uint32_t w = row[q >> 1];
                     const float smp = (float)((q & 1) ? (w >> 16) : (w & 0xffffu)) / 4.0f;
-                    const float val = __fsub_rn(rpix[q], smp);
+                    const float val = __fsub_rn(rpix(q), smp);
                     F = __fadd_rn(F, __fmul_rn(val, val));
                 }
                 gen_write_fit(g, a.out[r], rg, d, t, 0, a.smax);

@@ -89,11 +89,11 @@ def test_reference_core_with_hip_engine_matches_goldens(tmp_path, name, src, tgt
 
 @pytest.mark.gpu
 def test_hip_engine_failure_comes_back_on_the_callers_thread(tmp_path):
-    # 64×64 ranges (128×128 domains: the CLI accepts them, main.cpp:99) are beyond the engine's range
-    # sides (2..32): frac_search fails inside finalize() on the core's worker thread; the binding keeps
-    # the error and the driver's rethrowIfFailed() reports it after the workers joined (exit 6), where
-    # a throw on the worker would have been std::terminate (SIGABRT)
-    r = _run_core(tmp_path, "lenna_y", 512, 512, 128, 64, False, check=False)
+    # a 300×300 range against a 512×512 domain (the CLI accepts it, main.cpp:99) is beyond the engine's
+    # range sides (2..256, the largest whose S16 fits the key): frac_search fails inside finalize() on the
+    # core's worker thread; the binding keeps the error and the driver's rethrowIfFailed() reports it after
+    # the workers joined (exit 6), where a throw on the worker would have been std::terminate (SIGABRT)
+    r = _run_core(tmp_path, "lenna_y", 512, 512, 512, 300, False, check=False)
     assert r.returncode == 6, (r.returncode, r.stdout[-2000:], r.stderr[-2000:])
-    assert "HIP engine failed" in r.stderr and "range sides must be 2..32" in r.stderr
-    assert "64 ranges without a record" in r.stderr
+    assert "HIP engine failed" in r.stderr and "range sides must be 2..256" in r.stderr
+    assert "1 ranges without a record" in r.stderr

@@ -165,6 +165,10 @@ def main():
     planes["crop48"] = np.ascontiguousarray(y[256:304, 256:304])
     planes["crop60"] = np.ascontiguousarray(y[256:316, 256:316])
     planes["inexact48"] = np.ascontiguousarray(inexact[:48, :48])
+    # range sides above 32 (round 4): frames that are multiples of the item sizes (partition2.hpp:119)
+    planes["crop480"] = np.ascontiguousarray(y[16:496, 16:496])
+    planes["crop360"] = np.ascontiguousarray(y[100:460, 60:420])
+    planes["crop400"] = np.ascontiguousarray(y[56:456, 56:456])
     # Lenna RGB (the reference's own test input, decoded losslessly; checked against the
     # reference loader's planes below) and a seeded synthetic RGB frame with odd sizes
     from PIL import Image
@@ -226,6 +230,13 @@ def main():
         ("crop60_5to4", "crop60", dict(src=5, tgt=4, T=4)),
         ("inexact64_32to8_t8", "inexact64", dict(src=32, tgt=8, T=8)),
         ("inexact48_12to6", "inexact48", dict(src=12, tgt=6, T=4)),
+        # range sides above 32 (match_generic at any size, transformmatcher.h:80-111; ΣA as u32 above
+        # 16 wide, ImageStatistics.cpp:4-11): ratio 2 at 64, 48, 40 and 36, with T = 8, the classifier, a threshold
+        ("lenna_128to64", "lenna_y", dict(src=128, tgt=64, T=4)),
+        ("lenna_128to64_t8", "lenna_y", dict(src=128, tgt=64, T=8)),
+        ("crop480_96to48_cls", "crop480", dict(src=96, tgt=48, T=4, cls=True)),
+        ("crop400_80to40_thr", "crop400", dict(src=80, tgt=40, T=4, thr=110.0)),
+        ("crop360_72to36_t8", "crop360", dict(src=72, tgt=36, T=8)),
     ]
     for name, pk, p in jobs:
         if not want(name):
