@@ -58,7 +58,8 @@ def parse():
     ap.add_argument("--engine", default="auto", choices=["auto", "valu", "mfma"])
     ap.add_argument("--size", type=int, default=4096)
     ap.add_argument("--transforms", type=int, default=4)
-    ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of CPU-baseline sampling (0 = skip)")
+    ap.add_argument("--cpu-budget", type=float, default=45.0,
+                    help="cap in seconds on the CPU-baseline sample (1,024 ranges, ≈28 s at 16 threads; 0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every core this process may use")
     ap.add_argument("--alt-steps", type=int, default=2,
                     help="steps of the VALU engine (north_star's no-MFMA formulation) reported beside (0 = skip)")
@@ -127,13 +128,14 @@ def host_cores() -> tuple[int, dict]:
 
 def cpu_baseline(frame: np.ndarray, budget: float, threads: int, host: dict):
     """Reference CPU path (oracle/_ref, the unmodified reference built by oracle/ref/Makefile)
-    timed on this host on a bounded strided sample of the same workload; the oracle
+    timed on this host on SURVEY §8(d)'s sample of the same workload: the 1,024 ranges i·256 of the
+    C3 frame (every ⌈n/1024⌉-th range of another frame), capped at `budget` seconds; the oracle
     restatement ("port") when the reference build is absent."""
     from oracle import oracle as O
 
     H, W = frame.shape
     n_ranges = (W // 8) * (H // 8)
-    sel = np.arange(0, n_ranges, max(1, n_ranges // 4096), dtype=np.uint32)
+    sel = np.arange(0, n_ranges, max(1, -(-n_ranges // 1024)), dtype=np.uint32)
     t0 = time.perf_counter()
     if O.ref_lib() is not None:
         _, _, done = O.ref_estimate(frame, 16, 8, 4, sel=sel, threads=threads, budget_s=budget)

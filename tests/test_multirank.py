@@ -142,8 +142,9 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("world", [2])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_gloo_sharded_search_matches_single_rank(tmp_path, oracle, world):
+    # the world sizes the driver's scaling run uses (1/2/4/8 GPUs), with a ragged range count
     import fractencode_amd as F
     path = str(tmp_path / "full.npy")
     mp.spawn(_worker, args=(world, _free_port(), path), nprocs=world, join=True)
@@ -160,19 +161,20 @@ def test_gloo_sharded_search_matches_single_rank(tmp_path, oracle, world):
     np.testing.assert_array_equal(full["brightness"], want["o"])
 
 
-def test_gloo_cost_balanced_classifier_shards_match_single_rank(tmp_path, oracle):
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_gloo_cost_balanced_classifier_shards_match_single_rank(tmp_path, oracle, world):
     """Classifier on: cost-balanced (unequal-count) shards, padded all-gather, same records as one
-    rank (the oracle)."""
+    rank (the oracle), at the driver's world sizes."""
     import fractencode_amd as F
     path = str(tmp_path / "full.npy")
-    mp.spawn(_cls_worker, args=(2, _free_port(), path), nprocs=2, join=True)
+    mp.spawn(_cls_worker, args=(world, _free_port(), path), nprocs=world, join=True)
     full = np.load(path)
     rng = np.random.default_rng(5)
     plane = rng.integers(0, 256, (64, 96), dtype=np.uint8)
     doms = F.preclassify(plane, F.create_uniform_grid(96, 64, 16, 8))
     rngs = F.preclassify(plane, F.create_uniform_grid(96, 64, 8, 8))
-    plan = shard_plan(len(rngs), 2, range_costs(rngs, doms))
-    assert plan[0][1] - plan[0][0] != plan[1][1] - plan[1][0]  # the plan is not the equal split
+    plan = shard_plan(len(rngs), world, range_costs(rngs, doms))
+    assert plan != shard_plan(len(rngs), world)  # the plan is not the equal split
     want, _, _ = oracle.estimate(plane, doms.astype(oracle.ITEM_DTYPE), rngs.astype(oracle.ITEM_DTYPE),
                                  use_classifier=True)
     for a, b in (("dx", "dx"), ("dy", "dy"), ("transform", "t"), ("distance", "dist"), ("contrast", "s"),
