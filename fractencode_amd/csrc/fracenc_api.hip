@@ -292,6 +292,7 @@ struct frac_ctx {
     uint32_t engine_ran = FRAC_ENGINE_VALU;
     uint32_t form_ran = FRAC_FORM_DOT2;
     bool fit_rstat = false; // resolve_dft recorded the winners' sums (fit_rstat instead of fit_winner)
+    bool fit_fused = false; // resolve_dft wrote the records itself (no fit launch)
     uint64_t flops_ran = 0;
 
     int fail(int code, const std::string& msg)
@@ -1240,6 +1241,30 @@ inline bool dft_route(const frac_ctx* c)
     return (c->Teff == 4 || c->dft_copies == 2) && !c->virt && mfma_dft_enabled(c);
 }
 
+// The fit kernels' arguments for the current run (also carried by resolve_dft when it fuses the fit)
+inline FitArgs fit_args(const frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, uint32_t nr)
+{
+    FitArgs f;
+    f.tgt = dtgt;
+    f.tstride = tstride;
+    f.ranges = c->d_ranges.ptr;
+    f.doms = c->d_doms.ptr;
+    f.porig = c->d_porig.ptr;
+    f.pool = c->d_pool.ptr;
+    f.best_key = c->d_best_key.ptr;
+    f.nr = nr;
+    f.T = c->p.transforms;
+    f.hitH = c->hitH;
+    f.smax = c->p.s_max;
+    f.all_fallback = 0;
+    f.out = c->d_out.ptr;
+    f.aux = c->d_aux.ptr;
+    f.fb_count = c->d_fb_count.ptr;
+    f.fb_list = c->d_fb_list.ptr;
+    f.plan = c->qplan;
+    return f;
+}
+
 // work items a search launch covers: the host-built list, or a device-planned level's bound (its
 // workgroups past DevPlan::nwork leave at once)
 inline uint32_t launch_nwork(const frac_ctx* c, const std::vector<uint4>& w)
@@ -1532,7 +1557,9 @@ inline int launch_dft(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool i
         v.plan = c->qplan;
         FRAC_HIP(c, c->d_rstat.ensure(std::max<size_t>(nr, 1)));
         v.rstat = c->d_rstat.ptr;
-        c->fit_rstat = true;
+        v.fused_fit = 1; // the fit in the resolving wave (launch_all skips fit_rstat)
+        v.fit = fit_args(c, dtgt, tstride, nr);
+        c->fit_fused = true;
         // one-wave workgroups: a finished range frees its slot at once (0.254 vs 0.271 ms finish
         // against 4-wave workgroups, 30-sample A/B, profiles/r01/ab_fourier_variants.log)
         resolve_dft<false><<<std::max(1u, v.nslots), 64, 0, c->stream>>>(v);
@@ -1812,7 +1839,9 @@ int launch_tp(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool timing)
     v.rorb = c->d_dft_rorb.ptr;
     FRAC_HIP(c, c->d_rstat.ensure(std::max<size_t>(nr, 1)));
     v.rstat = c->d_rstat.ptr;
-    c->fit_rstat = true;
+    v.fused_fit = 1;
+    v.fit = fit_args(c, dtgt, tstride, nr);
+    c->fit_fused = true;
     // resolve_dft<true> (SORTED) keeps every tie of the ΣD4-ordered chunks but does not merge T = 8's
     // flipped copies (that is the !SORTED path): the tiled form exists for T = 4 only (prepare)
     v.flip_slots = 0;
@@ -2001,6 +2030,7 @@ int launch_all(frac_ctx* c)
     if (timing)
         FRAC_TRY(mark_event(c, 0));
     c->fit_rstat = false;
+    c->fit_fused = false;
     const bool use_mfma = c->engine == FRAC_ENGINE_MFMA && !c->all_fallback;
     // the Fourier path resets best_key and fb_count in its preparation kernel (dft_prep)
     const bool dft_inits = N == 8 && use_mfma && nr && dft_route(c);
@@ -2079,25 +2109,8 @@ int launch_all(frac_ctx* c)
         FRAC_TRY(mark_event(c, 2));
     if (c->virt) {
         FRAC_TRY(launch_gen_finish(c, g));
-    } else if (!c->all_fallback && nr) {
-        FitArgs f;
-        f.tgt = dtgt;
-        f.tstride = tstride;
-        f.ranges = c->d_ranges.ptr;
-        f.doms = c->d_doms.ptr;
-        f.porig = c->d_porig.ptr;
-        f.pool = c->d_pool.ptr;
-        f.best_key = c->d_best_key.ptr;
-        f.nr = nr;
-        f.T = c->p.transforms;
-        f.hitH = c->hitH;
-        f.smax = c->p.s_max;
-        f.all_fallback = 0;
-        f.out = c->d_out.ptr;
-        f.aux = c->d_aux.ptr;
-        f.fb_count = c->d_fb_count.ptr;
-        f.fb_list = c->d_fb_list.ptr;
-        f.plan = c->qplan;
+    } else if (!c->all_fallback && nr && !c->fit_fused) {
+        FitArgs f = fit_args(c, dtgt, tstride, nr);
         if (c->fit_rstat)
             fit_rstat<N><<<(nr + 255) / 256, 256, 0, c->stream>>>(f, c->d_rstat.ptr);
         else
@@ -2120,7 +2133,7 @@ int launch_all(frac_ctx* c)
         b.smax = c->p.s_max;
         b.out = c->d_out.ptr;
         b.aux = c->d_aux.ptr;
-        fallback_fp32<N><<<512, 256, 0, c->stream>>>(b);
+        fallback_fp32<N><<<kFallbackBlocks, 256, 0, c->stream>>>(b);
     }
     if (timing) {
         FRAC_TRY(mark_event(c, 3));

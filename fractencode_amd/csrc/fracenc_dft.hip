@@ -1405,6 +1405,13 @@ __device__ inline void resolve_dft_slot(const MfmaResolveArgs& a, uint32_t slot,
             w = f;
     }
     const uint32_t r = (uint32_t)ri;
+    if (a.fused_fit) { // the range's record right here: one launch less per run (C2: 5 µs of a 43 µs frame)
+        if (lane == 0) {
+            a.best_key[r] = w.bestk;
+            fit_rstat_range<8>(a.fit, r, w.bestk, make_uint4(w.bx, w.bs1 | (w.sr1 << 16), w.bs2, w.sr2));
+        }
+        return;
+    }
     if (lane == 0) {
         a.best_key[r] = w.bestk;
         if (a.rstat && w.bestk != kKeyNone)

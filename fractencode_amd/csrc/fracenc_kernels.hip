@@ -403,17 +403,14 @@ __device__ inline void fit_range(const FitArgs& a, uint32_t r, int sub)
 // ΣD4, ΣD4², Σr and Σr² (MfmaResolveArgs::rstat): one thread per range, no pixel or pool
 // reads; the transform comes from the selection key (resolve_dft emits hit-format keys for
 // every hit, so a miss-format key is a miss). Same formulas and fallback rule as fit_winner.
+//
+// One range's record from its selection key and the winner's sums st = {X_t, ΣD4 | Σr << 16, ΣD4²,
+// Σr²}: fit_rstat's body, also run by resolve_dft's wave when the fit is fused into it
 template <int N>
-__global__ void __launch_bounds__(256) fit_rstat(FitArgs a, const uint4* __restrict__ rstat)
+__device__ inline void fit_rstat_range(const FitArgs& a, uint32_t r, unsigned long long key, const uint4& st)
 {
     constexpr int NN = N * N;
-    if (a.plan)
-        a.nr = a.plan->nr;
-    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= a.nr)
-        return;
     const frac_grid_item rg = a.ranges[r];
-    const unsigned long long key = a.best_key[r];
     if (key == kKeyNone) {
         write_default(a.out[r], rg);
         a.aux[r] = RangeAux{0u, (uint32_t)kAuxEmpty};
@@ -429,13 +426,24 @@ __global__ void __launch_bounds__(256) fit_rstat(FitArgs a, const uint4* __restr
         return;
     }
     const frac_grid_item d = a.doms[a.porig[p]];
-    const uint4 st = rstat[r];
     const long long X = st.x, sD = st.y & 0xffffu, sA = st.y >> 16, sD2 = st.z, sA2 = st.w;
     const long long S16 = 16 * sA2 - 8 * X + sD2;
     const double dist = ((double)S16 * 0.0625) / (double)(d.w * d.h);
     write_fit(a.out[r], rg, d, t, (double)sA, (double)sA2, (double)sD * 0.25, (double)X * 0.25, (double)NN, a.smax,
               dist);
     a.aux[r] = RangeAux{p, hit ? (uint32_t)kAuxHit : 0u};
+}
+
+template <int N>
+__global__ void __launch_bounds__(256) fit_rstat(FitArgs a, const uint4* __restrict__ rstat)
+{
+    if (a.plan)
+        a.nr = a.plan->nr;
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= a.nr)
+        return;
+    const unsigned long long key = a.best_key[r];
+    fit_rstat_range<N>(a, r, key, key == kKeyNone ? make_uint4(0u, 0u, 0u, 0u) : rstat[r]);
 }
 
 // one wave per 64 / L ranges (a grid-stride form over fewer waves measured slower)
@@ -475,6 +483,9 @@ struct FallbackArgs {
     frac_encode_item* out;
     RangeAux* aux;
 };
+
+// one block per CU: an empty list (the usual case) costs the dispatch of these blocks only
+constexpr unsigned kFallbackBlocks = 256;
 
 template <int N>
 __global__ void __launch_bounds__(256) fallback_fp32(FallbackArgs a)

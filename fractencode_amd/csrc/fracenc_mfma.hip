@@ -581,6 +581,9 @@ struct MfmaResolveArgs {
     uint32_t flip_slots = 0;    // T = 8 Fourier: slot s's flipped copy is slot s + flip_slots (0: none)
     int merged = 0;             // resolve_mfma: entries hold the minimum over every transform (search_mfma VAR 128)
     const DevPlan* plan = nullptr; // device-planned search: nr, ntiles, nslots, flip_slots from the plan
+    // resolve_dft: the fit runs in the resolving wave (fit_rstat_range) instead of a fit_rstat launch
+    int fused_fit = 0;
+    FitArgs fit{};
 };
 
 __device__ inline void apply_plan(MfmaResolveArgs& a)
