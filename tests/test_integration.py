@@ -41,7 +41,8 @@ def test_binding_compiles_against_reference_headers(tmp_path):
 
 def _run_core(tmp_path, plane_name, W, H, src, tgt, cls, cpu=False, check=True):
     out = tmp_path / f"core_{src}_{tgt}_{cls}_{int(cpu)}.bin"
-    r = subprocess.run([DRIVER, os.path.join(GOLD, plane_name + ".u8"), str(W), str(H), str(src), str(tgt),
+    plane_path = plane_name if os.path.isabs(plane_name) else os.path.join(GOLD, plane_name + ".u8")
+    r = subprocess.run([DRIVER, plane_path, str(W), str(H), str(src), str(tgt),
                         str(int(cls)), "0", "-1", str(out), str(int(cpu))], timeout=600, capture_output=True, text=True)
     if not check:
         return r
@@ -89,11 +90,14 @@ def test_reference_core_with_hip_engine_matches_goldens(tmp_path, name, src, tgt
 
 @pytest.mark.gpu
 def test_hip_engine_failure_comes_back_on_the_callers_thread(tmp_path):
-    # a 300×300 range against a 512×512 domain (the CLI accepts it, main.cpp:99) is beyond the engine's
-    # range sides (2..256, the largest whose S16 fits the key): frac_search fails inside finalize() on the
-    # core's worker thread; the binding keeps the error and the driver's rethrowIfFailed() reports it after
-    # the workers joined (exit 6), where a throw on the worker would have been std::terminate (SIGABRT)
-    r = _run_core(tmp_path, "lenna_y", 512, 512, 512, 300, False, check=False)
+    # 512×512 ranges against 1024×1024 domains (the CLI accepts them, main.cpp:99; the grids are aligned,
+    # image/partition2.hpp:119) are beyond the engine's range sides (2..256, the largest whose S16 fits the
+    # key): frac_search fails inside finalize() on the core's worker thread; the binding keeps the error and
+    # the driver's rethrowIfFailed() reports it after the workers joined (exit 6), where a throw on the
+    # worker would have been std::terminate (SIGABRT)
+    plane = tmp_path / "flat1024.u8"
+    np.full((1024, 1024), 77, np.uint8).tofile(plane)
+    r = _run_core(tmp_path, str(plane), 1024, 1024, 1024, 512, False, check=False)
     assert r.returncode == 6, (r.returncode, r.stdout[-2000:], r.stderr[-2000:])
     assert "HIP engine failed" in r.stderr and "range sides must be 2..256" in r.stderr
-    assert "1 ranges without a record" in r.stderr
+    assert "4 ranges without a record" in r.stderr

@@ -5,7 +5,7 @@ set -euo pipefail
 R=$(pwd)
 O=$R/gpurun_out/r04_s1
 mkdir -p $O
-bash tools/gpu_suite.sh r04s1 -k "integration or failure_comes_back or quadtree or fourier_and_direct or operand_extremes or product_form or stress_frame or decoders_agree or goldens or classify"
+bash tools/gpu_suite.sh r04s1 -k "integration or failure_comes_back or quadtree or new_frame or default_cli or sampled_form or rectangular or fourier_and_direct or operand_extremes or product_form or stress_frame or decoders_agree or goldens or classify"
 timeout -k 10 300 python3 tools/bench_paths.py --only c4q c4 --steps 20 --warmup 3 > $O/paths.jsonl 2> $O/paths.err
 cat $O/paths.jsonl
 QT_CALLS=3 timeout -k 10 120 python3 tools/trace_c4q.py 0.05 > $O/trace_c4q.log 2>&1
