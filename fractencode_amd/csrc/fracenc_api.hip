@@ -188,7 +188,7 @@ struct frac_ctx {
     DBuf<uint4> d_work;
     DBuf<uint2> d_rbucket;
     DBuf<uint32_t> d_rord, d_rkey;           // bucket-sorted range order; per range bucket
-    DBuf<uint32_t> d_bk_keys, d_bk_keys2, d_bk_iota, d_bk_first, d_bk_err;
+    DBuf<uint32_t> d_bk_keys, d_bk_keys2, d_bk_iota, d_bk_first, d_bk_err, d_bk_cnt;
     DBuf<uint8_t> d_bk_tmp;
     size_t bk_tmp_bytes = 0;
     DBuf<unsigned long long> d_best_key;
@@ -480,38 +480,23 @@ int device_buckets(frac_ctx* c, int nb, uint32_t* dfirst, uint32_t* rfirst)
     HostTrace tr("buckets");
     const uint32_t m = std::max(std::max(nd, nr), 1u);
     FRAC_HIP(c, c->d_bk_keys.ensure(m));
-    FRAC_HIP(c, c->d_bk_keys2.ensure(m));
-    FRAC_HIP(c, c->d_bk_iota.ensure(m));
+    FRAC_HIP(c, c->d_bk_cnt.ensure((size_t)((m + kBkTile - 1) / kBkTile) * kMaxBuckets));
     FRAC_HIP(c, c->d_bk_first.ensure(2 * (kMaxBuckets + 1) + 1));
-    size_t need = 0;
-    FRAC_HIP(c, sort_pairs_u32(nullptr, need, c->d_bk_keys.ptr, c->d_bk_keys2.ptr, c->d_bk_iota.ptr, c->d_porig.ptr, m,
-                               3, c->stream));
-    if (need > c->bk_tmp_bytes) {
-        FRAC_HIP(c, c->d_bk_tmp.ensure(need));
-        c->bk_tmp_bytes = need;
-    }
     tr.mark("alloc");
     uint32_t* first = c->d_bk_first.ptr;
     uint32_t* err = first + 2 * (kMaxBuckets + 1);
     FRAC_HIP(c, hipMemsetAsync(err, 0, sizeof(uint32_t), c->stream));
     const uint8_t* tplane = c->same_plane ? c->d_src.ptr : c->d_tgt.ptr;
     const uint32_t tstride = c->same_plane ? c->d_sstride : c->d_tstride;
-    size_t tb = c->bk_tmp_bytes;
-    if (nd) { // a stored −1 is classified on the item's own plane (Classifier2::compare, Classifier2.cpp:70-81)
-        launch_bucket_keys(c->d_doms.ptr, nd, c->Sh, c->d_src.ptr, c->d_sstride, c->d_bk_keys.ptr, c->d_bk_iota.ptr,
-                           err, c->stream);
-        FRAC_HIP(c, sort_pairs_u32(c->d_bk_tmp.ptr, tb, c->d_bk_keys.ptr, c->d_bk_keys2.ptr, c->d_bk_iota.ptr,
-                                   c->d_porig.ptr, nd, 3, c->stream));
-    }
-    bucket_bounds<<<1, 64, 0, c->stream>>>(c->d_bk_keys2.ptr, nd, first);
-    tb = c->bk_tmp_bytes;
-    if (nr) {
-        launch_bucket_keys(c->d_ranges.ptr, nr, c->nh, tplane, tstride, c->d_rkey.ptr, c->d_bk_iota.ptr, err,
+    // a stored −1 is classified on the item's own plane (Classifier2::compare, Classifier2.cpp:70-81);
+    // the pool order porig and the bucket-sorted ranges rord by the stable bucket sort
+    if (nd)
+        launch_bucket_keys(c->d_doms.ptr, nd, c->Sh, c->d_src.ptr, c->d_sstride, c->d_bk_keys.ptr, nullptr, err,
                            c->stream);
-        FRAC_HIP(c, sort_pairs_u32(c->d_bk_tmp.ptr, tb, c->d_rkey.ptr, c->d_bk_keys2.ptr, c->d_bk_iota.ptr,
-                                   c->d_rord.ptr, nr, 3, c->stream));
-    }
-    bucket_bounds<<<1, 64, 0, c->stream>>>(c->d_bk_keys2.ptr, nr, first + kMaxBuckets + 1);
+    launch_bucket_sort(c->d_bk_keys.ptr, nd, nullptr, c->d_bk_cnt.ptr, first, c->d_porig.ptr, c->stream);
+    if (nr)
+        launch_bucket_keys(c->d_ranges.ptr, nr, c->nh, tplane, tstride, c->d_rkey.ptr, nullptr, err, c->stream);
+    launch_bucket_sort(c->d_rkey.ptr, nr, nullptr, c->d_bk_cnt.ptr, first + kMaxBuckets + 1, c->d_rord.ptr, c->stream);
     uint32_t h[2 * (kMaxBuckets + 1) + 1];
     tr.mark("enqueue");
     FRAC_HIP(c, hipMemcpyAsync(h, first, sizeof(h), hipMemcpyDeviceToHost, c->stream));
@@ -2210,6 +2195,10 @@ bool qt_device_planned(const frac_ctx* c, const frac_quadtree_params* qp)
 // the frame is done: one synchronisation for the leaf count and the counters, one for the leaves —
 // where the host-planned path synchronised twice per level (bucket counts, split count).  Records,
 // leaves and counters are those of the host-planned path.
+// the frame's counters (qt_level_stats, qt_plan): {rejected, hit, fallback, empty, -, total, eligible,
+// flops, overflow} in kQtShards copies, summed by the host
+constexpr uint32_t kQtShards = 32, kQtCounters = 9;
+
 int qt_encode_dev(frac_ctx* c, const frac_quadtree_params* qp, LevelGrid& level, frac_encode_item* out, size_t cap,
                   size_t* n_out, frac_stats* stats)
 {
@@ -2226,9 +2215,9 @@ int qt_encode_dev(frac_ctx* c, const frac_quadtree_params* qp, LevelGrid& level,
     FRAC_HIP(c, c->d_qt_next.ensure(std::max<size_t>(max_leaves, 1)));
     FRAC_HIP(c, c->d_qt_plan.ensure(6));
     FRAC_HIP(c, c->d_qt_first.ensure(5 * kFirst));
-    FRAC_HIP(c, c->d_qt_stats.ensure(9));
+    FRAC_HIP(c, c->d_qt_stats.ensure(kQtShards * kQtCounters));
     FRAC_HIP(c, c->d_bk_first.ensure(2 * (kMaxBuckets + 1) + 1));
-    FRAC_HIP(c, hipMemsetAsync(c->d_qt_stats.ptr, 0, 9 * sizeof(unsigned long long), c->stream));
+    FRAC_HIP(c, hipMemsetAsync(c->d_qt_stats.ptr, 0, kQtShards * kQtCounters * sizeof(unsigned long long), c->stream));
     // the first level's ranges: createUniformGrid(W, H, max, max), generated on the device
     const uint32_t nr0 = (uint32_t)frac_uniform_grid(W, H, qp->max_size, qp->max_size, nullptr, 0);
     if (nr0)
@@ -2288,8 +2277,6 @@ int qt_encode_dev(frac_ctx* c, const frac_quadtree_params* qp, LevelGrid& level,
         FRAC_HIP(c, c->d_aux.ensure(std::max<uint32_t>(nr_max, 1)));
         FRAC_HIP(c, c->d_fb_count.ensure(1));
         FRAC_HIP(c, c->d_bk_keys.ensure(mx));
-        FRAC_HIP(c, c->d_bk_keys2.ensure(mx));
-        FRAC_HIP(c, c->d_bk_iota.ensure(mx));
         FRAC_HIP(c, c->d_m_slot_range.ensure((size_t)nblocks_cap * 32 * cp));
         FRAC_HIP(c, c->d_m_rconst.ensure((size_t)nblocks_cap * 32 * cp));
         FRAC_HIP(c, c->d_m_tile_pos.ensure((size_t)ntiles_cap * 32));
@@ -2303,13 +2290,8 @@ int qt_encode_dev(frac_ctx* c, const frac_quadtree_params* qp, LevelGrid& level,
         FRAC_HIP(c, dptr.ensure((size_t)nblocks_cap * cp + 1));
         FRAC_HIP(c, dent.ensure(std::max<uint32_t>(nent_cap, 1)));
         FRAC_HIP(c, c->d_m_entries.ensure((size_t)nwork_cap * (fourier ? kDftBlocksPerWG : 4u * T) * 64));
-        size_t need = 0, sneed = 0;
-        FRAC_HIP(c, sort_pairs_u32(nullptr, need, c->d_bk_keys.ptr, c->d_bk_keys2.ptr, c->d_bk_iota.ptr, c->d_porig.ptr,
-                                   (uint32_t)mx, 3, c->stream));
-        if (need > c->bk_tmp_bytes) {
-            FRAC_HIP(c, c->d_bk_tmp.ensure(need));
-            c->bk_tmp_bytes = need;
-        }
+        size_t sneed = 0;
+        FRAC_HIP(c, c->d_bk_cnt.ensure((mx + kBkTile - 1) / kBkTile * kMaxBuckets));
         FRAC_HIP(c, hipcub::DeviceScan::ExclusiveSum(nullptr, sneed, c->d_qt_flags.ptr, c->d_qt_offs.ptr,
                                                      (int)std::max<uint32_t>(nr_max, 1), c->stream));
         if (sneed > c->qt_tmp_bytes) {
@@ -2320,23 +2302,17 @@ int qt_encode_dev(frac_ctx* c, const frac_quadtree_params* qp, LevelGrid& level,
         DevPlan* plan = c->d_qt_plan.ptr + lvi;
         const uint32_t* dn = lvi ? &plan->nr : nullptr; // the first level's count is the host's
         uint32_t* first = c->d_qt_first.ptr + (size_t)lv * kFirst;
-        uint32_t* err = c->d_bk_first.ptr + 2 * (kMaxBuckets + 1);
         if (nb > 1) {
-            // domains: keys + stable sort by bucket (the pool order porig) + bounds; ranges: the same over
-            // the worst case, the items past the level's count keyed kPadKey (last)
-            size_t tb = c->bk_tmp_bytes;
-            FRAC_HIP(c, hipMemsetAsync(err, 0, sizeof(uint32_t), c->stream));
-            launch_bucket_keys(c->d_doms.ptr, nd, 2 * n, c->d_src.ptr, c->d_sstride, c->d_bk_keys.ptr, c->d_bk_iota.ptr,
-                               err, c->stream);
-            FRAC_HIP(c, sort_pairs_u32(c->d_bk_tmp.ptr, tb, c->d_bk_keys.ptr, c->d_bk_keys2.ptr, c->d_bk_iota.ptr,
-                                       c->d_porig.ptr, nd, 3, c->stream));
-            bucket_bounds<<<1, 64, 0, c->stream>>>(c->d_bk_keys2.ptr, nd, first);
-            tb = c->bk_tmp_bytes;
-            launch_bucket_keys(c->d_ranges.ptr, nr_max, n, tplane, tstride, c->d_rkey.ptr, c->d_bk_iota.ptr, err,
+            // domains: keys + stable bucket sort (the pool order porig) + bounds; ranges: the same over the
+            // worst case, counting only the level's *dn (the grids' categories are −1, computed here:
+            // no invalid category can occur, so no error word)
+            launch_bucket_keys(c->d_doms.ptr, nd, 2 * n, c->d_src.ptr, c->d_sstride, c->d_bk_keys.ptr, nullptr,
+                               nullptr, c->stream);
+            launch_bucket_sort(c->d_bk_keys.ptr, nd, nullptr, c->d_bk_cnt.ptr, first, c->d_porig.ptr, c->stream);
+            launch_bucket_keys(c->d_ranges.ptr, nr_max, n, tplane, tstride, c->d_rkey.ptr, nullptr, nullptr,
                                c->stream, dn);
-            FRAC_HIP(c, sort_pairs_u32(c->d_bk_tmp.ptr, tb, c->d_rkey.ptr, c->d_bk_keys2.ptr, c->d_bk_iota.ptr,
-                                       c->d_rord.ptr, nr_max, 3, c->stream));
-            bucket_bounds<<<1, 64, 0, c->stream>>>(c->d_bk_keys2.ptr, nr_max, first + kMaxBuckets + 1);
+            launch_bucket_sort(c->d_rkey.ptr, nr_max, dn, c->d_bk_cnt.ptr, first + kMaxBuckets + 1, c->d_rord.ptr,
+                               c->stream);
         } else {
             if (nd)
                 fill_iota<<<(nd + 255) / 256, 256, 0, c->stream>>>(c->d_porig.ptr, nd);
@@ -2362,7 +2338,7 @@ int qt_encode_dev(frac_ctx* c, const frac_quadtree_params* qp, LevelGrid& level,
         pa.blk_ptr = dptr.ptr;
         pa.blk_ent = dent.ptr;
         pa.acc = c->d_qt_stats.ptr;
-        qt_plan<<<8, 256, 0, c->stream>>>(pa);
+        qt_plan<<<32, 256, 0, c->stream>>>(pa);
         QtFillArgs fa;
         fa.plan = plan;
         fa.rord = c->d_rord.ptr;
@@ -2403,7 +2379,7 @@ int qt_encode_dev(frac_ctx* c, const frac_quadtree_params* qp, LevelGrid& level,
         if (stats)
             qt_level_stats<<<(nr_max + 255) / 256, 256, 0, c->stream>>>(
                 c->d_aux.ptr, c->d_rkey.ptr, c->d_porig.ptr, nr_max, (uint64_t)nd, c->p.use_classifier ? 1 : 0,
-                QtBuckets{}, nullptr, c->d_qt_stats.ptr, plan);
+                QtBuckets{}, nullptr, c->d_qt_stats.ptr, plan, kQtShards, kQtCounters);
         level.out();
         qt_flags<<<(nr_max + 255) / 256, 256, 0, c->stream>>>(c->d_out.ptr, nr_max, n > qp->min_size ? 1 : 0,
                                                              qp->split_distance, c->d_qt_flags.ptr, plan);
@@ -2428,11 +2404,15 @@ int qt_encode_dev(frac_ctx* c, const frac_quadtree_params* qp, LevelGrid& level,
     // the frame's one round trip for the counts: leaves (after the last level run), counters
     struct {
         DevPlan last;
-        unsigned long long acc[9];
+        unsigned long long acc[kQtCounters];
     } h{};
+    unsigned long long sh[kQtShards * kQtCounters];
     FRAC_HIP(c, hipMemcpyAsync(&h.last, c->d_qt_plan.ptr + lvi, sizeof(DevPlan), hipMemcpyDeviceToHost, c->stream));
-    FRAC_HIP(c, hipMemcpyAsync(h.acc, c->d_qt_stats.ptr, sizeof(h.acc), hipMemcpyDeviceToHost, c->stream));
+    FRAC_HIP(c, hipMemcpyAsync(sh, c->d_qt_stats.ptr, sizeof(sh), hipMemcpyDeviceToHost, c->stream));
     FRAC_HIP(c, hipStreamSynchronize(c->stream));
+    for (uint32_t k = 0; k < kQtShards; ++k)
+        for (uint32_t i = 0; i < kQtCounters; ++i)
+            h.acc[i] += sh[k * kQtCounters + i];
     if (lvi == 0)
         h.last.leaf_base = 0;
     if (h.acc[8])
@@ -2624,6 +2604,7 @@ void frac_destroy(frac_ctx* c)
     c->d_qt_tmp.release();
     c->d_rkey.release();
     c->d_bk_keys.release();
+    c->d_bk_cnt.release();
     c->d_bk_keys2.release();
     c->d_bk_iota.release();
     c->d_bk_first.release();

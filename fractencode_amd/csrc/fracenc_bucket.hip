@@ -10,6 +10,7 @@
 // boundaries, and the fills of the per-slot / per-tile / per-range maps the engines read.  The
 // host sees only the 2 × 8 bucket counts, from which it derives the small per-bucket layout
 // (BucketLayout) and the work lists — no per-item host loop and no per-item transfer.
+#include <algorithm>
 #include <type_traits>
 
 #include "fracenc_common.h"
@@ -51,11 +52,13 @@ __global__ void __launch_bounds__(256) bucket_keys(const frac_grid_item* __restr
     }
     if (lane == 0) {
         if (cat < -1 || cat > 5) {
-            atomicOr(err, 1u);
+            if (err)
+                atomicOr(err, 1u);
             cat = -1;
         }
         key[k] = (uint32_t)(cat + 1);
-        iota[k] = k;
+        if (iota)
+            iota[k] = k;
     }
 }
 
@@ -81,7 +84,8 @@ __global__ void __launch_bounds__(256) bucket_keys_rows(const frac_grid_item* __
         if (k >= nd) {
             if (k < n && j == 0) {
                 key[k] = kPadKey;
-                iota[k] = k;
+                if (iota)
+                    iota[k] = k;
             }
             return; // whole item groups leave together: the shuffles below see only live lanes
         }
@@ -122,11 +126,13 @@ __global__ void __launch_bounds__(256) bucket_keys_rows(const frac_grid_item* __
         cat = category4_dev(q[0], q[1], q[2], q[3]);
     }
     if (cat < -1 || cat > 5) {
-        atomicOr(err, 1u);
+        if (err)
+            atomicOr(err, 1u);
         cat = -1;
     }
     key[k] = (uint32_t)(cat + 1);
-    iota[k] = k;
+    if (iota)
+        iota[k] = k;
 }
 
 // bucket keys of `cnt` items of height h (every item of a grid has the size of the first); dn: the
@@ -155,6 +161,140 @@ inline void launch_bucket_keys(const frac_grid_item* items, uint32_t cnt, uint32
         rows(std::integral_constant<uint32_t, 64>());
     else
         bucket_keys<<<(cnt + 3) / 4, 256, 0, s>>>(items, cnt, plane, stride, key, iota, err);
+}
+
+// ---- stable bucket sort of item indices by a 3-bit key (the classifier buckets) ----
+// A counting sort in three launches, for at most kMaxBuckets keys: per 1,024-item tile the bucket
+// counts (bksort_count), per bucket the exclusive prefix over tiles and the bucket starts
+// (bksort_scan: first[b] = the first sorted position of bucket b, first[kMaxBuckets] = the count —
+// what bucket_bounds computed from the sorted keys), then each tile scatters its indices in index
+// order (bksort_scatter: wave ballots per key give the rank among the earlier lanes).  It replaces
+// rocPRIM's Onesweep for these 7 buckets: one third of the launches, no memsets (C4 quadtree: six
+// sorts per frame of ≈33 µs each).  dn (device-planned levels): the item count is *dn ≤ n; the
+// grids cover n.
+constexpr uint32_t kBkTile = 1024, kBkThreads = 256;
+
+__device__ inline uint32_t bk_count_of(const uint32_t* __restrict__ dn, uint32_t n) { return dn ? min(*dn, n) : n; }
+
+__global__ void __launch_bounds__(kBkThreads) bksort_count(const uint32_t* __restrict__ keys, uint32_t n,
+                                                           const uint32_t* __restrict__ dn, uint32_t* __restrict__ counts)
+{
+    __shared__ uint32_t part[kBkThreads / 64][kMaxBuckets];
+    n = bk_count_of(dn, n);
+    const uint32_t base = blockIdx.x * kBkTile, lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    uint32_t c[kMaxBuckets] = {};
+    for (uint32_t j = 0; j < kBkTile / kBkThreads; ++j) {
+        const uint32_t i = base + j * kBkThreads + threadIdx.x;
+        const uint32_t k = i < n ? keys[i] : (uint32_t)kMaxBuckets;
+#pragma unroll
+        for (uint32_t b = 0; b < (uint32_t)kMaxBuckets; ++b)
+            c[b] += (uint32_t)__builtin_popcountll(__ballot(k == b));
+    }
+    if (lane == 0)
+#pragma unroll
+        for (uint32_t b = 0; b < (uint32_t)kMaxBuckets; ++b)
+            part[wv][b] = c[b];
+    __syncthreads();
+    if (threadIdx.x < (uint32_t)kMaxBuckets) {
+        uint32_t t = 0;
+        for (uint32_t w = 0; w < kBkThreads / 64; ++w)
+            t += part[w][threadIdx.x];
+        counts[blockIdx.x * kMaxBuckets + threadIdx.x] = t;
+    }
+}
+
+// one block: offsets[tile][b] = first[b] + the bucket's items in earlier tiles (in place over counts)
+__global__ void __launch_bounds__(kBkThreads) bksort_scan(uint32_t* __restrict__ counts, uint32_t ntiles,
+                                                          uint32_t* __restrict__ first)
+{
+    __shared__ uint32_t tot[kMaxBuckets], run[kMaxBuckets];
+    __shared__ uint32_t buf[kBkThreads];
+    if (threadIdx.x < (uint32_t)kMaxBuckets)
+        tot[threadIdx.x] = 0;
+    __syncthreads();
+    for (uint32_t t = threadIdx.x; t < ntiles; t += kBkThreads)
+#pragma unroll
+        for (uint32_t b = 0; b < (uint32_t)kMaxBuckets; ++b)
+            atomicAdd(&tot[b], counts[t * kMaxBuckets + b]); // LDS atomics: ntiles ≤ a few hundred
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t acc = 0;
+        for (uint32_t b = 0; b < (uint32_t)kMaxBuckets; ++b) {
+            run[b] = acc;
+            first[b] = acc;
+            acc += tot[b];
+        }
+        first[kMaxBuckets] = acc;
+    }
+    __syncthreads();
+    for (uint32_t b = 0; b < (uint32_t)kMaxBuckets; ++b)
+        for (uint32_t t0 = 0; t0 < ntiles; t0 += kBkThreads) {
+            const uint32_t t = t0 + threadIdx.x;
+            const uint32_t v = t < ntiles ? counts[t * kMaxBuckets + b] : 0u;
+            buf[threadIdx.x] = v;
+            __syncthreads();
+            for (uint32_t o = 1; o < kBkThreads; o <<= 1) { // inclusive Hillis–Steele scan
+                const uint32_t x = threadIdx.x >= o ? buf[threadIdx.x - o] : 0u;
+                __syncthreads();
+                buf[threadIdx.x] += x;
+                __syncthreads();
+            }
+            if (t < ntiles)
+                counts[t * kMaxBuckets + b] = run[b] + buf[threadIdx.x] - v;
+            __syncthreads();
+            if (threadIdx.x == kBkThreads - 1)
+                run[b] += buf[threadIdx.x];
+            __syncthreads();
+        }
+}
+
+__global__ void __launch_bounds__(kBkThreads) bksort_scatter(const uint32_t* __restrict__ keys, uint32_t n,
+                                                             const uint32_t* __restrict__ dn,
+                                                             const uint32_t* __restrict__ offsets,
+                                                             uint32_t* __restrict__ out)
+{
+    __shared__ uint32_t wcnt[kBkThreads / 64][kMaxBuckets];
+    __shared__ uint32_t run[kMaxBuckets];
+    n = bk_count_of(dn, n);
+    const uint32_t base = blockIdx.x * kBkTile, lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    if (threadIdx.x < (uint32_t)kMaxBuckets)
+        run[threadIdx.x] = offsets[blockIdx.x * kMaxBuckets + threadIdx.x];
+    const unsigned long long below = lane ? (~0ull >> (64 - lane)) : 0ull;
+    for (uint32_t j = 0; j < kBkTile / kBkThreads; ++j) {
+        const uint32_t i = base + j * kBkThreads + threadIdx.x;
+        const uint32_t k = i < n ? keys[i] : (uint32_t)kMaxBuckets;
+        uint32_t mine = 0; // the rank among this wave's earlier lanes of the same key
+#pragma unroll
+        for (uint32_t b = 0; b < (uint32_t)kMaxBuckets; ++b) {
+            const unsigned long long m = __ballot(k == b);
+            if (k == b)
+                mine = (uint32_t)__builtin_popcountll(m & below);
+            if (lane == 0)
+                wcnt[wv][b] = (uint32_t)__builtin_popcountll(m);
+        }
+        __syncthreads();
+        if (k < (uint32_t)kMaxBuckets) {
+            uint32_t pos = run[k] + mine;
+            for (uint32_t w = 0; w < wv; ++w)
+                pos += wcnt[w][k];
+            out[pos] = i;
+        }
+        __syncthreads();
+        if (threadIdx.x < (uint32_t)kMaxBuckets)
+            for (uint32_t w = 0; w < kBkThreads / 64; ++w)
+                run[threadIdx.x] += wcnt[w][threadIdx.x];
+        __syncthreads();
+    }
+}
+
+// the three launches; counts: [⌈n / kBkTile⌉ · kMaxBuckets] scratch
+inline void launch_bucket_sort(const uint32_t* keys, uint32_t n, const uint32_t* dn, uint32_t* counts, uint32_t* first,
+                               uint32_t* out, hipStream_t s)
+{
+    const uint32_t nt = std::max<uint32_t>((n + kBkTile - 1) / kBkTile, 1u);
+    bksort_count<<<nt, kBkThreads, 0, s>>>(keys, n, dn, counts);
+    bksort_scan<<<1, kBkThreads, 0, s>>>(counts, nt, first);
+    bksort_scatter<<<nt, kBkThreads, 0, s>>>(keys, n, dn, counts, out);
 }
 
 __global__ void __launch_bounds__(256) fill_iota(uint32_t* __restrict__ out, uint32_t n)
@@ -268,8 +408,13 @@ __global__ void __launch_bounds__(256) qt_level_stats(const RangeAux* __restrict
                                                       int classifier, QtBuckets B,
                                                       const unsigned long long* __restrict__ sea_count,
                                                       unsigned long long* __restrict__ acc,
-                                                      const DevPlan* __restrict__ plan = nullptr)
+                                                      const DevPlan* __restrict__ plan = nullptr, uint32_t shards = 1,
+                                                      uint32_t stride = 5)
 {
+    // the block's sums, then one atomic per counter per block into shard blockIdx % shards (stride words
+    // apart): a few hundred blocks adding into one word serialise there (24 µs per C4 level); the host
+    // sums the shards
+    __shared__ unsigned long long part[4][4];
     const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
     if (plan) { // the buckets as the planner laid them out
         nr = plan->nr;
@@ -302,8 +447,15 @@ __global__ void __launch_bounds__(256) qt_level_stats(const RangeAux* __restrict
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1)
             v[i] += (unsigned long long)__shfl_xor((long long)v[i], o, 64);
-        if ((threadIdx.x & 63u) == 0 && v[i])
-            atomicAdd(&acc[i], v[i]);
+        if ((threadIdx.x & 63u) == 0)
+            part[threadIdx.x >> 6][i] = v[i];
+    }
+    __syncthreads();
+    if (threadIdx.x < 4) {
+        const unsigned long long t = part[0][threadIdx.x] + part[1][threadIdx.x] + part[2][threadIdx.x] +
+                                     part[3][threadIdx.x];
+        if (t)
+            atomicAdd(&acc[(blockIdx.x % shards) * stride + threadIdx.x], t);
     }
     if (sea_count && r == 0)
         atomicAdd(&acc[4], *sea_count);
@@ -388,65 +540,83 @@ struct QtPlanHeader {
     bool ok;
 };
 
-__device__ inline void qt_plan_header(const QtPlanArgs& a, QtPlanHeader& h)
+// the header, 16 threads: thread t < 8 lays out bucket t, then thread t < 16 the (copy t / 8, bucket t % 8)
+// entry; the prefix sums over the 8 buckets and 16 entries are one thread's (32-bit arithmetic throughout)
+__device__ inline void qt_plan_header(const QtPlanArgs& a, QtPlanHeader& h, uint32_t t)
 {
-    const uint32_t nr = a.nr_init != ~0u ? a.nr_init : a.plan->nr;
-    h.nr = nr;
+    constexpr uint32_t B = kMaxBuckets;
+    __shared__ uint32_t groups_s;
     BucketLayout& L = h.L;
-    L.nb = a.nb;
-    L.VT = 1;
-    uint32_t nbk = 0, nt = 0;
-    for (uint32_t b = 0; b < (uint32_t)kMaxBuckets; ++b) {
-        const bool in = b < a.nb;
-        L.dbeg[b] = in ? (a.dfirst ? a.dfirst[b] : 0u) : 0u;
-        L.dcnt[b] = in ? (a.dfirst ? a.dfirst[b + 1] - a.dfirst[b] : a.nd) : 0u;
-        // the last bucket ends where the padding keys begin (first[kPadKey] = the level's count)
-        L.rbeg[b] = in ? (a.rfirst ? a.rfirst[b] : 0u) : 0u;
-        L.rcnt[b] = in ? (a.rfirst ? min(a.rfirst[b + 1], nr) - min(a.rfirst[b], nr) : nr) : 0u;
-        h.blk_first[b] = nbk;
-        h.blk_count[b] = (L.rcnt[b] + 31) / 32;
-        nbk += h.blk_count[b];
-        L.tile_first[b] = nt;
-        h.tile_count[b] = (L.dcnt[b] + 31) / 32;
-        nt += h.tile_count[b];
-        L.slot_first[b] = 32 * h.blk_first[b];
+    if (t < B) {
+        const uint32_t nr = a.nr_init != ~0u ? a.nr_init : a.plan->nr;
+        const bool in = t < a.nb;
+        L.dbeg[t] = in ? (a.dfirst ? a.dfirst[t] : 0u) : 0u;
+        L.dcnt[t] = in ? (a.dfirst ? a.dfirst[t + 1] - a.dfirst[t] : a.nd) : 0u;
+        L.rbeg[t] = in ? (a.rfirst ? a.rfirst[t] : 0u) : 0u;
+        L.rcnt[t] = in ? (a.rfirst ? min(a.rfirst[t + 1], nr) - min(a.rfirst[t], nr) : nr) : 0u;
+        h.blk_count[t] = (L.rcnt[t] + 31) / 32;
+        h.tile_count[t] = (L.dcnt[t] + 31) / 32;
+        if (t == 0)
+            h.nr = nr;
     }
-    h.nblocks = nbk;
-    h.ntiles = nt;
-    uint64_t groups = 0;
-    for (uint32_t b = 0; b < a.nb; ++b)
-        if (h.tile_count[b])
-            groups += (uint64_t)(h.blk_count[b] + a.bpw - 1) / a.bpw * a.copies;
-    uint32_t w = 0, e = 0;
-    for (uint32_t cp = 0; cp < 2; ++cp) // every (copy, bucket) entry is written: the work loop scans them
-        for (uint32_t b = 0; b < (uint32_t)kMaxBuckets; ++b) {
-            const uint32_t tc = h.tile_count[b], bc = cp < a.copies ? h.blk_count[b] : 0u;
-            uint32_t ns = 0;
-            if (b < a.nb && tc && bc) {
-                uint64_t sp = groups ? (a.target + groups - 1) / groups : 1;
-                sp = max<uint64_t>(1, min<uint64_t>(sp, max(1u, tc / 4u)));
-                ns = (uint32_t)sp; // sp ≤ tc: every split holds at least one tile
-            }
-            if (cp == 0)
-                h.ns[b] = ns;
-            h.wbase[cp * kMaxBuckets + b] = w;
-            h.ebase[cp * kMaxBuckets + b] = e;
-            w += (bc + a.bpw - 1) / a.bpw * ns;
-            e += bc * ns;
+    __syncthreads();
+    if (t == 0) {
+        L.nb = a.nb;
+        L.VT = 1;
+        uint32_t nbk = 0, nt = 0, groups = 0;
+        for (uint32_t b = 0; b < B; ++b) {
+            h.blk_first[b] = nbk;
+            L.slot_first[b] = 32 * nbk;
+            nbk += h.blk_count[b];
+            L.tile_first[b] = nt;
+            nt += h.tile_count[b];
+            if (b < a.nb && h.tile_count[b])
+                groups += (h.blk_count[b] + a.bpw - 1) / a.bpw * a.copies;
         }
-    h.wbase[2 * kMaxBuckets] = w;
-    h.ebase[2 * kMaxBuckets] = e;
-    h.nwork = w;
-    h.nent = e;
-    h.ok = w <= a.nwork_cap && e <= a.nent_cap && nbk <= a.nblocks_cap && nt <= a.ntiles_cap;
+        h.nblocks = nbk;
+        h.ntiles = nt;
+        groups_s = groups;
+    }
+    __syncthreads();
+    uint32_t nw = 0, ne = 0;
+    if (t < 2 * B) {
+        const uint32_t cp = t / B, b = t % B, tc = h.tile_count[b], bc = cp < a.copies ? h.blk_count[b] : 0u;
+        uint32_t ns = 0;
+        if (b < a.nb && tc && bc) {
+            const uint32_t g = groups_s;
+            const uint32_t sp = g ? (a.target + g - 1) / g : 1u;
+            ns = max(1u, min(sp, max(1u, tc / 4u))); // ≤ tc: every split holds at least one tile
+        }
+        if (cp == 0)
+            h.ns[b] = ns;
+        nw = (bc + a.bpw - 1) / a.bpw * ns;
+        ne = bc * ns;
+        h.wbase[t] = nw; // counts first, prefix below
+        h.ebase[t] = ne;
+    }
+    __syncthreads();
+    if (t == 0) {
+        uint32_t w = 0, e = 0;
+        for (uint32_t q = 0; q < 2 * B; ++q) {
+            const uint32_t cw = h.wbase[q], ce = h.ebase[q];
+            h.wbase[q] = w;
+            h.ebase[q] = e;
+            w += cw;
+            e += ce;
+        }
+        h.wbase[2 * B] = w;
+        h.ebase[2 * B] = e;
+        h.nwork = w;
+        h.nent = e;
+        h.ok = w <= a.nwork_cap && e <= a.nent_cap && h.nblocks <= a.nblocks_cap && h.ntiles <= a.ntiles_cap;
+    }
+    __syncthreads();
 }
 
 __global__ void __launch_bounds__(256) qt_plan(QtPlanArgs a)
 {
     __shared__ QtPlanHeader h;
-    if (threadIdx.x == 0)
-        qt_plan_header(a, h);
-    __syncthreads();
+    qt_plan_header(a, h, threadIdx.x);
     const uint32_t gt = blockIdx.x * blockDim.x + threadIdx.x, gs = gridDim.x * blockDim.x;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         DevPlan& p = *a.plan;
@@ -480,8 +650,8 @@ __global__ void __launch_bounds__(256) qt_plan(QtPlanArgs a)
         const uint32_t cp = q / kMaxBuckets, b = q % kMaxBuckets, ns = h.ns[b], loc = w - h.wbase[q];
         const uint32_t g = (loc / ns) * a.bpw, sp = loc % ns, tc = h.tile_count[b];
         const uint32_t bf = cp * h.nblocks + h.blk_first[b];
-        const uint32_t t0 = h.L.tile_first[b] + (uint32_t)((uint64_t)tc * sp / ns);
-        const uint32_t t1 = h.L.tile_first[b] + (uint32_t)((uint64_t)tc * (sp + 1) / ns);
+        const uint32_t t0 = h.L.tile_first[b] + tc * sp / ns; // tc · ns ≤ 2^13 · 2^13: 32 bits
+        const uint32_t t1 = h.L.tile_first[b] + tc * (sp + 1) / ns;
         a.work[w] = make_uint4(bf + g, min(a.bpw, h.blk_count[b] - g), t0, t1);
     }
     // the CSR map: block (copy, bucket, k) holds one entry per split of its bucket

@@ -9,6 +9,7 @@
 //                   least-squares contrast/brightness (FP64) and its fp32 error
 //   fallback_fp32   ranges whose best error leaves the exact fp32 regime: sequential fp32
 //                   emulation of image/metrics.h over all candidates
+#pragma once
 #include "fracenc_common.h"
 
 namespace fracenc {

@@ -17,7 +17,9 @@
 // Lanes keep per (transform) the running min over domain tiles and the first tile that
 // attained it (strict '<' in domain order, encode/TransformEstimator2.hpp:34); hits
 // (S16 <= H) collapse to 0.  resolve_mfma then pins the exact domain inside that tile.
+#pragma once
 #include "fracenc_common.h"
+#include "fracenc_kernels.hip" // FitArgs, fit_rstat_range (resolve_dft fuses the fit)
 
 namespace fracenc {
 
@@ -457,8 +459,10 @@ __global__ void __launch_bounds__(256) search_mfma(MfmaSearchArgs a)
         }
     }
     if (active) {
+        // merged entries (VAR 128): slot t = 0 only, the one resolve_mfma reads
+        constexpr int TW = ((VAR & 128) != 0 && T > 1) ? 1 : T;
 #pragma unroll
-        for (int t = 0; t < T; ++t)
+        for (int t = 0; t < TW; ++t)
             a.entries[((size_t)(blockIdx.x * 4u + wv) * T + t) * 64 + lane] = make_uint2(best[t], btile[t]);
     }
 }
@@ -632,10 +636,13 @@ __global__ void __launch_bounds__(256) resolve_mfma(MfmaResolveArgs a)
     const uint32_t slot = a.range_slot[r];
     const uint32_t blk = slot >> 5, col = slot & 31u;
     const uint32_t e0 = a.blk_ptr[blk], e1 = a.blk_ptr[blk + 1];
-    const uint32_t nent = (e1 - e0) * a.T * 2u;
+    // merged entries (search_mfma VAR 128) hold the minimum over every transform in slot t = 0; the
+    // other T − 1 slots are never written to with a candidate, so only slot 0 is read (T× fewer loads)
+    const uint32_t TE = a.merged ? 1u : a.T;
+    const uint32_t nent = (e1 - e0) * TE * 2u;
     uint32_t vmin = 0xffffffffu;
     for (uint32_t j = lane; j < nent; j += 64) {
-        const uint32_t e = e0 + j / (2u * a.T), t = (j >> 1) % a.T, h = j & 1u;
+        const uint32_t e = e0 + j / (2u * TE), t = (j >> 1) % TE, h = j & 1u;
         vmin = min(vmin, a.entries[((size_t)a.blk_ent[e] * a.T + t) * 64 + col + 32 * h].x);
     }
 #pragma unroll
@@ -677,7 +684,7 @@ __global__ void __launch_bounds__(256) resolve_mfma(MfmaResolveArgs a)
         const uint32_t jl = c0 + (uint32_t)lane;
         uint2 enl = make_uint2(0xffffffffu, 0u);
         if (jl < nent) {
-            const uint32_t e = e0 + jl / (2u * a.T), t = (jl >> 1) % a.T, h = jl & 1u;
+            const uint32_t e = e0 + jl / (2u * TE), t = (jl >> 1) % TE, h = jl & 1u;
             enl = a.entries[((size_t)a.blk_ent[e] * a.T + t) * 64 + col + 32 * h];
         }
         unsigned long long match = __ballot(jl < nent && enl.x == vmin);
@@ -685,7 +692,7 @@ __global__ void __launch_bounds__(256) resolve_mfma(MfmaResolveArgs a)
             const int src = __ffsll((long long)match) - 1;
             match &= match - 1;
             const uint32_t j = c0 + (uint32_t)src;
-            const uint32_t t = (j >> 1) % a.T, h = j & 1u;
+            const uint32_t t = (j >> 1) % TE, h = j & 1u;
             const uint32_t ctile = (uint32_t)__builtin_amdgcn_readlane((int)enl.y, src);
             if (ctile > best_tile)
                 continue;
