@@ -178,13 +178,17 @@ def test_invalid_geometry_is_an_error(engine):
         mixed = np.concatenate([F.create_uniform_grid(64, 64, 16, 8), F.create_uniform_grid(64, 64, 12, 6)])
         with pytest.raises(F.FracError):  # domains of two sizes: refused when set
             e.set_domains(mixed)
-        e.set_domains(F.create_uniform_grid(64, 64, 64, 32))
-        with pytest.raises(F.FracError):  # ranges above the 32×32 limit
-            e.search(np.array([(0, 0, 48, 48, -1)], dtype=F.GRID_ITEM))
         e.set_domains(F.create_uniform_grid(64, 64, 16, 8))
         bad = np.array([(60, 60, 8, 8, -1)], dtype=F.GRID_ITEM)  # outside the plane
         with pytest.raises(F.FracError):
             e.search(bad)
+    with F.Engine(0, 4, engine=engine) as e:
+        e.set_frame(np.zeros((512, 512), np.uint8))
+        e.set_domains(F.create_uniform_grid(512, 512, 512, 256))
+        with pytest.raises(F.FracError, match="2..256"):  # ranges above the 256×256 limit (the key's S16 field)
+            e.search(np.array([(0, 0, 300, 300, -1)], dtype=F.GRID_ITEM))
+        out, _ = e.search(np.array([(0, 0, 256, 256, -1)], dtype=F.GRID_ITEM))  # the largest accepted
+        assert out["sw"][0] == 512 and out["distance"][0] == 0.0
 
 
 def _recompute_s16(p, out, n=8):
