@@ -1160,7 +1160,7 @@ inline int mfma_variant(frac_ctx* c, int& var)
     char* end = nullptr;
     const long x = strtol(v, &end, 10);
     static const int exact[] = {0,  1,  2,  3,  4,  5,  6,  7,  12, 20, 21, 22, 23, 24, 26,
-                                28, 27, 32, 33, 34, 35, 36, 64, 96, 98, 128, 130};
+                                28, 27, 32, 33, 34, 35, 36, 64, 96, 98, 128, 130, 386};
     static const int ablation[] = {8, 9, 16, 17, 41, 65, 73, 105, 201, 202, 203, 204, 205, 206, 207, 226, 227, 240, 241, 242, 243};
     bool ok = end && *end == 0;
     bool known = false;
@@ -1177,14 +1177,28 @@ inline int mfma_variant(frac_ctx* c, int& var)
     return FRAC_OK;
 }
 
+// the direct form's schedule variant for range side N: the shipped one (the float-C epilogue for
+// n ≤ 4, where it is exact), or in a tuning build FRAC_MFMA_VARIANT (386 falls back to 130 above n = 4)
+template <int N>
+int direct_variant(frac_ctx* c, int& var)
+{
+    FRAC_TRY(mfma_variant(c, var));
+    const bool knob = kTuningBuild && ab_knob("FRAC_MFMA_VARIANT") && *ab_knob("FRAC_MFMA_VARIANT");
+    if (!knob)
+        var = N <= 4 ? kDefaultMfmaVariant4 : kDefaultMfmaVariant;
+    if (N > 4 && (var & 256))
+        var = kDefaultMfmaVariant;
+    return FRAC_OK;
+}
+
 template <int N, int T>
 int launch_search_mfma(frac_ctx* c, const MfmaSearchArgs& a)
 {
     int var = 0;
-    FRAC_TRY(mfma_variant(c, var));
+    FRAC_TRY(direct_variant<N>(c, var));
 #ifndef FRAC_TUNING
     (void)var; // the product build: the shipped schedule only
-    launch_search_mfma_v<N, T, kDefaultMfmaVariant>(c, a);
+    launch_search_mfma_v<N, T, (N <= 4 ? kDefaultMfmaVariant4 : kDefaultMfmaVariant)>(c, a);
 #else
     switch (var) {
     case 0: launch_search_mfma_v<N, T, 0>(c, a); break;
@@ -1203,6 +1217,12 @@ int launch_search_mfma(frac_ctx* c, const MfmaSearchArgs& a)
     case 130: launch_search_mfma_v<N, T, 130>(c, a); break;
     case 8: launch_search_mfma_v<N, T, 8>(c, a); break;   // ablation: 1-value epilogue
     case 16: launch_search_mfma_v<N, T, 16>(c, a); break; // ablation: no MFMA
+    case 386:
+        if constexpr (N <= 4) {
+            launch_search_mfma_v<N, T, 386>(c, a); // the float-C epilogue
+            break;
+        }
+        [[fallthrough]];
     default: launch_search_mfma_v<N, T, kDefaultMfmaVariant>(c, a); break;
     }
 #endif
@@ -1561,8 +1581,12 @@ int launch_mfma(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool inits =
         if (dft_route(c))
             return launch_dft(c, dtgt, tstride, inits);
     }
+    int dvar = 0;
+    FRAC_TRY(direct_variant<N>(c, dvar));
+    const int fmode = (dvar & 256) ? 1 : 0; // the float-C epilogue: its row constants and B scaling
     if (c->ntiles) {
         MfmaDomainPrepArgs d;
+        d.fmode = fmode;
         d.pool = c->d_pool.ptr;
         d.negsd2 = c->d_negsd2.ptr;
         d.tile_pos = c->d_m_tile_pos.ptr;
@@ -1570,7 +1594,10 @@ int launch_mfma(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool inits =
         d.dtiles = c->d_m_dtiles.ptr;
         d.dconst = c->d_m_dconst.ptr;
         d.plan = c->qplan;
-        mfma_domain_prep<N><<<(c->ntiles * 32 + 255) / 256, 256, 0, c->stream>>>(d);
+        if constexpr (N == 16)
+            mfma_domain_prep16<<<(c->ntiles * 32 * MfmaGeom<16>::KS + 255) / 256, 256, 0, c->stream>>>(d);
+        else
+            mfma_domain_prep<N><<<(c->ntiles * 32 + 255) / 256, 256, 0, c->stream>>>(d);
     }
     if (c->nblocks) {
         MfmaRangePrepArgs r;
@@ -1583,6 +1610,7 @@ int launch_mfma(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool inits =
         r.rfrags = c->d_m_rfrags.ptr;
         r.rconst = c->d_m_rconst.ptr;
         r.plan = c->qplan;
+        r.fmode = fmode;
         const size_t threads = (size_t)c->nblocks * T * MfmaGeom<N>::KS * 64;
         // rconst is a sum of per-pixel terms, accumulated by the transform-0 threads (a planned level's
         // qt_fill_maps zeroed it)
@@ -1654,7 +1682,8 @@ int launch_mfma(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool inits =
         v.T = T;
         v.hitH = c->hitH;
         v.best_key = c->d_best_key.ptr;
-        v.merged = (N != 16 && T > 1 && (c->mfma_var_ran & 128)) ? 1 : 0; // search_mfma's entries merged over t
+        v.merged = (N != 16 && T > 1 && (c->mfma_var_ran & (128 | 256))) ? 1 : 0; // entries merged over t
+        v.fmode = (N != 16 && (c->mfma_var_ran & 256)) ? 1 : 0;                  // fmap'd float-C minima
         v.plan = c->qplan;
         resolve_mfma<N><<<(nr + 3) / 4, 256, 0, c->stream>>>(v);
     }

@@ -203,49 +203,42 @@ __global__ void __launch_bounds__(kBkThreads) bksort_count(const uint32_t* __res
     }
 }
 
-// one block: offsets[tile][b] = first[b] + the bucket's items in earlier tiles (in place over counts)
-__global__ void __launch_bounds__(kBkThreads) bksort_scan(uint32_t* __restrict__ counts, uint32_t ntiles,
-                                                          uint32_t* __restrict__ first)
+// one block of kMaxBuckets waves, wave b scanning bucket b: offsets[tile][b] = first[b] + the bucket's
+// items in earlier tiles (in place over counts).  Lane l takes a run of ⌈ntiles / 64⌉ tiles; the lanes'
+// run sums are scanned with shuffles, the buckets' totals meet once in LDS.
+__global__ void __launch_bounds__(64 * kMaxBuckets) bksort_scan(uint32_t* __restrict__ counts, uint32_t ntiles,
+                                                                uint32_t* __restrict__ first)
 {
-    __shared__ uint32_t tot[kMaxBuckets], run[kMaxBuckets];
-    __shared__ uint32_t buf[kBkThreads];
-    if (threadIdx.x < (uint32_t)kMaxBuckets)
-        tot[threadIdx.x] = 0;
-    __syncthreads();
-    for (uint32_t t = threadIdx.x; t < ntiles; t += kBkThreads)
+    __shared__ uint32_t tot[kMaxBuckets];
+    const uint32_t b = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    const uint32_t per = (ntiles + 63) / 64, t0 = min(lane * per, ntiles), t1 = min(t0 + per, ntiles);
+    uint32_t run = 0;
+    for (uint32_t t = t0; t < t1; ++t)
+        run += counts[t * kMaxBuckets + b];
+    uint32_t inc = run; // inclusive scan over the lanes
 #pragma unroll
-        for (uint32_t b = 0; b < (uint32_t)kMaxBuckets; ++b)
-            atomicAdd(&tot[b], counts[t * kMaxBuckets + b]); // LDS atomics: ntiles ≤ a few hundred
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t acc = 0;
-        for (uint32_t b = 0; b < (uint32_t)kMaxBuckets; ++b) {
-            run[b] = acc;
-            first[b] = acc;
-            acc += tot[b];
-        }
-        first[kMaxBuckets] = acc;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t x = (uint32_t)__shfl_up((int)inc, o, 64);
+        if ((int)lane >= o)
+            inc += x;
     }
+    if (lane == 63)
+        tot[b] = inc;
     __syncthreads();
-    for (uint32_t b = 0; b < (uint32_t)kMaxBuckets; ++b)
-        for (uint32_t t0 = 0; t0 < ntiles; t0 += kBkThreads) {
-            const uint32_t t = t0 + threadIdx.x;
-            const uint32_t v = t < ntiles ? counts[t * kMaxBuckets + b] : 0u;
-            buf[threadIdx.x] = v;
-            __syncthreads();
-            for (uint32_t o = 1; o < kBkThreads; o <<= 1) { // inclusive Hillis–Steele scan
-                const uint32_t x = threadIdx.x >= o ? buf[threadIdx.x - o] : 0u;
-                __syncthreads();
-                buf[threadIdx.x] += x;
-                __syncthreads();
-            }
-            if (t < ntiles)
-                counts[t * kMaxBuckets + b] = run[b] + buf[threadIdx.x] - v;
-            __syncthreads();
-            if (threadIdx.x == kBkThreads - 1)
-                run[b] += buf[threadIdx.x];
-            __syncthreads();
-        }
+    uint32_t base = 0;
+    for (uint32_t k = 0; k < b; ++k)
+        base += tot[k];
+    if (lane == 0) {
+        first[b] = base;
+        if (b == kMaxBuckets - 1)
+            first[kMaxBuckets] = base + tot[b];
+    }
+    uint32_t off = base + inc - run;
+    for (uint32_t t = t0; t < t1; ++t) {
+        const uint32_t c = counts[t * kMaxBuckets + b];
+        counts[t * kMaxBuckets + b] = off;
+        off += c;
+    }
 }
 
 __global__ void __launch_bounds__(kBkThreads) bksort_scatter(const uint32_t* __restrict__ keys, uint32_t n,
@@ -293,7 +286,7 @@ inline void launch_bucket_sort(const uint32_t* keys, uint32_t n, const uint32_t*
 {
     const uint32_t nt = std::max<uint32_t>((n + kBkTile - 1) / kBkTile, 1u);
     bksort_count<<<nt, kBkThreads, 0, s>>>(keys, n, dn, counts);
-    bksort_scan<<<1, kBkThreads, 0, s>>>(counts, nt, first);
+    bksort_scan<<<1, 64 * kMaxBuckets, 0, s>>>(counts, nt, first);
     bksort_scatter<<<nt, kBkThreads, 0, s>>>(keys, n, dn, counts, out);
 }
 
@@ -416,14 +409,12 @@ __global__ void __launch_bounds__(256) qt_level_stats(const RangeAux* __restrict
     // sums the shards
     __shared__ unsigned long long part[4][4];
     const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-    if (plan) { // the buckets as the planner laid them out
+    if (plan)
         nr = plan->nr;
-        B.nb = plan->L.nb;
-        for (uint32_t b = 0; b < (uint32_t)kMaxBuckets; ++b) {
-            B.beg[b] = plan->L.dbeg[b];
-            B.end[b] = plan->L.dbeg[b] + plan->L.dcnt[b];
-        }
-    }
+    // a bucket's pool positions: from the plan's layout (global memory, indexed by the range's bucket:
+    // a per-thread copy of the table would be indexed dynamically, i.e. live in scratch), else from B
+    auto dbeg = [&](uint32_t b) { return plan ? plan->L.dbeg[b] : B.beg[b]; };
+    auto dcnt = [&](uint32_t b) { return plan ? plan->L.dcnt[b] : B.end[b] - B.beg[b]; };
     unsigned long long v[4] = {0ull, 0ull, 0ull, 0ull}; // rejected, hit, fallback, empty
     if (r < nr) {
         const RangeAux ax = aux[r];
@@ -436,9 +427,9 @@ __global__ void __launch_bounds__(256) qt_level_stats(const RangeAux* __restrict
             if (ax.flags & kAuxHit) {
                 v[1] = 1;
                 if (classifier)
-                    v[0] = (unsigned long long)porig[ax.pos] - (ax.pos - B.beg[b]);
+                    v[0] = (unsigned long long)porig[ax.pos] - (ax.pos - dbeg(b));
             } else if (classifier) {
-                v[0] = nd - (B.end[b] - B.beg[b]);
+                v[0] = nd - dcnt(b);
             }
         }
     }

@@ -29,6 +29,26 @@ typedef float floatx16_t __attribute__((ext_vector_type(16)));
 constexpr uint32_t kMfmaPadConst = 0x70000000u; // e' of padding domains: v ≈ 1.9e9, never wins
 constexpr int kTilesPerStage = 4; // domain tiles per LDS stage (double-buffered)
 constexpr int kDefaultMfmaVariant = 130; // the minimum over transforms first (128), two v_min3 chains (2)
+// n ≤ 4: the row constant as the MFMA's C operand (256, the float-C epilogue below) on top of 130
+constexpr int kDefaultMfmaVariant4 = 386;
+
+// VAR bit 256, n ≤ 4 (the float-C epilogue): the B operand is 8·(128 − copy_t) ∈ [−1016, 1024] (exact
+// in f16) and the accumulator starts from the domain row's e_d = ΣD4² − 1024·ΣD4 ∈ [−2^22, 0], so
+//   acc = e_d − 8Z = S16 − c'_r,   c'_r = 16Σr² − 4080Σr + 8·65280·n² = V0 − rconst   (mfma_range_const)
+// exactly: every partial sum is bounded by 2^22 + 8·n²·128·510 ≤ 2^22 + 8.36e6 < 2^24 for n ≤ 4.  The
+// epilogue is then the minimum of the accumulators themselves — one v_min3_f32 per two candidates:
+// 2 VALU per row at T = 4 instead of 3.5 (T/2 + 1.5, VAR 130) — and the entries hold the float minimum
+// as an order-preserving u32 (fmap; 0 stays the hit sentinel, ~0u "no candidate").
+__host__ __device__ inline uint32_t fmap(float f)
+{
+    const uint32_t b = __builtin_bit_cast(uint32_t, f);
+    return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+__host__ __device__ inline float funmap(uint32_t u)
+{
+    return __builtin_bit_cast(float, (u & 0x80000000u) ? (u & 0x7fffffffu) : ~u);
+}
+constexpr float kFltPadE = 1.0e30f; // e of padding domain rows: never the minimum
 
 template <int N>
 struct MfmaGeom {
@@ -60,7 +80,49 @@ struct MfmaDomainPrepArgs {
     uint4* dtiles;              // [ntiles][KS][64] 16 B
     uint32_t* dconst;           // [ntiles][2][16]
     const DevPlan* plan = nullptr; // device-planned search: ntiles from the plan (the grid is a bound)
+    int fmode = 0;              // the float-C epilogue (VAR 256): dconst = float e_d, padding kFltPadE
 };
+
+// n = 16: 16 K-steps per row, one lane each (16-lane groups per tile row): the row's 128 pool words and
+// 32 fragment stores split 16 ways (one thread per row was a 128-load chain on 63 workgroups: 39 µs at
+// the C4 quadtree's first level); the row sum ΣD4 of the epilogue constant by a 16-lane reduction
+__global__ void __launch_bounds__(256) mfma_domain_prep16(MfmaDomainPrepArgs a)
+{
+    constexpr int N = 16, NN = N * N, KS = MfmaGeom<N>::KS;
+    if (a.plan)
+        a.ntiles = a.plan->ntiles;
+    const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid >= a.ntiles * 32u * KS) // whole 16-lane row groups leave together
+        return;
+    const uint32_t rg = gid / KS, s = gid % KS, tile = rg >> 5, row = rg & 31u;
+    const int p = a.tile_pos[rg];
+    int sumd = 0;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        _Float16 v8[8];
+        uint4 w = make_uint4(0x01fe01feu, 0x01fe01feu, 0x01fe01feu, 0x01fe01feu); // padding rows: 510 (0)
+        if (p >= 0)
+            w = *reinterpret_cast<const uint4*>(a.pool + (size_t)p * (NN / 2) + 8 * s + 4 * h);
+        const uint32_t ww[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int dv = (int)((ww[j >> 1] >> (16 * (j & 1))) & 0xffffu);
+            if (p >= 0)
+                sumd += dv;
+            v8[j] = (_Float16)(dv - 510);
+        }
+        a.dtiles[((size_t)tile * KS + s) * 64 + row + 32 * h] = __builtin_bit_cast(uint4, v8);
+    }
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1)
+        sumd += __shfl_xor(sumd, o, 64);
+    if (s == 0) {
+        const int sd2 = p >= 0 ? -a.negsd2[p] : 0;
+        const uint32_t e = p >= 0 ? (uint32_t)(sd2 - 1024 * sumd) + (1u << 28) : kMfmaPadConst;
+        const uint32_t hh = (row >> 2) & 1u, i = (row & 3u) + 4u * (row >> 3);
+        a.dconst[(size_t)tile * 32 + hh * 16 + i] = e;
+    }
+}
 
 template <int N>
 __global__ void __launch_bounds__(256) mfma_domain_prep(MfmaDomainPrepArgs a)
@@ -95,9 +157,12 @@ __global__ void __launch_bounds__(256) mfma_domain_prep(MfmaDomainPrepArgs a)
     }
     if (p >= 0)
         sd2 = -a.negsd2[p];
-    // n ≤ 8: v = (bits(acc) << 3) + e with bits(acc) = 0x4B400000 − Z;  n = 16: v = (int(acc) << 3) + e
-    const uint32_t e = p >= 0 ? (uint32_t)(sd2 - 1024 * sumd) + (N == 16 ? (1u << 28) : (uint32_t)-0x58000000)
-                              : kMfmaPadConst;
+    // n ≤ 8: v = (bits(acc) << 3) + e with bits(acc) = 0x4B400000 − Z;  n = 16: v = (int(acc) << 3) + e;
+    // the float-C epilogue: e_d itself, the accumulator's start
+    uint32_t e = p >= 0 ? (uint32_t)(sd2 - 1024 * sumd) + (N == 16 ? (1u << 28) : (uint32_t)-0x58000000)
+                        : kMfmaPadConst;
+    if (a.fmode)
+        e = __float_as_uint(p >= 0 ? (float)(sd2 - 1024 * sumd) : kFltPadE);
     // row = (i&3) + 8(i>>2) + 4h  ⇔  h = (row>>2)&1, i = (row&3) + 4(row>>3)
     const uint32_t h = (row >> 2) & 1u, i = (row & 3u) + 4u * (row >> 3);
     a.dconst[(size_t)tile * 32 + h * 16 + i] = e;
@@ -120,6 +185,7 @@ struct MfmaRangePrepArgs {
     uint32_t* rorb = nullptr;  // dft_range_prep: [nblocks*32][32] pixel pairs in orbit order (resolve_dft)
     uint32_t flip_from = ~0u;  // dft_range_prep: blocks from here on hold their range read through Flip (T = 8)
     const DevPlan* plan = nullptr; // device-planned search: the block count (and flip_from) from the plan
+    int fmode = 0;             // mfma_range_prep, the float-C epilogue: B = 8·(128 − copy_t)
 };
 
 // the range-block count of a device-planned search (T = 8 Fourier: the originals and their copies)
@@ -158,7 +224,7 @@ __global__ void __launch_bounds__(256) mfma_range_prep(MfmaRangePrepArgs a)
                 rv = a.tgt[(size_t)(rg.y + pix / N) * a.tstride + rg.x + (pix % N)];
                 part += 4080 * rv - 16 * rv * rv;
             }
-            v8[j] = (_Float16)(128 - rv);
+            v8[j] = (_Float16)(a.fmode ? 8 * (128 - rv) : 128 - rv);
         }
         // rconst = −16Σr² + 4080Σr + const (mfma_range_const) mod 2^32: the transform-0 threads add
         // their pixels' terms to the zeroed word, the first of them the constant
@@ -293,6 +359,36 @@ __device__ inline void compute_stage(const uint4* __restrict__ la, uint32_t nt, 
             }
         };
         constexpr bool PRIO = (VAR & 32) != 0, LATE_E = (VAR & 64) != 0;
+        if constexpr ((VAR & 256) != 0) {
+            static_assert(N <= 4, "the float-C epilogue is exact for n <= 4 only");
+            read_e();
+            floatx16_t c;
+#pragma unroll
+            for (int i = 0; i < 16; ++i)
+                c[i] = __uint_as_float(e[i]);
+            floatx16_t acc[T];
+#pragma unroll
+            for (int t = 0; t < T; ++t)
+                acc[t] = mfma_tile<N, T>(af, bf[t], c);
+            float m = __builtin_inff();
+            if constexpr (T == 1) {
+#pragma unroll
+                for (int i = 0; i < 16; i += 2)
+                    m = __builtin_fminf(__builtin_fminf(m, acc[0][i]), acc[0][i + 1]);
+            } else {
+                static_assert(T % 2 == 0 && T >= 4, "T = 4 or 8: three, then pairs, then the last with the running min");
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    float r = __builtin_fminf(__builtin_fminf(acc[0][i], acc[1][i]), acc[2][i]);
+#pragma unroll
+                    for (int t = 3; t + 1 < T; t += 2)
+                        r = __builtin_fminf(__builtin_fminf(r, acc[t][i]), acc[t + 1][i]);
+                    m = __builtin_fminf(__builtin_fminf(m, r), acc[T - 1][i]);
+                }
+            }
+            cm[0] = min(cm[0], fmap(m));
+            continue;
+        }
         if constexpr (LATE_E) {
             // the first transform's MFMAs wait only for the A fragments; the epilogue
             // constants are read while they run
@@ -401,8 +497,16 @@ __global__ void __launch_bounds__(256) search_mfma(MfmaSearchArgs a)
         for (int s = 0; s < KS; ++s)
             bf[t][s] = __builtin_bit_cast(half8_t, a.rfrags[((size_t)(blk * T + t) * KS + s) * 64 + lane]);
     uint32_t hl = 0;
-    if constexpr (HITS)
-        hl = a.hitH + a.rconst[blk * 32 + (lane & 31u)];
+    if constexpr (HITS) {
+        if constexpr ((VAR & 256) != 0) {
+            // S16 ≤ H ⟺ acc ≤ H − c'_r = H − V0 + rconst; acc is an integer below 2^24 in magnitude, so
+            // the clamped bound is exact in f32
+            const int64_t lim = (int64_t)a.hitH - mfma_v0(N * N) + (int64_t)(int32_t)a.rconst[blk * 32 + (lane & 31u)];
+            hl = fmap((float)max<int64_t>(-(1ll << 24), min<int64_t>(lim, 1ll << 24)));
+        } else {
+            hl = a.hitH + a.rconst[blk * 32 + (lane & 31u)];
+        }
+    }
 
     floatx16_t cinit;
 #pragma unroll
@@ -460,7 +564,7 @@ __global__ void __launch_bounds__(256) search_mfma(MfmaSearchArgs a)
     }
     if (active) {
         // merged entries (VAR 128): slot t = 0 only, the one resolve_mfma reads
-        constexpr int TW = ((VAR & 128) != 0 && T > 1) ? 1 : T;
+        constexpr int TW = ((VAR & (128 | 256)) != 0 && T > 1) ? 1 : T;
 #pragma unroll
         for (int t = 0; t < TW; ++t)
             a.entries[((size_t)(blockIdx.x * 4u + wv) * T + t) * 64 + lane] = make_uint2(best[t], btile[t]);
@@ -584,6 +688,7 @@ struct MfmaResolveArgs {
     uint4* rstat = nullptr;     // [nr] the winner's {X_t, ΣD4 | Σr << 16, ΣD4², Σr²} (fit_rstat)
     uint32_t flip_slots = 0;    // T = 8 Fourier: slot s's flipped copy is slot s + flip_slots (0: none)
     int merged = 0;             // resolve_mfma: entries hold the minimum over every transform (search_mfma VAR 128)
+    int fmode = 0;              // resolve_mfma: the entries are fmap'd float-C minima (search_mfma VAR 256)
     const DevPlan* plan = nullptr; // device-planned search: nr, ntiles, nslots, flip_slots from the plan
     // resolve_dft: the fit runs in the resolving wave (fit_rstat_range) instead of a fit_rstat launch
     int fused_fit = 0;
@@ -673,7 +778,9 @@ __global__ void __launch_bounds__(256) resolve_mfma(MfmaResolveArgs a)
         sr2u = __builtin_amdgcn_udot2(__builtin_bit_cast(ushort2_t, cp[w]), __builtin_bit_cast(ushort2_t, cp[w]), sr2u,
                                       false);
     const int64_t sr2 = (int64_t)quad_sum(sr2u);
-    const int64_t target = (int64_t)vmin - (int64_t)a.rconst[slot]; // best S16 (when vmin != sentinel)
+    // best S16 (when vmin is not a sentinel): v − c_r, or for the float-C entries acc + c'_r = acc + V0 − c_r
+    const int64_t target = a.fmode ? (int64_t)funmap(vmin) + mfma_v0(NN) - (int64_t)(int32_t)a.rconst[slot]
+                                   : (int64_t)vmin - (int64_t)a.rconst[slot];
     // hits: the sentinel 0 (kernel run with H > 0), or a best error that meets H = 0
     const bool hit = a.hitH >= 0 && (vmin == 0 || target <= a.hitH);
     unsigned long long bestk = kKeyNone;

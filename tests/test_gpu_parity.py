@@ -331,6 +331,34 @@ def test_mfma_forms_at_operand_extremes(kind, form):
         assert st["rejected_mappings"] == wst["rejected_mappings"]
 
 
+@pytest.mark.parametrize("n", [2, 4])
+@pytest.mark.parametrize("kind", ["binary", "blocks2", "noise"])
+def test_float_c_epilogue_at_operand_extremes(n, kind):
+    """n ≤ 4 runs the direct form with the float-C epilogue (search_mfma VAR 386): the accumulator starts
+    from the domain row's ΣD4² − 1024·ΣD4 and the B operand is 8·(128 − r), exact while every partial sum
+    stays below 2^24 (2^22 + 8·n²·128·510).  On 0/255 frames that drive both to their bounds, with T = 4 / 8,
+    the classifier and a hit threshold, the records and reject counts equal the VALU engine's; the sampled
+    form's T = 1 rows (16→4) too."""
+    rng = np.random.default_rng(zlib.crc32(f"fc{kind}{n}".encode()))
+    S = 128
+    p = rng.integers(0, 256, (S, S), dtype=np.uint8) if kind == "noise" else _extreme_plane(rng, S, kind)
+    cases = [(2 * n, 4, False, 0.0), (2 * n, 8, True, 0.0), (2 * n, 4, False, 30.0)]
+    if n == 4:
+        cases.append((16, 4, True, 0.0))  # 16 → 4: the sampled form's search_mfma<4, 1>
+    for src, T, cls, thr in cases:
+        doms, rngs = F.create_uniform_grid(S, S, src, src // 2), F.create_uniform_grid(S, S, n, n)
+        outs = {}
+        for eng in (F.ENGINE_VALU, F.ENGINE_MFMA):
+            with F.Engine(0, T, cls, thr, -1.0, eng) as e:
+                e.set_frame(p)
+                e.set_domains(doms)
+                outs[eng] = e.search(rngs)
+        (a, sa), (b, sb) = outs[F.ENGINE_VALU], outs[F.ENGINE_MFMA]
+        assert sb["engine"] == F.ENGINE_MFMA
+        assert a.tobytes() == b.tobytes(), f"{kind} n={n} src={src} T={T} cls={cls} thr={thr}"
+        assert sa["rejected_mappings"] == sb["rejected_mappings"] and sa["hit_ranges"] == sb["hit_ranges"]
+
+
 @pytest.mark.parametrize("kind", ["binary", "blocks8", "orbits", "noise"])
 def test_t8_fourier_flipped_copies_at_operand_extremes(kind):
     """T = 8 on the Fourier path: each range block runs a second time read through Flip

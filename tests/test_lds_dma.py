@@ -26,13 +26,13 @@ FAMILIES = ("search_dft<", "search_mfma<", "search_mfma16<")
 # one instance per family, as the product library instantiates them: the shipped C3 search first
 # (variant 35 = 1|kDftChain|kDft6|kDftFast6|kDftUnroll|kDftBufDma: buffer_load … lds stages and the
 # zero-tail reads of the guarded epilogue), then the SEA tiled form's exact six-MFMA tile (9217,
-# global_load_lds stages) and the direct form's shipped schedule (130)
+# global_load_lds stages) and the direct form's shipped schedule for n <= 4 (386, the float-C epilogue)
 INSTANCES = {
     "search_dft35": "template __global__ void fracenc::search_dft<false, 123905, 8u, 4u, false>(fracenc::DftArgs);",
     "search_dft35_hits": "template __global__ void fracenc::search_dft<true, 123905, 8u, 4u, false>(fracenc::DftArgs);",
     "search_dft": "template __global__ void fracenc::search_dft<false, 9217, 8u, 4u, true>(fracenc::DftArgs);",
     "search_dft_hits": "template __global__ void fracenc::search_dft<true, 9217, 8u, 4u, true>(fracenc::DftArgs);",
-    "search_mfma": "template __global__ void fracenc::search_mfma<4, 4, false, 130>(fracenc::MfmaSearchArgs);",
+    "search_mfma": "template __global__ void fracenc::search_mfma<4, 4, false, 386>(fracenc::MfmaSearchArgs);",
     "search_mfma16": "template __global__ void fracenc::search_mfma16<4, false>(fracenc::MfmaSearchArgs);",
 }
 
