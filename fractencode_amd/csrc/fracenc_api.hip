@@ -1684,6 +1684,11 @@ int launch_mfma(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool inits =
         v.best_key = c->d_best_key.ptr;
         v.merged = (N != 16 && T > 1 && (c->mfma_var_ran & (128 | 256))) ? 1 : 0; // entries merged over t
         v.fmode = (N != 16 && (c->mfma_var_ran & 256)) ? 1 : 0;                  // fmap'd float-C minima
+        if (!c->virt) { // the fit in the resolving wave (the sampled form fits at its own points: gen_fit)
+            v.fused_fit = 1;
+            v.fit = fit_args(c, dtgt, tstride, nr);
+            c->fit_fused = true;
+        }
         v.plan = c->qplan;
         resolve_mfma<N><<<(nr + 3) / 4, 256, 0, c->stream>>>(v);
     }

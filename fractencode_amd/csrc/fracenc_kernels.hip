@@ -407,6 +407,37 @@ __device__ inline void fit_range(const FitArgs& a, uint32_t r, int sub)
 //
 // One range's record from its selection key and the winner's sums st = {X_t, ΣD4 | Σr << 16, ΣD4²,
 // Σr²}: fit_rstat's body, also run by resolve_dft's wave when the fit is fused into it
+// One range's record from its selection key and the winner's exact sums (X_t, ΣD4, Σr, ΣD4², Σr²):
+// the resolve kernels' fused fit (resolve_dft through fit_rstat_range, resolve_mfma directly)
+template <int N>
+__device__ inline void fit_sums_range(const FitArgs& a, uint32_t r, unsigned long long key, long long X, long long sD,
+                                      long long sA, long long sD2, long long sA2)
+{
+    constexpr int NN = N * N;
+    const frac_grid_item rg = a.ranges[r];
+    if (key == kKeyNone) {
+        write_default(a.out[r], rg);
+        a.aux[r] = RangeAux{0u, (uint32_t)kAuxEmpty};
+        return;
+    }
+    const uint32_t p = key_pos(key);
+    // a miss-format key whose error meets H is a hit too (the resolve emits hit-format keys for hits)
+    const bool hit = (key >> 63) == 0;
+    const long long err = hit ? 0 : (long long)((key >> 27) & 0xfffffffffull);
+    const int t = hit ? (int)(key & 7u) : (int)(a.T - 1 - (uint32_t)(key & 7u));
+    if (!hit && err >= kExactLimit) { // fp32 regime: fallback_fp32 writes the record
+        a.aux[r] = RangeAux{p, (uint32_t)kAuxFallback};
+        a.fb_list[atomicAdd(a.fb_count, 1u)] = r;
+        return;
+    }
+    const frac_grid_item d = a.doms[a.porig[p]];
+    const long long S16 = 16 * sA2 - 8 * X + sD2;
+    const double dist = ((double)S16 * 0.0625) / (double)(d.w * d.h);
+    write_fit(a.out[r], rg, d, t, (double)sA, (double)sA2, (double)sD * 0.25, (double)X * 0.25, (double)NN, a.smax,
+              dist);
+    a.aux[r] = RangeAux{p, hit ? (uint32_t)kAuxHit : 0u};
+}
+
 template <int N>
 __device__ inline void fit_rstat_range(const FitArgs& a, uint32_t r, unsigned long long key, const uint4& st)
 {

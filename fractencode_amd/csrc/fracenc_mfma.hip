@@ -636,8 +636,8 @@ __global__ void __launch_bounds__(64 * T) search_mfma16(MfmaSearchArgs a)
     };
     const uint32_t nstage = (wk.w - wk.z + kTilesPerStage16 - 1) / kTilesPerStage16;
     auto stage_nt = [&](uint32_t st) { return min((uint32_t)kTilesPerStage16, wk.w - (wk.z + st * kTilesPerStage16)); };
-    // chunks of kTilesPerStage (4) tiles for resolve_mfma: two stages per chunk, both
-    // reported under the chunk's first tile
+    // each stage (2 tiles) is its own chunk for resolve_mfma (which scans kTilesPerStage16 tiles at n = 16:
+    // half the 512-byte rows a coarser chunk made it re-read)
     if (nstage)
         stage_tiles<KS, 64 * T>(lds0, a.dtiles, a.dconst, wk.z, stage_nt(0));
     for (uint32_t st = 0; st < nstage; st += 2) {
@@ -650,7 +650,7 @@ __global__ void __launch_bounds__(64 * T) search_mfma16(MfmaSearchArgs a)
             stage_barrier();
             if (st + 2 < nstage)
                 stage_tiles<KS, 64 * T>(lds0, a.dtiles, a.dconst, tb + 2 * kTilesPerStage16, stage_nt(st + 2));
-            compute(lds1, stage_nt(st + 1), tb);
+            compute(lds1, stage_nt(st + 1), tb + kTilesPerStage16);
         }
     }
     a.entries[((size_t)blockIdx.x * T + t) * 64 + lane] = make_uint2(best, btile);
@@ -753,10 +753,14 @@ __global__ void __launch_bounds__(256) resolve_mfma(MfmaResolveArgs a)
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1)
         vmin = min(vmin, (uint32_t)__shfl_xor((int)vmin, o, 64));
-    if (vmin == 0xffffffffu)
-        return; // no eligible domain: best_key stays "none"
+    if (vmin == 0xffffffffu) { // no eligible domain: best_key stays "none"
+        if (a.fused_fit && lane == 0)
+            fit_sums_range<N>(a.fit, r, kKeyNone, 0, 0, 0, 0, 0);
+        return;
+    }
     const frac_grid_item rg = a.ranges[r];
     const int i = lane >> 2, g = lane & 3;
+    constexpr uint32_t kOnes = 0x00010001u;
     // the lane's slice of the copy under transform ct (rebuilt when an entry's t differs)
     uint32_t cp[WPL];
     int ct = -1;
@@ -772,12 +776,16 @@ __global__ void __launch_bounds__(256) resolve_mfma(MfmaResolveArgs a)
         ct = t;
     };
     build_copy(0);
-    uint32_t sr2u = 0; // Σr² (every pixel meets exactly one domain cell)
+    uint32_t sr2u = 0, sr1u = 0; // Σr², Σr (every pixel meets exactly one domain cell)
 #pragma unroll
-    for (int w = 0; w < WPL; ++w)
+    for (int w = 0; w < WPL; ++w) {
         sr2u = __builtin_amdgcn_udot2(__builtin_bit_cast(ushort2_t, cp[w]), __builtin_bit_cast(ushort2_t, cp[w]), sr2u,
                                       false);
+        sr1u = __builtin_amdgcn_udot2(__builtin_bit_cast(ushort2_t, cp[w]), __builtin_bit_cast(ushort2_t, kOnes), sr1u,
+                                      false);
+    }
     const int64_t sr2 = (int64_t)quad_sum(sr2u);
+    const int64_t sr1 = (int64_t)quad_sum(sr1u);
     // best S16 (when vmin is not a sentinel): v − c_r, or for the float-C entries acc + c'_r = acc + V0 − c_r
     const int64_t target = a.fmode ? (int64_t)funmap(vmin) + mfma_v0(NN) - (int64_t)(int32_t)a.rconst[slot]
                                    : (int64_t)vmin - (int64_t)a.rconst[slot];
@@ -785,6 +793,7 @@ __global__ void __launch_bounds__(256) resolve_mfma(MfmaResolveArgs a)
     const bool hit = a.hitH >= 0 && (vmin == 0 || target <= a.hitH);
     unsigned long long bestk = kKeyNone;
     uint32_t best_tile = 0xffffffffu;
+    int64_t bx = 0, bsd = 0, bsd2 = 0; // the best key's X_t, ΣD4, ΣD4² (the fused fit)
     // only the entries holding the minimum are re-evaluated: the lanes test 64 entries at a
     // time and the wave walks the ballot of matches (the cost does not grow with the splits)
     for (uint32_t c0 = 0; c0 < nent; c0 += 64) {
@@ -812,8 +821,8 @@ __global__ void __launch_bounds__(256) resolve_mfma(MfmaResolveArgs a)
                     build_copy((int)tt);
                 // the entry names the first tile of the chunk that attained the minimum: scan the
                 // chunk's tiles in order; the first matching row is the earliest domain
-                for (uint32_t tile = ctile; tile < min(ctile + (uint32_t)kTilesPerStage, a.ntiles) && tile <= best_tile;
-                     ++tile) {
+                constexpr uint32_t CH = N == 16 ? (uint32_t)kTilesPerStage16 : (uint32_t)kTilesPerStage;
+                for (uint32_t tile = ctile; tile < min(ctile + CH, a.ntiles) && tile <= best_tile; ++tile) {
                     const int p = a.tile_pos[tile * 32 + row];
                     uint32_t d[WPL];
                     if (p >= 0 && g * WPL < K2) {
@@ -844,6 +853,12 @@ __global__ void __launch_bounds__(256) resolve_mfma(MfmaResolveArgs a)
                                                     __builtin_bit_cast(ushort2_t, d[w]), xu, false);
                     const int64_t X = (int64_t)quad_sum(xu);
                     const int64_t s16 = p >= 0 ? 16 * sr2 - 8 * X - (int64_t)a.negsd2[p] : 0;
+                    uint32_t sdu = 0; // ΣD4 of the row (the fused fit)
+#pragma unroll
+                    for (int w = 0; w < WPL; ++w)
+                        sdu = __builtin_amdgcn_udot2(__builtin_bit_cast(ushort2_t, d[w]),
+                                                     __builtin_bit_cast(ushort2_t, kOnes), sdu, false);
+                    const uint32_t sd1 = quad_sum(sdu);
                     const bool ok = p >= 0 && g == 0 && (hit ? (s16 <= a.hitH) : (s16 == target));
                     const unsigned long long mask = __ballot(ok);
                     if (mask) {
@@ -855,6 +870,9 @@ __global__ void __launch_bounds__(256) resolve_mfma(MfmaResolveArgs a)
                         if (k < bestk) {
                             bestk = k;
                             best_tile = tile;
+                            bx = (int64_t)(uint32_t)__shfl((int)(uint32_t)X, first, 64);
+                            bsd = (int64_t)(uint32_t)__shfl((int)sd1, first, 64);
+                            bsd2 = -(int64_t)a.negsd2[pf];
                         }
                         break;
                     }
@@ -862,8 +880,11 @@ __global__ void __launch_bounds__(256) resolve_mfma(MfmaResolveArgs a)
             }
         }
     }
-    if (lane == 0)
+    if (lane == 0) {
         a.best_key[r] = bestk;
+        if (a.fused_fit) // the record right here: no fit_winner launch
+            fit_sums_range<N>(a.fit, r, bestk, bx, bsd, sr1, bsd2, sr2);
+    }
 }
 
 } // namespace fracenc
