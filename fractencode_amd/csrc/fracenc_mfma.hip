@@ -887,4 +887,161 @@ __global__ void __launch_bounds__(256) resolve_mfma(MfmaResolveArgs a)
     }
 }
 
+// resolve_small<N> (n ∈ {2, 4}, T ∈ {4, 8}): resolve_mfma restated for rows short enough to sit in one
+// lane.  Lane l takes tile row i = l >> 2 of a matching entry's lane half and the transforms t ≡ l (mod 4)
+// (t and t + 4 at T = 8), each with the whole pool row (n²/2 ≤ 8 words) against its own copy of the range,
+// so a chunk's 4 tiles × 16 rows × T transforms take one pass per tile instead of one per (tile,
+// transform); the wave's least selection key picks the first hit in (domain, transform) order, else the
+// exact least error with ties to the earliest domain, then the later transform — resolve_mfma's order.
+// The first tile holding a match ends the walk (later tiles hold later pool positions).  With
+// fused_fit the record is written here (fit_sums_range), from the winning lane's sums.
+template <int N>
+__global__ void __launch_bounds__(256) resolve_small(MfmaResolveArgs a)
+{
+    static_assert(N == 2 || N == 4, "one pool row per lane");
+    constexpr int NN = N * N, K2 = NN / 2;
+    constexpr uint32_t kOnes = 0x00010001u;
+    apply_plan(a);
+    const uint32_t r = blockIdx.x * 4u + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (r >= a.nr)
+        return;
+    const uint32_t slot = a.range_slot[r];
+    const uint32_t blk = slot >> 5, col = slot & 31u;
+    const uint32_t e0 = a.blk_ptr[blk], e1 = a.blk_ptr[blk + 1];
+    const uint32_t TE = a.merged ? 1u : a.T;
+    const uint32_t nent = (e1 - e0) * TE * 2u;
+    uint32_t vmin = 0xffffffffu;
+    for (uint32_t j = lane; j < nent; j += 64) {
+        const uint32_t e = e0 + j / (2u * TE), t = (j >> 1) % TE, h = j & 1u;
+        vmin = min(vmin, a.entries[((size_t)a.blk_ent[e] * a.T + t) * 64 + col + 32 * h].x);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1)
+        vmin = min(vmin, (uint32_t)__shfl_xor((int)vmin, o, 64));
+    if (vmin == 0xffffffffu) {
+        if (a.fused_fit && lane == 0)
+            fit_sums_range<N>(a.fit, r, kKeyNone, 0, 0, 0, 0, 0);
+        return;
+    }
+    const frac_grid_item rg = a.ranges[r];
+    const int i = lane >> 2, t0 = lane & 3;
+    const bool two = a.T == 8;
+    // the lane's copies of the range under t0 (and t0 + 4): the pixels meeting pool cells 2k, 2k + 1
+    uint32_t cp[2][K2];
+    uint32_t sr1u = 0, sr2u = 0;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+        const Aff af = lut(t0 + 4 * c);
+#pragma unroll
+        for (int k = 0; k < K2; ++k)
+            cp[c][k] = (c == 0 || two) ? range_pix_inv<N>(a.tgt, a.tstride, rg, af, 2 * k) |
+                                             (range_pix_inv<N>(a.tgt, a.tstride, rg, af, 2 * k + 1) << 16)
+                                       : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < K2; ++k) {
+        sr2u = __builtin_amdgcn_udot2(__builtin_bit_cast(ushort2_t, cp[0][k]), __builtin_bit_cast(ushort2_t, cp[0][k]),
+                                      sr2u, false);
+        sr1u = __builtin_amdgcn_udot2(__builtin_bit_cast(ushort2_t, cp[0][k]), __builtin_bit_cast(ushort2_t, kOnes),
+                                      sr1u, false);
+    }
+    const int64_t sr2 = (int64_t)sr2u, sr1 = (int64_t)sr1u; // every lane holds the whole range
+    const int64_t target = a.fmode ? (int64_t)funmap(vmin) + mfma_v0(NN) - (int64_t)(int32_t)a.rconst[slot]
+                                   : (int64_t)vmin - (int64_t)a.rconst[slot];
+    const bool hit = a.hitH >= 0 && (vmin == 0 || target <= a.hitH);
+    unsigned long long bestk = kKeyNone;
+    uint32_t best_tile = 0xffffffffu;
+    int64_t bx = 0, bsd = 0, bsd2 = 0;
+    for (uint32_t c0 = 0; c0 < nent; c0 += 64) {
+        const uint32_t jl = c0 + (uint32_t)lane;
+        uint2 enl = make_uint2(0xffffffffu, 0u);
+        if (jl < nent) {
+            const uint32_t e = e0 + jl / (2u * TE), t = (jl >> 1) % TE, h = jl & 1u;
+            enl = a.entries[((size_t)a.blk_ent[e] * a.T + t) * 64 + col + 32 * h];
+        }
+        unsigned long long match = __ballot(jl < nent && enl.x == vmin);
+        while (match) {
+            const int src = __ffsll((long long)match) - 1;
+            match &= match - 1;
+            const uint32_t j = c0 + (uint32_t)src, h = j & 1u;
+            const uint32_t ctile = (uint32_t)__builtin_amdgcn_readlane((int)enl.y, src);
+            if (ctile > best_tile)
+                continue;
+            const int row = (i & 3) + 8 * (i >> 2) + 4 * (int)h;
+            for (uint32_t tile = ctile; tile < min(ctile + (uint32_t)kTilesPerStage, a.ntiles) && tile <= best_tile;
+                 ++tile) {
+                const int p = a.tile_pos[tile * 32 + row];
+                uint32_t d[K2];
+                if (p >= 0) {
+                    const uint32_t* dp = a.pool + (size_t)p * K2;
+                    if constexpr (K2 == 8) {
+                        const uint4 v0 = reinterpret_cast<const uint4*>(dp)[0], v1 = reinterpret_cast<const uint4*>(dp)[1];
+                        d[0] = v0.x, d[1] = v0.y, d[2] = v0.z, d[3] = v0.w, d[4] = v1.x, d[5] = v1.y, d[6] = v1.z, d[7] = v1.w;
+                    } else {
+#pragma unroll
+                        for (int k = 0; k < K2; ++k)
+                            d[k] = dp[k];
+                    }
+                } else {
+#pragma unroll
+                    for (int k = 0; k < K2; ++k)
+                        d[k] = 0u;
+                }
+                uint32_t sd1u = 0;
+#pragma unroll
+                for (int k = 0; k < K2; ++k)
+                    sd1u = __builtin_amdgcn_udot2(__builtin_bit_cast(ushort2_t, d[k]), __builtin_bit_cast(ushort2_t, kOnes),
+                                                  sd1u, false);
+                const int64_t nsd2 = p >= 0 ? (int64_t)a.negsd2[p] : 0;
+                unsigned long long mk = kKeyNone; // the lane's least key over its transforms
+                int64_t mx = 0;
+#pragma unroll
+                for (int c = 0; c < 2; ++c) {
+                    if (c == 1 && !two)
+                        break;
+                    uint32_t xu = 0;
+#pragma unroll
+                    for (int k = 0; k < K2; ++k)
+                        xu = __builtin_amdgcn_udot2(__builtin_bit_cast(ushort2_t, cp[c][k]),
+                                                    __builtin_bit_cast(ushort2_t, d[k]), xu, false);
+                    const int64_t s16 = 16 * sr2 - 8 * (int64_t)xu - nsd2;
+                    const uint32_t tt = (uint32_t)(t0 + 4 * c);
+                    if (p >= 0 && (hit ? (s16 <= a.hitH) : (s16 == target))) {
+                        const unsigned long long k =
+                            hit ? key_hit((uint32_t)p, tt) : key_miss((uint64_t)s16, (uint32_t)p, a.T - 1 - tt);
+                        if (k < mk) {
+                            mk = k;
+                            mx = (int64_t)xu;
+                        }
+                    }
+                }
+                unsigned long long wk = mk; // the wave's least key of the tile
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) {
+                    const unsigned long long ok2 = ((unsigned long long)lane_xor((uint32_t)(wk >> 32), lane, o) << 32) |
+                                                   lane_xor((uint32_t)wk, lane, o);
+                    wk = ok2 < wk ? ok2 : wk;
+                }
+                if (wk != kKeyNone) {
+                    if (wk < bestk) {
+                        const int src2 = __ffsll((long long)__ballot(mk == wk)) - 1;
+                        bestk = wk;
+                        best_tile = tile;
+                        bx = (int64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)mx, src2);
+                        bsd = (int64_t)(uint32_t)__builtin_amdgcn_readlane((int)sd1u, src2);
+                        bsd2 = -(int64_t)(int32_t)__builtin_amdgcn_readlane((int)(int32_t)nsd2, src2);
+                    }
+                    break; // later tiles of the chunk hold later pool positions
+                }
+            }
+        }
+    }
+    if (lane == 0) {
+        a.best_key[r] = bestk;
+        if (a.fused_fit)
+            fit_sums_range<N>(a.fit, r, bestk, bx, bsd, sr1, bsd2, sr2);
+    }
+}
+
 } // namespace fracenc
