@@ -480,7 +480,7 @@ int device_buckets(frac_ctx* c, int nb, uint32_t* dfirst, uint32_t* rfirst)
     HostTrace tr("buckets");
     const uint32_t m = std::max(std::max(nd, nr), 1u);
     FRAC_HIP(c, c->d_bk_keys.ensure(m));
-    FRAC_HIP(c, c->d_bk_cnt.ensure((size_t)((m + kBkTile - 1) / kBkTile) * kMaxBuckets));
+    FRAC_HIP(c, c->d_bk_cnt.ensure((size_t)(2 * ((m + kBkTile - 1) / kBkTile) + 2) * kMaxBuckets));
     FRAC_HIP(c, c->d_bk_first.ensure(2 * (kMaxBuckets + 1) + 1));
     tr.mark("alloc");
     uint32_t* first = c->d_bk_first.ptr;
@@ -493,10 +493,12 @@ int device_buckets(frac_ctx* c, int nb, uint32_t* dfirst, uint32_t* rfirst)
     if (nd)
         launch_bucket_keys(c->d_doms.ptr, nd, c->Sh, c->d_src.ptr, c->d_sstride, c->d_bk_keys.ptr, nullptr, err,
                            c->stream);
-    launch_bucket_sort(c->d_bk_keys.ptr, nd, nullptr, c->d_bk_cnt.ptr, first, c->d_porig.ptr, c->stream);
     if (nr)
         launch_bucket_keys(c->d_ranges.ptr, nr, c->nh, tplane, tstride, c->d_rkey.ptr, nullptr, err, c->stream);
-    launch_bucket_sort(c->d_rkey.ptr, nr, nullptr, c->d_bk_cnt.ptr, first + kMaxBuckets + 1, c->d_rord.ptr, c->stream);
+    const BkSeg sd = bk_seg_of(c->d_bk_keys.ptr, nd, nullptr, c->d_bk_cnt.ptr, first, c->d_porig.ptr);
+    const BkSeg sr = bk_seg_of(c->d_rkey.ptr, nr, nullptr, c->d_bk_cnt.ptr + (size_t)sd.tiles * kMaxBuckets,
+                               first + kMaxBuckets + 1, c->d_rord.ptr);
+    launch_bucket_sorts(sd, sr, c->stream);
     uint32_t h[2 * (kMaxBuckets + 1) + 1];
     tr.mark("enqueue");
     FRAC_HIP(c, hipMemcpyAsync(h, first, sizeof(h), hipMemcpyDeviceToHost, c->stream));
@@ -2332,14 +2334,8 @@ int qt_encode_dev(frac_ctx* c, const frac_quadtree_params* qp, LevelGrid& level,
         FRAC_HIP(c, dptr.ensure((size_t)nblocks_cap * cp + 1));
         FRAC_HIP(c, dent.ensure(std::max<uint32_t>(nent_cap, 1)));
         FRAC_HIP(c, c->d_m_entries.ensure((size_t)nwork_cap * (fourier ? kDftBlocksPerWG : 4u * T) * 64));
-        size_t sneed = 0;
-        FRAC_HIP(c, c->d_bk_cnt.ensure((mx + kBkTile - 1) / kBkTile * kMaxBuckets));
-        FRAC_HIP(c, hipcub::DeviceScan::ExclusiveSum(nullptr, sneed, c->d_qt_flags.ptr, c->d_qt_offs.ptr,
-                                                     (int)std::max<uint32_t>(nr_max, 1), c->stream));
-        if (sneed > c->qt_tmp_bytes) {
-            FRAC_HIP(c, c->d_qt_tmp.ensure(sneed));
-            c->qt_tmp_bytes = sneed;
-        }
+        FRAC_HIP(c, c->d_bk_cnt.ensure(((size_t)(nd + kBkTile - 1) / kBkTile + (nr_max + kBkTile - 1) / kBkTile + 2) *
+                                       kMaxBuckets));
         tr.mark("level buffers");
         DevPlan* plan = c->d_qt_plan.ptr + lvi;
         const uint32_t* dn = lvi ? &plan->nr : nullptr; // the first level's count is the host's
@@ -2350,11 +2346,13 @@ int qt_encode_dev(frac_ctx* c, const frac_quadtree_params* qp, LevelGrid& level,
             // no invalid category can occur, so no error word)
             launch_bucket_keys(c->d_doms.ptr, nd, 2 * n, c->d_src.ptr, c->d_sstride, c->d_bk_keys.ptr, nullptr,
                                nullptr, c->stream);
-            launch_bucket_sort(c->d_bk_keys.ptr, nd, nullptr, c->d_bk_cnt.ptr, first, c->d_porig.ptr, c->stream);
             launch_bucket_keys(c->d_ranges.ptr, nr_max, n, tplane, tstride, c->d_rkey.ptr, nullptr, nullptr,
                                c->stream, dn);
-            launch_bucket_sort(c->d_rkey.ptr, nr_max, dn, c->d_bk_cnt.ptr, first + kMaxBuckets + 1, c->d_rord.ptr,
-                               c->stream);
+            // both sorts in one set of launches (the range counts after the domain counts in the scratch)
+            const BkSeg sd = bk_seg_of(c->d_bk_keys.ptr, nd, nullptr, c->d_bk_cnt.ptr, first, c->d_porig.ptr);
+            const BkSeg sr = bk_seg_of(c->d_rkey.ptr, nr_max, dn, c->d_bk_cnt.ptr + (size_t)sd.tiles * kMaxBuckets,
+                                       first + kMaxBuckets + 1, c->d_rord.ptr);
+            launch_bucket_sorts(sd, sr, c->stream);
         } else {
             if (nd)
                 fill_iota<<<(nd + 255) / 256, 256, 0, c->stream>>>(c->d_porig.ptr, nd);
@@ -2380,9 +2378,7 @@ int qt_encode_dev(frac_ctx* c, const frac_quadtree_params* qp, LevelGrid& level,
         pa.blk_ptr = dptr.ptr;
         pa.blk_ent = dent.ptr;
         pa.acc = c->d_qt_stats.ptr;
-        qt_plan<<<32, 256, 0, c->stream>>>(pa);
-        QtFillArgs fa;
-        fa.plan = plan;
+        QtFillArgs& fa = pa.fill;
         fa.rord = c->d_rord.ptr;
         fa.rkey = c->d_rkey.ptr;
         fa.copies = cp;
@@ -2394,7 +2390,8 @@ int qt_encode_dev(frac_ctx* c, const frac_quadtree_params* qp, LevelGrid& level,
         fa.rconst = fourier ? nullptr : c->d_m_rconst.ptr;
         fa.best_key = c->d_best_key.ptr;
         fa.fb_count = c->d_fb_count.ptr;
-        qt_fill_maps<<<(fa.nthreads + 255) / 256, 256, 0, c->stream>>>(fa);
+        // the layout, work lists, CSR map and per-item maps: one launch
+        qt_plan<<<std::max(32u, (fa.nthreads + 255) / 256), 256, 0, c->stream>>>(pa);
         // the level's search, on the bounds: launch_all in plan mode
         c->m_work.clear();
         c->m8_work.clear();
@@ -2418,20 +2415,31 @@ int qt_encode_dev(frac_ctx* c, const frac_quadtree_params* qp, LevelGrid& level,
         if (timing)
             runs.push_back(c->hist_runs - 1);
         tr.mark("level launch");
-        if (stats)
-            qt_level_stats<<<(nr_max + 255) / 256, 256, 0, c->stream>>>(
-                c->d_aux.ptr, c->d_rkey.ptr, c->d_porig.ptr, nr_max, (uint64_t)nd, c->p.use_classifier ? 1 : 0,
-                QtBuckets{}, nullptr, c->d_qt_stats.ptr, plan, kQtShards, kQtCounters);
         level.out();
-        qt_flags<<<(nr_max + 255) / 256, 256, 0, c->stream>>>(c->d_out.ptr, nr_max, n > qp->min_size ? 1 : 0,
-                                                             qp->split_distance, c->d_qt_flags.ptr, plan);
-        size_t tb = c->qt_tmp_bytes;
-        FRAC_HIP(c, hipcub::DeviceScan::ExclusiveSum(c->d_qt_tmp.ptr, tb, c->d_qt_flags.ptr, c->d_qt_offs.ptr,
-                                                     (int)nr_max, c->stream));
-        qt_scatter<<<(nr_max + 255) / 256, 256, 0, c->stream>>>(c->d_out.ptr, c->d_ranges.ptr, nr_max,
-                                                               c->d_qt_flags.ptr, c->d_qt_offs.ptr,
-                                                               c->d_qt_leaves.ptr, 0, c->d_qt_next.ptr, nullptr,
-                                                               plan, plan + 1);
+        // the level transition: split counts and counters, their prefix and the next count, leaves and quadrants
+        QtSplitArgs sa;
+        sa.out = c->d_out.ptr;
+        sa.ranges = c->d_ranges.ptr;
+        sa.plan = plan;
+        sa.next = plan + 1;
+        sa.nmax = nr_max;
+        sa.can_split = n > qp->min_size ? 1 : 0;
+        sa.split = qp->split_distance;
+        sa.tcount = c->d_qt_flags.ptr;
+        sa.leaves = c->d_qt_leaves.ptr;
+        sa.next_ranges = c->d_qt_next.ptr;
+        sa.aux = c->d_aux.ptr;
+        sa.rkey = c->d_rkey.ptr;
+        sa.porig = c->d_porig.ptr;
+        sa.nd = nd;
+        sa.classifier = c->p.use_classifier ? 1 : 0;
+        sa.acc = stats ? c->d_qt_stats.ptr : nullptr;
+        sa.shards = kQtShards;
+        sa.stride = kQtCounters;
+        const uint32_t ntl = std::max<uint32_t>((nr_max + kBkTile - 1) / kBkTile, 1u);
+        qt_split_count<<<ntl, kBkThreads, 0, c->stream>>>(sa);
+        qt_split_scan<<<1, 64, 0, c->stream>>>(sa, ntl);
+        qt_split_emit<<<ntl, kBkThreads, 0, c->stream>>>(sa);
         std::swap(c->d_ranges, c->d_qt_next);
         // the next level: at most four quadrants per range, at most the full grid of its size (counted in
         // closed form: frac_uniform_grid's count loop took 0.2 ms of host time for the 2×2 grid at 2048²)

@@ -174,18 +174,38 @@ inline void launch_bucket_keys(const frac_grid_item* items, uint32_t cnt, uint32
 // grids cover n.
 constexpr uint32_t kBkTile = 1024, kBkThreads = 256;
 
-__device__ inline uint32_t bk_count_of(const uint32_t* __restrict__ dn, uint32_t n) { return dn ? min(*dn, n) : n; }
+// one sort: keys [n] (or the first *dn of them), per-tile counts scratch, bucket starts, sorted indices
+struct BkSeg {
+    const uint32_t* keys;
+    uint32_t n;
+    const uint32_t* dn;
+    uint32_t* counts; // [tiles · kMaxBuckets]
+    uint32_t* first;  // [kMaxBuckets + 1]
+    uint32_t* out;
+    uint32_t tiles;   // ⌈n / kBkTile⌉
+};
 
-__global__ void __launch_bounds__(kBkThreads) bksort_count(const uint32_t* __restrict__ keys, uint32_t n,
-                                                           const uint32_t* __restrict__ dn, uint32_t* __restrict__ counts)
+// Two independent sorts per launch (a quadtree level's domains and ranges): blocks [0, s0.tiles) take s0,
+// the rest s1 (s1.tiles = 0: one sort).
+__device__ inline const BkSeg& bk_seg(const BkSeg& s0, const BkSeg& s1, uint32_t& blk)
+{
+    if (blk < s0.tiles)
+        return s0;
+    blk -= s0.tiles;
+    return s1;
+}
+
+__global__ void __launch_bounds__(kBkThreads) bksort_count(BkSeg s0, BkSeg s1)
 {
     __shared__ uint32_t part[kBkThreads / 64][kMaxBuckets];
-    n = bk_count_of(dn, n);
-    const uint32_t base = blockIdx.x * kBkTile, lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    uint32_t blk = blockIdx.x;
+    const BkSeg& s = bk_seg(s0, s1, blk);
+    const uint32_t n = s.dn ? min(*s.dn, s.n) : s.n;
+    const uint32_t base = blk * kBkTile, lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     uint32_t c[kMaxBuckets] = {};
     for (uint32_t j = 0; j < kBkTile / kBkThreads; ++j) {
         const uint32_t i = base + j * kBkThreads + threadIdx.x;
-        const uint32_t k = i < n ? keys[i] : (uint32_t)kMaxBuckets;
+        const uint32_t k = i < n ? s.keys[i] : (uint32_t)kMaxBuckets;
 #pragma unroll
         for (uint32_t b = 0; b < (uint32_t)kMaxBuckets; ++b)
             c[b] += (uint32_t)__builtin_popcountll(__ballot(k == b));
@@ -199,22 +219,23 @@ __global__ void __launch_bounds__(kBkThreads) bksort_count(const uint32_t* __res
         uint32_t t = 0;
         for (uint32_t w = 0; w < kBkThreads / 64; ++w)
             t += part[w][threadIdx.x];
-        counts[blockIdx.x * kMaxBuckets + threadIdx.x] = t;
+        s.counts[blk * kMaxBuckets + threadIdx.x] = t;
     }
 }
 
-// one block of kMaxBuckets waves, wave b scanning bucket b: offsets[tile][b] = first[b] + the bucket's
-// items in earlier tiles (in place over counts).  Lane l takes a run of ⌈ntiles / 64⌉ tiles; the lanes'
-// run sums are scanned with shuffles, the buckets' totals meet once in LDS.
-__global__ void __launch_bounds__(64 * kMaxBuckets) bksort_scan(uint32_t* __restrict__ counts, uint32_t ntiles,
-                                                                uint32_t* __restrict__ first)
+// one block per sort of kMaxBuckets waves, wave b scanning bucket b: offsets[tile][b] = first[b] + the
+// bucket's items in earlier tiles (in place over counts).  Lane l takes a run of ⌈tiles / 64⌉ tiles; the
+// lanes' run sums are scanned with shuffles, the buckets' totals meet once in LDS.
+__global__ void __launch_bounds__(64 * kMaxBuckets) bksort_scan(BkSeg s0, BkSeg s1)
 {
     __shared__ uint32_t tot[kMaxBuckets];
+    const BkSeg& s = blockIdx.x == 0 ? s0 : s1;
+    const uint32_t ntiles = s.tiles;
     const uint32_t b = threadIdx.x >> 6, lane = threadIdx.x & 63u;
     const uint32_t per = (ntiles + 63) / 64, t0 = min(lane * per, ntiles), t1 = min(t0 + per, ntiles);
     uint32_t run = 0;
     for (uint32_t t = t0; t < t1; ++t)
-        run += counts[t * kMaxBuckets + b];
+        run += s.counts[t * kMaxBuckets + b];
     uint32_t inc = run; // inclusive scan over the lanes
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -229,33 +250,32 @@ __global__ void __launch_bounds__(64 * kMaxBuckets) bksort_scan(uint32_t* __rest
     for (uint32_t k = 0; k < b; ++k)
         base += tot[k];
     if (lane == 0) {
-        first[b] = base;
+        s.first[b] = base;
         if (b == kMaxBuckets - 1)
-            first[kMaxBuckets] = base + tot[b];
+            s.first[kMaxBuckets] = base + tot[b];
     }
     uint32_t off = base + inc - run;
     for (uint32_t t = t0; t < t1; ++t) {
-        const uint32_t c = counts[t * kMaxBuckets + b];
-        counts[t * kMaxBuckets + b] = off;
+        const uint32_t c = s.counts[t * kMaxBuckets + b];
+        s.counts[t * kMaxBuckets + b] = off;
         off += c;
     }
 }
 
-__global__ void __launch_bounds__(kBkThreads) bksort_scatter(const uint32_t* __restrict__ keys, uint32_t n,
-                                                             const uint32_t* __restrict__ dn,
-                                                             const uint32_t* __restrict__ offsets,
-                                                             uint32_t* __restrict__ out)
+__global__ void __launch_bounds__(kBkThreads) bksort_scatter(BkSeg s0, BkSeg s1)
 {
     __shared__ uint32_t wcnt[kBkThreads / 64][kMaxBuckets];
     __shared__ uint32_t run[kMaxBuckets];
-    n = bk_count_of(dn, n);
-    const uint32_t base = blockIdx.x * kBkTile, lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    uint32_t blk = blockIdx.x;
+    const BkSeg& s = bk_seg(s0, s1, blk);
+    const uint32_t n = s.dn ? min(*s.dn, s.n) : s.n;
+    const uint32_t base = blk * kBkTile, lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     if (threadIdx.x < (uint32_t)kMaxBuckets)
-        run[threadIdx.x] = offsets[blockIdx.x * kMaxBuckets + threadIdx.x];
+        run[threadIdx.x] = s.counts[blk * kMaxBuckets + threadIdx.x];
     const unsigned long long below = lane ? (~0ull >> (64 - lane)) : 0ull;
     for (uint32_t j = 0; j < kBkTile / kBkThreads; ++j) {
         const uint32_t i = base + j * kBkThreads + threadIdx.x;
-        const uint32_t k = i < n ? keys[i] : (uint32_t)kMaxBuckets;
+        const uint32_t k = i < n ? s.keys[i] : (uint32_t)kMaxBuckets;
         uint32_t mine = 0; // the rank among this wave's earlier lanes of the same key
 #pragma unroll
         for (uint32_t b = 0; b < (uint32_t)kMaxBuckets; ++b) {
@@ -270,7 +290,7 @@ __global__ void __launch_bounds__(kBkThreads) bksort_scatter(const uint32_t* __r
             uint32_t pos = run[k] + mine;
             for (uint32_t w = 0; w < wv; ++w)
                 pos += wcnt[w][k];
-            out[pos] = i;
+            s.out[pos] = i;
         }
         __syncthreads();
         if (threadIdx.x < (uint32_t)kMaxBuckets)
@@ -280,14 +300,26 @@ __global__ void __launch_bounds__(kBkThreads) bksort_scatter(const uint32_t* __r
     }
 }
 
-// the three launches; counts: [⌈n / kBkTile⌉ · kMaxBuckets] scratch
+inline BkSeg bk_seg_of(const uint32_t* keys, uint32_t n, const uint32_t* dn, uint32_t* counts, uint32_t* first,
+                       uint32_t* out)
+{
+    return BkSeg{keys, n, dn, counts, first, out, std::max<uint32_t>((n + kBkTile - 1) / kBkTile, 1u)};
+}
+
+// the three launches for one or two sorts (s1.tiles = 0: one)
+inline void launch_bucket_sorts(const BkSeg& s0, const BkSeg& s1, hipStream_t st)
+{
+    const uint32_t nt = s0.tiles + s1.tiles;
+    bksort_count<<<nt, kBkThreads, 0, st>>>(s0, s1);
+    bksort_scan<<<s1.tiles ? 2 : 1, 64 * kMaxBuckets, 0, st>>>(s0, s1);
+    bksort_scatter<<<nt, kBkThreads, 0, st>>>(s0, s1);
+}
+
 inline void launch_bucket_sort(const uint32_t* keys, uint32_t n, const uint32_t* dn, uint32_t* counts, uint32_t* first,
                                uint32_t* out, hipStream_t s)
 {
-    const uint32_t nt = std::max<uint32_t>((n + kBkTile - 1) / kBkTile, 1u);
-    bksort_count<<<nt, kBkThreads, 0, s>>>(keys, n, dn, counts);
-    bksort_scan<<<1, 64 * kMaxBuckets, 0, s>>>(counts, nt, first);
-    bksort_scatter<<<nt, kBkThreads, 0, s>>>(keys, n, dn, counts, out);
+    BkSeg none{};
+    launch_bucket_sorts(bk_seg_of(keys, n, dn, counts, first, out), none, s);
 }
 
 __global__ void __launch_bounds__(256) fill_iota(uint32_t* __restrict__ out, uint32_t n)
@@ -495,6 +527,211 @@ __global__ void __launch_bounds__(256) qt_scatter(const frac_encode_item* __rest
     }
 }
 
+// ---- the level transition of a device-planned quadtree level in three launches ----
+// (qt_level_stats + qt_flags + a scan + qt_scatter restated): per 1,024-range tile the split count and
+// the level's counters (qt_split_count), the tiles' exclusive prefix and the next level's count
+// (qt_split_scan), then the tile's leaves and quadrants in index order (qt_split_emit, the ranks from
+// wave ballots as in bksort_scatter).  A range splits when the level may split and its distance
+// exceeds the threshold; leaves keep the search order, quadrants their parents' order.
+struct QtSplitArgs {
+    const frac_encode_item* out;  // the level's records
+    const frac_grid_item* ranges; // the level's ranges
+    const DevPlan* plan;          // nr, leaf_base of this level; layout (stats)
+    DevPlan* next;                // receives the next level's nr and leaf_base
+    uint32_t nmax;                // the grid's bound
+    int can_split;
+    double split;
+    uint32_t* tcount;             // [tiles] splits per tile, then their exclusive prefix
+    frac_encode_item* leaves;
+    frac_grid_item* next_ranges;
+    // the level's frac_stats counters (qt_level_stats), when acc is not null
+    const RangeAux* aux;
+    const uint32_t* rkey;
+    const uint32_t* porig;
+    uint64_t nd;
+    int classifier;
+    unsigned long long* acc;
+    uint32_t shards, stride;
+};
+
+__device__ inline bool qt_splits(const QtSplitArgs& a, uint32_t i, uint32_t n)
+{
+    return i < n && a.can_split && a.out[i].match.score.distance > a.split;
+}
+
+__global__ void __launch_bounds__(kBkThreads) qt_split_count(QtSplitArgs a)
+{
+    __shared__ uint32_t wc[kBkThreads / 64];
+    __shared__ unsigned long long part[kBkThreads / 64][4];
+    const uint32_t n = min(a.plan->nr, a.nmax);
+    const uint32_t base = blockIdx.x * kBkTile, lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    uint32_t c = 0;
+    unsigned long long v[4] = {0ull, 0ull, 0ull, 0ull}; // rejected, hit, fallback, empty
+    const BucketLayout& L = a.plan->L;
+    for (uint32_t j = 0; j < kBkTile / kBkThreads; ++j) {
+        const uint32_t i = base + j * kBkThreads + threadIdx.x;
+        c += (uint32_t)__builtin_popcountll(__ballot(qt_splits(a, i, n)));
+        if (a.acc && i < n) { // qt_level_stats' counting, restated
+            const RangeAux ax = a.aux[i];
+            const uint32_t b = a.classifier ? a.rkey[i] : 0u;
+            if (ax.flags & kAuxEmpty) {
+                v[3] += 1;
+                v[0] += a.classifier ? a.nd : 0ull;
+            } else {
+                v[2] += (ax.flags & kAuxFallback) ? 1ull : 0ull;
+                if (ax.flags & kAuxHit) {
+                    v[1] += 1;
+                    if (a.classifier)
+                        v[0] += (unsigned long long)a.porig[ax.pos] - (ax.pos - L.dbeg[b]);
+                } else if (a.classifier) {
+                    v[0] += a.nd - L.dcnt[b];
+                }
+            }
+        }
+    }
+    if (lane == 0)
+        wc[wv] = c;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1)
+            v[k] += (unsigned long long)__shfl_xor((long long)v[k], o, 64);
+        if (lane == 0)
+            part[wv][k] = v[k];
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = 0;
+        for (uint32_t w = 0; w < kBkThreads / 64; ++w)
+            t += wc[w];
+        a.tcount[blockIdx.x] = t;
+    }
+    if (a.acc && threadIdx.x < 4) {
+        unsigned long long t = 0;
+        for (uint32_t w = 0; w < kBkThreads / 64; ++w)
+            t += part[w][threadIdx.x];
+        if (t)
+            atomicAdd(&a.acc[(blockIdx.x % a.shards) * a.stride + threadIdx.x], t);
+    }
+}
+
+// one wave: the tiles' exclusive prefix of split counts (in place), the next level's count and leaf base
+__global__ void __launch_bounds__(64) qt_split_scan(QtSplitArgs a, uint32_t ntiles)
+{
+    const uint32_t lane = threadIdx.x;
+    const uint32_t per = (ntiles + 63) / 64, t0 = min(lane * per, ntiles), t1 = min(t0 + per, ntiles);
+    uint32_t run = 0;
+    for (uint32_t t = t0; t < t1; ++t)
+        run += a.tcount[t];
+    uint32_t inc = run;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t x = (uint32_t)__shfl_up((int)inc, o, 64);
+        if ((int)lane >= o)
+            inc += x;
+    }
+    uint32_t off = inc - run;
+    for (uint32_t t = t0; t < t1; ++t) {
+        const uint32_t cnt = a.tcount[t];
+        a.tcount[t] = off;
+        off += cnt;
+    }
+    if (lane == 63) {
+        const uint32_t n = min(a.plan->nr, a.nmax), lb = a.plan->leaf_base;
+        a.next->nr = 4 * inc;
+        a.next->leaf_base = lb + n - inc;
+    }
+}
+
+__global__ void __launch_bounds__(kBkThreads) qt_split_emit(QtSplitArgs a)
+{
+    __shared__ uint32_t wcnt[kBkThreads / 64];
+    __shared__ uint32_t run;
+    const uint32_t n = min(a.plan->nr, a.nmax), leaf_base = a.plan->leaf_base;
+    const uint32_t base = blockIdx.x * kBkTile, lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    if (threadIdx.x == 0)
+        run = a.tcount[blockIdx.x];
+    const unsigned long long below = lane ? (~0ull >> (64 - lane)) : 0ull;
+    for (uint32_t j = 0; j < kBkTile / kBkThreads; ++j) {
+        const uint32_t i = base + j * kBkThreads + threadIdx.x;
+        const bool sp = qt_splits(a, i, n);
+        const unsigned long long m = __ballot(sp);
+        if (lane == 0)
+            wcnt[wv] = (uint32_t)__builtin_popcountll(m);
+        __syncthreads();
+        uint32_t o = run + (uint32_t)__builtin_popcountll(m & below); // splits before item i
+        for (uint32_t w = 0; w < wv; ++w)
+            o += wcnt[w];
+        if (i < n) {
+            if (sp) {
+                const frac_grid_item r = a.ranges[i];
+                const uint32_t h = r.w / 2;
+                a.next_ranges[4 * o + 0] = frac_grid_item{r.x, r.y, h, h, -1};
+                a.next_ranges[4 * o + 1] = frac_grid_item{r.x + h, r.y, h, h, -1};
+                a.next_ranges[4 * o + 2] = frac_grid_item{r.x, r.y + h, h, h, -1};
+                a.next_ranges[4 * o + 3] = frac_grid_item{r.x + h, r.y + h, h, h, -1};
+            } else {
+                a.leaves[leaf_base + (i - o)] = a.out[i];
+            }
+        }
+        __syncthreads();
+        if (threadIdx.x == 0)
+            for (uint32_t w = 0; w < kBkThreads / 64; ++w)
+                run += wcnt[w];
+        __syncthreads();
+    }
+}
+
+// The per-item maps of a planned level (fill_range_slots, fill_tile_pos and fill_rbucket restated, run
+// by qt_plan's threads), and the run's resets: best_key (none yet), the direct form's zeroed rconst
+// words (mfma_range_prep accumulates into them), the fallback count.
+struct QtFillArgs {
+    const uint32_t* rord;     // bucket-sorted range order
+    const uint32_t* rkey;     // per range: its bucket
+    uint32_t copies;          // T = 8 Fourier: slot s ≥ nblocks·32 is the flipped copy of s − nblocks·32
+    uint32_t nthreads;        // the grid's bound: max(slots, tile rows, ranges)
+    int32_t* slot_range;
+    uint32_t* range_slot;
+    int32_t* tile_pos;
+    uint2* rbucket;
+    uint32_t* rconst;         // zeroed per slot when not null (the direct form)
+    unsigned long long* best_key;
+    uint32_t* fb_count;
+};
+
+__device__ inline void qt_fill_item(const QtFillArgs& a, const BucketLayout& L, uint32_t nblocks, uint32_t ntiles,
+                                    uint32_t nr, uint32_t i)
+{
+    const uint32_t nslots = nblocks * 32u;
+    if (i < nslots * a.copies) {
+        const uint32_t s = i % nslots, b = layout_bucket_of_slot(L, s), k = s - L.slot_first[b];
+        int32_t r = -1;
+        if (k < L.rcnt[b]) {
+            r = (int32_t)a.rord[L.rbeg[b] + k];
+            if (i < nslots)
+                a.range_slot[r] = s;
+        }
+        a.slot_range[i] = r;
+        if (a.rconst)
+            a.rconst[i] = 0u;
+    }
+    if (i < ntiles * 32u) {
+        const uint32_t tile = i >> 5;
+        uint32_t b = 0;
+        for (uint32_t k = 1; k < L.nb; ++k)
+            b = tile >= L.tile_first[k] ? k : b;
+        const uint32_t j = i - 32u * L.tile_first[b];
+        a.tile_pos[i] = j < L.dcnt[b] ? (int32_t)(L.dbeg[b] + j) : -1;
+    }
+    if (i < nr) {
+        const uint32_t b = a.rkey[i];
+        a.rbucket[i] = make_uint2(L.dbeg[b], L.dbeg[b] + L.dcnt[b]);
+        a.best_key[i] = ~0ull;
+    }
+    if (i == 0)
+        *a.fb_count = 0u;
+}
+
 // ---- the device planner of a quadtree level (prepare()'s layout and work lists, restated) ----
 // From the bucket bounds of the level's domains and ranges (bucket_bounds over the sorted keys)
 // it lays out the MFMA engine's 32-slot range blocks and 32-row domain tiles per bucket, and writes
@@ -520,6 +757,7 @@ struct QtPlanArgs {
     uint32_t* blk_ptr;       // [nblocks·copies + 1]
     uint32_t* blk_ent;
     unsigned long long* acc; // frame counters: [5] total mappings, [6] eligible pairs, [7] flops, [8] overflow
+    QtFillArgs fill;         // the per-item maps, filled by the same launch (from the header in LDS)
 };
 
 struct QtPlanHeader {
@@ -662,61 +900,10 @@ __global__ void __launch_bounds__(256) qt_plan(QtPlanArgs a)
         for (uint32_t sp = 0; sp < ns; ++sp)
             a.blk_ent[base + sp] = (h.wbase[q] + (k / a.bpw) * ns + sp) * a.bpw + k % a.bpw;
     }
-}
-
-// The per-item maps of a planned level (fill_range_slots, fill_tile_pos and fill_rbucket in one
-// launch over the worst case), and the run's resets: best_key (none yet), the direct form's
-// zeroed rconst words (mfma_range_prep accumulates into them), the fallback count.
-struct QtFillArgs {
-    const DevPlan* plan;
-    const uint32_t* rord;     // bucket-sorted range order
-    const uint32_t* rkey;     // per range: its bucket
-    uint32_t copies;          // T = 8 Fourier: slot s ≥ nblocks·32 is the flipped copy of s − nblocks·32
-    uint32_t nthreads;        // the grid's bound: max(slots, tile rows, ranges)
-    int32_t* slot_range;
-    uint32_t* range_slot;
-    int32_t* tile_pos;
-    uint2* rbucket;
-    uint32_t* rconst;         // zeroed per slot when not null (the direct form)
-    unsigned long long* best_key;
-    uint32_t* fb_count;
-};
-
-__global__ void __launch_bounds__(256) qt_fill_maps(QtFillArgs a)
-{
+    // the per-item maps, one item per thread of the grid (sized for fill.nthreads)
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= a.nthreads)
-        return;
-    const DevPlan& p = *a.plan;
-    const BucketLayout& L = p.L;
-    const uint32_t nslots = p.nblocks * 32u;
-    if (i < nslots * a.copies) {
-        const uint32_t s = i % nslots, b = layout_bucket_of_slot(L, s), k = s - L.slot_first[b];
-        int32_t r = -1;
-        if (k < L.rcnt[b]) {
-            r = (int32_t)a.rord[L.rbeg[b] + k];
-            if (i < nslots)
-                a.range_slot[r] = s;
-        }
-        a.slot_range[i] = r;
-        if (a.rconst)
-            a.rconst[i] = 0u;
-    }
-    if (i < p.ntiles * 32u) {
-        const uint32_t tile = i >> 5;
-        uint32_t b = 0;
-        for (uint32_t k = 1; k < L.nb; ++k)
-            b = tile >= L.tile_first[k] ? k : b;
-        const uint32_t j = i - 32u * L.tile_first[b];
-        a.tile_pos[i] = j < L.dcnt[b] ? (int32_t)(L.dbeg[b] + j) : -1;
-    }
-    if (i < p.nr) {
-        const uint32_t b = a.rkey[i];
-        a.rbucket[i] = make_uint2(L.dbeg[b], L.dbeg[b] + L.dcnt[b]);
-        a.best_key[i] = ~0ull;
-    }
-    if (i == 0)
-        *a.fb_count = 0u;
+    if (i < a.fill.nthreads)
+        qt_fill_item(a.fill, h.L, h.nblocks, h.ntiles, h.nr, i);
 }
 
 // createUniformGrid(W, H, size, off) on the device (image/partition2.hpp:123-133, frac_uniform_grid2):
