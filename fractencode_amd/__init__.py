@@ -409,21 +409,25 @@ class Engine:
                                           height, max_iter, rms_eps, plane.ctypes.data, C.byref(it), C.byref(rms)))
         return plane, it.value, rms.value
 
-    def encode_quadtree(self, max_size: int = 16, min_size: int = 4, split_distance: float = 10.0, out=None):
+    def encode_quadtree(self, max_size: int = 16, min_size: int = 4, split_distance: float = 10.0, out=None,
+                        allow_short: bool = False):
         """Quadtree partition of the frame set on this engine (frac_encode_quadtree): ranges of
         max_size split into quadrants while their best distance exceeds split_distance, down to
         min_size.  Returns (encode items of mixed sizes, summed stats dict).  With `out` (an
         ENCODE_ITEM array of at least (W/min_size)·(H/min_size) items, e.g. pinned host memory)
-        the items are written there and a view of it is returned, without a copy."""
+        the items are written there and a view of it is returned, without a copy; pinned host memory is
+        written by the device directly (no copy command).  allow_short: `out` may be shorter — the items
+        past it are counted (the stats) but not written, and the returned view is cut to `out`."""
         qp = FracQuadtreeParams(max_size, min_size, split_distance)
         n = C.c_size_t(0)
         st = FracStats()
         W, H = self._frame_wh
         cap = max((W // min_size) * (H // min_size), 1)
         if out is not None:
-            if out.dtype != ENCODE_ITEM or not out.flags.c_contiguous or len(out) < cap:
+            if out.dtype != ENCODE_ITEM or not out.flags.c_contiguous or (len(out) < cap and not allow_short):
                 raise ValueError(f"out must be a contiguous ENCODE_ITEM array of at least {cap} items")
             buf = out
+            cap = len(out)
         else:
             # one pass with a worst-case capacity (every range at min_size), in a buffer kept across
             # calls: a fresh one costs a page fault per 4 KiB on first touch
@@ -431,7 +435,9 @@ class Engine:
             if buf is None or len(buf) < cap:
                 buf = self._qt_buf = np.empty(cap, dtype=ENCODE_ITEM)
         self._check(lib().frac_encode_quadtree(self._ctx, C.byref(qp), buf.ctypes.data, cap, C.byref(n), C.byref(st)))
-        return (buf[: n.value] if out is not None else buf[: n.value].copy()), st.as_dict()
+        d = st.as_dict()
+        d["items"] = n.value
+        return (buf[: min(n.value, cap)] if out is not None else buf[: n.value].copy()), d
 
     def classify(self, items: np.ndarray, target_plane: bool = False) -> np.ndarray:
         """BrightnessBlocksClassifier2 categories of `items` computed on the device plane set by

@@ -263,6 +263,7 @@ struct frac_ctx {
     // device-planned quadtree levels (frac_encode_quadtree, MFMA engine): the levels' plans (+1 for
     // the count after the last), their bucket bounds, and the first level's range grid
     DBuf<DevPlan> d_qt_plan;
+    QtFrameSum* h_qt_sum = nullptr; // pinned, mapped: qt_finish writes the frame's counts there
     DBuf<uint32_t> d_qt_first;
     DBuf<frac_grid_item> d_qt_r0;
     uint32_t qt_r0_key[3] = {0, 0, 0};
@@ -2267,6 +2268,25 @@ int qt_encode_dev(frac_ctx* c, const frac_quadtree_params* qp, LevelGrid& level,
     if (nr0)
         qt_uniform_grid<<<(nr0 + 255) / 256, 256, 0, c->stream>>>((W - qp->max_size) / qp->max_size + 1, nr0,
                                                                   qp->max_size, qp->max_size, c->d_ranges.ptr);
+    // the leaves go straight into the caller's buffer when it is pinned host memory the device can write
+    // (the emit kernels write them over PCIe while the later levels run); else into d_qt_leaves and one
+    // copy at the end
+    frac_encode_item* leaves = c->d_qt_leaves.ptr;
+    uint32_t leaf_cap = (uint32_t)std::min<size_t>(max_leaves, 0xffffffffu);
+    bool direct = false;
+    if (out && cap) {
+        hipPointerAttribute_t at{};
+        void* dp = nullptr;
+        if (hipPointerGetAttributes(&at, out) == hipSuccess && at.type == hipMemoryTypeHost &&
+            hipHostGetDevicePointer(&dp, out, 0) == hipSuccess && dp) {
+            leaves = reinterpret_cast<frac_encode_item*>(dp);
+            leaf_cap = (uint32_t)std::min<size_t>(cap, 0xffffffffu);
+            direct = true;
+        }
+        (void)hipGetLastError(); // pageable memory is not an error
+    }
+    if (!c->h_qt_sum)
+        FRAC_HIP(c, hipHostMalloc(reinterpret_cast<void**>(&c->h_qt_sum), sizeof(QtFrameSum)));
     uint32_t nr_bound = nr0; // the level's worst-case range count
     int lvi = 0;             // level index (plans 0..4; plan lvi + 1 receives the next count)
     std::vector<uint64_t> runs; // the levels' timing-history runs
@@ -2426,7 +2446,8 @@ int qt_encode_dev(frac_ctx* c, const frac_quadtree_params* qp, LevelGrid& level,
         sa.can_split = n > qp->min_size ? 1 : 0;
         sa.split = qp->split_distance;
         sa.tcount = c->d_qt_flags.ptr;
-        sa.leaves = c->d_qt_leaves.ptr;
+        sa.leaves = leaves;
+        sa.leaf_cap = leaf_cap;
         sa.next_ranges = c->d_qt_next.ptr;
         sa.aux = c->d_aux.ptr;
         sa.rkey = c->d_rkey.ptr;
@@ -2454,25 +2475,23 @@ int qt_encode_dev(frac_ctx* c, const frac_quadtree_params* qp, LevelGrid& level,
     c->ranges_set = false;
     c->dirty = true;
     c->ran = false;
-    // the frame's one round trip for the counts: leaves (after the last level run), counters
+    // the frame's one round trip: qt_finish writes the leaf count and the summed counters into pinned
+    // memory (the leaves are already in the caller's buffer when it is pinned)
+    void* dsum = nullptr;
+    FRAC_HIP(c, hipHostGetDevicePointer(&dsum, c->h_qt_sum, 0));
+    qt_finish<<<1, 64, 0, c->stream>>>(c->d_qt_plan.ptr + lvi, lvi ? 1 : 0, c->d_qt_stats.ptr, kQtShards, kQtCounters,
+                                       reinterpret_cast<QtFrameSum*>(dsum));
+    FRAC_HIP(c, hipStreamSynchronize(c->stream));
     struct {
-        DevPlan last;
         unsigned long long acc[kQtCounters];
     } h{};
-    unsigned long long sh[kQtShards * kQtCounters];
-    FRAC_HIP(c, hipMemcpyAsync(&h.last, c->d_qt_plan.ptr + lvi, sizeof(DevPlan), hipMemcpyDeviceToHost, c->stream));
-    FRAC_HIP(c, hipMemcpyAsync(sh, c->d_qt_stats.ptr, sizeof(sh), hipMemcpyDeviceToHost, c->stream));
-    FRAC_HIP(c, hipStreamSynchronize(c->stream));
-    for (uint32_t k = 0; k < kQtShards; ++k)
-        for (uint32_t i = 0; i < kQtCounters; ++i)
-            h.acc[i] += sh[k * kQtCounters + i];
-    if (lvi == 0)
-        h.last.leaf_base = 0;
+    for (uint32_t i = 0; i < kQtCounters; ++i)
+        h.acc[i] = c->h_qt_sum->acc[i];
     if (h.acc[8])
         return c->fail(FRAC_E_STATE, "quadtree: a level's layout exceeded its planned bounds");
-    const uint32_t n_leaves = h.last.leaf_base;
+    const uint32_t n_leaves = c->h_qt_sum->leaves;
     *n_out = n_leaves;
-    if (out && n_leaves)
+    if (out && n_leaves && !direct)
         FRAC_HIP(c, hipMemcpy(out, c->d_qt_leaves.ptr, std::min<size_t>(cap, n_leaves) * sizeof(frac_encode_item),
                               hipMemcpyDeviceToHost));
     tr.mark("leaves D2H");
@@ -2667,6 +2686,8 @@ void frac_destroy(frac_ctx* c)
     c->d_dec_sum.release();
     if (c->h_dec_sum)
         (void)hipHostFree(c->h_dec_sum);
+    if (c->h_qt_sum)
+        (void)hipHostFree(c->h_qt_sum);
     for (auto& ev : c->ev)
         if (ev)
             (void)hipEventDestroy(ev);

@@ -542,7 +542,8 @@ struct QtSplitArgs {
     int can_split;
     double split;
     uint32_t* tcount;             // [tiles] splits per tile, then their exclusive prefix
-    frac_encode_item* leaves;
+    frac_encode_item* leaves;     // device memory, or the caller's pinned host buffer (written over PCIe)
+    uint32_t leaf_cap;            // leaves past it are not written (the caller's capacity)
     frac_grid_item* next_ranges;
     // the level's frac_stats counters (qt_level_stats), when acc is not null
     const RangeAux* aux;
@@ -670,7 +671,7 @@ __global__ void __launch_bounds__(kBkThreads) qt_split_emit(QtSplitArgs a)
                 a.next_ranges[4 * o + 1] = frac_grid_item{r.x + h, r.y, h, h, -1};
                 a.next_ranges[4 * o + 2] = frac_grid_item{r.x, r.y + h, h, h, -1};
                 a.next_ranges[4 * o + 3] = frac_grid_item{r.x + h, r.y + h, h, h, -1};
-            } else {
+            } else if (leaf_base + (i - o) < a.leaf_cap) {
                 a.leaves[leaf_base + (i - o)] = a.out[i];
             }
         }
@@ -730,6 +731,28 @@ __device__ inline void qt_fill_item(const QtFillArgs& a, const BucketLayout& L, 
     }
     if (i == 0)
         *a.fb_count = 0u;
+}
+
+// The frame's result for the host in one write to pinned memory: the leaf count (the leaf base after the
+// last level) and the counters summed over their shards — no copy command and no second round trip.
+struct QtFrameSum {
+    uint32_t leaves, pad_;
+    unsigned long long acc[9];
+};
+
+__global__ void __launch_bounds__(64) qt_finish(const DevPlan* __restrict__ last, int ran,
+                                                const unsigned long long* __restrict__ acc, uint32_t shards,
+                                                uint32_t stride, QtFrameSum* __restrict__ dst)
+{
+    const uint32_t i = threadIdx.x;
+    if (i < stride && i < 9) {
+        unsigned long long t = 0;
+        for (uint32_t k = 0; k < shards; ++k)
+            t += acc[k * stride + i];
+        dst->acc[i] = t;
+    }
+    if (i == 0)
+        dst->leaves = ran ? last->leaf_base : 0u;
 }
 
 // ---- the device planner of a quadtree level (prepare()'s layout and work lists, restated) ----

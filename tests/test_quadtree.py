@@ -176,3 +176,25 @@ def test_gpu_quadtree_device_planned_across_frames():
                 want, sw = f.encode_quadtree(16, 4, 4.0)
             np.testing.assert_array_equal(got, want, err_msg=f"frame {i}")
             assert sg["rejected_mappings"] == sw["rejected_mappings"], i
+
+
+@pytest.mark.gpu
+def test_gpu_quadtree_leaves_into_pinned_memory():
+    # a pinned `out` is written by the device directly (the emit kernels, over PCIe); the same items as a
+    # pageable buffer's copy path, and a short pinned buffer receives exactly its prefix
+    import torch
+    p = plane("lenna_y")
+    cap = (512 // 4) ** 2
+    pinned = torch.empty(cap * F.ENCODE_ITEM.itemsize, dtype=torch.uint8).pin_memory().numpy().view(F.ENCODE_ITEM)
+    with F.Engine(0, 4, True) as e:
+        e.set_frame(p)
+        want, sw = e.encode_quadtree(16, 4, 4.0)
+        got, sg = e.encode_quadtree(16, 4, 4.0, out=pinned)
+        np.testing.assert_array_equal(got, want)
+        assert np.shares_memory(got, pinned) and sg["rejected_mappings"] == sw["rejected_mappings"]
+        pinned[:] = np.zeros(1, dtype=F.ENCODE_ITEM)
+        short = pinned[: len(want) // 3]
+        part, sp = e.encode_quadtree(16, 4, 4.0, out=short, allow_short=True)
+        assert sp["items"] == len(want) and len(part) == len(short)
+        np.testing.assert_array_equal(part, want[: len(short)])
+        assert (pinned[len(short):] == np.zeros(1, dtype=F.ENCODE_ITEM)).all()  # nothing past the capacity
