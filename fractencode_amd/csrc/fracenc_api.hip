@@ -1280,6 +1280,39 @@ inline uint32_t launch_nwork(const frac_ctx* c, const std::vector<uint4>& w)
     return c->qplan ? c->qp_nwork_cap : (uint32_t)w.size();
 }
 
+#ifdef FRAC_CLOCK_STAMP
+// the diagnostic clock build (tools/build_tuning.py --stamps): search_dft stamps s_memtime and
+// s_memrealtime around its loop, per workgroup, into this buffer; frac_clock_stamps reads the last
+// launch's.  Never in the product or the plain tuning build.
+static unsigned long long* g_stamps = nullptr;
+static size_t g_stamps_cap = 0;
+static unsigned g_stamps_n = 0;
+static unsigned long long* clock_stamps_for(unsigned nwg)
+{
+    if (nwg > g_stamps_cap) {
+        if (g_stamps)
+            (void)hipFree(g_stamps);
+        g_stamps = nullptr;
+        g_stamps_cap = 0;
+        if (hipMalloc(&g_stamps, (size_t)nwg * 4 * sizeof(unsigned long long)) != hipSuccess)
+            return nullptr;
+        g_stamps_cap = nwg;
+    }
+    g_stamps_n = nwg;
+    return g_stamps;
+}
+extern "C" int frac_clock_stamps(unsigned long long* out, size_t cap_workgroups)
+{
+    if (!g_stamps || !out)
+        return -1;
+    const size_t n = std::min<size_t>(g_stamps_n, cap_workgroups);
+    if (hipDeviceSynchronize() != hipSuccess ||
+        hipMemcpy(out, g_stamps, n * 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess)
+        return -1;
+    return (int)n;
+}
+#endif
+
 // n = 8, T = 4: the C4-Fourier search (6 MFMAs per 32×32 tile pair instead of 16).  inits: reset
 // best_key and fb_count in the preparation kernel (launch_all skipped its memsets)
 inline int launch_dft(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool inits)
@@ -1379,6 +1412,9 @@ inline int launch_dft(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool i
         da.tguard = c->d_dft_tguard.ptr;
         da.trmax = c->d_dft_trmax.ptr;
         const unsigned nwg = nwork;
+#ifdef FRAC_CLOCK_STAMP
+        da.stamps = clock_stamps_for(nwg);
+#endif
         const bool hits = c->hitH > 0;
         constexpr uint32_t W8 = kDftBlocksPerWG;
 #ifndef FRAC_TUNING

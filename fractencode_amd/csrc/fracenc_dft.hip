@@ -190,6 +190,7 @@ struct DftArgs {
     const uint32_t* choff; // CHUNKED: [work] first chunk entry of the work item (fracenc_tp.hip)
     const int32_t* trmax;  // kDftFast6: [ntiles] the largest block R6 whose guard holds against the
                            // tile, (kFast6Limit − max Σb²) / max 2·D6 (−1: none)
+    unsigned long long* stamps = nullptr; // FRAC_CLOCK_STAMP builds only: [workgroups][4] clock stamps
 };
 
 // ---------------------------------------------------------------------------
@@ -1043,6 +1044,11 @@ __global__ void __launch_bounds__(64 * WAVES) search_dft(DftArgs d)
     if constexpr ((VAR & kDftPrio) != 0)
         if (wv >= WAVES / 2)
             __builtin_amdgcn_s_setprio(1);
+#ifdef FRAC_CLOCK_STAMP
+    // diagnostic build only (tools/clock_stamp.py, MI355X_MICROARCH.md "DVFS give-back"): the shader
+    // clock over this workgroup's loop is Δs_memtime ÷ Δs_memrealtime × 100 MHz
+    const unsigned long long ck0 = __builtin_amdgcn_s_memtime(), rt0 = __builtin_amdgcn_s_memrealtime();
+#endif
     if (nstage)
         stage(lds0, wk.z, stage_nt(0));
     for (uint32_t st = 0; st < nstage; st += 2) {
@@ -1069,6 +1075,16 @@ __global__ void __launch_bounds__(64 * WAVES) search_dft(DftArgs d)
                              tb + c0);
         }
     }
+#ifdef FRAC_CLOCK_STAMP
+    {
+        const unsigned long long ck1 = __builtin_amdgcn_s_memtime(), rt1 = __builtin_amdgcn_s_memrealtime();
+        if (threadIdx.x == 0 && d.stamps) { // a vector store from lane 0; nothing in the kernel reads it
+            ulonglong2* sp = reinterpret_cast<ulonglong2*>(d.stamps + (size_t)blockIdx.x * 4);
+            sp[0] = make_ulonglong2(ck0, ck1);
+            sp[1] = make_ulonglong2(rt0, rt1);
+        }
+    }
+#endif
     if (active && !CHUNKED)
         a.entries[(size_t)(blockIdx.x * WAVES + wv) * 64 + lane] = make_uint2(__float_as_uint(best * kOut), btile);
 }

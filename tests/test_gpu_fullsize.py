@@ -200,26 +200,30 @@ def test_c5_rgb_4096_three_planes_quantized_decode(oracle):
 C5_DECODE_ITERS = 20
 
 
-def _engines_identical(p, tag, T=4):
+def _engines_identical(p, tag, T=4, dsize=16, rsize=8):
     """The VALU engine (v_dot2, integer — the north-star formulation) and the MFMA engine (f16 Fourier
     form) are independent implementations of the same search: their records must be byte-identical
     for every range of the frame (the SEA engine's too: its bound only skips candidates; at T = 8 the
     direct MFMA form instead, beside the Fourier form's flipped copies)."""
     H, W = p.shape
-    doms = F.create_uniform_grid(W, H, 16, 8)
-    rngs = F.create_uniform_grid(W, H, 8, 8)
+    doms = F.create_uniform_grid(W, H, dsize, 8)
+    rngs = F.create_uniform_grid(W, H, rsize, rsize)
     outs = {}
     forms = {}
     third = ("sea", F.ENGINE_SEA, 0) if T == 4 else ("direct", F.ENGINE_MFMA, F.FLAG_DIRECT_FORM)
-    for name, eng, fl in (("mfma", F.ENGINE_MFMA, 0), ("valu", F.ENGINE_VALU, 0), third):
+    engines = [("mfma", F.ENGINE_MFMA, 0), ("valu", F.ENGINE_VALU, 0)] + ([third] if rsize == 8 else [])
+    for name, eng, fl in engines:
         with F.Engine(0, T, False, 0.0, -1.0, eng, flags=fl) as e:
             e.set_frame(p)
             e.set_domains(doms)
             outs[name], st = e.search(rngs)
             forms[name] = st["search_form"]
-    assert forms["mfma"] == F.FORM_FOURIER and forms["valu"] == F.FORM_DOT2, forms
+    if rsize == 8:
+        assert forms["mfma"] == F.FORM_FOURIER and forms["valu"] == F.FORM_DOT2, forms
+    else:
+        assert forms["mfma"] != forms["valu"], forms  # two different search forms
     assert len(outs["mfma"]) == len(rngs)
-    for name in ("valu", third[0]):
+    for name, _, _ in engines[1:]:
         same = outs[name] == outs["mfma"]
         assert same.all(), f"{tag}: {name} differs from mfma at {int((~same).sum())} ranges, first {np.nonzero(~same)[0][:5]}"
 
@@ -236,3 +240,15 @@ def test_c3_t8_all_ranges_valu_equals_mfma():
     # all 8 transforms at C3 size: the Fourier form with the flipped range copies, the exhaustive VALU
     # engine and the direct MFMA form agree on every one of the 262,144 records
     _engines_identical(plane("s1_4096"), "C3 T=8", T=8)
+
+
+@pytest.mark.parametrize("name", ["c5_u", "c5_v"])
+def test_c5_chroma_all_ranges_valu_equals_mfma(name):
+    # C5's U and V planes (rgb2yuv on the host, as the Quantizer run feeds them): every record
+    _engines_identical(plane(name), f"C5 {name[-1].upper()}")
+
+
+def test_16to4_4096_all_ranges_valu_equals_mfma():
+    # the CLI default geometry (16 -> 4) on the C3 frame: the MFMA engine's n = 4 form (float-C
+    # epilogue) and the VALU engine agree on all 1,048,576 records
+    _engines_identical(plane("s1_4096"), "16to4 4096", dsize=16, rsize=4)
