@@ -970,8 +970,8 @@ int prepare(frac_ctx* c)
         int var = 0;
         FRAC_TRY(mfma_variant(c, var));
         const bool four_wave = dft_four_wave(var);
-        if (n == 16) // search_mfma16: one range block per workgroup (T waves)
-            build_work(1, 4096, c->m_work, c->m_blk_ptr, c->m_blk_ent, false);
+        if (n == 16) // search_mfma16: mfma16_bpw(T) range blocks per 4-wave workgroup
+            build_work(mfma16_bpw((uint32_t)T), 4096, c->m_work, c->m_blk_ptr, c->m_blk_ent, false);
         else if (!fourier || four_wave) // the 8-wave Fourier search reads only its own list
             build_work(4, 8192, c->m_work, c->m_blk_ptr, c->m_blk_ent, false);
         else {
@@ -1294,20 +1294,21 @@ static unsigned long long* clock_stamps_for(unsigned nwg)
             (void)hipFree(g_stamps);
         g_stamps = nullptr;
         g_stamps_cap = 0;
-        if (hipMalloc(&g_stamps, (size_t)nwg * 4 * sizeof(unsigned long long)) != hipSuccess)
+        if (hipMalloc(&g_stamps, (size_t)nwg * kClockStampWords * sizeof(unsigned long long)) != hipSuccess)
             return nullptr;
         g_stamps_cap = nwg;
     }
     g_stamps_n = nwg;
     return g_stamps;
 }
+// out: [cap_workgroups][kClockStampWords]
 extern "C" int frac_clock_stamps(unsigned long long* out, size_t cap_workgroups)
 {
     if (!g_stamps || !out)
         return -1;
     const size_t n = std::min<size_t>(g_stamps_n, cap_workgroups);
     if (hipDeviceSynchronize() != hipSuccess ||
-        hipMemcpy(out, g_stamps, n * 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess)
+        hipMemcpy(out, g_stamps, n * kClockStampWords * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess)
         return -1;
     return (int)n;
 }
@@ -1605,8 +1606,10 @@ inline int launch_dft(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool i
         v.fit = fit_args(c, dtgt, tstride, nr);
         c->fit_fused = true;
         // one-wave workgroups: a finished range frees its slot at once (0.254 vs 0.271 ms finish
-        // against 4-wave workgroups, 30-sample A/B, profiles/r01/ab_fourier_variants.log)
-        resolve_dft<false><<<std::max(1u, v.nslots), 64, 0, c->stream>>>(v);
+        // against 4-wave workgroups, 30-sample A/B, profiles/r01/ab_fourier_variants.log); T = 8: two
+        // waves, the slot and its flipped copy resolved at the same time
+        v.paired = c->dft_copies == 2 ? 1 : 0;
+        resolve_dft<false><<<std::max(1u, v.nslots), v.paired ? 128 : 64, 0, c->stream>>>(v);
     }
     return FRAC_OK;
 }
@@ -1650,12 +1653,16 @@ int launch_mfma(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool inits =
         r.rconst = c->d_m_rconst.ptr;
         r.plan = c->qplan;
         r.fmode = fmode;
-        const size_t threads = (size_t)c->nblocks * T * MfmaGeom<N>::KS * 64;
-        // rconst is a sum of per-pixel terms, accumulated by the transform-0 threads (a planned level's
-        // qt_fill_maps zeroed it)
-        if (!c->qplan)
-            FRAC_HIP(c, hipMemsetAsync(c->d_m_rconst.ptr, 0, (size_t)c->nblocks * 32 * sizeof(uint32_t), c->stream));
-        mfma_range_prep<N><<<(unsigned)((threads + 255) / 256), 256, 0, c->stream>>>(r);
+        if constexpr (N == 16) { // one workgroup per range block, the constants written directly
+            mfma_range_prep16<<<c->nblocks, 256, 0, c->stream>>>(r);
+        } else {
+            const size_t threads = (size_t)c->nblocks * T * MfmaGeom<N>::KS * 64;
+            // rconst is a sum of per-pixel terms, accumulated by the transform-0 threads (a planned level's
+            // qt_fill_maps zeroed it)
+            if (!c->qplan)
+                FRAC_HIP(c, hipMemsetAsync(c->d_m_rconst.ptr, 0, (size_t)c->nblocks * 32 * sizeof(uint32_t), c->stream));
+            mfma_range_prep<N><<<(unsigned)((threads + 255) / 256), 256, 0, c->stream>>>(r);
+        }
     }
     if (c->p.flags & FRAC_FLAG_TIMING)
         FRAC_TRY(mark_event(c, 1));
@@ -1675,19 +1682,19 @@ int launch_mfma(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool inits =
         a.hitH = (uint32_t)std::max<int64_t>(c->hitH, 0);
         a.entries = c->d_m_entries.ptr;
         a.plan = c->qplan;
-        if constexpr (N == 16) { // one range block × its T transforms per workgroup
+        if constexpr (N == 16) { // 4-wave workgroups: mfma16_bpw(T) range blocks × their T transforms
             const unsigned nwg = nwork;
             const bool hits = c->hitH > 0;
             if (T == 8) {
                 if (hits)
-                    search_mfma16<8, true><<<nwg, 512, 0, c->stream>>>(a);
+                    search_mfma16<8, true><<<nwg, 256, 0, c->stream>>>(a);
                 else
-                    search_mfma16<8, false><<<nwg, 512, 0, c->stream>>>(a);
+                    search_mfma16<8, false><<<nwg, 256, 0, c->stream>>>(a);
             } else if (T == 1) {
                 if (hits)
-                    search_mfma16<1, true><<<nwg, 64, 0, c->stream>>>(a);
+                    search_mfma16<1, true><<<nwg, 256, 0, c->stream>>>(a);
                 else
-                    search_mfma16<1, false><<<nwg, 64, 0, c->stream>>>(a);
+                    search_mfma16<1, false><<<nwg, 256, 0, c->stream>>>(a);
             } else {
                 if (hits)
                     search_mfma16<4, true><<<nwg, 256, 0, c->stream>>>(a);
@@ -1723,6 +1730,8 @@ int launch_mfma(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool inits =
         v.best_key = c->d_best_key.ptr;
         v.merged = (N != 16 && T > 1 && (c->mfma_var_ran & (128 | 256))) ? 1 : 0; // entries merged over t
         v.fmode = (N != 16 && (c->mfma_var_ran & 256)) ? 1 : 0;                  // fmap'd float-C minima
+        if constexpr (N == 16)
+            v.rfrags = c->d_m_rfrags.ptr; // the range copies from search_mfma16's B fragments
         if (!c->virt) { // the fit in the resolving wave (the sampled form fits at its own points: gen_fit)
             v.fused_fit = 1;
             v.fit = fit_args(c, dtgt, tstride, nr);
@@ -2358,7 +2367,7 @@ int qt_encode_dev(frac_ctx* c, const frac_quadtree_params* qp, LevelGrid& level,
         const bool fourier = n == 8 && mfma_dft_enabled(c);
         c->dft_copies = fourier && T == 8 ? 2u : 1u;
         const uint32_t cp = c->dft_copies, KS = (n * n + 15) / 16;
-        const uint32_t bpw = n == 16 ? 1u : fourier ? kDftBlocksPerWG : 4u;
+        const uint32_t bpw = n == 16 ? mfma16_bpw(T) : fourier ? kDftBlocksPerWG : 4u;
         const uint32_t target = n == 16 ? 4096u : fourier ? 8192u / kDftBlocksPerWG * 4u : 8192u;
         const uint32_t nblocks_cap = (nr_max + 31) / 32 + (uint32_t)nb;
         const uint32_t ntiles_cap = (nd + 31) / 32 + (uint32_t)nb;

@@ -771,7 +771,7 @@ struct QtPlanArgs {
     uint32_t nb;             // buckets: 7 with the classifier, 1 without
     uint32_t nd;             // domains of the level
     uint32_t nr_init;        // the first level: its range count (host-known); ~0u: plan->nr (qt_scatter)
-    uint32_t bpw;            // range blocks per work item (search_dft 8, search_mfma 4, search_mfma16 1)
+    uint32_t bpw;            // range blocks per work item (search_dft 8, search_mfma 4, search_mfma16 mfma16_bpw(T))
     uint32_t target;         // target work items (workgroups)
     uint32_t copies;         // T = 8 Fourier: 2 (flipped copies), else 1
     uint32_t mfma_per_pair;  // MFMA 32x32x16 per (range block, domain tile) pair: flops accounting

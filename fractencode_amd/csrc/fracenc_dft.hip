@@ -190,8 +190,11 @@ struct DftArgs {
     const uint32_t* choff; // CHUNKED: [work] first chunk entry of the work item (fracenc_tp.hip)
     const int32_t* trmax;  // kDftFast6: [ntiles] the largest block R6 whose guard holds against the
                            // tile, (kFast6Limit − max Σb²) / max 2·D6 (−1: none)
-    unsigned long long* stamps = nullptr; // FRAC_CLOCK_STAMP builds only: [workgroups][4] clock stamps
+    unsigned long long* stamps = nullptr; // FRAC_CLOCK_STAMP builds only: [workgroups][kClockStampWords]
 };
+// per workgroup: s_memtime and s_memrealtime before / after the loop, HW_ID | XCC_ID << 32, and the
+// work item's tile range first | end << 32
+constexpr uint32_t kClockStampWords = 6;
 
 // ---------------------------------------------------------------------------
 // dft_domain_build: pool_build + dft_domain_prep in one pass for the Fourier path.  One
@@ -1078,10 +1081,14 @@ __global__ void __launch_bounds__(64 * WAVES) search_dft(DftArgs d)
 #ifdef FRAC_CLOCK_STAMP
     {
         const unsigned long long ck1 = __builtin_amdgcn_s_memtime(), rt1 = __builtin_amdgcn_s_memrealtime();
-        if (threadIdx.x == 0 && d.stamps) { // a vector store from lane 0; nothing in the kernel reads it
-            ulonglong2* sp = reinterpret_cast<ulonglong2*>(d.stamps + (size_t)blockIdx.x * 4);
+        // where the workgroup ran: HW_ID (CU, SE, …) and XCC_ID, read by s_getreg (hwreg 4 and 20)
+        const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4), xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20);
+        if (threadIdx.x == 0 && d.stamps) { // vector stores from lane 0; nothing in the kernel reads them
+            ulonglong2* sp = reinterpret_cast<ulonglong2*>(d.stamps + (size_t)blockIdx.x * kClockStampWords);
             sp[0] = make_ulonglong2(ck0, ck1);
             sp[1] = make_ulonglong2(rt0, rt1);
+            sp[2] = make_ulonglong2((unsigned long long)hw | ((unsigned long long)xcc << 32),
+                                    (unsigned long long)wk.z | ((unsigned long long)wk.w << 32));
         }
     }
 #endif
@@ -1406,21 +1413,9 @@ __device__ inline DftResolved resolve_dft_eval(const MfmaResolveArgs& a, uint32_
     return res;
 }
 
-// the slot's range record: its least key (with T = 8's flipped copy, the lesser of the two) and the
-// winner's sums for fit_rstat (every lane holds the same after resolve_dft_eval)
-template <bool SORTED>
-__device__ inline void resolve_dft_slot(const MfmaResolveArgs& a, uint32_t slot, int lane)
+// range r's record from its resolved winner w (every lane holds the same after resolve_dft_eval)
+__device__ inline void resolve_dft_record(const MfmaResolveArgs& a, uint32_t r, const DftResolved& w, int lane)
 {
-    const int ri = a.slot_range[slot];
-    if (ri < 0)
-        return;
-    DftResolved w = resolve_dft_eval<SORTED>(a, slot, lane, false);
-    if (!SORTED && a.flip_slots) {
-        const DftResolved f = resolve_dft_eval<SORTED>(a, slot + a.flip_slots, lane, true);
-        if (f.bestk < w.bestk)
-            w = f;
-    }
-    const uint32_t r = (uint32_t)ri;
     if (a.fused_fit) { // the range's record right here: one launch less per run (C2: 5 µs of a 43 µs frame)
         if (lane == 0) {
             a.best_key[r] = w.bestk;
@@ -1435,6 +1430,55 @@ __device__ inline void resolve_dft_slot(const MfmaResolveArgs& a, uint32_t slot,
     }
 }
 
+// the slot's range record: its least key (with T = 8's flipped copy, the lesser of the two) and the
+// winner's sums for fit_rstat (every lane holds the same after resolve_dft_eval)
+template <bool SORTED>
+__device__ inline void resolve_dft_slot(const MfmaResolveArgs& a, uint32_t slot, int lane)
+{
+    const int ri = a.slot_range[slot];
+    if (ri < 0)
+        return;
+    DftResolved w = resolve_dft_eval<SORTED>(a, slot, lane, false);
+    if (!SORTED && a.flip_slots) {
+        const DftResolved f = resolve_dft_eval<SORTED>(a, slot + a.flip_slots, lane, true);
+        if (f.bestk < w.bestk)
+            w = f;
+    }
+    resolve_dft_record(a, (uint32_t)ri, w, lane);
+}
+
+// T = 8 with the flipped copies (MfmaResolveArgs::paired): a two-wave workgroup per slot, wave 0
+// resolving the slot and wave 1 its flipped copy at the same time (the one-wave form ran the two
+// one after the other); wave 0 keeps the lesser key and writes the record
+__device__ inline void resolve_dft_pair(const MfmaResolveArgs& a, uint32_t slot, uint32_t wave, int lane)
+{
+    __shared__ unsigned long long fkey;
+    __shared__ uint32_t fsums[5];
+    const int ri = a.slot_range[slot]; // the same for both waves: the barrier below is reached by both or neither
+    if (ri < 0)
+        return;
+    const DftResolved w = resolve_dft_eval<false>(a, slot + wave * a.flip_slots, lane, wave == 1);
+    if (wave == 1 && lane == 0) {
+        fkey = w.bestk;
+        fsums[0] = w.bx;
+        fsums[1] = w.bs1;
+        fsums[2] = w.bs2;
+        fsums[3] = w.sr1;
+        fsums[4] = w.sr2;
+    }
+    __syncthreads();
+    if (wave == 0) {
+        DftResolved f;
+        f.bestk = fkey;
+        f.bx = fsums[0];
+        f.bs1 = fsums[1];
+        f.bs2 = fsums[2];
+        f.sr1 = fsums[3];
+        f.sr2 = fsums[4];
+        resolve_dft_record(a, (uint32_t)ri, f.bestk < w.bestk ? f : w, lane);
+    }
+}
+
 // One wave per slot, in slot order (the 32 ranges of a block read the same entry lines back to
 // back); launched as one- or four-wave workgroups. A grid of fewer, longer-lived waves striding over the slots measured slower (452 vs
 // 372 µs at C3 in the SEA tiled form).
@@ -1443,6 +1487,14 @@ template <bool SORTED = false>
 __global__ void __launch_bounds__(256) resolve_dft(MfmaResolveArgs a)
 {
     apply_plan(a);
+    if constexpr (!SORTED) {
+        if (a.paired) { // two-wave workgroups: the slot and its flipped copy at once
+            const uint32_t slot = blockIdx.x;
+            if (slot < a.nslots)
+                resolve_dft_pair(a, slot, __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), threadIdx.x & 63);
+            return;
+        }
+    }
     // the slot is wave-uniform: readfirstlane lets its loads go through the scalar unit
     const uint32_t slot = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
     if (slot < a.nslots)

@@ -241,6 +241,73 @@ __global__ void __launch_bounds__(256) mfma_range_prep(MfmaRangePrepArgs a)
     a.rfrags[((size_t)(b * a.T + t) * KS + s) * 64 + lane] = __builtin_bit_cast(uint4, v8);
 }
 
+// mfma_range_prep16: mfma_range_prep at n = 16, one 256-thread workgroup per range block.  The 32
+// ranges' pixels are read once into LDS (coalesced byte rows, 8 KiB), each range's constant is a
+// wave reduction written directly (no atomics, no zeroed word), and the T·16·64 fragments are
+// gathered from LDS and written 16 B per lane.  (The thread-per-fragment form read every pixel T
+// times from global memory with byte loads and atomically added 512 partial constants per block.)
+// Rows of the LDS image are 260 bytes apart, so the 32 columns of a fragment read hit 32 banks.
+constexpr uint32_t kRp16Row = 260;
+
+__global__ void __launch_bounds__(256) mfma_range_prep16(MfmaRangePrepArgs a)
+{
+    constexpr int N = 16, NN = 256, KS = MfmaGeom<16>::KS;
+    apply_plan(a, 1);
+    const uint32_t b = blockIdx.x;
+    if (b >= a.nblocks)
+        return;
+    __shared__ uint8_t px[32 * kRp16Row];
+    __shared__ int32_t slot_ri[32];
+    if (threadIdx.x < 32)
+        slot_ri[threadIdx.x] = a.slot_range[b * 32 + threadIdx.x];
+    __syncthreads();
+    // 32 ranges × 256 pixels: thread t reads bytes t, t + 256, … (a range's 16-byte rows are contiguous
+    // across 16 threads); an empty slot reads as 128, whose fragment values are 0
+    for (uint32_t i = threadIdx.x; i < 32u * NN; i += 256u) {
+        const uint32_t col = i / NN, q = i % NN;
+        const int ri = slot_ri[col];
+        uint8_t v = 128;
+        if (ri >= 0) {
+            const frac_grid_item rg = a.ranges[ri];
+            v = a.tgt[(size_t)(rg.y + q / N) * a.tstride + rg.x + (q % N)];
+        }
+        px[col * kRp16Row + q] = v;
+    }
+    __syncthreads();
+    // the range constants: 8 threads per range, 32 pixels each, then a reduction over the 8 lanes
+    {
+        const uint32_t col = threadIdx.x >> 3, part = threadIdx.x & 7u;
+        int32_t s1 = 0, s2 = 0;
+#pragma unroll 8
+        for (uint32_t q = part * 32; q < part * 32 + 32; ++q) {
+            const int32_t v = px[col * kRp16Row + q];
+            s1 += v;
+            s2 += v * v;
+        }
+#pragma unroll
+        for (int o = 4; o > 0; o >>= 1) {
+            s1 += __shfl_xor(s1, o, 64);
+            s2 += __shfl_xor(s2, o, 64);
+        }
+        if (part == 0)
+            a.rconst[b * 32 + col] = slot_ri[col] >= 0 ? mfma_range_const(NN, s1, s2) : 0u;
+    }
+    // the fragments: output word o = ((t·KS + s)·64 + lane), lane = col + 32h, k = 16s + 8h + j
+    const uint32_t nout = a.T * KS * 64u;
+    for (uint32_t o = threadIdx.x; o < nout; o += 256u) {
+        const uint32_t lane = o & 63u, s = (o >> 6) % KS, t = (o >> 6) / KS;
+        const uint32_t col = lane & 31u, h = lane >> 5;
+        _Float16 v8[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int k = 16 * (int)s + 8 * (int)h + j;
+            const int rv = px[col * kRp16Row + inv_index<N>((int)t, k)];
+            v8[j] = (_Float16)(a.fmode ? 8 * (128 - rv) : 128 - rv);
+        }
+        a.rfrags[((size_t)b * a.T * KS) * 64 + o] = __builtin_bit_cast(uint4, v8);
+    }
+}
+
 // ---------------------------------------------------------------------------
 // search_mfma<N, T, HITS>: workgroup = 4 waves = 4 range blocks of one bucket; the
 // domain tiles [tile_begin, tile_end) of that bucket are staged through LDS and shared.
@@ -575,45 +642,79 @@ __global__ void __launch_bounds__(256) search_mfma(MfmaSearchArgs a)
 // search_mfma16<T, HITS>: the direct form for n = 16 (K = 256: 16 MFMAs per transform and
 // tile pair).  |Z| ≤ 256·128·510 < 2^24, so the fp32 accumulation from 0 is exact, but the
 // offset-binary epilogue of n ≤ 8 needs |Z| < 2^22: here acc = −Z is converted to an
-// integer and v = (int(acc) << 3) + e (e carries V0 = 2^28, mfma_range_const).  The B
-// fragments of one transform take 64 VGPRs, so a workgroup is T waves = one range block ×
-// its T transforms sharing the LDS stages (2 tiles of 16 KiB + row constants, double
-// buffered).  Entries keep search_mfma's layout with one block per work item
-// ((work·1 + 0)·T + t), so resolve_mfma reads them unchanged.
+// integer and v = (int(acc) << 3) + e (e carries V0 = 2^28, mfma_range_const).
+//
+// A workgroup is 4 waves sharing the LDS stages (2 tiles of 16 KiB + row constants, double
+// buffered): Mfma16Shape<T>::BPW range blocks × T / TPW transform groups, each wave holding the B
+// fragments of TPW = 2 transforms of its block (128 VGPRs), so every A fragment read from LDS feeds
+// two MFMAs.  With one transform per wave (one block × T waves) the LDS read stream matched the
+// MFMA stream byte for byte (1 KiB per 32-cycle MFMA per wave, 16 waves per CU: LDS co-bound).
+// Entries keep search_mfma's layout, ((work·BPW + block)·T + t)·64 + lane, so resolve_mfma reads
+// them unchanged.
 // ---------------------------------------------------------------------------
 constexpr int kTilesPerStage16 = 2;
 
+template <int T>
+struct Mfma16Shape {
+    static constexpr int TPW = T >= 2 ? 2 : 1; // transforms per wave
+    static constexpr int GPB = T / TPW;        // waves per range block
+    static constexpr int BPW = 4 / GPB;        // range blocks per workgroup (4 waves)
+    static_assert(GPB * BPW == 4, "4 waves per workgroup");
+};
+// the host's work lists at n = 16 (build_work / qt_plan): blocks per work item
+constexpr uint32_t mfma16_bpw(uint32_t T) { return T >= 8 ? 1u : T >= 2 ? 2u : 4u; }
+
 template <int T, bool HITS>
-__global__ void __launch_bounds__(64 * T) search_mfma16(MfmaSearchArgs a)
+__global__ void __launch_bounds__(256, 2) search_mfma16(MfmaSearchArgs a)
 {
-    constexpr int KS = MfmaGeom<16>::KS; // 16
+    using Sh = Mfma16Shape<T>;
+    constexpr int KS = MfmaGeom<16>::KS, TPW = Sh::TPW; // 16
+    static_assert(mfma16_bpw(T) == (uint32_t)Sh::BPW, "host and kernel agree on the blocks per work item");
     constexpr int STAGE = kTilesPerStage16 * KS * 64 + kTilesPerStage16 * 8;
     if (past_plan(a))
         return;
     __shared__ uint4 lds0[STAGE];
     __shared__ uint4 lds1[STAGE];
     const uint4 wk = a.work[blockIdx.x];
-    const uint32_t t = threadIdx.x >> 6, lane = threadIdx.x & 63u;
-    const uint32_t blk = wk.x;
-    half8_t bf[KS];
+    const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    const uint32_t kb = wv / Sh::GPB, t0 = (wv % Sh::GPB) * TPW;
+    const bool active = kb < wk.y; // wave-uniform: a work item with fewer blocks idles its other waves
+    const uint32_t blk = wk.x + (active ? kb : 0u);
+    half8_t bf[TPW][KS];
 #pragma unroll
-    for (int s = 0; s < KS; ++s)
-        bf[s] = __builtin_bit_cast(half8_t, a.rfrags[((size_t)(blk * T + t) * KS + s) * 64 + lane]);
+    for (int j = 0; j < TPW; ++j)
+#pragma unroll
+        for (int s = 0; s < KS; ++s)
+            bf[j][s] = __builtin_bit_cast(half8_t, a.rfrags[((size_t)(blk * T + t0 + j) * KS + s) * 64 + lane]);
     uint32_t hl = 0;
     if constexpr (HITS)
         hl = a.hitH + a.rconst[blk * 32 + (lane & 31u)];
     const floatx16_t zero = {};
-    uint32_t best = 0xffffffffu, btile = 0;
+    uint32_t best[TPW], btile[TPW];
+#pragma unroll
+    for (int j = 0; j < TPW; ++j) {
+        best[j] = 0xffffffffu;
+        btile[j] = 0;
+    }
     const uint32_t h = lane >> 5;
     auto compute = [&](const uint4* la, uint32_t nt, uint32_t tb) {
         const uint4* lc = la + nt * KS * 64u;
-        uint32_t cm = 0xffffffffu;
-        for (uint32_t q = 0; q < nt; ++q) {
-            floatx16_t acc = zero;
+        uint32_t cm[TPW];
 #pragma unroll
-            for (int s = 0; s < KS; ++s)
-                acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(half8_t, la[(q * KS + s) * 64 + lane]),
-                                                           bf[s], acc, 0, 0, 0);
+        for (int j = 0; j < TPW; ++j)
+            cm[j] = 0xffffffffu;
+        for (uint32_t q = 0; q < nt; ++q) {
+            floatx16_t acc[TPW];
+#pragma unroll
+            for (int j = 0; j < TPW; ++j)
+                acc[j] = zero;
+#pragma unroll
+            for (int s = 0; s < KS; ++s) {
+                const half8_t af = __builtin_bit_cast(half8_t, la[(q * KS + s) * 64 + lane]);
+#pragma unroll
+                for (int j = 0; j < TPW; ++j)
+                    acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af, bf[j][s], acc[j], 0, 0, 0);
+            }
             uint32_t e[16];
 #pragma unroll
             for (int c4 = 0; c4 < 4; ++c4) {
@@ -624,14 +725,19 @@ __global__ void __launch_bounds__(64 * T) search_mfma16(MfmaSearchArgs a)
                 e[4 * c4 + 3] = v.w;
             }
 #pragma unroll
-            for (int i = 0; i < 16; ++i)
-                cm = min(cm, ((uint32_t)(int32_t)acc[i] << 3) + e[i]); // acc: exact integer, |acc| < 2^24
+            for (int j = 0; j < TPW; ++j)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) // acc: exact integer, |acc| < 2^24
+                    cm[j] = min(cm[j], ((uint32_t)(int32_t)acc[j][i] << 3) + e[i]);
         }
-        if constexpr (HITS)
-            cm = cm <= hl ? 0u : cm; // any hit in the chunk: the first-hit chunk wins
-        if (cm < best) {
-            best = cm;
-            btile = tb;
+#pragma unroll
+        for (int j = 0; j < TPW; ++j) {
+            if constexpr (HITS)
+                cm[j] = cm[j] <= hl ? 0u : cm[j]; // any hit in the chunk: the first-hit chunk wins
+            if (cm[j] < best[j]) {
+                best[j] = cm[j];
+                btile[j] = tb;
+            }
         }
     };
     const uint32_t nstage = (wk.w - wk.z + kTilesPerStage16 - 1) / kTilesPerStage16;
@@ -639,21 +745,26 @@ __global__ void __launch_bounds__(64 * T) search_mfma16(MfmaSearchArgs a)
     // each stage (2 tiles) is its own chunk for resolve_mfma (which scans kTilesPerStage16 tiles at n = 16:
     // half the 512-byte rows a coarser chunk made it re-read)
     if (nstage)
-        stage_tiles<KS, 64 * T>(lds0, a.dtiles, a.dconst, wk.z, stage_nt(0));
+        stage_tiles<KS, 256>(lds0, a.dtiles, a.dconst, wk.z, stage_nt(0));
     for (uint32_t st = 0; st < nstage; st += 2) {
         const uint32_t tb = wk.z + st * kTilesPerStage16;
         stage_barrier();
         if (st + 1 < nstage)
-            stage_tiles<KS, 64 * T>(lds1, a.dtiles, a.dconst, tb + kTilesPerStage16, stage_nt(st + 1));
-        compute(lds0, stage_nt(st), tb);
+            stage_tiles<KS, 256>(lds1, a.dtiles, a.dconst, tb + kTilesPerStage16, stage_nt(st + 1));
+        if (active)
+            compute(lds0, stage_nt(st), tb);
         if (st + 1 < nstage) {
             stage_barrier();
             if (st + 2 < nstage)
-                stage_tiles<KS, 64 * T>(lds0, a.dtiles, a.dconst, tb + 2 * kTilesPerStage16, stage_nt(st + 2));
-            compute(lds1, stage_nt(st + 1), tb + kTilesPerStage16);
+                stage_tiles<KS, 256>(lds0, a.dtiles, a.dconst, tb + 2 * kTilesPerStage16, stage_nt(st + 2));
+            if (active)
+                compute(lds1, stage_nt(st + 1), tb + kTilesPerStage16);
         }
     }
-    a.entries[((size_t)blockIdx.x * T + t) * 64 + lane] = make_uint2(best, btile);
+    if (active)
+#pragma unroll
+        for (int j = 0; j < TPW; ++j)
+            a.entries[(((size_t)blockIdx.x * Sh::BPW + kb) * T + t0 + j) * 64 + lane] = make_uint2(best[j], btile[j]);
 }
 
 // ---------------------------------------------------------------------------
@@ -693,6 +804,11 @@ struct MfmaResolveArgs {
     // resolve_dft: the fit runs in the resolving wave (fit_rstat_range) instead of a fit_rstat launch
     int fused_fit = 0;
     FitArgs fit{};
+    // resolve_mfma<16>: the range copies are read back from search_mfma16's B fragments (128 − copy_t,
+    // f16) instead of gathered pixel by pixel from the plane
+    const uint4* rfrags = nullptr;
+    // resolve_dft, T = 8: two-wave workgroups, one slot and its flipped copy each (flip_slots > 0)
+    int paired = 0;
 };
 
 __device__ inline void apply_plan(MfmaResolveArgs& a)
@@ -765,6 +881,28 @@ __global__ void __launch_bounds__(256) resolve_mfma(MfmaResolveArgs a)
     uint32_t cp[WPL];
     int ct = -1;
     auto build_copy = [&](int t) {
+        if constexpr (N == 16) {
+            if (a.rfrags) {
+                // words g·WPL … g·WPL + 31 = pixels k = 64g … 64g + 63 of copy_t: fragments s = 4g … 4g + 3,
+                // both lane halves h (k = 16s + 8h + j)
+#pragma unroll
+                for (int sl = 0; sl < 4; ++sl)
+#pragma unroll
+                    for (int hh = 0; hh < 2; ++hh) {
+                        const uint4 f = a.rfrags[((size_t)(blk * a.T + (uint32_t)t) * MfmaGeom<16>::KS + 4 * g + sl) * 64 +
+                                                 col + 32 * hh];
+                        const uint32_t fw[4] = {f.x, f.y, f.z, f.w};
+#pragma unroll
+                        for (int m = 0; m < 4; ++m) {
+                            const uint32_t lo = (uint32_t)(128 - (int)__builtin_bit_cast(_Float16, (uint16_t)(fw[m] & 0xffffu)));
+                            const uint32_t hi = (uint32_t)(128 - (int)__builtin_bit_cast(_Float16, (uint16_t)(fw[m] >> 16)));
+                            cp[sl * 8 + hh * 4 + m] = lo | (hi << 16);
+                        }
+                    }
+                ct = t;
+                return;
+            }
+        }
         const Aff af = lut(t);
 #pragma unroll
         for (int w = 0; w < WPL; ++w) {

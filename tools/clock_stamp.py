@@ -5,8 +5,9 @@ search_dft stamps s_memtime and s_memrealtime around its loop per workgroup.  Fo
 runs the C3 frame back to back for --seconds (≥ 2 s: the clock settles under load), then reads the
 last launch's stamps: per workgroup clock = Δs_memtime ÷ Δs_memrealtime × 100 MHz; prints the
 median / p10 / p90 over workgroups and the launch's span (first start to last end, in µs) as
-one JSON line per variant.
-usage: FRAC_LIB=fractencode_amd/libfracenc_stamps.so tools/clock_stamp.py 35,240 [--seconds 2.5]"""
+one JSON line per variant.  --dump DIR: each variant's last-launch stamps (with the workgroup's XCC, HW_ID
+and tile range) to DIR/stamps_<variant>.npy for tools/l2_model.py.
+usage: FRAC_LIB=fractencode_amd/libfracenc_stamps.so tools/clock_stamp.py 35,240 [--seconds 2.5] [--dump DIR]"""
 import ctypes
 import json
 import os
@@ -22,6 +23,8 @@ from fractencode_amd.synth import value_noise  # noqa: E402
 
 variants = (sys.argv[1] if len(sys.argv) > 1 else "35,240").split(",")
 seconds = float(sys.argv[sys.argv.index("--seconds") + 1]) if "--seconds" in sys.argv else 2.5
+dump = sys.argv[sys.argv.index("--dump") + 1] if "--dump" in sys.argv else None
+WORDS = 6  # fracenc_dft.hip kClockStampWords
 lib = ctypes.CDLL(F.LIB_PATH)
 if not hasattr(lib, "frac_clock_stamps"):
     sys.exit(f"{F.LIB_PATH} is not the diagnostic clock build (tools/build_tuning.py --stamps)")
@@ -43,13 +46,19 @@ with F.Engine(0, 4, False, 0.0, -1.0, F.ENGINE_MFMA, timing=True) as e:
         while time.perf_counter() - t0 < seconds:
             e.run()
             n += 1
+            if n % 16 == 0:  # bound the queue: the loop's clock is the device's
+                e.fetch()
         _, st = e.fetch()
         cap = 1 << 16
-        buf = (ctypes.c_ulonglong * (cap * 4))()
+        buf = (ctypes.c_ulonglong * (cap * WORDS))()
         got = lib.frac_clock_stamps(buf, cap)
         if got <= 0:
             sys.exit(f"variant {v}: no stamps ({got})")
-        s = np.frombuffer(buf, dtype=np.uint64, count=got * 4).reshape(got, 4).astype(np.float64)
+        raw = np.frombuffer(buf, dtype=np.uint64, count=got * WORDS).reshape(got, WORDS).copy()
+        if dump:
+            os.makedirs(dump, exist_ok=True)
+            np.save(os.path.join(dump, f"stamps_{v}.npy"), raw)
+        s = raw[:, :4].astype(np.float64)
         dck, drt = s[:, 1] - s[:, 0], s[:, 3] - s[:, 2]
         ok = drt > 0
         mhz = dck[ok] / drt[ok] * REALTIME_HZ / 1e6
