@@ -971,7 +971,7 @@ int prepare(frac_ctx* c)
         FRAC_TRY(mfma_variant(c, var));
         const bool four_wave = dft_four_wave(var);
         if (n == 16) // search_mfma16: mfma16_bpw(T) range blocks per 4-wave workgroup
-            build_work(mfma16_bpw((uint32_t)T), 4096, c->m_work, c->m_blk_ptr, c->m_blk_ent, false);
+            build_work(mfma16_bpw(c->Teff), 4096, c->m_work, c->m_blk_ptr, c->m_blk_ent, false); // Teff: 1 when sampled
         else if (!fourier || four_wave) // the 8-wave Fourier search reads only its own list
             build_work(4, 8192, c->m_work, c->m_blk_ptr, c->m_blk_ent, false);
         else {
