@@ -866,10 +866,14 @@ int prepare(frac_ctx* c)
         auto build_work = [&](uint32_t bpw, size_t target_wgs, std::vector<uint4>& work,
                               std::vector<uint32_t>& blk_ptr, std::vector<uint32_t>& blk_ent, bool xcd_order) {
             std::vector<uint32_t> split_of; // domain split of each work item
-            size_t groups = 0;
+            // splits per bucket in proportion to its tiles, so every work item covers about
+            // (groups × tiles) / target_wgs group-tiles — an equal count per bucket gave the small
+            // buckets' items a few tiles each (their fixed cost of loading B fragments dominating) and
+            // the large buckets' long ones the tail; Σ groups_b·splits_b ≤ target_wgs + groups
+            uint64_t gtiles = 0;
             for (int b = 0; b < nb; ++b)
                 if (tile_count[b])
-                    groups += (blk_count[b] + bpw - 1) / bpw * c->dft_copies;
+                    gtiles += (uint64_t)((blk_count[b] + bpw - 1) / bpw * c->dft_copies) * tile_count[b];
             // every block of bucket b gets one entry per domain split of b: the CSR map is
             // sized by a count pass, then filled in work order (no per-block lists)
             const uint32_t ncp = c->dft_copies, nbt = c->nblocks * ncp; // T = 8 Fourier: flipped copies
@@ -878,7 +882,7 @@ int prepare(frac_ctx* c)
             for (int b = 0; b < nb; ++b) {
                 if (!tile_count[b] || !blk_count[b])
                     continue;
-                size_t splits = groups ? (target_wgs + groups - 1) / groups : 1;
+                size_t splits = gtiles ? (size_t)(((uint64_t)target_wgs * tile_count[b] + gtiles - 1) / gtiles) : 1;
                 splits = std::max<size_t>(1, std::min<size_t>(splits, std::max<uint32_t>(1u, tile_count[b] / 4u)));
                 uint32_t ns = 0;
                 for (size_t sp = 0; sp < splits; ++sp)
@@ -971,7 +975,7 @@ int prepare(frac_ctx* c)
         FRAC_TRY(mfma_variant(c, var));
         const bool four_wave = dft_four_wave(var);
         if (n == 16) // search_mfma16: mfma16_bpw(T) range blocks per 4-wave workgroup
-            build_work(mfma16_bpw(c->Teff), 4096, c->m_work, c->m_blk_ptr, c->m_blk_ent, false); // Teff: 1 when sampled
+            build_work(mfma16_bpw(c->Teff), kMfma16TargetWgs, c->m_work, c->m_blk_ptr, c->m_blk_ent, false); // Teff: 1 when sampled
         else if (!fourier || four_wave) // the 8-wave Fourier search reads only its own list
             build_work(4, 8192, c->m_work, c->m_blk_ptr, c->m_blk_ent, false);
         else {
@@ -2368,7 +2372,7 @@ int qt_encode_dev(frac_ctx* c, const frac_quadtree_params* qp, LevelGrid& level,
         c->dft_copies = fourier && T == 8 ? 2u : 1u;
         const uint32_t cp = c->dft_copies, KS = (n * n + 15) / 16;
         const uint32_t bpw = n == 16 ? mfma16_bpw(T) : fourier ? kDftBlocksPerWG : 4u;
-        const uint32_t target = n == 16 ? 4096u : fourier ? 8192u / kDftBlocksPerWG * 4u : 8192u;
+        const uint32_t target = n == 16 ? kMfma16TargetWgs : fourier ? 8192u / kDftBlocksPerWG * 4u : 8192u;
         const uint32_t nblocks_cap = (nr_max + 31) / 32 + (uint32_t)nb;
         const uint32_t ntiles_cap = (nd + 31) / 32 + (uint32_t)nb;
         const uint32_t groups_cap = (nblocks_cap * cp + bpw - 1) / bpw + (uint32_t)nb * cp;

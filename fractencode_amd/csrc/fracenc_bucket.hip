@@ -759,7 +759,7 @@ __global__ void __launch_bounds__(64) qt_finish(const DevPlan* __restrict__ last
 // From the bucket bounds of the level's domains and ranges (bucket_bounds over the sorted keys)
 // it lays out the MFMA engine's 32-slot range blocks and 32-row domain tiles per bucket, and writes
 // the search's work items {first block, blocks, tile begin, tile end} — groups of `bpw` blocks of one
-// bucket × splits of the bucket's tiles, splits = ⌈target / groups⌉ capped at tiles / 4, in
+// bucket × splits of the bucket's tiles, splits = ⌈target · tiles / Σ groups·tiles⌉ capped at tiles / 4, in
 // prepare()'s (copy, bucket, group, split) order — and the CSR map block → entries (work·bpw + k)
 // the resolve kernels read.  Every count goes to the DevPlan; the launches that follow use
 // worst-case grids.  The frame's counters get the level's total / eligible pairs and the MFMA
@@ -797,7 +797,7 @@ struct QtPlanHeader {
 __device__ inline void qt_plan_header(const QtPlanArgs& a, QtPlanHeader& h, uint32_t t)
 {
     constexpr uint32_t B = kMaxBuckets;
-    __shared__ uint32_t groups_s;
+    __shared__ unsigned long long gtiles_s;
     BucketLayout& L = h.L;
     if (t < B) {
         const uint32_t nr = a.nr_init != ~0u ? a.nr_init : a.plan->nr;
@@ -815,7 +815,8 @@ __device__ inline void qt_plan_header(const QtPlanArgs& a, QtPlanHeader& h, uint
     if (t == 0) {
         L.nb = a.nb;
         L.VT = 1;
-        uint32_t nbk = 0, nt = 0, groups = 0;
+        uint32_t nbk = 0, nt = 0;
+        unsigned long long gtiles = 0; // Σ groups × tiles
         for (uint32_t b = 0; b < B; ++b) {
             h.blk_first[b] = nbk;
             L.slot_first[b] = 32 * nbk;
@@ -823,11 +824,11 @@ __device__ inline void qt_plan_header(const QtPlanArgs& a, QtPlanHeader& h, uint
             L.tile_first[b] = nt;
             nt += h.tile_count[b];
             if (b < a.nb && h.tile_count[b])
-                groups += (h.blk_count[b] + a.bpw - 1) / a.bpw * a.copies;
+                gtiles += (unsigned long long)((h.blk_count[b] + a.bpw - 1) / a.bpw * a.copies) * h.tile_count[b];
         }
         h.nblocks = nbk;
         h.ntiles = nt;
-        groups_s = groups;
+        gtiles_s = gtiles;
     }
     __syncthreads();
     uint32_t nw = 0, ne = 0;
@@ -835,8 +836,9 @@ __device__ inline void qt_plan_header(const QtPlanArgs& a, QtPlanHeader& h, uint
         const uint32_t cp = t / B, b = t % B, tc = h.tile_count[b], bc = cp < a.copies ? h.blk_count[b] : 0u;
         uint32_t ns = 0;
         if (b < a.nb && tc && bc) {
-            const uint32_t g = groups_s;
-            const uint32_t sp = g ? (a.target + g - 1) / g : 1u;
+            // splits in proportion to the bucket's tiles (prepare()'s build_work): ⌈target·tc / Σ groups·tiles⌉
+            const uint64_t gt = gtiles_s;
+            const uint32_t sp = gt ? (uint32_t)(((uint64_t)a.target * tc + gt - 1) / gt) : 1u;
             ns = max(1u, min(sp, max(1u, tc / 4u))); // ≤ tc: every split holds at least one tile
         }
         if (cp == 0)

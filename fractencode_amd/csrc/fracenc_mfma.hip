@@ -257,21 +257,39 @@ __global__ void __launch_bounds__(256) mfma_range_prep16(MfmaRangePrepArgs a)
     if (b >= a.nblocks)
         return;
     __shared__ uint8_t px[32 * kRp16Row];
-    __shared__ int32_t slot_ri[32];
-    if (threadIdx.x < 32)
-        slot_ri[threadIdx.x] = a.slot_range[b * 32 + threadIdx.x];
+    __shared__ frac_grid_item slot_rg[32];
+    __shared__ int32_t slot_ok[32];
+    if (threadIdx.x < 32) {
+        const int ri = a.slot_range[b * 32 + threadIdx.x];
+        slot_ok[threadIdx.x] = ri >= 0;
+        if (ri >= 0)
+            slot_rg[threadIdx.x] = a.ranges[ri];
+    }
     __syncthreads();
-    // 32 ranges × 256 pixels: thread t reads bytes t, t + 256, … (a range's 16-byte rows are contiguous
-    // across 16 threads); an empty slot reads as 128, whose fragment values are 0
-    for (uint32_t i = threadIdx.x; i < 32u * NN; i += 256u) {
-        const uint32_t col = i / NN, q = i % NN;
-        const int ri = slot_ri[col];
-        uint8_t v = 128;
-        if (ri >= 0) {
-            const frac_grid_item rg = a.ranges[ri];
-            v = a.tgt[(size_t)(rg.y + q / N) * a.tstride + rg.x + (q % N)];
+    // 32 ranges × 16 rows: two rows per thread, each 16 bytes (four 4-byte loads when the row is
+    // aligned, else byte loads), all independent; an empty slot reads as 128, whose fragment values are 0
+#pragma unroll
+    for (uint32_t k = 0; k < 2; ++k) {
+        const uint32_t row = threadIdx.x + 256u * k, col = row >> 4, y = row & 15u;
+        uint32_t w[4] = {0x80808080u, 0x80808080u, 0x80808080u, 0x80808080u};
+        if (slot_ok[col]) {
+            const frac_grid_item rg = slot_rg[col];
+            const uint8_t* src = a.tgt + (size_t)(rg.y + y) * a.tstride + rg.x;
+            if (((uintptr_t)src & 3u) == 0) {
+                const uint32_t* s4 = reinterpret_cast<const uint32_t*>(src);
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    w[q] = s4[q];
+            } else {
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    w[q] = src[4 * q] | (src[4 * q + 1] << 8) | (src[4 * q + 2] << 16) | ((uint32_t)src[4 * q + 3] << 24);
+            }
         }
-        px[col * kRp16Row + q] = v;
+        uint32_t* dst = reinterpret_cast<uint32_t*>(px + col * kRp16Row + y * N);
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            dst[q] = w[q];
     }
     __syncthreads();
     // the range constants: 8 threads per range, 32 pixels each, then a reduction over the 8 lanes
@@ -290,7 +308,7 @@ __global__ void __launch_bounds__(256) mfma_range_prep16(MfmaRangePrepArgs a)
             s2 += __shfl_xor(s2, o, 64);
         }
         if (part == 0)
-            a.rconst[b * 32 + col] = slot_ri[col] >= 0 ? mfma_range_const(NN, s1, s2) : 0u;
+            a.rconst[b * 32 + col] = slot_ok[col] ? mfma_range_const(NN, s1, s2) : 0u;
     }
     // the fragments: output word o = ((t·KS + s)·64 + lane), lane = col + 32h, k = 16s + 8h + j
     const uint32_t nout = a.T * KS * 64u;
@@ -663,6 +681,9 @@ struct Mfma16Shape {
 };
 // the host's work lists at n = 16 (build_work / qt_plan): blocks per work item
 constexpr uint32_t mfma16_bpw(uint32_t T) { return T >= 8 ? 1u : T >= 2 ? 2u : 4u; }
+// target workgroups of an n = 16 search (4 rounds of the 512 resident): a work item's fixed cost —
+// 32 KiB of B fragments per wave and the first stage's DMA — stays small beside its tiles
+constexpr uint32_t kMfma16TargetWgs = 2048;
 
 template <int T, bool HITS>
 __global__ void __launch_bounds__(256, 2) search_mfma16(MfmaSearchArgs a)
