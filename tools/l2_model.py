@@ -34,41 +34,52 @@ z, w = (raw[:, 5] & 0xFFFFFFFF).astype(np.int64), (raw[:, 5] >> 32).astype(np.in
 nwg = len(raw)
 cap_tiles = int(l2_mib * 2**20 // TILE_B)
 
-# per workgroup the range fragments at its start, then one event per 4-tile stage
-ev_t, ev_x, ev_tile, ev_n = [], [], [], []
-for g in range(nwg):
-    nt = int(w[g] - z[g])
-    if nt <= 0:
-        continue
-    ns = (nt + STAGE - 1) // STAGE
-    k = np.arange(ns)
-    ev_t.append(rt0[g] + (rt1[g] - rt0[g]) * k / ns)
-    ev_x.append(np.full(ns, xcc[g]))
-    ev_tile.append(z[g] + STAGE * k)
-    ev_n.append(np.minimum(STAGE, nt - STAGE * k))
-ev_t, ev_x = np.concatenate(ev_t), np.concatenate(ev_x)
-ev_tile, ev_n = np.concatenate(ev_tile), np.concatenate(ev_n)
+def lru_misses(t_start, t_end):
+    """Tile misses per XCC of the workgroups' reads replayed through an LRU of cap_tiles."""
+    ev_t, ev_x, ev_tile, ev_n = [], [], [], []
+    for g in range(nwg):
+        nt = int(w[g] - z[g])
+        if nt <= 0:
+            continue
+        ns = (nt + STAGE - 1) // STAGE
+        k = np.arange(ns)
+        ev_t.append(t_start[g] + (t_end[g] - t_start[g]) * k / ns)
+        ev_x.append(np.full(ns, xcc[g]))
+        ev_tile.append(z[g] + STAGE * k)
+        ev_n.append(np.minimum(STAGE, nt - STAGE * k))
+    ev_t, ev_x = np.concatenate(ev_t), np.concatenate(ev_x)
+    ev_tile, ev_n = np.concatenate(ev_tile), np.concatenate(ev_n)
+    out = {}
+    for x in np.unique(ev_x):
+        sel = np.nonzero(ev_x == x)[0]
+        order = sel[np.argsort(ev_t[sel], kind="stable")]
+        lru = collections.OrderedDict()
+        m = 0
+        for e in order:
+            t0 = int(ev_tile[e])
+            for t in range(t0, t0 + int(ev_n[e])):
+                if t in lru:
+                    lru.move_to_end(t)
+                else:
+                    m += 1
+                    lru[t] = None
+                    if len(lru) > cap_tiles:
+                        lru.popitem(last=False)
+        out[int(x)] = m
+    return out
 
-miss_tiles = 0
-per_xcc = {}
-for x in np.unique(ev_x):
-    sel = np.nonzero(ev_x == x)[0]
-    order = sel[np.argsort(ev_t[sel], kind="stable")]
-    lru = collections.OrderedDict()
-    m = 0
-    for e in order:
-        t0 = int(ev_tile[e])
-        for t in range(t0, t0 + int(ev_n[e])):
-            if t in lru:
-                lru.move_to_end(t)
-            else:
-                m += 1
-                lru[t] = None
-                if len(lru) > cap_tiles:
-                    lru.popitem(last=False)
-    per_xcc[int(x)] = m
-    miss_tiles += m
 
+per_xcc = lru_misses(rt0, rt1)
+miss_tiles = sum(per_xcc.values())
+# the same replay on a lockstep timeline: per XCC, the workgroups in start order in generations of 64,
+# each generation starting together when the previous one ends (every loop the median duration)
+med = float(np.median(rt1 - rt0))
+ls0 = np.zeros(nwg)
+for x in np.unique(xcc):
+    gs = np.nonzero(xcc == x)[0]
+    gs = gs[np.argsort(rt0[gs], kind="stable")]
+    ls0[gs] = (np.arange(len(gs)) // 64) * med
+lock_lru = sum(lru_misses(ls0, ls0 + med).values())
 model_b = miss_tiles * TILE_B + nwg * bpw * RFRAG_B
 # lockstep: per XCC, generations of (resident) workgroups each read their splits' distinct tiles once
 resident = 64  # 32 CUs × 2 workgroups (108 VGPRs: 4 waves per SIMD; 8-wave workgroups)
@@ -90,7 +101,6 @@ print(json.dumps({"stamps": path, "workgroups": nwg, "xcc_count": int(len(np.uni
                   "wg_loop_us": {"p10": round(float(np.percentile(dur, 10)), 1),
                                  "median": round(float(np.median(dur)), 1),
                                  "p90": round(float(np.percentile(dur, 90)), 1)},
-                  "start_spread_us_p90_minus_p10_per_xcc": round(float(np.median(
-                      [np.percentile(rt0[xcc == x], 90) - np.percentile(rt0[xcc == x], 10) for x in np.unique(xcc)])) / 100.0, 1),
                   "timeline_lru_model_bytes": int(model_b), "timeline_lru_miss_tiles_per_xcc": per_xcc,
-                  "lockstep_model_bytes": int(lock_b)}, indent=1))
+                  "lockstep_model_bytes": int(lock_b),
+                  "lockstep_timeline_lru_bytes": int(lock_lru * TILE_B + nwg * bpw * RFRAG_B)}, indent=1))

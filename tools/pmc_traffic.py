@@ -1,36 +1,58 @@
 #!/usr/bin/env python3
-"""Writes profiles/pmc_search.json from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (separate
-runs, kB per dispatch) of bench.py: HBM-side bytes per search launch, FETCH_SIZE doubled on gfx950
-(MI355X_MICROARCH.md §HBM: 16-B/lane streaming reads are tallied at half their bytes).
-usage: tools/pmc_traffic.py FORM KERNEL_PREFIX FETCH_CSV WRITE_CSV SOURCE_NOTE"""
+"""Writes profiles/pmc_search.json's FORM entry from rocprofv3 --pmc passes (separate runs) over the
+same program: fabric read bytes per search launch from the sized read-request counters, write bytes
+from WRITE_SIZE, and FETCH_SIZE beside them with the factor between the two.
+
+Read bytes = 32·TCC_EA0_RDREQ_32B + 64·TCC_EA0_RDREQ_64B + 128·TCC_EA0_RDREQ_128B (sums over the
+XCDs' L2 channels).  rocprofv3's FETCH_SIZE tallies every request above 32 B at 64 B, so on gfx950
+it reads half the bytes of the 128-byte requests a 16-B-per-lane streaming read makes
+(MI355X_MICROARCH.md §HBM; calibrated on this kernel's own access pattern by tools/fetch_calib.hip:
+1 GiB read once = 8,388,608 128-B requests, FETCH_SIZE 524,288 kB).  The counters see the L2's
+misses to the fabric; Infinity Cache hits are among them.
+usage: tools/pmc_traffic.py FORM KERNEL_PREFIX RDREQ_CSV FETCH_CSV WRITE_CSV SOURCE_NOTE"""
 import csv
 import json
 import os
 import sys
 
-form, prefix, fcsv, wcsv, note = sys.argv[1:6]
+form, prefix, rcsv, fcsv, wcsv, note = sys.argv[1:7]
 
 
-def avg(path):
-    tot, disp = 0.0, set()
+def per_dispatch(path):
+    tot, disp = {}, set()
     for r in csv.DictReader(open(path)):
         if r["Kernel_Name"].startswith(prefix):
-            tot += float(r["Counter_Value"])
+            tot[r["Counter_Name"]] = tot.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
             disp.add(r["Dispatch_Id"])
-    return tot / max(1, len(disp)), len(disp)
+    n = max(1, len(disp))
+    return {k: v / n for k, v in tot.items()}, len(disp)
 
 
-f, nf = avg(fcsv)
-w, nw = avg(wcsv)
-path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "pmc_search.json")
+rq, nr = per_dispatch(rcsv)
+fe, nf = per_dispatch(fcsv)
+wr, nw = per_dispatch(wcsv)
+n32, n64, n128 = (rq.get(f"TCC_EA0_RDREQ_{s}B_sum", 0.0) for s in (32, 64, 128))
+read_b = 32 * n32 + 64 * n64 + 128 * n128
+fetch_kb, write_kb = fe.get("FETCH_SIZE", 0.0), wr.get("WRITE_SIZE", 0.0)
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+path = os.path.join(ROOT, "profiles", "pmc_search.json")
 d = json.load(open(path)) if os.path.exists(path) else {}
-d["_doc"] = ("HBM-side bytes per search launch from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes, "
-             "kB units), corrected per MI355X_MICROARCH.md §HBM: FETCH_SIZE doubled on gfx950, WRITE_SIZE as "
-             "reported.  Keyed by frac_stats.search_form.")
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+d["_doc"] = ("Fabric-side bytes per search launch (rocprofv3 --pmc, separate passes): reads from the sized L2 "
+             "read-request counters, 32·RDREQ_32B + 64·RDREQ_64B + 128·RDREQ_128B; writes from WRITE_SIZE (kB). "
+             "FETCH_SIZE is kept beside them: it tallies a 128-B request at 64 B, so it reads half of a 16-B/lane "
+             "streaming read on gfx950 (MI355X_MICROARCH.md §HBM; calibrated on this kernel's access pattern by "
+             "tools/fetch_calib.hip, profiles/r04/traffic/). Keyed by frac_stats.search_form and the build's "
+             "source id.")
+sys.path.insert(0, ROOT)
 from fractencode_amd import source_id  # noqa: E402
 
-d[form] = {"kernel": prefix, "source_id": source_id(), "fetch_size_kb": round(f, 1), "write_size_kb": round(w, 1), "dispatches": [nf, nw],
-           "hbm_bytes_per_launch": int(round((2 * f + w) * 1024)), "source": note}
+d[form] = {"kernel": prefix, "source_id": source_id(), "dispatches": [nr, nf, nw],
+           "rdreq_32b": round(n32, 1), "rdreq_64b": round(n64, 1), "rdreq_128b": round(n128, 1),
+           "read_bytes": int(round(read_b)), "fetch_size_kb": round(fetch_kb, 1),
+           "fetch_size_to_bytes": round(read_b / (fetch_kb * 1024), 4) if fetch_kb else None,
+           "write_size_kb": round(write_kb, 1),
+           "correction": "reads from the sized request counters (128-B requests at 128 B); FETCH_SIZE x2 agrees "
+                         "within the 64-B requests' share",
+           "hbm_bytes_per_launch": int(round(read_b + write_kb * 1024)), "source": note}
 json.dump(d, open(path, "w"), indent=1)
 print(json.dumps(d[form]))
