@@ -1658,7 +1658,12 @@ int launch_mfma(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool inits =
         r.plan = c->qplan;
         r.fmode = fmode;
         if constexpr (N == 16) { // one workgroup per range block, the constants written directly
-            mfma_range_prep16<<<c->nblocks, 256, 0, c->stream>>>(r);
+            if (T == 8)
+                mfma_range_prep16<8><<<c->nblocks, 256, 0, c->stream>>>(r);
+            else if (T == 1)
+                mfma_range_prep16<1><<<c->nblocks, 256, 0, c->stream>>>(r);
+            else
+                mfma_range_prep16<4><<<c->nblocks, 256, 0, c->stream>>>(r);
         } else {
             const size_t threads = (size_t)c->nblocks * T * MfmaGeom<N>::KS * 64;
             // rconst is a sum of per-pixel terms, accumulated by the transform-0 threads (a planned level's

@@ -249,6 +249,7 @@ __global__ void __launch_bounds__(256) mfma_range_prep(MfmaRangePrepArgs a)
 // Rows of the LDS image are 260 bytes apart, so the 32 columns of a fragment read hit 32 banks.
 constexpr uint32_t kRp16Row = 260;
 
+template <int T>
 __global__ void __launch_bounds__(256) mfma_range_prep16(MfmaRangePrepArgs a)
 {
     constexpr int N = 16, NN = 256, KS = MfmaGeom<16>::KS;
@@ -310,19 +311,22 @@ __global__ void __launch_bounds__(256) mfma_range_prep16(MfmaRangePrepArgs a)
         if (part == 0)
             a.rconst[b * 32 + col] = slot_ok[col] ? mfma_range_const(NN, s1, s2) : 0u;
     }
-    // the fragments: output word o = ((t·KS + s)·64 + lane), lane = col + 32h, k = 16s + 8h + j
-    const uint32_t nout = a.T * KS * 64u;
-    for (uint32_t o = threadIdx.x; o < nout; o += 256u) {
-        const uint32_t lane = o & 63u, s = (o >> 6) % KS, t = (o >> 6) / KS;
-        const uint32_t col = lane & 31u, h = lane >> 5;
+    // the fragments: output word o = ((t·KS + s)·64 + lane), lane = col + 32h, k = 16s + 8h + j; thread
+    // x takes o = x + 256m, so t = m / 4 is a constant of each unrolled step (the permutation affine)
+    const uint32_t lane = threadIdx.x & 63u, col = lane & 31u, h = lane >> 5;
+#pragma unroll
+    for (int m = 0; m < T * KS * 64 / 256; ++m) {
+        constexpr int kPerT = KS * 64 / 256; // 4 steps per transform
+        const int t = m / kPerT;
+        const uint32_t o = threadIdx.x + 256u * (uint32_t)m, s = (o >> 6) % KS;
         _Float16 v8[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             const int k = 16 * (int)s + 8 * (int)h + j;
-            const int rv = px[col * kRp16Row + inv_index<N>((int)t, k)];
+            const int rv = px[col * kRp16Row + inv_index<N>(t, k)];
             v8[j] = (_Float16)(a.fmode ? 8 * (128 - rv) : 128 - rv);
         }
-        a.rfrags[((size_t)b * a.T * KS) * 64 + o] = __builtin_bit_cast(uint4, v8);
+        a.rfrags[((size_t)b * T * KS) * 64 + o] = __builtin_bit_cast(uint4, v8);
     }
 }
 
@@ -882,20 +886,10 @@ __global__ void __launch_bounds__(256) resolve_mfma(MfmaResolveArgs a)
     // other T − 1 slots are never written to with a candidate, so only slot 0 is read (T× fewer loads)
     const uint32_t TE = a.merged ? 1u : a.T;
     const uint32_t nent = (e1 - e0) * TE * 2u;
-    uint32_t vmin = 0xffffffffu;
-    for (uint32_t j = lane; j < nent; j += 64) {
-        const uint32_t e = e0 + j / (2u * TE), t = (j >> 1) % TE, h = j & 1u;
-        vmin = min(vmin, a.entries[((size_t)a.blk_ent[e] * a.T + t) * 64 + col + 32 * h].x);
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1)
-        vmin = min(vmin, (uint32_t)__shfl_xor((int)vmin, o, 64));
-    if (vmin == 0xffffffffu) { // no eligible domain: best_key stays "none"
-        if (a.fused_fit && lane == 0)
-            fit_sums_range<N>(a.fit, r, kKeyNone, 0, 0, 0, 0, 0);
-        return;
-    }
+    // the range, its constant and its transform-0 copy do not depend on the entries: their loads are
+    // issued first, so their latency overlaps the entries' (the copy is built below)
     const frac_grid_item rg = a.ranges[r];
+    const uint32_t rc = a.rconst[slot];
     const int i = lane >> 2, g = lane & 3;
     constexpr uint32_t kOnes = 0x00010001u;
     // the lane's slice of the copy under transform ct (rebuilt when an entry's t differs)
@@ -935,6 +929,27 @@ __global__ void __launch_bounds__(256) resolve_mfma(MfmaResolveArgs a)
         ct = t;
     };
     build_copy(0);
+    // the entries: the first 128 stay in registers (enr) for the match pass below, which reloads
+    // only past them
+    uint2 enr0 = make_uint2(0xffffffffu, 0u), enr1 = enr0;
+    uint32_t vmin = 0xffffffffu;
+    for (uint32_t j = lane; j < nent; j += 64) {
+        const uint32_t e = e0 + j / (2u * TE), t = (j >> 1) % TE, h = j & 1u;
+        const uint2 en = a.entries[((size_t)a.blk_ent[e] * a.T + t) * 64 + col + 32 * h];
+        if (j < 64)
+            enr0 = en;
+        else if (j < 128)
+            enr1 = en;
+        vmin = min(vmin, en.x);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1)
+        vmin = min(vmin, (uint32_t)__shfl_xor((int)vmin, o, 64));
+    if (vmin == 0xffffffffu) { // no eligible domain: best_key stays "none"
+        if (a.fused_fit && lane == 0)
+            fit_sums_range<N>(a.fit, r, kKeyNone, 0, 0, 0, 0, 0);
+        return;
+    }
     uint32_t sr2u = 0, sr1u = 0; // Σr², Σr (every pixel meets exactly one domain cell)
 #pragma unroll
     for (int w = 0; w < WPL; ++w) {
@@ -946,8 +961,8 @@ __global__ void __launch_bounds__(256) resolve_mfma(MfmaResolveArgs a)
     const int64_t sr2 = (int64_t)quad_sum(sr2u);
     const int64_t sr1 = (int64_t)quad_sum(sr1u);
     // best S16 (when vmin is not a sentinel): v − c_r, or for the float-C entries acc + c'_r = acc + V0 − c_r
-    const int64_t target = a.fmode ? (int64_t)funmap(vmin) + mfma_v0(NN) - (int64_t)(int32_t)a.rconst[slot]
-                                   : (int64_t)vmin - (int64_t)a.rconst[slot];
+    const int64_t target = a.fmode ? (int64_t)funmap(vmin) + mfma_v0(NN) - (int64_t)(int32_t)rc
+                                   : (int64_t)vmin - (int64_t)rc;
     // hits: the sentinel 0 (kernel run with H > 0), or a best error that meets H = 0
     const bool hit = a.hitH >= 0 && (vmin == 0 || target <= a.hitH);
     unsigned long long bestk = kKeyNone;
@@ -957,8 +972,8 @@ __global__ void __launch_bounds__(256) resolve_mfma(MfmaResolveArgs a)
     // time and the wave walks the ballot of matches (the cost does not grow with the splits)
     for (uint32_t c0 = 0; c0 < nent; c0 += 64) {
         const uint32_t jl = c0 + (uint32_t)lane;
-        uint2 enl = make_uint2(0xffffffffu, 0u);
-        if (jl < nent) {
+        uint2 enl = c0 == 0 ? enr0 : enr1;
+        if (c0 >= 128 && jl < nent) {
             const uint32_t e = e0 + jl / (2u * TE), t = (jl >> 1) % TE, h = jl & 1u;
             enl = a.entries[((size_t)a.blk_ent[e] * a.T + t) * 64 + col + 32 * h];
         }
@@ -981,8 +996,16 @@ __global__ void __launch_bounds__(256) resolve_mfma(MfmaResolveArgs a)
                 // the entry names the first tile of the chunk that attained the minimum: scan the
                 // chunk's tiles in order; the first matching row is the earliest domain
                 constexpr uint32_t CH = N == 16 ? (uint32_t)kTilesPerStage16 : (uint32_t)kTilesPerStage;
-                for (uint32_t tile = ctile; tile < min(ctile + CH, a.ntiles) && tile <= best_tile; ++tile) {
-                    const int p = a.tile_pos[tile * 32 + row];
+                int pch[CH]; // the chunk's rows' pool positions, loaded together
+#pragma unroll
+                for (uint32_t q = 0; q < CH; ++q)
+                    pch[q] = ctile + q < a.ntiles ? a.tile_pos[(ctile + q) * 32 + row] : -1;
+#pragma unroll
+                for (uint32_t q = 0; q < CH; ++q) {
+                    const uint32_t tile = ctile + q;
+                    if (tile >= a.ntiles || tile > best_tile)
+                        break;
+                    const int p = pch[q];
                     uint32_t d[WPL];
                     if (p >= 0 && g * WPL < K2) {
                         const uint32_t* dp = a.pool + (size_t)p * K2 + g * WPL;
