@@ -882,7 +882,8 @@ int prepare(frac_ctx* c)
             for (int b = 0; b < nb; ++b) {
                 if (!tile_count[b] || !blk_count[b])
                     continue;
-                size_t splits = gtiles ? (size_t)(((uint64_t)target_wgs * tile_count[b] + gtiles - 1) / gtiles) : 1;
+                const uint64_t tw = work_target(target_wgs, gtiles);
+                size_t splits = gtiles ? (size_t)((tw * tile_count[b] + gtiles - 1) / gtiles) : 1;
                 splits = std::max<size_t>(1, std::min<size_t>(splits, std::max<uint32_t>(1u, tile_count[b] / 4u)));
                 uint32_t ns = 0;
                 for (size_t sp = 0; sp < splits; ++sp)
@@ -1274,6 +1275,11 @@ inline FitArgs fit_args(const frac_ctx* c, const uint8_t* dtgt, uint32_t tstride
     f.fb_count = c->d_fb_count.ptr;
     f.fb_list = c->d_fb_list.ptr;
     f.plan = c->qplan;
+    // the fused fits evaluate their fp32-regime ranges in the resolving wave (the all-fallback regime
+    // lists every range for fallback_fp32 instead)
+    f.inline_fallback = c->all_fallback ? 0 : 1;
+    f.rbucket = c->d_rbucket.ptr;
+    f.thr = c->p.rms_threshold;
     return f;
 }
 
@@ -2200,7 +2206,8 @@ int launch_all(frac_ctx* c)
             fit_winner<N><<<std::max(1u, (nr + 4 * (64 / fit_lanes<N>()) - 1) / (4 * (64 / fit_lanes<N>()))), 256, 0,
                             c->stream>>>(f);
     }
-    if (nr && !c->virt) {
+    // the fused resolvers ran their fp32-regime ranges themselves (FitArgs::inline_fallback): no launch
+    if (nr && !c->virt && !(c->fit_fused && !c->all_fallback)) {
         FallbackArgs b;
         b.tgt = dtgt;
         b.tstride = tstride;

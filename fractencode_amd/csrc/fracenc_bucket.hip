@@ -837,8 +837,8 @@ __device__ inline void qt_plan_header(const QtPlanArgs& a, QtPlanHeader& h, uint
         uint32_t ns = 0;
         if (b < a.nb && tc && bc) {
             // splits in proportion to the bucket's tiles (prepare()'s build_work): ⌈target·tc / Σ groups·tiles⌉
-            const uint64_t gt = gtiles_s;
-            const uint32_t sp = gt ? (uint32_t)(((uint64_t)a.target * tc + gt - 1) / gt) : 1u;
+            const uint64_t gt = gtiles_s, tw = work_target(a.target, gt);
+            const uint32_t sp = gt ? (uint32_t)((tw * tc + gt - 1) / gt) : 1u;
             ns = max(1u, min(sp, max(1u, tc / 4u))); // ≤ tc: every split holds at least one tile
         }
         if (cp == 0)

@@ -121,6 +121,17 @@ struct RangeAux {
 };
 
 constexpr int kMaxBuckets = 8; // 7 classifier buckets (categories −1..5); 1 without the classifier
+// the searches' work lists aim at ≥ this many domain tiles per work item (group of range blocks ×
+// domain split): on a small frame the target workgroup count would otherwise cut one 4-tile stage per
+// workgroup, every workgroup paying its B-fragment loads and first DMA for one stage (C2: 992
+// workgroups of 4 tiles in two rounds), and the resolve scanning one entry per split
+constexpr uint32_t kMinTilesPerWork = 8;
+// the effective target: at most one work item per kMinTilesPerWork group-tiles
+__host__ __device__ inline uint64_t work_target(uint64_t target, uint64_t gtiles)
+{
+    const uint64_t cap = gtiles / kMinTilesPerWork;
+    return cap < 1 ? 1 : (cap < target ? cap : target);
+}
 
 // per-bucket layout, passed by value to the fill kernels (or read from a DevPlan)
 struct BucketLayout {

@@ -250,6 +250,11 @@ struct FitArgs {
     uint32_t* fb_count;
     uint32_t* fb_list;
     const DevPlan* plan = nullptr; // device-planned search: nr from the plan (the grid is a bound)
+    // the resolvers' fused fits: a range whose key leaves the exact regime is evaluated in fp32 by the
+    // resolving wave itself (fallback_wave), and no fallback_fp32 launch follows
+    int inline_fallback = 0;
+    const uint2* rbucket = nullptr; // per range its bucket's pool slice [x, y) (fallback_wave)
+    double thr = 0.0;               // the hit threshold on the fp32 distance (fallback_wave)
 };
 
 __device__ inline void write_fit(frac_encode_item& o, const frac_grid_item& rg, const frac_grid_item& d, int t,
@@ -519,6 +524,70 @@ struct FallbackArgs {
 // one block per CU: an empty list (the usual case) costs the dispatch of these blocks only
 constexpr unsigned kFallbackBlocks = 256;
 
+// one candidate (pool position bk.x + pl, transform t) of a range in the reference's fp32 arithmetic
+// (rpix: the range's pixels as floats), as its selection key
+template <int N>
+__device__ inline unsigned long long fallback_key(const uint32_t* __restrict__ pool, const float* rpix, uint32_t p,
+                                                  uint32_t pl, int t, uint32_t T, double thr)
+{
+    constexpr int NN = N * N;
+    const uint32_t* dp = pool + (size_t)p * (NN / 2);
+    float F = 0.0f;
+    for (int q = 0; q < NN; ++q) {
+        const int f = fwd_index<N>(t, q);
+        const uint32_t fw = dp[f >> 1];
+        const float smp = (float)((f & 1) ? (fw >> 16) : (fw & 0xffffu)) / 4.0f;
+        const float val = __fsub_rn(rpix[q], smp);
+        F = __fadd_rn(F, __fmul_rn(val, val));
+    }
+    const double dist = (double)F / (double)(4 * NN);
+    if (dist <= thr)
+        return ((unsigned long long)pl << 3) | (unsigned long long)t;
+    return kKeyMiss | ((unsigned long long)__float_as_uint(F) << 27) | ((unsigned long long)pl << 3) |
+           (unsigned long long)(T - 1 - t);
+}
+
+// range r's record from its least fp32 key k (kKeyNone: no candidate)
+template <int N>
+__device__ inline void fallback_record(const uint32_t* __restrict__ pool, const frac_grid_item* doms,
+                                       const uint32_t* porig, uint32_t T, double smax, frac_encode_item* out,
+                                       RangeAux* aux, uint32_t r, const frac_grid_item& rg, const uint2& bk,
+                                       unsigned long long k, const float* rpix)
+{
+    constexpr int NN = N * N;
+    if (k == kKeyNone) {
+        write_default(out[r], rg);
+        aux[r] = RangeAux{0u, (uint32_t)kAuxEmpty};
+        return;
+    }
+    const bool hit = (k >> 63) == 0;
+    const uint32_t pl = (uint32_t)((k >> 3) & 0xffffffu);
+    const int t = hit ? (int)(k & 7u) : (int)(T - 1 - (uint32_t)(k & 7u));
+    const uint32_t p = bk.x + pl;
+    const frac_grid_item d = doms[porig[p]];
+    const uint32_t* dp = pool + (size_t)p * (NN / 2);
+    long long sA = 0, sA2 = 0, sD = 0, X = 0;
+    float Fh = 0.0f;
+    for (int q = 0; q < NN; ++q) {
+        const int rv = (int)rpix[q];
+        const uint32_t dw = dp[q >> 1];
+        const int dv = (q & 1) ? (int)(dw >> 16) : (int)(dw & 0xffffu);
+        const int f = fwd_index<N>(t, q);
+        const uint32_t fw = dp[f >> 1];
+        const int fv = (f & 1) ? (int)(fw >> 16) : (int)(fw & 0xffffu);
+        sA += rv;
+        sA2 += rv * rv;
+        sD += dv;
+        X += (long long)rv * fv;
+        const float val = __fsub_rn(rpix[q], (float)fv / 4.0f);
+        Fh = __fadd_rn(Fh, __fmul_rn(val, val));
+    }
+    const double dist = (double)Fh / (double)(d.w * d.h);
+    write_fit(out[r], rg, d, t, (double)sA, (double)sA2, (double)sD * 0.25, (double)X * 0.25, (double)NN, smax,
+              dist);
+    aux[r] = RangeAux{p, (uint32_t)(kAuxFallback | (hit ? kAuxHit : 0u))};
+}
+
 template <int N>
 __global__ void __launch_bounds__(256) fallback_fp32(FallbackArgs a)
 {
@@ -537,24 +606,7 @@ __global__ void __launch_bounds__(256) fallback_fp32(FallbackArgs a)
         unsigned long long best = kKeyNone;
         const uint32_t ncand = (bk.y - bk.x) * a.T;
         for (uint32_t c = threadIdx.x; c < ncand; c += blockDim.x) {
-            const uint32_t pl = c / a.T;
-            const int t = (int)(c % a.T);
-            const uint32_t* dp = a.pool + (size_t)(bk.x + pl) * (NN / 2);
-            float F = 0.0f;
-            for (int q = 0; q < NN; ++q) {
-                const int f = fwd_index<N>(t, q);
-                const uint32_t fw = dp[f >> 1];
-                const float smp = (float)((f & 1) ? (fw >> 16) : (fw & 0xffffu)) / 4.0f;
-                const float val = __fsub_rn(rpix[q], smp);
-                F = __fadd_rn(F, __fmul_rn(val, val));
-            }
-            const double dist = (double)F / (double)(4 * NN);
-            unsigned long long key;
-            if (dist <= a.thr)
-                key = ((unsigned long long)pl << 3) | (unsigned long long)t;
-            else
-                key = kKeyMiss | ((unsigned long long)__float_as_uint(F) << 27) | ((unsigned long long)pl << 3) |
-                      (unsigned long long)(a.T - 1 - t);
+            const unsigned long long key = fallback_key<N>(a.pool, rpix, bk.x + c / a.T, c / a.T, (int)(c % a.T), a.T, a.thr);
             best = key < best ? key : best;
         }
         red[threadIdx.x] = best;
@@ -567,43 +619,50 @@ __global__ void __launch_bounds__(256) fallback_fp32(FallbackArgs a)
             }
             __syncthreads();
         }
-        if (threadIdx.x == 0) {
-            const unsigned long long k = red[0];
-            if (k != kKeyNone) {
-                const bool hit = (k >> 63) == 0;
-                const uint32_t pl = (uint32_t)((k >> 3) & 0xffffffu);
-                const int t = hit ? (int)(k & 7u) : (int)(a.T - 1 - (uint32_t)(k & 7u));
-                const float F = hit ? 0.0f : __uint_as_float((uint32_t)((k >> 27) & 0xffffffffull));
-                const uint32_t p = bk.x + pl;
-                const frac_grid_item d = a.doms[a.porig[p]];
-                const uint32_t* dp = a.pool + (size_t)p * (NN / 2);
-                long long sA = 0, sA2 = 0, sD = 0, X = 0;
-                float Fh = 0.0f;
-                for (int q = 0; q < NN; ++q) {
-                    const int rv = (int)rpix[q];
-                    const uint32_t dw = dp[q >> 1];
-                    const int dv = (q & 1) ? (int)(dw >> 16) : (int)(dw & 0xffffu);
-                    const int f = fwd_index<N>(t, q);
-                    const uint32_t fw = dp[f >> 1];
-                    const int fv = (f & 1) ? (int)(fw >> 16) : (int)(fw & 0xffffu);
-                    sA += rv;
-                    sA2 += rv * rv;
-                    sD += dv;
-                    X += (long long)rv * fv;
-                    const float val = __fsub_rn(rpix[q], (float)fv / 4.0f);
-                    Fh = __fadd_rn(Fh, __fmul_rn(val, val));
-                }
-                (void)F;
-                const double dist = (double)Fh / (double)(d.w * d.h);
-                write_fit(a.out[r], rg, d, t, (double)sA, (double)sA2, (double)sD * 0.25, (double)X * 0.25,
-                          (double)NN, a.smax, dist);
-                a.aux[r] = RangeAux{p, (uint32_t)(kAuxFallback | (hit ? kAuxHit : 0u))};
-            } else {
-                write_default(a.out[r], rg);
-                a.aux[r] = RangeAux{0u, (uint32_t)kAuxEmpty};
-            }
-        }
+        if (threadIdx.x == 0)
+            fallback_record<N>(a.pool, a.doms, a.porig, a.T, a.smax, a.out, a.aux, r, rg, bk, red[0], rpix);
     }
+}
+
+// fallback_fp32's evaluation of range r by one wave (the resolvers' fused fits, FitArgs::inline_fallback):
+// the range's pixels in this wave's LDS row, the candidates across the lanes, a wave minimum of the keys.
+// Counted in fb_count (the run's fallback_ranges) but not listed: no fallback_fp32 launch follows.
+template <int N>
+__device__ inline void fallback_wave(const FitArgs& a, uint32_t r, int lane)
+{
+    constexpr int NN = N * N;
+    __shared__ float rpix_w[4][NN]; // resolve workgroups have at most 4 waves
+    float* rpix = rpix_w[(threadIdx.x >> 6) & 3u];
+    const frac_grid_item rg = a.ranges[r];
+    const uint2 bk = a.rbucket[r];
+    for (int q = lane; q < NN; q += 64)
+        rpix[q] = (float)(int16_t)a.tgt[(size_t)(rg.y + q / N) * a.tstride + rg.x + (q % N)];
+    // the LDS writes above and the reads below are one wave's, issued in order: keep the compiler's order
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    unsigned long long best = kKeyNone;
+    const uint32_t ncand = (bk.y - bk.x) * a.T;
+    for (uint32_t c = (uint32_t)lane; c < ncand; c += 64) {
+        const unsigned long long key = fallback_key<N>(a.pool, rpix, bk.x + c / a.T, c / a.T, (int)(c % a.T), a.T, a.thr);
+        best = key < best ? key : best;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long ob = ((unsigned long long)(uint32_t)__shfl_xor((int)(uint32_t)(best >> 32), o, 64) << 32) |
+                                      (uint32_t)__shfl_xor((int)(uint32_t)best, o, 64);
+        best = ob < best ? ob : best;
+    }
+    if (lane == 0) {
+        atomicAdd(a.fb_count, 1u);
+        fallback_record<N>(a.pool, a.doms, a.porig, a.T, a.smax, a.out, a.aux, r, rg, bk, best, rpix);
+    }
+}
+
+// the fused fits' exit to the fp32 regime: a miss whose exact error is at least kExactLimit
+__device__ inline bool key_needs_fallback(unsigned long long key)
+{
+    return key != kKeyNone && (key >> 63) != 0 && (long long)((key >> 27) & 0xfffffffffull) >= kExactLimit;
 }
 
 // ---------------------------------------------------------------------------
