@@ -1,6 +1,6 @@
 #!/bin/bash
 # round 4 session 11: fallback in the resolving wave (no fallback_fp32 launch after fused fits), resolve_dft chunk prefetch,
-# at least 8 tiles per work item.  Full suite, C4 / C4q rates, C4q and C2 kernel traces.
+# at least 8 tiles per work item, quadtree leaves copied on a second stream.  Full suite, C4 / C4q rates, C4q and C2 kernel traces.
 set -euo pipefail
 R=$(pwd)
 O=$R/gpurun_out/r04_s11
