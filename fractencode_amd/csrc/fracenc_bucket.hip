@@ -187,19 +187,28 @@ struct BkSeg {
 
 // Two independent sorts per launch (a quadtree level's domains and ranges): blocks [0, s0.tiles) take s0,
 // the rest s1 (s1.tiles = 0: one sort).
-__device__ inline const BkSeg& bk_seg(const BkSeg& s0, const BkSeg& s1, uint32_t& blk)
+// (by value, field by field: a reference selected between the two kernel arguments put them in scratch)
+__device__ inline BkSeg bk_seg(const BkSeg& s0, const BkSeg& s1, uint32_t& blk)
 {
-    if (blk < s0.tiles)
-        return s0;
-    blk -= s0.tiles;
-    return s1;
+    const bool a = blk < s0.tiles;
+    if (!a)
+        blk -= s0.tiles;
+    BkSeg s;
+    s.keys = a ? s0.keys : s1.keys;
+    s.n = a ? s0.n : s1.n;
+    s.dn = a ? s0.dn : s1.dn;
+    s.counts = a ? s0.counts : s1.counts;
+    s.first = a ? s0.first : s1.first;
+    s.out = a ? s0.out : s1.out;
+    s.tiles = a ? s0.tiles : s1.tiles;
+    return s;
 }
 
 __global__ void __launch_bounds__(kBkThreads) bksort_count(BkSeg s0, BkSeg s1)
 {
     __shared__ uint32_t part[kBkThreads / 64][kMaxBuckets];
     uint32_t blk = blockIdx.x;
-    const BkSeg& s = bk_seg(s0, s1, blk);
+    const BkSeg s = bk_seg(s0, s1, blk);
     const uint32_t n = s.dn ? min(*s.dn, s.n) : s.n;
     const uint32_t base = blk * kBkTile, lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     uint32_t c[kMaxBuckets] = {};
@@ -267,7 +276,7 @@ __global__ void __launch_bounds__(kBkThreads) bksort_scatter(BkSeg s0, BkSeg s1)
     __shared__ uint32_t wcnt[kBkThreads / 64][kMaxBuckets];
     __shared__ uint32_t run[kMaxBuckets];
     uint32_t blk = blockIdx.x;
-    const BkSeg& s = bk_seg(s0, s1, blk);
+    const BkSeg s = bk_seg(s0, s1, blk);
     const uint32_t n = s.dn ? min(*s.dn, s.n) : s.n;
     const uint32_t base = blk * kBkTile, lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     if (threadIdx.x < (uint32_t)kMaxBuckets)
