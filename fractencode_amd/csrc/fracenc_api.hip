@@ -1387,7 +1387,7 @@ inline int launch_dft(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool i
         in.fb_count = c->d_fb_count.ptr;
         in.fbc = 0; // the Fourier path never runs with all_fallback
     }
-    in.dblocks = (c->ntiles * 32 + 255) / 256;
+    in.dblocks = (c->ntiles * 64 + 255) / 256; // two lanes per tile row (dft_domain_build_pair_at)
     in.plan = c->qplan;
     in.copies = c->dft_copies;
     const unsigned pg = in.dblocks + (nbk * 32 + 255) / 256;

@@ -366,6 +366,142 @@ __device__ __forceinline__ void dft_domain_build_at(uint32_t tid, const MfmaDoma
     }
 }
 
+// dft_domain_build_at restated with two lanes per tile row (dft_prep, round 4): lane h of a row loads
+// the plane rows of D4 rows 4h … 4h + 3, writes that half of the pool row, and puts it in LDS; each lane
+// then reads the cells of orbits 8h … 8h + 7 back (LDS addresses from the orbit table, no register
+// indexing) and builds that lane half of the fragments and of the tile-order copy.  Σb², ΣD4² and the
+// guard terms meet in a lane-pair shuffle.  On a small frame the single-thread chain per row ran one
+// wave per CU on a quarter of the CUs (C2: 16 workgroups); this halves the chain and doubles the waves.
+// A tile's 32 rows are one wave's 64 lanes, so the tile guards stay a wave reduction.
+constexpr uint32_t kDbRowWords = 33; // LDS words per row: 32 + 1 of padding (rows in distinct banks)
+template <bool F5>
+__device__ __forceinline__ void dft_domain_build_pair_at(uint32_t tid2, const MfmaDomainPrepArgs& a,
+                                                         const DftDomainBuildArgs& s, uint2* __restrict__ tguard,
+                                                         int32_t* __restrict__ trmax)
+{
+    constexpr int KS = F5 ? 5 : 4;
+    __shared__ uint32_t rows[128 * kDbRowWords]; // 256 threads = 128 rows
+    const uint32_t gid = tid2 >> 1, hh = tid2 & 1u;
+    if (gid >= a.ntiles * 32u) // whole tiles (whole waves) leave together
+        return;
+    const uint32_t tile = gid >> 5, row = gid & 31u;
+    uint32_t* lrow = rows + ((threadIdx.x >> 1) & 127u) * kDbRowWords;
+    const int p = a.tile_pos[gid];
+    uint32_t w[16]; // words 16hh … 16hh + 15 of the row: D4 rows 4hh … 4hh + 3, two cells per word
+    int sq = 0;
+    if (p >= 0) {
+        const frac_grid_item d = s.doms[s.porig[p]];
+        const uint8_t* base = s.src + (size_t)(d.y + 8 * hh) * s.sstride + d.x;
+        if ((((uintptr_t)base | s.sstride) & 7u) == 0) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const uint2* r0 = reinterpret_cast<const uint2*>(base + (size_t)(2 * i) * s.sstride);
+                const uint2* r1 = reinterpret_cast<const uint2*>(base + (size_t)(2 * i + 1) * s.sstride);
+                const uint2 a0 = r0[0], a1 = r0[1], b0 = r1[0], b1 = r1[1];
+                w[4 * i + 0] = pair_sums(a0.x, b0.x);
+                w[4 * i + 1] = pair_sums(a0.y, b0.y);
+                w[4 * i + 2] = pair_sums(a1.x, b1.x);
+                w[4 * i + 3] = pair_sums(a1.y, b1.y);
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                const uint8_t* q = base + (size_t)(2 * (k / 4)) * s.sstride + 4 * (k % 4);
+                const uint32_t w0 = q[0] | (q[1] << 8) | (q[2] << 16) | ((uint32_t)q[3] << 24);
+                const uint8_t* q1 = q + s.sstride;
+                const uint32_t w1 = q1[0] | (q1[1] << 8) | (q1[2] << 16) | ((uint32_t)q1[3] << 24);
+                w[k] = pair_sums(w0, w1);
+            }
+        }
+        uint4* pw = reinterpret_cast<uint4*>(s.pool + (size_t)p * 32 + 16 * hh);
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            pw[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const int lo = (int)(w[k] & 0xffffu), hi = (int)(w[k] >> 16);
+            sq += lo * lo + hi * hi;
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+            w[k] = 0x02000200u; // padding: b = 0
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+        lrow[16 * hh + k] = w[k];
+    sq += __shfl_xor(sq, 1, 64);
+    if (p >= 0 && hh == 0)
+        s.negsd2[p] = -sq;
+    // the pair's LDS writes above are one wave's and precede its reads below in program order
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const uint16_t* cells = reinterpret_cast<const uint16_t*>(lrow);
+    // orbits 8hh … 8hh + 7: their four cells each (the table's entries, selected by the lane half)
+    int cv[8][4];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            cv[j][k] = cells[hh ? kOrb8.p[8 + j][k] : kOrb8.p[j][k]];
+    if (p >= 0) {
+        // the tile-order copy for resolve_dft, orbit o as (D_{o,0} | D_{o,1} << 16), (D_{o,2} | D_{o,3} << 16)
+        uint4* tw = reinterpret_cast<uint4*>(s.tpool + (size_t)gid * 32 + 16 * hh);
+#pragma unroll
+        for (int v = 0; v < 4; ++v)
+            tw[v] = make_uint4((uint32_t)cv[2 * v][0] | ((uint32_t)cv[2 * v][1] << 16),
+                               (uint32_t)cv[2 * v][2] | ((uint32_t)cv[2 * v][3] << 16),
+                               (uint32_t)cv[2 * v + 1][0] | ((uint32_t)cv[2 * v + 1][1] << 16),
+                               (uint32_t)cv[2 * v + 1][2] | ((uint32_t)cv[2 * v + 1][3] << 16));
+    }
+    int sb2 = 0, dinf = 0;
+    _Float16 comp[KS][8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int b0 = cv[j][0] - 512, b1 = cv[j][1] - 512, b2 = cv[j][2] - 512, b3 = cv[j][3] - 512;
+        sb2 += b0 * b0 + b1 * b1 + b2 * b2 + b3 * b3;
+        const int sb = b0 + b2, ub = b1 + b3, gb = b0 - b2, db = b1 - b3;
+        dinf = F5 ? max(dinf, max(abs(sb + ub), abs(sb - ub))) : max(dinf, max(abs(sb), abs(ub)));
+        if constexpr (F5) {
+            comp[0][j] = (_Float16)(sb + ub);
+            comp[1][j] = (_Float16)(sb - ub);
+            comp[2][j] = (_Float16)gb;
+            comp[3][j] = (_Float16)(gb - db);
+            comp[4][j] = (_Float16)(-db - gb);
+        } else {
+            comp[0][j] = (_Float16)sb;
+            comp[1][j] = (_Float16)ub;
+            comp[2][j] = (_Float16)gb;
+            comp[3][j] = (_Float16)db;
+        }
+    }
+#pragma unroll
+    for (int st = 0; st < KS; ++st)
+        a.dtiles[((size_t)tile * KS + st) * 64 + row + 32 * hh] = __builtin_bit_cast(uint4, comp[st]);
+    sb2 += __shfl_xor(sb2, 1, 64);
+    dinf = max(dinf, __shfl_xor(dinf, 1, 64));
+    if (hh == 0) {
+        const float ny = p >= 0 ? (F5 ? -0.5f * (float)sb2 : -(float)sb2) : kDftPadY;
+        const uint32_t h = (row >> 2) & 1u, i = (row & 3u) + 4u * (row >> 3);
+        a.dconst[(size_t)tile * (kDftCS * 4) + h * 16 + i] = __float_as_uint(ny);
+    }
+    uint32_t gx = p >= 0 ? (uint32_t)((F5 ? 2 : 4) * dinf) : 0u, gy = p >= 0 ? (uint32_t)sb2 : 0u;
+    // the tile's guard terms over its 32 rows (lanes 2·row + hh of one wave): a wave maximum
+#pragma unroll
+    for (int o = 32; o > 1; o >>= 1) {
+        gx = max(gx, (uint32_t)__shfl_xor((int)gx, o, 64));
+        gy = max(gy, (uint32_t)__shfl_xor((int)gy, o, 64));
+    }
+    if (row == 0 && hh == 0) {
+        tguard[tile] = make_uint2(gx, gy);
+        if (F5 && trmax)
+            trmax[tile] = (int64_t)gy > kFast6Limit ? -1
+                          : gx == 0                  ? INT32_MAX
+                                                     : (int32_t)min<int64_t>((kFast6Limit - gy) / gx, INT32_MAX);
+    }
+}
+
 template <bool BYPOS = false, bool F5 = false>
 __global__ void __launch_bounds__(256) dft_domain_build(MfmaDomainPrepArgs a, DftDomainBuildArgs s,
                                                         uint2* __restrict__ tguard, int32_t* __restrict__ trmax = nullptr)
@@ -534,7 +670,7 @@ __global__ void __launch_bounds__(256) dft_prep(MfmaDomainPrepArgs d, DftDomainB
     if (gt == 0 && in.fb_count)
         *in.fb_count = in.fbc;
     if (blockIdx.x < in.dblocks)
-        dft_domain_build_at<false, FORM != 4>(gt, d, s, tguard, trmax);
+        dft_domain_build_pair_at<FORM != 4>(gt, d, s, tguard, trmax); // two lanes per tile row
     else
         dft_range_prep_at<FORM>((blockIdx.x - in.dblocks) * blockDim.x + threadIdx.x, r, rguard);
 }
