@@ -264,10 +264,6 @@ struct frac_ctx {
     // the count after the last), their bucket bounds, and the first level's range grid
     DBuf<DevPlan> d_qt_plan;
     QtFrameSum* h_qt_sum = nullptr; // pinned, mapped: qt_finish writes the frame's counts there
-    // the quadtree's leaf copies into the caller's pinned buffer (qt_copy_leaves): a second stream, so a
-    // level's leaves cross PCIe while the next level computes; an event per hand-off each way
-    hipStream_t qt_leaf_stream = nullptr;
-    hipEvent_t qt_leaf_ev[2] = {nullptr, nullptr};
     DBuf<uint32_t> d_qt_first;
     DBuf<frac_grid_item> d_qt_r0;
     uint32_t qt_r0_key[3] = {0, 0, 0};
@@ -2347,11 +2343,6 @@ int qt_encode_dev(frac_ctx* c, const frac_quadtree_params* qp, LevelGrid& level,
             leaves = reinterpret_cast<frac_encode_item*>(dp);
             leaf_cap = (uint32_t)std::min<size_t>(cap, 0xffffffffu);
             direct = true;
-            if (!c->qt_leaf_stream)
-                FRAC_HIP(c, hipStreamCreateWithFlags(&c->qt_leaf_stream, hipStreamNonBlocking));
-            for (auto& ev : c->qt_leaf_ev)
-                if (!ev)
-                    FRAC_HIP(c, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
         }
         (void)hipGetLastError(); // pageable memory is not an error
     }
@@ -2516,11 +2507,9 @@ int qt_encode_dev(frac_ctx* c, const frac_quadtree_params* qp, LevelGrid& level,
         sa.can_split = n > qp->min_size ? 1 : 0;
         sa.split = qp->split_distance;
         sa.tcount = c->d_qt_flags.ptr;
-        // into the caller's pinned buffer: a level that splits emits its leaves into device memory, and
-        // qt_copy_leaves on the leaf stream moves them across PCIe while the next level runs; the last
-        // level writes its own straight across (nothing left to overlap)
-        const bool via_dev = direct && sa.can_split;
-        sa.leaves = via_dev ? c->d_qt_leaves.ptr : leaves;
+        // (a second stream copying a level's leaves across PCIe while the next level ran measured slower: the
+        // copy kernel's PCIe writes stalled the next level's bucket keys 11 → 71 µs)
+        sa.leaves = leaves;
         sa.leaf_cap = leaf_cap;
         sa.next_ranges = c->d_qt_next.ptr;
         sa.aux = c->d_aux.ptr;
@@ -2535,12 +2524,6 @@ int qt_encode_dev(frac_ctx* c, const frac_quadtree_params* qp, LevelGrid& level,
         qt_split_count<<<ntl, kBkThreads, 0, c->stream>>>(sa);
         qt_split_scan<<<1, 64, 0, c->stream>>>(sa, ntl);
         qt_split_emit<<<ntl, kBkThreads, 0, c->stream>>>(sa);
-        if (via_dev) {
-            FRAC_HIP(c, hipEventRecord(c->qt_leaf_ev[0], c->stream));
-            FRAC_HIP(c, hipStreamWaitEvent(c->qt_leaf_stream, c->qt_leaf_ev[0], 0));
-            qt_copy_leaves<<<128, 256, 0, c->qt_leaf_stream>>>(plan, reinterpret_cast<const uint4*>(c->d_qt_leaves.ptr),
-                                                               reinterpret_cast<uint4*>(leaves), leaf_cap);
-        }
         std::swap(c->d_ranges, c->d_qt_next);
         // the next level: at most four quadrants per range, at most the full grid of its size (counted in
         // closed form: frac_uniform_grid's count loop took 0.2 ms of host time for the 2×2 grid at 2048²)
@@ -2557,10 +2540,6 @@ int qt_encode_dev(frac_ctx* c, const frac_quadtree_params* qp, LevelGrid& level,
     c->ran = false;
     // the frame's one round trip: qt_finish writes the leaf count and the summed counters into pinned
     // memory (the leaves are already in the caller's buffer when it is pinned)
-    if (direct) { // the frame's count is read once every leaf copy has landed
-        FRAC_HIP(c, hipEventRecord(c->qt_leaf_ev[1], c->qt_leaf_stream));
-        FRAC_HIP(c, hipStreamWaitEvent(c->stream, c->qt_leaf_ev[1], 0));
-    }
     void* dsum = nullptr;
     FRAC_HIP(c, hipHostGetDevicePointer(&dsum, c->h_qt_sum, 0));
     qt_finish<<<1, 64, 0, c->stream>>>(c->d_qt_plan.ptr + lvi, lvi ? 1 : 0, c->d_qt_stats.ptr, kQtShards, kQtCounters,
@@ -2772,11 +2751,6 @@ void frac_destroy(frac_ctx* c)
         (void)hipHostFree(c->h_dec_sum);
     if (c->h_qt_sum)
         (void)hipHostFree(c->h_qt_sum);
-    for (auto& ev : c->qt_leaf_ev)
-        if (ev)
-            (void)hipEventDestroy(ev);
-    if (c->qt_leaf_stream)
-        (void)hipStreamDestroy(c->qt_leaf_stream);
     for (auto& ev : c->ev)
         if (ev)
             (void)hipEventDestroy(ev);

@@ -692,21 +692,6 @@ __global__ void __launch_bounds__(kBkThreads) qt_split_emit(QtSplitArgs a)
     }
 }
 
-// A level's leaves [plan->leaf_base, next->leaf_base) from device memory into the caller's pinned buffer
-// (its device-mapped address), clipped to the caller's capacity: run on the context's leaf stream, so the
-// PCIe writes overlap the next level's kernels (qt_split_emit writing them across itself stalled on PCIe).
-__global__ void __launch_bounds__(256) qt_copy_leaves(const DevPlan* plan, const uint4* __restrict__ src,
-                                                      uint4* __restrict__ dst, uint32_t leaf_cap)
-{
-    const uint32_t lb = plan[0].leaf_base, le = min(plan[1].leaf_base, leaf_cap);
-    if (le <= lb)
-        return;
-    constexpr uint32_t kWords = sizeof(frac_encode_item) / sizeof(uint4);
-    const size_t n = (size_t)(le - lb) * kWords, off = (size_t)lb * kWords;
-    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
-        dst[off + i] = src[off + i];
-}
-
 // The per-item maps of a planned level (fill_range_slots, fill_tile_pos and fill_rbucket restated, run
 // by qt_plan's threads), and the run's resets: best_key (none yet), the direct form's zeroed rconst
 // words (mfma_range_prep accumulates into them), the fallback count.

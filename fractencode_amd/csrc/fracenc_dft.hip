@@ -1434,28 +1434,16 @@ __device__ inline DftResolved resolve_dft_eval(const MfmaResolveArgs& a, uint32_
                 }
                 continue;
             }
-            // the chunk's rows — pool positions (for the key) and D4 from the tile-order copy — loaded
-            // together up front: one round trip for the chunk instead of one per tile (ΣD4² is summed
-            // here rather than loaded through the position)
-            int pch[kTilesPerStage];
-            uint4 dch[kTilesPerStage][2];
-#pragma unroll
-            for (uint32_t q = 0; q < kTilesPerStage; ++q) {
-                const uint32_t tile = min(en.y + q, a.ntiles - 1u);
-                pch[q] = a.tile_pos[tile * 32 + row];
-                const uint4* dp = reinterpret_cast<const uint4*>(a.tpool + ((size_t)tile * 32 + row) * 32 + g * (PG / 2));
-                dch[q][0] = dp[0];
-                dch[q][1] = dp[1];
-            }
-#pragma unroll
-            for (uint32_t q = 0; q < kTilesPerStage; ++q) {
-                const uint32_t tile = en.y + q;
-                if (tile >= a.ntiles)
-                    break;
-                if (!((tmask >> q) & 1u))
+            for (uint32_t tile = en.y; tile < min(en.y + (uint32_t)kTilesPerStage, a.ntiles); ++tile) {
+                if (!((tmask >> (tile - en.y)) & 1u))
                     continue;
-                const int p = pch[q];
-                const uint4 d0 = dch[q][0], d1 = dch[q][1];
+                // the row's pool position (for the key) and its D4 from the tile-order copy are
+                // independent loads; ΣD4² is summed here rather than loaded through the position.
+                // (Loading the chunk's four tiles up front saved 1 µs at C2 but took 24 more VGPRs:
+                // 4 instead of 6 waves per SIMD cost the C4 quadtree's 65k-range level 21 µs.)
+                const int p = a.tile_pos[tile * 32 + row];
+                const uint4* dp = reinterpret_cast<const uint4*>(a.tpool + ((size_t)tile * 32 + row) * 32 + g * (PG / 2));
+                const uint4 d0 = dp[0], d1 = dp[1];
                 const uint32_t dv[PG / 2] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w};
                 uint32_t dr[PG / 2]; // t = 1 pairs
 #pragma unroll
