@@ -3,7 +3,7 @@
 tree is untouched): each SUB is FILE:OLD=>NEW, an exact one-time replacement in csrc/FILE.  The
 library goes to OUT (use it with FRAC_LIB=OUT in tools/bench_paths.py; bench.py refuses a foreign
 library for its headline).
-usage: tools/build_variant.py OUT.so 'fracenc_api.hip:old text=>new text' [...]"""
+usage: tools/build_variant.py [--git REV] OUT.so 'fracenc_api.hip:old text=>new text' [...]"""
 import os
 import shutil
 import subprocess
@@ -14,12 +14,22 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import __graft_entry__ as G  # noqa: E402
 
-out = os.path.abspath(sys.argv[1])
+args = sys.argv[1:]
+rev = None
+if args and args[0] == "--git":  # the sources of a committed revision instead of the working tree
+    rev, args = args[1], args[2:]
+out = os.path.abspath(args[0])
 with tempfile.TemporaryDirectory() as d:
     pkg = os.path.join(d, "fractencode_amd")
     shutil.copytree(G.CSRC, os.path.join(pkg, "csrc"))
     shutil.copytree(os.path.join(ROOT, "include"), os.path.join(d, "include"))
-    for sub in sys.argv[2:]:
+    if rev:
+        for sub_dir, dst in (("fractencode_amd/csrc", os.path.join(pkg, "csrc")), ("include", os.path.join(d, "include"))):
+            names = subprocess.check_output(["git", "ls-tree", "--name-only", rev, sub_dir + "/"], cwd=ROOT, text=True).split()
+            for name in names:
+                data = subprocess.check_output(["git", "show", f"{rev}:{name}"], cwd=ROOT)
+                open(os.path.join(dst, os.path.basename(name)), "wb").write(data)
+    for sub in args[1:]:
         fname, rest = sub.split(":", 1)
         old, new = rest.split("=>", 1)
         path = os.path.join(pkg, "csrc", fname)
