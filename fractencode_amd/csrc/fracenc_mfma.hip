@@ -431,60 +431,6 @@ __device__ inline void compute_stage(const uint4* __restrict__ la, uint32_t nt, 
     constexpr int KS = MfmaGeom<N>::KS;
     const uint4* lc = la + nt * KS * 64u;
     const uint32_t h = lane >> 5;
-    if constexpr ((VAR & 256) != 0) {
-        // the float-C epilogue (n ≤ 4), the stage's tiles unrolled with the next tile's A fragments and row
-        // constants read before this tile's epilogue: their LDS latency overlaps the epilogue instead of
-        // stalling the next MFMAs (the rolled loop waited lgkmcnt(0) before every tile's MFMAs)
-        static_assert(N <= 4, "the float-C epilogue is exact for n <= 4 only");
-        static_assert(T == 1 || (T % 2 == 0 && T >= 4), "T = 1, 4 or 8");
-        auto load = [&](uint32_t q, half8_t (&af)[KS], floatx16_t& c) {
-#pragma unroll
-            for (int s = 0; s < KS; ++s)
-                af[s] = __builtin_bit_cast(half8_t, la[(q * KS + s) * 64 + lane]);
-#pragma unroll
-            for (int c4 = 0; c4 < 4; ++c4) {
-                const uint4 v = lc[q * 8 + h * 4 + c4];
-                c[4 * c4 + 0] = __uint_as_float(v.x);
-                c[4 * c4 + 1] = __uint_as_float(v.y);
-                c[4 * c4 + 2] = __uint_as_float(v.z);
-                c[4 * c4 + 3] = __uint_as_float(v.w);
-            }
-        };
-        // A fragments double-buffered; the row constants single: the next tile's are read once this tile's
-        // MFMAs have taken theirs as C (16 VGPRs fewer: the kernel stays at 4 waves per SIMD)
-        half8_t af[2][KS];
-        floatx16_t c;
-        load(0, af[0], c);
-#pragma unroll
-        for (uint32_t q = 0; q < (uint32_t)kTilesPerStage; ++q) {
-            if (q >= nt)
-                break;
-            const int b = q & 1;
-            floatx16_t acc[T];
-#pragma unroll
-            for (int t = 0; t < T; ++t)
-                acc[t] = mfma_tile<N, T>(af[b], bf[t], c);
-            if (q + 1 < nt)
-                load(q + 1, af[b ^ 1], c);
-            float m = __builtin_inff();
-            if constexpr (T == 1) {
-#pragma unroll
-                for (int i = 0; i < 16; i += 2)
-                    m = __builtin_fminf(__builtin_fminf(m, acc[0][i]), acc[0][i + 1]);
-            } else {
-#pragma unroll
-                for (int i = 0; i < 16; ++i) {
-                    float r = __builtin_fminf(__builtin_fminf(acc[0][i], acc[1][i]), acc[2][i]);
-#pragma unroll
-                    for (int t = 3; t + 1 < T; t += 2)
-                        r = __builtin_fminf(__builtin_fminf(r, acc[t][i]), acc[t + 1][i]);
-                    m = __builtin_fminf(__builtin_fminf(m, r), acc[T - 1][i]);
-                }
-            }
-            cm[0] = min(cm[0], fmap(m));
-        }
-        return;
-    }
     for (uint32_t q = 0; q < nt; ++q) {
         half8_t af[KS];
 #pragma unroll
@@ -502,6 +448,36 @@ __device__ inline void compute_stage(const uint4* __restrict__ la, uint32_t nt, 
             }
         };
         constexpr bool PRIO = (VAR & 32) != 0, LATE_E = (VAR & 64) != 0;
+        if constexpr ((VAR & 256) != 0) {
+            static_assert(N <= 4, "the float-C epilogue is exact for n <= 4 only");
+            read_e();
+            floatx16_t c;
+#pragma unroll
+            for (int i = 0; i < 16; ++i)
+                c[i] = __uint_as_float(e[i]);
+            floatx16_t acc[T];
+#pragma unroll
+            for (int t = 0; t < T; ++t)
+                acc[t] = mfma_tile<N, T>(af, bf[t], c);
+            float m = __builtin_inff();
+            if constexpr (T == 1) {
+#pragma unroll
+                for (int i = 0; i < 16; i += 2)
+                    m = __builtin_fminf(__builtin_fminf(m, acc[0][i]), acc[0][i + 1]);
+            } else {
+                static_assert(T % 2 == 0 && T >= 4, "T = 4 or 8: three, then pairs, then the last with the running min");
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    float r = __builtin_fminf(__builtin_fminf(acc[0][i], acc[1][i]), acc[2][i]);
+#pragma unroll
+                    for (int t = 3; t + 1 < T; t += 2)
+                        r = __builtin_fminf(__builtin_fminf(r, acc[t][i]), acc[t + 1][i]);
+                    m = __builtin_fminf(__builtin_fminf(m, r), acc[T - 1][i]);
+                }
+            }
+            cm[0] = min(cm[0], fmap(m));
+            continue;
+        }
         if constexpr (LATE_E) {
             // the first transform's MFMAs wait only for the A fragments; the epilogue
             // constants are read while they run
@@ -584,7 +560,7 @@ __device__ inline void compute_stage(const uint4* __restrict__ la, uint32_t nt, 
 //   128: the minimum over the transforms on the accumulator bits first (entries merged over
 //      t; resolve_mfma with MfmaResolveArgs::merged evaluates every transform of a match)
 template <int N, int T, bool HITS, int VAR>
-__global__ void __launch_bounds__(256, ((VAR & 256) != 0 && T <= 4) ? 4 : 1) search_mfma(MfmaSearchArgs a)
+__global__ void __launch_bounds__(256) search_mfma(MfmaSearchArgs a)
 {
     static_assert(kTuningBuild || (VAR & (8 | 16)) == 0, "search_mfma ablations exist only in FRAC_TUNING builds");
     if (past_plan(a))
@@ -746,66 +722,38 @@ __global__ void __launch_bounds__(256, 2) search_mfma16(MfmaSearchArgs a)
         btile[j] = 0;
     }
     const uint32_t h = lane >> 5;
-    // one tile's MFMAs into acc (its A fragments read from LDS as they are consumed)
-    auto tile_mfma = [&](const uint4* la, uint32_t q, floatx16_t (&acc)[TPW]) {
-#pragma unroll
-        for (int j = 0; j < TPW; ++j)
-            acc[j] = zero;
-#pragma unroll
-        for (int s = 0; s < KS; ++s) {
-            const half8_t af = __builtin_bit_cast(half8_t, la[(q * KS + s) * 64 + lane]);
-#pragma unroll
-            for (int j = 0; j < TPW; ++j)
-                acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af, bf[j][s], acc[j], 0, 0, 0);
-        }
-    };
-    // one tile's epilogue: v = (int(acc) << 3) + e per row, folded into cm
-    auto tile_epi = [&](const uint4* lc, uint32_t q, const floatx16_t (&acc)[TPW], uint32_t (&cm)[TPW]) {
-        uint32_t e[16];
-#pragma unroll
-        for (int c4 = 0; c4 < 4; ++c4) {
-            const uint4 v = lc[q * 8 + h * 4 + c4];
-            e[4 * c4 + 0] = v.x;
-            e[4 * c4 + 1] = v.y;
-            e[4 * c4 + 2] = v.z;
-            e[4 * c4 + 3] = v.w;
-        }
-#pragma unroll
-        for (int j = 0; j < TPW; ++j)
-#pragma unroll
-            for (int i = 0; i < 16; ++i) // acc: exact integer, |acc| < 2^24
-                cm[j] = min(cm[j], ((uint32_t)(int32_t)acc[j][i] << 3) + e[i]);
-    };
-    // a stage's two tiles software-pipelined: the second tile's MFMAs are issued in one scheduling region
-    // with the first tile's epilogue, so its VALU fills the MFMA gaps of this wave (the accumulators of two
-    // tiles: 32 more VGPRs, still two waves per SIMD)
     auto compute = [&](const uint4* la, uint32_t nt, uint32_t tb) {
         const uint4* lc = la + nt * KS * 64u;
         uint32_t cm[TPW];
 #pragma unroll
         for (int j = 0; j < TPW; ++j)
             cm[j] = 0xffffffffu;
-        floatx16_t a0[TPW];
-        tile_mfma(la, 0, a0);
-        if (nt > 1) {
-            floatx16_t a1[TPW];
-            tile_mfma(la, 1, a1);
-            tile_epi(lc, 0, a0, cm);
-            // the interleave (the compiler otherwise issues the 32 MFMAs as one block, then the epilogue):
-            // per K-step one A-fragment read, its TPW MFMAs, and a share of the first tile's epilogue VALU
-            // (A-fragment reads run four K-steps ahead of their MFMAs)
-            __builtin_amdgcn_sched_group_barrier(0x100, 8, 0); // the epilogue's row-constant reads, A 0..3
+        for (uint32_t q = 0; q < nt; ++q) {
+            floatx16_t acc[TPW];
 #pragma unroll
-            for (int k = 0; k < KS; ++k) {
-                __builtin_amdgcn_sched_group_barrier(0x008, TPW, 0);     // MFMA
-                __builtin_amdgcn_sched_group_barrier(0x002, 3 * TPW, 0); // VALU
-                if (k + 4 < KS)
-                    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0); // DS read of A k + 4
+            for (int j = 0; j < TPW; ++j)
+                acc[j] = zero;
+#pragma unroll
+            for (int s = 0; s < KS; ++s) {
+                const half8_t af = __builtin_bit_cast(half8_t, la[(q * KS + s) * 64 + lane]);
+#pragma unroll
+                for (int j = 0; j < TPW; ++j)
+                    acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af, bf[j][s], acc[j], 0, 0, 0);
             }
-            __builtin_amdgcn_sched_barrier(0);
-            tile_epi(lc, 1, a1, cm);
-        } else {
-            tile_epi(lc, 0, a0, cm);
+            uint32_t e[16];
+#pragma unroll
+            for (int c4 = 0; c4 < 4; ++c4) {
+                const uint4 v = lc[q * 8 + h * 4 + c4];
+                e[4 * c4 + 0] = v.x;
+                e[4 * c4 + 1] = v.y;
+                e[4 * c4 + 2] = v.z;
+                e[4 * c4 + 3] = v.w;
+            }
+#pragma unroll
+            for (int j = 0; j < TPW; ++j)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) // acc: exact integer, |acc| < 2^24
+                    cm[j] = min(cm[j], ((uint32_t)(int32_t)acc[j][i] << 3) + e[i]);
         }
 #pragma unroll
         for (int j = 0; j < TPW; ++j) {
