@@ -1084,7 +1084,9 @@ __global__ void __launch_bounds__(256) resolve_mfma(MfmaResolveArgs a)
 // The first tile holding a match ends the walk (later tiles hold later pool positions).  With
 // fused_fit the record is written here (fit_sums_range), from the winning lane's sums.
 template <int N>
-__global__ void __launch_bounds__(256) resolve_small(MfmaResolveArgs a)
+// 6 waves per SIMD (80 VGPRs, 2 spilled): the kernel is latency-bound, and 4 → 5 → 6 waves took the C4
+// quadtree's level 4 from 128 to 110 to 100 µs (tools/gpu_r04_s16.sh)
+__global__ void __launch_bounds__(256, 6) resolve_small(MfmaResolveArgs a)
 {
     static_assert(N == 2 || N == 4, "one pool row per lane");
     constexpr int NN = N * N, K2 = NN / 2;
