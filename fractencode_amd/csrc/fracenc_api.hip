@@ -1386,7 +1386,7 @@ inline int launch_dft(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool i
     in.dblocks = (c->ntiles * 64 + 255) / 256; // two lanes per tile row (dft_domain_build_pair_at)
     in.plan = c->qplan;
     in.copies = c->dft_copies;
-    const unsigned pg = in.dblocks + (nbk * 32 + 255) / 256;
+    const unsigned pg = in.dblocks + (nbk * 64 + 255) / 256; // two lanes per range slot (dft_range_prep_pair_at)
     if (pg || inits) {
         int32_t* trmax = f5 ? c->d_dft_trmax.ptr : nullptr;
         const dim3 grid(std::max(pg, 1u));

@@ -631,6 +631,124 @@ __device__ __forceinline__ void dft_range_prep_at(uint32_t gid, const MfmaRangeP
         rguard[b] = g1;
 }
 
+// dft_range_prep_at restated with two lanes per range slot (dft_prep, round 4), as the domain build: lane h
+// loads rows 4h … 4h + 3 of the range into LDS; each lane then reads the pixels of orbits 8h … 8h + 7 back
+// (T = 8's flipped copies read through the Flip permutation: the same table, another address) and builds that
+// lane half of the fragments and of the orbit-ordered pixel pairs.  Σa² and R6 meet in a lane-pair shuffle;
+// a block's 32 slots are one wave, so its guard stays a wave maximum.
+template <int FORM>
+__device__ __forceinline__ void dft_range_prep_pair_at(uint32_t gid2, const MfmaRangePrepArgs& a,
+                                                       uint32_t* __restrict__ rguard)
+{
+    constexpr int N = 8, NBF = FORM == 6 ? 6 : FORM == 5 ? 5 : kDftRangeFrags;
+    constexpr uint32_t kRow = 68; // LDS bytes per slot: 64 + 4 of padding
+    __shared__ uint8_t px[128 * kRow];
+    const uint32_t gid = gid2 >> 1, hh = gid2 & 1u;
+    if (gid >= a.nblocks * 32u) // whole blocks (whole waves) leave together
+        return;
+    const uint32_t b = gid >> 5, col = gid & 31u;
+    uint8_t* lp = px + ((threadIdx.x >> 1) & 127u) * kRow;
+    const int ri = a.slot_range[gid];
+    uint2 w[4] = {make_uint2(0x80808080u, 0x80808080u), make_uint2(0x80808080u, 0x80808080u),
+                  make_uint2(0x80808080u, 0x80808080u), make_uint2(0x80808080u, 0x80808080u)}; // empty: a = 0
+    if (ri >= 0) {
+        const frac_grid_item rg = a.ranges[ri];
+        const uint8_t* base = a.tgt + (size_t)(rg.y + 4 * hh) * a.tstride + rg.x;
+        if ((((uintptr_t)base | a.tstride) & 7u) == 0) {
+#pragma unroll
+            for (int y = 0; y < 4; ++y)
+                w[y] = *reinterpret_cast<const uint2*>(base + (size_t)y * a.tstride);
+        } else {
+#pragma unroll
+            for (int y = 0; y < 4; ++y) {
+                const uint8_t* q = base + (size_t)y * a.tstride;
+                w[y] = make_uint2(q[0] | (q[1] << 8) | (q[2] << 16) | ((uint32_t)q[3] << 24),
+                                  q[4] | (q[5] << 8) | (q[6] << 16) | ((uint32_t)q[7] << 24));
+            }
+        }
+    }
+    uint32_t* lw = reinterpret_cast<uint32_t*>(lp);
+#pragma unroll
+    for (int y = 0; y < 4; ++y) {
+        lw[8 * hh + 2 * y] = w[y].x;
+        lw[8 * hh + 2 * y + 1] = w[y].y;
+    }
+    // the pair's LDS writes above are one wave's and precede its reads below in program order
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // T = 8: the block's flipped copy, a'(q) = a(Flip q) (dft_range_prep_at)
+    const bool flip = ri >= 0 && b >= a.flip_from;
+    int av[8][4]; // orbits 8hh … 8hh + 7, their four pixels − 128
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int q0 = kOrb8.p[j][k], q1 = kOrb8.p[8 + j][k];
+            const int q = hh ? q1 : q0, qf = hh ? fwd_index<N>(4, q1) : fwd_index<N>(4, q0);
+            av[j][k] = (int)lp[flip ? qf : q] - 128;
+        }
+    int sa2 = 0, r1 = 0;
+    _Float16 comp[NBF][8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int a0 = av[j][0], a1 = av[j][1], a2 = av[j][2], a3 = av[j][3];
+        sa2 += a0 * a0 + a1 * a1 + a2 * a2 + a3 * a3;
+        const int sa = a0 + a2, ua = a1 + a3, al = a0 - a2, be = a1 - a3;
+        r1 += FORM == 6 ? abs(sa + ua) + abs(sa - ua) : abs(sa) + abs(ua);
+        if constexpr (FORM == 5) {
+            comp[0][j] = (_Float16)(sa + ua);
+            comp[1][j] = (_Float16)(sa - ua);
+            comp[2][j] = (_Float16)(2 * (al + be));
+            comp[3][j] = (_Float16)(-2 * be);
+            comp[4][j] = (_Float16)(2 * al);
+        } else if constexpr (FORM == 6) {
+            comp[0][j] = (_Float16)(sa + ua);
+            comp[1][j] = (_Float16)(sa - ua);
+            comp[2][j] = (_Float16)(ua - sa);
+            comp[3][j] = (_Float16)(2 * (al + be));
+            comp[4][j] = (_Float16)(-2 * be);
+            comp[5][j] = (_Float16)(2 * al);
+        } else {
+            comp[0][j] = (_Float16)sa;
+            comp[1][j] = (_Float16)ua;
+            comp[2][j] = (_Float16)(4 * sa);
+            comp[3][j] = (_Float16)(4 * ua);
+            comp[4][j] = (_Float16)al;
+            comp[5][j] = (_Float16)be;
+            comp[6][j] = (_Float16)(-al);
+        }
+    }
+    if (ri < 0) { // an empty slot's fragments are zero (its pixels read as 128 above: already so), no guard
+        sa2 = 0;
+        r1 = 0;
+    }
+#pragma unroll
+    for (int f = 0; f < NBF; ++f)
+        a.rfrags[((size_t)b * NBF + f) * 64 + col + 32 * hh] = __builtin_bit_cast(uint4, comp[f]);
+    sa2 += __shfl_xor(sa2, 1, 64);
+    r1 += __shfl_xor(r1, 1, 64);
+    if (hh == 0)
+        a.rconst[gid] = ri >= 0 ? (uint32_t)(16 * sa2) : 0u; // 16Σa² ≤ 2^24
+    if (a.rorb) {
+        // raw pixels r = a + 128, orbit o as the pairs (r_{o,0} | r_{o,1} << 16), (r_{o,2} | r_{o,3} << 16)
+        uint4* ro = reinterpret_cast<uint4*>(a.rorb + (size_t)gid * 32 + 16 * hh);
+#pragma unroll
+        for (int v = 0; v < 4; ++v)
+            ro[v] = make_uint4((uint32_t)(av[2 * v][0] + 128) | ((uint32_t)(av[2 * v][1] + 128) << 16),
+                               (uint32_t)(av[2 * v][2] + 128) | ((uint32_t)(av[2 * v][3] + 128) << 16),
+                               (uint32_t)(av[2 * v + 1][0] + 128) | ((uint32_t)(av[2 * v + 1][1] + 128) << 16),
+                               (uint32_t)(av[2 * v + 1][2] + 128) | ((uint32_t)(av[2 * v + 1][3] + 128) << 16));
+    }
+    // the block's guard: a maximum over its 32 slots (lanes 2·col + hh of one wave), one writer
+    uint32_t g1 = (uint32_t)r1;
+#pragma unroll
+    for (int o = 32; o > 1; o >>= 1)
+        g1 = max(g1, (uint32_t)__shfl_xor((int)g1, o, 64));
+    if (col == 0 && hh == 0)
+        rguard[b] = g1;
+}
+
 template <int FORM = 4>
 __global__ void __launch_bounds__(256) dft_range_prep(MfmaRangePrepArgs a, uint32_t* __restrict__ rguard)
 {
@@ -671,8 +789,8 @@ __global__ void __launch_bounds__(256) dft_prep(MfmaDomainPrepArgs d, DftDomainB
         *in.fb_count = in.fbc;
     if (blockIdx.x < in.dblocks)
         dft_domain_build_pair_at<FORM != 4>(gt, d, s, tguard, trmax); // two lanes per tile row
-    else
-        dft_range_prep_at<FORM>((blockIdx.x - in.dblocks) * blockDim.x + threadIdx.x, r, rguard);
+    else // two lanes per range slot
+        dft_range_prep_pair_at<FORM>((blockIdx.x - in.dblocks) * blockDim.x + threadIdx.x, r, rguard);
 }
 
 // ---------------------------------------------------------------------------
