@@ -649,3 +649,33 @@ def test_rectangular_ranges_random_planes_match_oracle(oracle, engine):
         want, rej, _ = oracle.estimate(p, doms, rngs, T=T, thr=thr, use_classifier=cls)
         assert_same(out, {k: want[k] for k in FIELDS}, f"rect {rs} {ds} T={T}")
         assert st["rejected_mappings"] == rej
+
+
+@pytest.mark.parametrize("n,T", [(8, 4), (8, 8), (16, 4), (16, 8)])
+def test_fp32_regime_in_the_resolving_wave(n, T):
+    """Ranges whose best exact error is at least 2^24 (S16) take the reference's fp32 arithmetic
+    (image/metrics.h:37-50).  The MFMA engine's fused resolvers (resolve_small / resolve_dft / resolve_mfma)
+    evaluate them in the resolving wave (fallback_wave) and launch no fallback_fp32; the VALU engine lists
+    them for the fallback_fp32 kernel.  Isolated bright n×n blocks 4n apart on a black frame: every
+    domain is mostly dark (at most a quarter of its cells bright: S16 ≥ 48·1020² at n = 8), so each bright range
+    is in the fp32 regime.  Records, fallback counts and reject counts agree, and the fallback count is the
+    bright blocks'.  (n ≤ 4 never reaches the regime: 16 cells · 1020² < 2^24.)"""
+    S = 32 * n
+    p = np.zeros((S, S), np.uint8)
+    nb = 0
+    for y in range(n, S - n, 4 * n):
+        for x in range(n, S - n, 4 * n):
+            p[y:y + n, x:x + n] = 255
+            nb += 1
+    doms, rngs = F.create_uniform_grid(S, S, 2 * n, n), F.create_uniform_grid(S, S, n, n)
+    outs = {}
+    for eng in (F.ENGINE_VALU, F.ENGINE_MFMA):
+        with F.Engine(0, T, False, 0.0, -1.0, eng) as e:
+            e.set_frame(p)
+            e.set_domains(doms)
+            outs[eng] = e.search(rngs)
+    (a, sa), (b, sb) = outs[F.ENGINE_VALU], outs[F.ENGINE_MFMA]
+    assert sb["engine"] == F.ENGINE_MFMA
+    assert sa["fallback_ranges"] == sb["fallback_ranges"] == nb, (sa["fallback_ranges"], sb["fallback_ranges"], nb)
+    assert a.tobytes() == b.tobytes()
+    assert sa["rejected_mappings"] == sb["rejected_mappings"]
