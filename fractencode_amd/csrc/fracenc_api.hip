@@ -2139,8 +2139,8 @@ int launch_all(frac_ctx* c)
     const GenArgs g = gen_args(c, dtgt, tstride);
     if (P && c->virt) // the sampled form: one row per (domain, transform), fracenc_gen.hip
         gen_pool_build<<<(P + 255) / 256, 256, 0, c->stream>>>(g);
-    else if (P && !fused_pool) { // groups of min(n²/2, 64) lanes per pool position
-        const unsigned nblk = (unsigned)(((uint64_t)P * std::min(N * N / 2, 64) + 255) / 256);
+    else if (P && !fused_pool) { // pool_lanes<N>() lanes per pool position
+        const unsigned nblk = (unsigned)(((uint64_t)P * pool_lanes<N>() + 255) / 256);
         pool_build<N><<<nblk, 256, 0, c->stream>>>(dsrc, c->d_sstride, c->d_doms.ptr, c->d_porig.ptr, P, c->d_pool.ptr,
                                                    c->d_negsd2.ptr);
     }

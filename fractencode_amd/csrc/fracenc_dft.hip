@@ -220,11 +220,7 @@ struct DftDomainBuildArgs {
     uint32_t npos = 0;                // BYPOS: P
 };
 
-__device__ inline uint32_t pair_sums(uint32_t w0, uint32_t w1)
-{
-    constexpr uint32_t M = 0x00ff00ffu;
-    return (w0 & M) + ((w0 >> 8) & M) + (w1 & M) + ((w1 >> 8) & M);
-}
+// pair_sums: fracenc_kernels.hip (pool_build)
 
 // BYPOS (the SEA tiled form, whose tiles hold domains in ΣD4 order): one thread per pool
 // position in domain order, so neighbouring threads read overlapping plane rows, and the

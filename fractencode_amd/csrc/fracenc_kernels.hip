@@ -31,35 +31,77 @@ __device__ inline long long wave_sum_ll(long long v)
 }
 
 // ---------------------------------------------------------------------------
-// pool_build: one group of LPD = min(64, n²/2) lanes per domain pool position p (bucket
-// order), 64/LPD positions per wave; lane k of a group writes pool words k, k + LPD, ...
-// D4[i][j] is the 2×2 sum at domain pixel (2j, 2i): SamplerBilinear::sample's integer sum
-// (image/sampler.h:21-38) for the identity transform at range pixel (j, i).
+// pool_build: D4[i][j] is the 2×2 sum at domain pixel (2j, 2i): SamplerBilinear::sample's integer sum
+// (image/sampler.h:21-38) for the identity transform at range pixel (j, i).  n ≥ 4: one lane per D4 row
+// (n lanes per pool position p, bucket order): the row's two plane rows read as 32-bit words when the
+// domain origin and the stride are 4-byte aligned (the ratio-2 grids at offset n ≥ 4 are), two cells per
+// word pair — (w & 0x00ff00ff) + ((w >> 8) & 0x00ff00ff) over both rows is the packed u16 pair the pool
+// stores; byte loads otherwise.  n = 2: one lane per pool word.  (One lane per pool word with 8 byte loads
+// each ran the C4 quadtree's 261k-domain n = 4 level at 16 µs.)
 // ---------------------------------------------------------------------------
+__device__ inline uint32_t pair_sums(uint32_t w0, uint32_t w1)
+{
+    constexpr uint32_t M = 0x00ff00ffu;
+    return (w0 & M) + ((w0 >> 8) & M) + (w1 & M) + ((w1 >> 8) & M);
+}
+
+template <int N>
+__host__ __device__ constexpr int pool_lanes()
+{
+    return N >= 4 ? N : N * N / 2; // lanes per pool position
+}
+
 template <int N>
 __global__ void __launch_bounds__(256) pool_build(const uint8_t* __restrict__ src, uint32_t sstride,
                                                   const frac_grid_item* __restrict__ doms,
                                                   const uint32_t* __restrict__ porig, uint32_t P,
                                                   uint32_t* __restrict__ pool, int32_t* __restrict__ negsd2)
 {
-    constexpr int NN = N * N, K2 = NN / 2, LPD = K2 < 64 ? K2 : 64;
+    constexpr int NN = N * N, K2 = NN / 2, LPD = pool_lanes<N>();
+    static_assert(64 % LPD == 0, "a pool position's lanes sit in one wave");
     const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t p = gid / LPD;
     const int k0 = (int)(gid % LPD);
     int sq = 0;
     if (p < P) {
         const frac_grid_item d = doms[porig[p]];
-        for (int k = k0; k < K2; k += LPD) {
-            int v[2];
+        if constexpr (N >= 4) {
+            // lane k0: D4 row k0 = plane rows d.y + 2k0, + 1, columns d.x … d.x + 2N − 1; words N/2
+            const uint8_t* r0 = src + (size_t)(d.y + 2u * (uint32_t)k0) * sstride + d.x;
+            const uint8_t* r1 = r0 + sstride;
+            uint32_t* out = pool + (size_t)p * K2 + (size_t)k0 * (N / 2);
+            if ((((uintptr_t)r0 | sstride) & 3u) == 0) {
 #pragma unroll
-            for (int e = 0; e < 2; ++e) {
-                const int qi = 2 * k + e;
-                const uint32_t x = d.x + 2u * (qi % N), y = d.y + 2u * (qi / N);
-                const uint8_t* r0 = src + (size_t)y * sstride + x;
-                v[e] = (int)r0[0] + (int)r0[1] + (int)r0[sstride] + (int)r0[sstride + 1];
-                sq += v[e] * v[e];
+                for (int w = 0; w < N / 2; ++w) {
+                    const uint32_t v = pair_sums(reinterpret_cast<const uint32_t*>(r0)[w],
+                                                 reinterpret_cast<const uint32_t*>(r1)[w]);
+                    const int lo = (int)(v & 0xffffu), hi = (int)(v >> 16);
+                    sq += lo * lo + hi * hi;
+                    out[w] = v;
+                }
+            } else {
+#pragma unroll
+                for (int w = 0; w < N / 2; ++w) {
+                    const uint8_t* a = r0 + 4 * w;
+                    const uint8_t* b = r1 + 4 * w;
+                    const int lo = (int)a[0] + a[1] + b[0] + b[1], hi = (int)a[2] + a[3] + b[2] + b[3];
+                    sq += lo * lo + hi * hi;
+                    out[w] = (uint32_t)lo | ((uint32_t)hi << 16);
+                }
             }
-            pool[(size_t)p * K2 + k] = (uint32_t)v[0] | ((uint32_t)v[1] << 16);
+        } else {
+            for (int k = k0; k < K2; k += LPD) {
+                int v[2];
+#pragma unroll
+                for (int e = 0; e < 2; ++e) {
+                    const int qi = 2 * k + e;
+                    const uint32_t x = d.x + 2u * (qi % N), y = d.y + 2u * (qi / N);
+                    const uint8_t* r0 = src + (size_t)y * sstride + x;
+                    v[e] = (int)r0[0] + (int)r0[1] + (int)r0[sstride] + (int)r0[sstride + 1];
+                    sq += v[e] * v[e];
+                }
+                pool[(size_t)p * K2 + k] = (uint32_t)v[0] | ((uint32_t)v[1] << 16);
+            }
         }
     }
 #pragma unroll
