@@ -135,7 +135,29 @@ __global__ void __launch_bounds__(256) mfma_domain_prep(MfmaDomainPrepArgs a)
         return;
     const uint32_t tile = gid >> 5, row = gid & 31u;
     const int p = a.tile_pos[gid];
-    int sumd = 0, sd2 = 0;
+    // the pool row, read whole (16-byte loads where it has a multiple of 4 words) alongside −ΣD4²
+    constexpr int K2 = NN / 2, K2R = (K2 + 3) / 4 * 4;
+    uint32_t w[K2R];
+    int sd2 = 0;
+    if (p >= 0) {
+        if constexpr (K2 % 4 == 0) {
+            const uint4* pr = reinterpret_cast<const uint4*>(a.pool + (size_t)p * K2);
+#pragma unroll
+            for (int q = 0; q < K2 / 4; ++q) {
+                const uint4 v = pr[q];
+                w[4 * q] = v.x;
+                w[4 * q + 1] = v.y;
+                w[4 * q + 2] = v.z;
+                w[4 * q + 3] = v.w;
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < K2; ++q)
+                w[q] = a.pool[(size_t)p * K2 + q];
+        }
+        sd2 = -a.negsd2[p];
+    }
+    int sumd = 0;
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
 #pragma unroll
@@ -146,8 +168,7 @@ __global__ void __launch_bounds__(256) mfma_domain_prep(MfmaDomainPrepArgs a)
                 const int k = 16 * s + 8 * h + j;
                 int dv = 510; // padding k (n = 2) and padding rows contribute 0
                 if (p >= 0 && k < NN) {
-                    const uint32_t w = a.pool[(size_t)p * (NN / 2) + (k >> 1)];
-                    dv = (k & 1) ? (int)(w >> 16) : (int)(w & 0xffffu);
+                    dv = (k & 1) ? (int)(w[k >> 1] >> 16) : (int)(w[k >> 1] & 0xffffu);
                     sumd += dv;
                 }
                 v8[j] = (_Float16)(dv - 510);
@@ -155,8 +176,6 @@ __global__ void __launch_bounds__(256) mfma_domain_prep(MfmaDomainPrepArgs a)
             a.dtiles[((size_t)tile * KS + s) * 64 + row + 32 * h] = __builtin_bit_cast(uint4, v8);
         }
     }
-    if (p >= 0)
-        sd2 = -a.negsd2[p];
     // n ≤ 8: v = (bits(acc) << 3) + e with bits(acc) = 0x4B400000 − Z;  n = 16: v = (int(acc) << 3) + e;
     // the float-C epilogue: e_d itself, the accumulator's start
     uint32_t e = p >= 0 ? (uint32_t)(sd2 - 1024 * sumd) + (N == 16 ? (1u << 28) : (uint32_t)-0x58000000)
