@@ -32,10 +32,16 @@ lib.frac_clock_stamps.restype = ctypes.c_int
 lib.frac_clock_stamps.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_size_t]
 REALTIME_HZ = 100e6  # s_memrealtime: the constant 100 MHz reference
 
-S = 4096
-plane = value_noise(S, S, 1234)
+# --c2: BASELINE configs[1] instead (Lenna 512², T = 8) — where the search is latency-bound
+c2 = "--c2" in sys.argv
+if c2:
+    S, T = 512, 8
+    plane = np.fromfile(os.path.join(ROOT, "tests", "golden", "lenna_y.u8"), np.uint8).reshape(S, S)
+else:
+    S, T = 4096, 4
+    plane = value_noise(S, S, 1234)
 os.environ["FRAC_MFMA_DFT"] = "1"
-with F.Engine(0, 4, False, 0.0, -1.0, F.ENGINE_MFMA, timing=True) as e:
+with F.Engine(0, T, False, 0.0, -1.0, F.ENGINE_MFMA, timing=True) as e:
     e.set_frame(plane)
     e.set_domains(F.create_uniform_grid(S, S, 16, 8))
     e.set_ranges(F.create_uniform_grid(S, S, 8, 8))
@@ -68,5 +74,7 @@ with F.Engine(0, 4, False, 0.0, -1.0, F.ENGINE_MFMA, timing=True) as e:
                           "clock_mhz_p10": round(float(np.percentile(mhz, 10)), 1),
                           "clock_mhz_p90": round(float(np.percentile(mhz, 90)), 1),
                           "wg_loop_us_median": round(float(np.median(drt[ok])) / REALTIME_HZ * 1e6, 2),
+                          "wg_loop_us_max": round(float(drt[ok].max()) / REALTIME_HZ * 1e6, 2),
+                          "wg_start_spread_us": round(float(s[:, 2].max() - s[:, 2].min()) / REALTIME_HZ * 1e6, 2),
                           "launch_span_us": round(float(span_us), 2),
                           "ms_search_event": round(float(st["ms_search"]), 4)}), flush=True)
