@@ -1646,13 +1646,8 @@ int launch_mfma(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool inits =
         d.dtiles = c->d_m_dtiles.ptr;
         d.dconst = c->d_m_dconst.ptr;
         d.plan = c->qplan;
-        if constexpr (N == 16) {
-            // the tile-order copy of the pool rows for resolve_mfma<16> (the Fourier path's tpool buffer: the
-            // two are never live in one run)
-            FRAC_HIP(c, c->d_dft_tpool.ensure(std::max<size_t>((size_t)c->ntiles * 32 * (N * N / 2), 1)));
-            d.tpool16 = c->d_dft_tpool.ptr;
+        if constexpr (N == 16)
             mfma_domain_prep16<<<(c->ntiles * 32 * MfmaGeom<16>::KS + 255) / 256, 256, 0, c->stream>>>(d);
-        }
         else
             mfma_domain_prep<N><<<(c->ntiles * 32 + 255) / 256, 256, 0, c->stream>>>(d);
     }
@@ -1750,10 +1745,8 @@ int launch_mfma(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool inits =
         v.best_key = c->d_best_key.ptr;
         v.merged = (N != 16 && T > 1 && (c->mfma_var_ran & (128 | 256))) ? 1 : 0; // entries merged over t
         v.fmode = (N != 16 && (c->mfma_var_ran & 256)) ? 1 : 0;                  // fmap'd float-C minima
-        if constexpr (N == 16) {
+        if constexpr (N == 16)
             v.rfrags = c->d_m_rfrags.ptr; // the range copies from search_mfma16's B fragments
-            v.tpool16 = c->d_dft_tpool.ptr; // the pool rows in tile order (mfma_domain_prep16)
-        }
         if (!c->virt) { // the fit in the resolving wave (the sampled form fits at its own points: gen_fit)
             v.fused_fit = 1;
             v.fit = fit_args(c, dtgt, tstride, nr);

@@ -81,7 +81,6 @@ struct MfmaDomainPrepArgs {
     uint32_t* dconst;           // [ntiles][2][16]
     const DevPlan* plan = nullptr; // device-planned search: ntiles from the plan (the grid is a bound)
     int fmode = 0;              // the float-C epilogue (VAR 256): dconst = float e_d, padding kFltPadE
-    uint32_t* tpool16 = nullptr; // n = 16: [ntiles*32][128] the pool rows again in tile order (resolve_mfma)
 };
 
 // n = 16: 16 K-steps per row, one lane each (16-lane groups per tile row): the row's 128 pool words and
@@ -104,8 +103,6 @@ __global__ void __launch_bounds__(256) mfma_domain_prep16(MfmaDomainPrepArgs a)
         uint4 w = make_uint4(0x01fe01feu, 0x01fe01feu, 0x01fe01feu, 0x01fe01feu); // padding rows: 510 (0)
         if (p >= 0)
             w = *reinterpret_cast<const uint4*>(a.pool + (size_t)p * (NN / 2) + 8 * s + 4 * h);
-        if (a.tpool16) // the tile-order copy: resolve_mfma<16> reads a row without its pool position first
-            *reinterpret_cast<uint4*>(a.tpool16 + (size_t)rg * (NN / 2) + 8 * s + 4 * h) = w;
         const uint32_t ww[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
@@ -854,9 +851,6 @@ struct MfmaResolveArgs {
     // resolve_mfma<16>: the range copies are read back from search_mfma16's B fragments (128 − copy_t,
     // f16) instead of gathered pixel by pixel from the plane
     const uint4* rfrags = nullptr;
-    // resolve_mfma<16>: the pool rows in tile order (mfma_domain_prep16), so a row's words and its pool
-    // position load together, and ΣD4² is summed from the row instead of loaded through the position
-    const uint32_t* tpool16 = nullptr;
     // resolve_dft, T = 8: two-wave workgroups, one slot and its flipped copy each (flip_slots > 0)
     int paired = 0;
 };
@@ -1032,10 +1026,8 @@ __global__ void __launch_bounds__(256) resolve_mfma(MfmaResolveArgs a)
                         break;
                     const int p = pch[q];
                     uint32_t d[WPL];
-                    const bool t16 = N == 16 && a.tpool16 != nullptr;
                     if (p >= 0 && g * WPL < K2) {
-                        const uint32_t* dp = t16 ? a.tpool16 + ((size_t)tile * 32 + row) * K2 + g * WPL
-                                                 : a.pool + (size_t)p * K2 + g * WPL;
+                        const uint32_t* dp = a.pool + (size_t)p * K2 + g * WPL;
                         if constexpr (WPL % 4 == 0) {
 #pragma unroll
                             for (int w = 0; w < WPL; w += 4) {
@@ -1061,18 +1053,7 @@ __global__ void __launch_bounds__(256) resolve_mfma(MfmaResolveArgs a)
                         xu = __builtin_amdgcn_udot2(__builtin_bit_cast(ushort2_t, cp[w]),
                                                     __builtin_bit_cast(ushort2_t, d[w]), xu, false);
                     const int64_t X = (int64_t)quad_sum(xu);
-                    int64_t sd2row = 0; // ΣD4² of the row: from the row itself on the tile-order path
-                    if (t16) {
-                        uint32_t q2 = 0;
-#pragma unroll
-                        for (int w = 0; w < WPL; ++w)
-                            q2 = __builtin_amdgcn_udot2(__builtin_bit_cast(ushort2_t, d[w]), __builtin_bit_cast(ushort2_t, d[w]),
-                                                        q2, false);
-                        sd2row = (int64_t)quad_sum(q2); // ≤ 256·1020² < 2^32
-                    } else if (p >= 0) {
-                        sd2row = -(int64_t)a.negsd2[p];
-                    }
-                    const int64_t s16 = p >= 0 ? 16 * sr2 - 8 * X + sd2row : 0;
+                    const int64_t s16 = p >= 0 ? 16 * sr2 - 8 * X - (int64_t)a.negsd2[p] : 0;
                     uint32_t sdu = 0; // ΣD4 of the row (the fused fit)
 #pragma unroll
                     for (int w = 0; w < WPL; ++w)
@@ -1092,7 +1073,7 @@ __global__ void __launch_bounds__(256) resolve_mfma(MfmaResolveArgs a)
                             best_tile = tile;
                             bx = (int64_t)(uint32_t)__shfl((int)(uint32_t)X, first, 64);
                             bsd = (int64_t)(uint32_t)__shfl((int)sd1, first, 64);
-                            bsd2 = (int64_t)(uint32_t)__shfl((int)(uint32_t)sd2row, first, 64);
+                            bsd2 = -(int64_t)a.negsd2[pf];
                         }
                         break;
                     }
