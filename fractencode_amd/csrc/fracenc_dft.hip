@@ -1491,8 +1491,9 @@ __device__ inline DftResolved resolve_dft_eval(const MfmaResolveArgs& a, uint32_
         sr1 = __builtin_amdgcn_udot2(__builtin_bit_cast(ushort2_t, rp[q]), __builtin_bit_cast(ushort2_t, kOnes), sr1,
                                      false);
     }
-    sr2u = quad_sum(sr2u);
-    sr1 = quad_sum(sr1);
+    // every quad holds the whole range: the sums are wave-uniform (scalar registers from here on)
+    sr2u = (uint32_t)__builtin_amdgcn_readfirstlane((int)quad_sum(sr2u));
+    sr1 = (uint32_t)__builtin_amdgcn_readfirstlane((int)quad_sum(sr1));
     const int sr2 = (int)sr2u; // Σr² ≤ 64·255²
     const uint32_t e0 = a.blk_ptr[blk], e1 = a.blk_ptr[blk + 1];
     const uint32_t nent = (e1 - e0) * 2u;
@@ -1508,6 +1509,7 @@ __device__ inline DftResolved resolve_dft_eval(const MfmaResolveArgs& a, uint32_
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1)
         vmax = __builtin_fmaxf(vmax, __uint_as_float(lane_xor(__float_as_uint(vmax), lane, o)));
+    vmax = __uint_as_float((uint32_t)__builtin_amdgcn_readfirstlane((int)__float_as_uint(vmax))); // wave-uniform
     if (!(vmax > -1.0e29f))
         return res; // only padding rows: no eligible domain, best_key stays "none"
     const int64_t sa16 = (int64_t)a.rconst[slot];
@@ -1559,12 +1561,6 @@ __device__ inline DftResolved resolve_dft_eval(const MfmaResolveArgs& a, uint32_
                 const uint4* dp = reinterpret_cast<const uint4*>(a.tpool + ((size_t)tile * 32 + row) * 32 + g * (PG / 2));
                 const uint4 d0 = dp[0], d1 = dp[1];
                 const uint32_t dv[PG / 2] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w};
-                uint32_t dr[PG / 2]; // t = 1 pairs
-#pragma unroll
-                for (int o = 0; o < PG / 4; ++o) {
-                    dr[2 * o] = __builtin_amdgcn_alignbit(dv[2 * o + 1], dv[2 * o], 16);
-                    dr[2 * o + 1] = __builtin_amdgcn_alignbit(dv[2 * o], dv[2 * o + 1], 16);
-                }
                 uint32_t sd2 = 0, sd1 = 0;
 #pragma unroll
                 for (int q = 0; q < PG / 2; ++q) {
@@ -1584,7 +1580,10 @@ __device__ inline DftResolved resolve_dft_eval(const MfmaResolveArgs& a, uint32_
 #pragma unroll
                     for (int q = 0; q < PG / 2; ++q) {
                         // pair q of orbit q/2 for transform t (see the lane map above)
-                        const uint32_t dq = (t & 1) ? dr[q ^ (t >> 1)] : dv[q ^ (t >> 1)];
+                        // t odd: the rotated pairs, rebuilt per transform (a t = 1 copy held across
+                        // the loop would take 8 more VGPRs)
+                        const int qs = q ^ (t >> 1);
+                        const uint32_t dq = (t & 1) ? __builtin_amdgcn_alignbit(dv[qs ^ 1], dv[qs], 16) : dv[qs];
                         X = __builtin_amdgcn_udot2(__builtin_bit_cast(ushort2_t, rp[q]), __builtin_bit_cast(ushort2_t, dq),
                                                    X, false);
                     }
@@ -1742,7 +1741,7 @@ __device__ inline void resolve_dft_pair(const MfmaResolveArgs& a, uint32_t slot,
 // 372 µs at C3 in the SEA tiled form).
 
 template <bool SORTED = false>
-__global__ void __launch_bounds__(256) resolve_dft(MfmaResolveArgs a)
+__global__ void __launch_bounds__(256, 8) resolve_dft(MfmaResolveArgs a)
 {
     apply_plan(a);
     if constexpr (!SORTED) {

@@ -964,6 +964,7 @@ __global__ void __launch_bounds__(256) resolve_mfma(MfmaResolveArgs a)
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1)
         vmin = min(vmin, (uint32_t)__shfl_xor((int)vmin, o, 64));
+    vmin = (uint32_t)__builtin_amdgcn_readfirstlane((int)vmin); // wave-uniform: a scalar register
     if (vmin == 0xffffffffu) { // no eligible domain: best_key stays "none"
         if (a.fused_fit && lane == 0)
             fit_sums_range<N>(a.fit, r, kKeyNone, 0, 0, 0, 0, 0);
@@ -977,8 +978,9 @@ __global__ void __launch_bounds__(256) resolve_mfma(MfmaResolveArgs a)
         sr1u = __builtin_amdgcn_udot2(__builtin_bit_cast(ushort2_t, cp[w]), __builtin_bit_cast(ushort2_t, kOnes), sr1u,
                                       false);
     }
-    const int64_t sr2 = (int64_t)quad_sum(sr2u);
-    const int64_t sr1 = (int64_t)quad_sum(sr1u);
+    // every quad holds the whole copy: the sums are wave-uniform (scalar registers)
+    const int64_t sr2 = (int64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)quad_sum(sr2u));
+    const int64_t sr1 = (int64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)quad_sum(sr1u));
     // best S16 (when vmin is not a sentinel): v − c_r, or for the float-C entries acc + c'_r = acc + V0 − c_r
     const int64_t target = a.fmode ? (int64_t)funmap(vmin) + mfma_v0(NN) - (int64_t)(int32_t)rc
                                    : (int64_t)vmin - (int64_t)rc;
@@ -1128,6 +1130,7 @@ __global__ void __launch_bounds__(256, 6) resolve_small(MfmaResolveArgs a)
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1)
         vmin = min(vmin, (uint32_t)__shfl_xor((int)vmin, o, 64));
+    vmin = (uint32_t)__builtin_amdgcn_readfirstlane((int)vmin); // wave-uniform: a scalar register
     if (vmin == 0xffffffffu) {
         if (a.fused_fit && lane == 0)
             fit_sums_range<N>(a.fit, r, kKeyNone, 0, 0, 0, 0, 0);
@@ -1155,7 +1158,9 @@ __global__ void __launch_bounds__(256, 6) resolve_small(MfmaResolveArgs a)
         sr1u = __builtin_amdgcn_udot2(__builtin_bit_cast(ushort2_t, cp[0][k]), __builtin_bit_cast(ushort2_t, kOnes),
                                       sr1u, false);
     }
-    const int64_t sr2 = (int64_t)sr2u, sr1 = (int64_t)sr1u; // every lane holds the whole range
+    // every lane holds the whole range: the sums are wave-uniform (scalar registers)
+    const int64_t sr2 = (int64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)sr2u),
+                  sr1 = (int64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)sr1u);
     const int64_t target = a.fmode ? (int64_t)funmap(vmin) + mfma_v0(NN) - (int64_t)(int32_t)a.rconst[slot]
                                    : (int64_t)vmin - (int64_t)a.rconst[slot];
     const bool hit = a.hitH >= 0 && (vmin == 0 || target <= a.hitH);
