@@ -743,10 +743,6 @@ __global__ void __launch_bounds__(256, 2) search_mfma16(MfmaSearchArgs a)
     const uint32_t h = lane >> 5;
     auto compute = [&](const uint4* la, uint32_t nt, uint32_t tb) {
         const uint4* lc = la + nt * KS * 64u;
-        uint32_t cm[TPW];
-#pragma unroll
-        for (int j = 0; j < TPW; ++j)
-            cm[j] = 0xffffffffu;
         for (uint32_t q = 0; q < nt; ++q) {
             floatx16_t acc[TPW];
 #pragma unroll
@@ -768,26 +764,26 @@ __global__ void __launch_bounds__(256, 2) search_mfma16(MfmaSearchArgs a)
                 e[4 * c4 + 2] = v.z;
                 e[4 * c4 + 3] = v.w;
             }
+            // the entry names the tile itself (a chunk of one tile), so resolve_mfma<16> re-reads one tile's
+            // rows per match, not a stage's: 3 VALU per tile and transform here against 16 rows of 512 B there
 #pragma unroll
-            for (int j = 0; j < TPW; ++j)
+            for (int j = 0; j < TPW; ++j) {
+                uint32_t cm = 0xffffffffu;
 #pragma unroll
                 for (int i = 0; i < 16; ++i) // acc: exact integer, |acc| < 2^24
-                    cm[j] = min(cm[j], ((uint32_t)(int32_t)acc[j][i] << 3) + e[i]);
-        }
-#pragma unroll
-        for (int j = 0; j < TPW; ++j) {
-            if constexpr (HITS)
-                cm[j] = cm[j] <= hl ? 0u : cm[j]; // any hit in the chunk: the first-hit chunk wins
-            if (cm[j] < best[j]) {
-                best[j] = cm[j];
-                btile[j] = tb;
+                    cm = min(cm, ((uint32_t)(int32_t)acc[j][i] << 3) + e[i]);
+                if constexpr (HITS)
+                    cm = cm <= hl ? 0u : cm; // any hit in the tile: the first-hit tile wins
+                if (cm < best[j]) {
+                    best[j] = cm;
+                    btile[j] = tb + q;
+                }
             }
         }
     };
     const uint32_t nstage = (wk.w - wk.z + kTilesPerStage16 - 1) / kTilesPerStage16;
     auto stage_nt = [&](uint32_t st) { return min((uint32_t)kTilesPerStage16, wk.w - (wk.z + st * kTilesPerStage16)); };
-    // each stage (2 tiles) is its own chunk for resolve_mfma (which scans kTilesPerStage16 tiles at n = 16:
-    // half the 512-byte rows a coarser chunk made it re-read)
+    // stages of 2 tiles, double buffered; each tile is its own chunk for resolve_mfma
     if (nstage)
         stage_tiles<KS, 256>(lds0, a.dtiles, a.dconst, wk.z, stage_nt(0));
     for (uint32_t st = 0; st < nstage; st += 2) {
@@ -915,37 +911,35 @@ __global__ void __launch_bounds__(256) resolve_mfma(MfmaResolveArgs a)
     uint32_t cp[WPL];
     int ct = -1;
     auto build_copy = [&](int t) {
-        if constexpr (N == 16) {
-            if (a.rfrags) {
-                // words g·WPL … g·WPL + 31 = pixels k = 64g … 64g + 63 of copy_t: fragments s = 4g … 4g + 3,
-                // both lane halves h (k = 16s + 8h + j)
+        if constexpr (N == 16) { // always from the fragments (the host sets rfrags for every n = 16 resolve)
+            // words g·WPL … g·WPL + 31 = pixels k = 64g … 64g + 63 of copy_t: fragments s = 4g … 4g + 3,
+            // both lane halves h (k = 16s + 8h + j)
 #pragma unroll
-                for (int sl = 0; sl < 4; ++sl)
+            for (int sl = 0; sl < 4; ++sl)
 #pragma unroll
-                    for (int hh = 0; hh < 2; ++hh) {
-                        const uint4 f = a.rfrags[((size_t)(blk * a.T + (uint32_t)t) * MfmaGeom<16>::KS + 4 * g + sl) * 64 +
-                                                 col + 32 * hh];
-                        const uint32_t fw[4] = {f.x, f.y, f.z, f.w};
+                for (int hh = 0; hh < 2; ++hh) {
+                    const uint4 f = a.rfrags[((size_t)(blk * a.T + (uint32_t)t) * MfmaGeom<16>::KS + 4 * g + sl) * 64 +
+                                             col + 32 * hh];
+                    const uint32_t fw[4] = {f.x, f.y, f.z, f.w};
 #pragma unroll
-                        for (int m = 0; m < 4; ++m) {
-                            const uint32_t lo = (uint32_t)(128 - (int)__builtin_bit_cast(_Float16, (uint16_t)(fw[m] & 0xffffu)));
-                            const uint32_t hi = (uint32_t)(128 - (int)__builtin_bit_cast(_Float16, (uint16_t)(fw[m] >> 16)));
-                            cp[sl * 8 + hh * 4 + m] = lo | (hi << 16);
-                        }
+                    for (int m = 0; m < 4; ++m) {
+                        const uint32_t lo = (uint32_t)(128 - (int)__builtin_bit_cast(_Float16, (uint16_t)(fw[m] & 0xffffu)));
+                        const uint32_t hi = (uint32_t)(128 - (int)__builtin_bit_cast(_Float16, (uint16_t)(fw[m] >> 16)));
+                        cp[sl * 8 + hh * 4 + m] = lo | (hi << 16);
                     }
-                ct = t;
-                return;
-            }
-        }
-        const Aff af = lut(t);
+                }
+            ct = t;
+        } else {
+            const Aff af = lut(t);
 #pragma unroll
-        for (int w = 0; w < WPL; ++w) {
-            const int k = g * WPL + w;
-            cp[w] = k < K2 ? range_pix_inv<N>(a.tgt, a.tstride, rg, af, 2 * k) |
-                                 (range_pix_inv<N>(a.tgt, a.tstride, rg, af, 2 * k + 1) << 16)
-                           : 0u;
+            for (int w = 0; w < WPL; ++w) {
+                const int k = g * WPL + w;
+                cp[w] = k < K2 ? range_pix_inv<N>(a.tgt, a.tstride, rg, af, 2 * k) |
+                                     (range_pix_inv<N>(a.tgt, a.tstride, rg, af, 2 * k + 1) << 16)
+                               : 0u;
+            }
+            ct = t;
         }
-        ct = t;
     };
     build_copy(0);
     // the entries: the first 128 stay in registers (enr) for the match pass below, which reloads
@@ -1016,7 +1010,7 @@ __global__ void __launch_bounds__(256) resolve_mfma(MfmaResolveArgs a)
                     build_copy((int)tt);
                 // the entry names the first tile of the chunk that attained the minimum: scan the
                 // chunk's tiles in order; the first matching row is the earliest domain
-                constexpr uint32_t CH = N == 16 ? (uint32_t)kTilesPerStage16 : (uint32_t)kTilesPerStage;
+                constexpr uint32_t CH = N == 16 ? 1u : (uint32_t)kTilesPerStage; // search_mfma16: one-tile chunks
                 int pch[CH]; // the chunk's rows' pool positions, loaded together
 #pragma unroll
                 for (uint32_t q = 0; q < CH; ++q)
