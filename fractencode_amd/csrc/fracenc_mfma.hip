@@ -946,6 +946,9 @@ __global__ void __launch_bounds__(256) resolve_mfma(MfmaResolveArgs a)
     // only past them
     uint2 enr0 = make_uint2(0xffffffffu, 0u), enr1 = enr0;
     uint32_t vmin = 0xffffffffu;
+    // not unrolled: an unrolled copy kept a dozen iterations' index divisions in flight and set the
+    // kernel's register peak (160 VGPRs, 3 waves per SIMD at n = 16); nent is ≤ 128 in the common case
+#pragma nounroll
     for (uint32_t j = lane; j < nent; j += 64) {
         const uint32_t e = e0 + j / (2u * TE), t = (j >> 1) % TE, h = j & 1u;
         const uint2 en = a.entries[((size_t)a.blk_ent[e] * a.T + t) * 64 + col + 32 * h];
@@ -1117,7 +1120,8 @@ __global__ void __launch_bounds__(256, 6) resolve_small(MfmaResolveArgs a)
     const uint32_t TE = a.merged ? 1u : a.T;
     const uint32_t nent = (e1 - e0) * TE * 2u;
     uint32_t vmin = 0xffffffffu;
-    for (uint32_t j = lane; j < nent; j += 64) {
+#pragma nounroll
+    for (uint32_t j = lane; j < nent; j += 64) { // not unrolled, as in resolve_mfma
         const uint32_t e = e0 + j / (2u * TE), t = (j >> 1) % TE, h = j & 1u;
         vmin = min(vmin, a.entries[((size_t)a.blk_ent[e] * a.T + t) * 64 + col + 32 * h].x);
     }
