@@ -1780,6 +1780,10 @@ int launch_tp(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool timing)
 {
     const uint32_t nr = (uint32_t)nranges(c), P = c->npos;
     const uint32_t nt = c->ntiles, nbk = c->nblocks, ng = (uint32_t)c->tp_groups.size();
+    // resolve_dft<true> keeps one copy per slot: T = 8's flipped copies would go unmerged here, and
+    // prepare() routes only T = 4 to the tiled form (c->tp)
+    if (c->p.transforms != 4)
+        return c->fail(FRAC_E_STATE, "the tiled SEA form runs T = 4 only");
     c->form_ran = FRAC_FORM_SEA_MFMA;
     c->flops_ran = 0;
     c->evaluated_ran = 0;
