@@ -2199,7 +2199,7 @@ int launch_all(frac_ctx* c)
                 else
                     search_valu<N, 4, false><<<grid, block, 0, c->stream>>>(a);
             }
-        } else {
+        } else if constexpr (N < 16) { // n = 16 never takes a 4-copy group (4 × 128 words of copies would spill)
             if (hits)
                 search_valu<N, 4, true><<<grid, block, 0, c->stream>>>(a);
             else
