@@ -499,11 +499,10 @@ int device_buckets(frac_ctx* c, int nb, uint32_t* dfirst, uint32_t* rfirst)
     const uint32_t tstride = c->same_plane ? c->d_sstride : c->d_tstride;
     // a stored −1 is classified on the item's own plane (Classifier2::compare, Classifier2.cpp:70-81);
     // the pool order porig and the bucket-sorted ranges rord by the stable bucket sort
-    if (nd)
-        launch_bucket_keys(c->d_doms.ptr, nd, c->Sh, c->d_src.ptr, c->d_sstride, c->d_bk_keys.ptr, nullptr, err,
-                           c->stream);
-    if (nr)
-        launch_bucket_keys(c->d_ranges.ptr, nr, c->nh, tplane, tstride, c->d_rkey.ptr, nullptr, err, c->stream);
+    // both grids' keys, in one launch for the usual 2n → n geometry
+    launch_bucket_keys_pair(KeySeg{c->d_doms.ptr, nd, c->d_src.ptr, c->d_sstride, c->d_bk_keys.ptr, nullptr, err, nullptr},
+                            c->Sh, KeySeg{c->d_ranges.ptr, nr, tplane, tstride, c->d_rkey.ptr, nullptr, err, nullptr},
+                            c->nh, c->stream);
     const BkSeg sd = bk_seg_of(c->d_bk_keys.ptr, nd, nullptr, c->d_bk_cnt.ptr, first, c->d_porig.ptr);
     const BkSeg sr = bk_seg_of(c->d_rkey.ptr, nr, nullptr, c->d_bk_cnt.ptr + (size_t)sd.tiles * kMaxBuckets,
                                first + kMaxBuckets + 1, c->d_rord.ptr);
@@ -2437,10 +2436,9 @@ int qt_encode_dev(frac_ctx* c, const frac_quadtree_params* qp, LevelGrid& level,
             // domains: keys + stable bucket sort (the pool order porig) + bounds; ranges: the same over the
             // worst case, counting only the level's *dn (the grids' categories are −1, computed here:
             // no invalid category can occur, so no error word)
-            launch_bucket_keys(c->d_doms.ptr, nd, 2 * n, c->d_src.ptr, c->d_sstride, c->d_bk_keys.ptr, nullptr,
-                               nullptr, c->stream);
-            launch_bucket_keys(c->d_ranges.ptr, nr_max, n, tplane, tstride, c->d_rkey.ptr, nullptr, nullptr,
-                               c->stream, dn);
+            launch_bucket_keys_pair(
+                KeySeg{c->d_doms.ptr, nd, c->d_src.ptr, c->d_sstride, c->d_bk_keys.ptr, nullptr, nullptr, nullptr}, 2 * n,
+                KeySeg{c->d_ranges.ptr, nr_max, tplane, tstride, c->d_rkey.ptr, nullptr, nullptr, dn}, n, c->stream);
             // both sorts in one set of launches (the range counts after the domain counts in the scratch)
             const BkSeg sd = bk_seg_of(c->d_bk_keys.ptr, nd, nullptr, c->d_bk_cnt.ptr, first, c->d_porig.ptr);
             const BkSeg sr = bk_seg_of(c->d_rkey.ptr, nr_max, dn, c->d_bk_cnt.ptr + (size_t)sd.tiles * kMaxBuckets,

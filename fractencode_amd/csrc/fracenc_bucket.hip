@@ -70,14 +70,29 @@ __global__ void __launch_bounds__(256) bucket_keys(const frac_grid_item* __restr
 // items [*dn, n) of the worst-case grid get the padding key kPadKey, which sorts after every bucket.
 constexpr uint32_t kPadKey = 7; // categories −1..5 are keys 0..6; the 3-bit radix sort keeps 7 last
 
+// one grid's keys (bucket_keys_rows, and either half of bucket_keys_rows2)
+struct KeySeg {
+    const frac_grid_item* items;
+    uint32_t n;
+    const uint8_t* plane;
+    uint32_t stride;
+    uint32_t* key;
+    uint32_t* iota;
+    uint32_t* err;
+    const uint32_t* dn;
+};
+
 template <uint32_t L>
-__global__ void __launch_bounds__(256) bucket_keys_rows(const frac_grid_item* __restrict__ items, uint32_t n,
-                                                        const uint8_t* __restrict__ plane, uint32_t stride,
-                                                        uint32_t* __restrict__ key, uint32_t* __restrict__ iota,
-                                                        uint32_t* __restrict__ err, const uint32_t* __restrict__ dn)
+__device__ inline void keys_rows_item(const KeySeg& sg, uint32_t gid)
 {
     static_assert(L >= 1 && L <= 64 && (L & (L - 1)) == 0, "lanes per item: a power of two up to 64");
-    const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+    const frac_grid_item* __restrict__ items = sg.items;
+    const uint8_t* __restrict__ plane = sg.plane;
+    uint32_t* __restrict__ key = sg.key;
+    uint32_t* __restrict__ iota = sg.iota;
+    uint32_t* __restrict__ err = sg.err;
+    const uint32_t n = sg.n, stride = sg.stride;
+    const uint32_t* dn = sg.dn;
     const uint32_t k = gid / L, j = gid % L;
     if (dn) {
         const uint32_t nd = min(*dn, n);
@@ -135,6 +150,24 @@ __global__ void __launch_bounds__(256) bucket_keys_rows(const frac_grid_item* __
         iota[k] = k;
 }
 
+template <uint32_t L>
+__global__ void __launch_bounds__(256) bucket_keys_rows(KeySeg sg)
+{
+    keys_rows_item<L>(sg, blockIdx.x * blockDim.x + threadIdx.x);
+}
+
+// Two grids' keys in one launch (a level's domains, 2n rows high, and its ranges, n rows): blocks
+// [0, nb0) take s0 with L0 lanes per item, the rest s1 with L1.  The blocks are whole item groups of
+// either grid, so the shuffles stay within one grid.
+template <uint32_t L0, uint32_t L1>
+__global__ void __launch_bounds__(256) bucket_keys_rows2(KeySeg s0, KeySeg s1, uint32_t nb0)
+{
+    if (blockIdx.x < nb0)
+        keys_rows_item<L0>(s0, blockIdx.x * blockDim.x + threadIdx.x);
+    else
+        keys_rows_item<L1>(s1, (blockIdx.x - nb0) * blockDim.x + threadIdx.x);
+}
+
 // bucket keys of `cnt` items of height h (every item of a grid has the size of the first); dn: the
 // device-side count of a worst-case grid of cnt items (items ≤ 64 rows high only)
 inline void launch_bucket_keys(const frac_grid_item* items, uint32_t cnt, uint32_t h, const uint8_t* plane,
@@ -144,8 +177,8 @@ inline void launch_bucket_keys(const frac_grid_item* items, uint32_t cnt, uint32
     auto rows = [&](auto lanes) {
         constexpr uint32_t L = decltype(lanes)::value;
         const uint64_t threads = (uint64_t)cnt * L;
-        bucket_keys_rows<L><<<(unsigned)((threads + 255) / 256), 256, 0, s>>>(items, cnt, plane, stride, key, iota, err,
-                                                                             dn);
+        bucket_keys_rows<L><<<(unsigned)((threads + 255) / 256), 256, 0, s>>>(
+            KeySeg{items, cnt, plane, stride, key, iota, err, dn});
     };
     if (h <= 2)
         rows(std::integral_constant<uint32_t, 2>());
@@ -161,6 +194,31 @@ inline void launch_bucket_keys(const frac_grid_item* items, uint32_t cnt, uint32
         rows(std::integral_constant<uint32_t, 64>());
     else
         bucket_keys<<<(cnt + 3) / 4, 256, 0, s>>>(items, cnt, plane, stride, key, iota, err);
+}
+
+// a level's domain keys (items 2h rows high) and range keys (h rows) in one launch when h ∈ {4, 8, 16}
+// (the C4 frame and the quadtree's levels), else the two launches of launch_bucket_keys
+inline void launch_bucket_keys_pair(const KeySeg& d, uint32_t dh, const KeySeg& r, uint32_t rh, hipStream_t s)
+{
+    auto pair = [&](auto lanes) {
+        constexpr uint32_t L = decltype(lanes)::value; // range rows; the domains take 2L
+        const unsigned nb0 = (unsigned)(((uint64_t)d.n * 2 * L + 255) / 256);
+        const unsigned nb1 = (unsigned)(((uint64_t)r.n * L + 255) / 256);
+        bucket_keys_rows2<2 * L, L><<<nb0 + nb1, 256, 0, s>>>(d, r, nb0);
+    };
+    if (d.n && r.n && dh == 2 * rh && rh > 2 && rh <= 16 && (rh & (rh - 1)) == 0) {
+        if (rh == 4)
+            pair(std::integral_constant<uint32_t, 4>());
+        else if (rh == 8)
+            pair(std::integral_constant<uint32_t, 8>());
+        else
+            pair(std::integral_constant<uint32_t, 16>());
+        return;
+    }
+    if (d.n)
+        launch_bucket_keys(d.items, d.n, dh, d.plane, d.stride, d.key, d.iota, d.err, s, d.dn);
+    if (r.n)
+        launch_bucket_keys(r.items, r.n, rh, r.plane, r.stride, r.key, r.iota, r.err, s, r.dn);
 }
 
 // ---- stable bucket sort of item indices by a 3-bit key (the classifier buckets) ----
