@@ -2532,7 +2532,6 @@ int qt_encode_dev(frac_ctx* c, const frac_quadtree_params* qp, LevelGrid& level,
         sa.stride = kQtCounters;
         const uint32_t ntl = std::max<uint32_t>((nr_max + kBkTile - 1) / kBkTile, 1u);
         qt_split_count<<<ntl, kBkThreads, 0, c->stream>>>(sa);
-        qt_split_scan<<<1, 64, 0, c->stream>>>(sa, ntl);
         qt_split_emit<<<ntl, kBkThreads, 0, c->stream>>>(sa);
         std::swap(c->d_ranges, c->d_qt_next);
         // the next level: at most four quadrants per range, at most the full grid of its size (counted in

@@ -594,11 +594,12 @@ __global__ void __launch_bounds__(256) qt_scatter(const frac_encode_item* __rest
     }
 }
 
-// ---- the level transition of a device-planned quadtree level in three launches ----
+// ---- the level transition of a device-planned quadtree level in two launches ----
 // (qt_level_stats + qt_flags + a scan + qt_scatter restated): per 1,024-range tile the split count and
-// the level's counters (qt_split_count), the tiles' exclusive prefix and the next level's count
-// (qt_split_scan), then the tile's leaves and quadrants in index order (qt_split_emit, the ranks from
-// wave ballots as in bksort_scatter).  A range splits when the level may split and its distance
+// the level's counters (qt_split_count), then per tile its prefix over the earlier tiles' counts (the
+// first tile also writes the next level's count and leaf base) and the tile's leaves and quadrants in
+// index order (qt_split_emit, the ranks from wave ballots as in bksort_scatter; a separate one-wave scan
+// launch cost 4.9 µs per level).  A range splits when the level may split and its distance
 // exceeds the threshold; leaves keep the search order, quadrants their parents' order.
 struct QtSplitArgs {
     const frac_encode_item* out;  // the level's records
@@ -608,7 +609,7 @@ struct QtSplitArgs {
     uint32_t nmax;                // the grid's bound
     int can_split;
     double split;
-    uint32_t* tcount;             // [tiles] splits per tile, then their exclusive prefix
+    uint32_t* tcount;             // [tiles] splits per tile (qt_split_emit sums the earlier ones)
     frac_encode_item* leaves;     // device memory, or the caller's pinned host buffer (written over PCIe)
     uint32_t leaf_cap;            // leaves past it are not written (the caller's capacity)
     frac_grid_item* next_ranges;
@@ -683,42 +684,32 @@ __global__ void __launch_bounds__(kBkThreads) qt_split_count(QtSplitArgs a)
     }
 }
 
-// one wave: the tiles' exclusive prefix of split counts (in place), the next level's count and leaf base
-__global__ void __launch_bounds__(64) qt_split_scan(QtSplitArgs a, uint32_t ntiles)
-{
-    const uint32_t lane = threadIdx.x;
-    const uint32_t per = (ntiles + 63) / 64, t0 = min(lane * per, ntiles), t1 = min(t0 + per, ntiles);
-    uint32_t run = 0;
-    for (uint32_t t = t0; t < t1; ++t)
-        run += a.tcount[t];
-    uint32_t inc = run;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t x = (uint32_t)__shfl_up((int)inc, o, 64);
-        if ((int)lane >= o)
-            inc += x;
-    }
-    uint32_t off = inc - run;
-    for (uint32_t t = t0; t < t1; ++t) {
-        const uint32_t cnt = a.tcount[t];
-        a.tcount[t] = off;
-        off += cnt;
-    }
-    if (lane == 63) {
-        const uint32_t n = min(a.plan->nr, a.nmax), lb = a.plan->leaf_base;
-        a.next->nr = 4 * inc;
-        a.next->leaf_base = lb + n - inc;
-    }
-}
-
 __global__ void __launch_bounds__(kBkThreads) qt_split_emit(QtSplitArgs a)
 {
     __shared__ uint32_t wcnt[kBkThreads / 64];
     __shared__ uint32_t run;
     const uint32_t n = min(a.plan->nr, a.nmax), leaf_base = a.plan->leaf_base;
     const uint32_t base = blockIdx.x * kBkTile, lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-    if (threadIdx.x == 0)
-        run = a.tcount[blockIdx.x];
+    if (wv == 0) { // the splits of the tiles before this one, read from qt_split_count's per-tile counts
+        uint32_t before = 0, total = 0;
+        for (uint32_t t = lane; t < gridDim.x; t += 64) {
+            const uint32_t ct = a.tcount[t];
+            before += t < blockIdx.x ? ct : 0u;
+            total += ct;
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            before += (uint32_t)__shfl_xor((int)before, o, 64);
+            total += (uint32_t)__shfl_xor((int)total, o, 64);
+        }
+        if (lane == 0) {
+            run = before;
+            if (blockIdx.x == 0) { // the next level's count and leaf base
+                a.next->nr = 4 * total;
+                a.next->leaf_base = leaf_base + n - total;
+            }
+        }
+    }
     const unsigned long long below = lane ? (~0ull >> (64 - lane)) : 0ull;
     for (uint32_t j = 0; j < kBkTile / kBkThreads; ++j) {
         const uint32_t i = base + j * kBkThreads + threadIdx.x;
