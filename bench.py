@@ -4,23 +4,29 @@
 Workload (BASELINE.json configs[2]): one 4096×4096 grayscale frame
 (synthetic S1 value noise, seed 1234), 8×8 ranges (262,144), 16×16 domains at stride 8
 (261,121), the reference's 4 transforms, exhaustive (no classifier), rms threshold 0.
-A step = one full search of the frame's ranges already resident in HBM: domain-pool
-build, search, winner fit, fp32 fallback and — for N > 1 — the RCCL all-gather of the
-32-byte (domain, transform, s, o, rms) winner tuples.  Ranges are sharded contiguously over
-ranks (fixed total work: strong scaling).
+Ranges are sharded contiguously over ranks (fixed total work: strong scaling).
 
-Beside `value` the line carries:
+`value` is BASELINE.md's / SURVEY §8(d)'s end-to-end step, the span the reference's own timer
+wraps (main.cpp:164-168, the whole Encoder2): per step the frame H2D from pinned host memory
+(each rank uploads its own copy), domain-pool build, search, winner fit and fp32 fallback of this
+rank's shard, its 32-byte (domain, transform, s, o, rms) tuples packed on the device, the RCCL
+all-gather of every rank's tuples (N > 1) and the gathered tuples D2H into pinned host memory —
+serial, one frame after another.  Beside it the line carries:
+  device_value  the same search with the frame already resident in HBM and the tuples left there
+                (the all-gather still runs for N > 1): the device-only rate
+  stream_value  the end-to-end step through two contexts alternating frames, so frame k+1's
+                upload and frame k−1's download overlap frame k's search
   roofline      the search kernel against the dense f16 MFMA peak: `achieved` = the matrix flops
                 the search issues per launch (its algorithm's count) ÷ the kernel's mean duration
-                over exactly the timed steps (library HIP events on the kernel's stream,
+                over exactly the headline's timed steps (library HIP events on the kernel's stream,
                 frac_timing_history); `direct_form` = the §8(d) direct-form op count over the same
                 time (an algorithmic-equivalent rate, not a hardware fraction); `traffic` = HBM
                 bytes per launch from the committed rocprofv3 PMC passes of THIS library build
                 (null when profiles/pmc_search.json was taken from another build)
-  e2e           the same workload through the host boundary (§8(d)): per step the frame H2D from
-                pinned memory, the search, and the tuples D2H into pinned memory; `pipelined` = the same
-                with two contexts alternating frames, so frame k+1's upload and frame k−1's download
-                overlap frame k's search
+  arith         what `dtype` "f16" means here: exact integer arithmetic in f16 containers
+  records       a digest of the gathered tuples (equal across N = 1/2/4/8 iff the shards' gathered
+                records equal the single-rank run's), and the checks that each rank's slice of the
+                gathered tuples is its own shard and that the end-to-end and device legs agree
   cpu_baseline  the unmodified reference (oracle/_ref) on a bounded sample, all the host cores this
                 process may use (affinity, capped by the cgroup CPU quota), CPU model recorded
 
@@ -28,10 +34,13 @@ Run:  python bench.py [--gpus N] [--steps K] [--warmup W] [--engine valu|mfma|au
 --gpus N > 1 without WORLD_SIZE in the environment: this process launches N ranks itself
 (torch.distributed.run as a child process, before anything touches the GPU) and exits with its
 status; under torch.distributed.run (WORLD_SIZE set) it runs one rank per GPU over RCCL.
+The step, the all-gather and the line's core fields (FrameStep, timed, headline_fields) take any
+engine object and process-group backend: tests/test_bench_ranks.py runs them on `gloo` ranks.
 """
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
 import socket
@@ -48,9 +57,12 @@ METRIC = "range-blocks/s (1/2/4/8 GPU) + achieved HBM GB/s vs roofline, 8×8 ran
 VALU_PEAK_TOPS = 157.3  # MI355X vector peak (MI355X_MICROARCH.md: 256 CU x 2.4 GHz x 256 op/clk)
 MFMA_F16_PEAK_TFLOPS = 2500.0  # dense f16 MFMA peak (MI355X_MICROARCH.md)
 HBM_PEAK_GBS = 8000.0
+ARITH = ("exact integer: f16 operands are integers |x| <= 2048 (exact in f16), fp32 accumulation with every "
+         "partial sum < 2^24 (guarded per tile pair), winners re-resolved in integer arithmetic, fit in fp64")
+TUPLE_BYTES = 32
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
@@ -63,10 +75,11 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every core this process may use")
     ap.add_argument("--alt-steps", type=int, default=2,
                     help="steps of the VALU engine (north_star's no-MFMA formulation) reported beside (0 = skip)")
-    ap.add_argument("--e2e-steps", type=int, default=-1, help="steps of the host-boundary leg (-1 = --steps)")
+    ap.add_argument("--side-steps", type=int, default=-1,
+                    help="steps of the device-resident and stream legs (-1 = --steps, 0 = skip)")
     ap.add_argument("--ab", action="store_true",
                     help="allow FRAC_LIB / A/B knobs in the environment (the line is then marked, not a headline)")
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
 # environment knobs the library (or the package) reads that change which code runs: the headline
@@ -88,17 +101,19 @@ def check_headline_env(args) -> list:
     return knobs
 
 
-def launch_ranks(args) -> int:
-    """N ranks on this node via torch.distributed.run (a child process; this parent never initialises
-    the GPU, so no exec happens after GPU init)."""
+def launch_ranks(nproc: int, script: str | None = None, argv: list | None = None, env: dict | None = None) -> int:
+    """`nproc` ranks on this node via torch.distributed.run (a child process; this parent never
+    initialises the GPU, so no exec happens after GPU init).  Returns the launcher's exit status,
+    which is non-zero when any rank failed."""
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
-    env = dict(os.environ)
+    env = dict(os.environ if env is None else env)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
-           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *sys.argv[1:]]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), script or os.path.abspath(__file__),
+           *(sys.argv[1:] if argv is None else argv)]
     return subprocess.call(cmd, env=env)
 
 
@@ -175,12 +190,115 @@ def load_traffic(form: str):
     return e.get("hbm_bytes_per_launch"), e.get("source")
 
 
+# ---------------------------------------------------------------------------------------------
+# the step, its timing and the line's core fields: any engine object (set_frame / run /
+# copy_tuples_device or fetch_tuples), any process-group backend (nccl on the GPU, gloo on the CPU)
+# ---------------------------------------------------------------------------------------------
+
+def _sync(dev) -> None:
+    import torch
+
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+
+
+def max_over_ranks(x: float, world: int, dev) -> float:
+    """The largest of every rank's `x` (the slowest rank's time)."""
+    if world == 1:
+        return x
+    import torch
+    import torch.distributed as dist
+
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def timed(fn, steps: int, world: int, dev) -> tuple[float, float]:
+    """`steps` calls of fn bracketed by a barrier + device synchronisation on both sides; returns
+    (this rank's seconds, the maximum over ranks)."""
+    import torch.distributed as dist
+
+    _sync(dev)
+    if world > 1:
+        dist.barrier()
+    _sync(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    _sync(dev)
+    if world > 1:
+        dist.barrier()
+    _sync(dev)
+    mine = time.perf_counter() - t0
+    return mine, max_over_ranks(mine, world, dev)
+
+
+class FrameStep:
+    """The headline step (BASELINE.md "Metric"): the frame H2D from the caller's
+    pinned host plane, the search of this rank's shard (frame-dependent preparation included), the
+    shard's 32-byte tuples into the all-gather buffer, the all-gather (whenever a process group is
+    up), and the gathered tuples D2H into pinned host memory.  `device_resident=True`: the frame is
+    not uploaded and the gathered tuples stay on the device (the device-only leg)."""
+
+    def __init__(self, eng, frame, plan, rank: int, dev, device_resident: bool = False):
+        import torch
+
+        self.eng, self.frame, self.plan, self.rank, self.dev = eng, frame, plan, rank, dev
+        self.device_resident = device_resident
+        a, b = plan[rank]
+        self.n_mine = b - a
+        cap = max((q - p for p, q in plan), default=0)
+        self.local = torch.zeros(cap * TUPLE_BYTES, dtype=torch.uint8, device=dev)
+        self.h_out = torch.empty(plan[-1][1] * TUPLE_BYTES, dtype=torch.uint8, pin_memory=dev.type == "cuda")
+        self.gathered = None
+
+    def __call__(self) -> None:
+        import torch
+
+        from fractencode_amd.distributed import gather_tuples
+
+        if not self.device_resident:
+            self.eng.set_frame(self.frame)  # H2D (returns once the plane is on the device)
+        self.eng.run()
+        if self.local.is_cuda:  # packed on the device, on the engine's (= torch's current) stream
+            if self.n_mine:
+                self.eng.copy_tuples_device(self.local.data_ptr())
+        elif self.n_mine:  # CPU backend: the engine hands back host tuples
+            t = np.ascontiguousarray(self.eng.fetch_tuples())
+            self.local[: self.n_mine * TUPLE_BYTES] = torch.from_numpy(t.view(np.uint8))
+        self.gathered = gather_tuples(self.local, self.plan)
+        if not self.device_resident:
+            self.h_out.copy_(self.gathered, non_blocking=True)  # D2H into pinned memory
+
+    def tuples_bytes(self) -> bytes:
+        """The last step's gathered tuples (after a synchronisation)."""
+        src = self.gathered if self.device_resident else self.h_out
+        return src.cpu().numpy().tobytes()
+
+    def own_slice_ok(self, own: bytes) -> bool:
+        """This rank's slice of the gathered tuples is its own shard's."""
+        a, b = self.plan[self.rank]
+        return self.tuples_bytes()[a * TUPLE_BYTES: b * TUPLE_BYTES] == own
+
+
+def headline_fields(nr_total: int, world: int, steps: int, warmup: int, elapsed_max: float) -> dict:
+    """The contract's core fields from the slowest rank's time over the timed steps."""
+    return {"metric": METRIC, "value": round(nr_total / (elapsed_max / steps), 1), "unit": "range-blocks/s",
+            "n_gpus": world, "steps": steps, "warmup": warmup, "ms_per_step": round(1e3 * elapsed_max / steps, 3),
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None}
+
+
+def digest(b: bytes) -> str:
+    return hashlib.sha256(b).hexdigest()[:16]
+
+
 def main(args):
     import torch
     import torch.distributed as dist
 
     import fractencode_amd as F
-    from fractencode_amd.distributed import TUPLE_BYTES, gather_tuples, plan_capacity, shard_plan
+    from fractencode_amd.distributed import shard_plan
     from fractencode_amd.synth import value_noise
 
     knobs = check_headline_env(args)
@@ -215,59 +333,42 @@ def main(args):
     mine = rngs[start:stop]
     engine_id = {"auto": F.ENGINE_AUTO, "valu": F.ENGINE_VALU, "mfma": F.ENGINE_MFMA}[args.engine]
 
-    # one dedicated stream for the engine and the RCCL gather, so the all-gather is ordered after
-    # the record copy (the legacy null stream cannot be handed to the library: NULL = its own stream)
+    # one dedicated stream for the engine, the tuple copies and the RCCL gather, so every copy and the
+    # all-gather are ordered after the kernels (the legacy null stream cannot be handed to the
+    # library: NULL = its own stream)
     stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
     eng = F.Engine(dev.index, args.transforms, False, 0.0, -1.0, engine_id, timing=True)
     eng.set_stream(stream.cuda_stream)
-    d_frame = torch.from_numpy(frame).to(dev)  # the frame is resident in HBM before timing
-    eng.set_frame(d_frame)
+    h_frame = torch.from_numpy(frame).pin_memory()  # the caller's plane, in pinned host memory
+    eng.set_frame(h_frame.numpy())
     eng.set_domains(doms)
     eng.set_ranges(mine)
-    mine_bytes = torch.zeros(plan_capacity(plan) * TUPLE_BYTES, dtype=torch.uint8, device=dev)
 
-    def step():
-        eng.run()
-        if world > 1:  # RCCL all-gather of the 32-byte (domain, t, s, o, rms) tuples (same stream)
-            eng.copy_tuples_device(mine_bytes.data_ptr())
-            gather_tuples(mine_bytes, plan)
-
+    # ---- headline: the end-to-end step ----
+    step = FrameStep(eng, h_frame.numpy(), plan, rank, dev)
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize(dev)
+    _sync(dev)
     eng.timing_history()  # drop the warmup runs: the history now covers exactly the timed steps
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    elapsed = time.perf_counter() - t0
+    _, elapsed = timed(step, args.steps, world, dev)
     hist = eng.timing_history()  # per-run HIP events of the K timed steps (on the kernel's stream)
     # the library keeps the last 256 runs: with more steps the mean is over the last 256 of them
     assert len(hist) == min(args.steps, 256), (len(hist), args.steps)
-    _, st = eng.fetch()
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    main_out, st = eng.fetch()  # the timed steps' records (the SEA engine is checked against them)
+    gathered = step.tuples_bytes()
+    own = eng.fetch_tuples().tobytes() if len(mine) else b""
+    checks = {"own_slice_in_gather": step.own_slice_ok(own)}
 
     kernel_ms = float(np.mean(hist["ms_search"]))
-    ms_per_step = 1000.0 * elapsed / args.steps
-    value = nr_total / (elapsed / args.steps)
     engine_name = {1: "valu", 2: "mfma"}.get(st["engine"], "valu")
     form = F.FORM_NAMES.get(st["search_form"], engine_name)
     n_d = len(doms)
     direct_ops = 2 * 64 * args.transforms * n_d * len(mine)  # one MAC per pixel per candidate
     traffic, traffic_src = load_traffic(form)
     if engine_name == "mfma":
-        # the matrix flops the search issues: the Fourier form's own count (8 MFMA 32x32x16 per
-        # 32-range × 32-domain tile pair), half the direct form's §8(d) count for the same result
+        # the matrix flops the search issues: the Fourier form's own count (6 MFMA 32x32x16 per
+        # 32-range × 32-domain tile pair), fewer than the direct form's §8(d) count for the same result
         work = st["matrix_flops"]
         bound, peak, unit = "mfma", MFMA_F16_PEAK_TFLOPS, "TFLOP/s"
     else:
@@ -289,92 +390,76 @@ def main(args):
         roof["traffic_source"] = traffic_src
     else:
         roof["traffic_note"] = traffic_src
-    line = {
-        "metric": METRIC,
-        "value": round(value, 1),
-        "unit": "range-blocks/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(ms_per_step, 3),
-        "higher_is_better": True,
-        "scaling": "strong",
-        "vs_baseline": None,
+    line = headline_fields(nr_total, world, args.steps, args.warmup, elapsed)
+    line.update({
         "dtype": "u16" if engine_name == "valu" else "f16",
+        "arith": ARITH if engine_name == "mfma" else "exact integer (u16 x u16 -> u32 dot products), fit in fp64",
         "data": "synthetic",
         "config": {"workload": f"C3: {S}x{S} S1 value-noise frame (seed 1234), 8x8 ranges ({nr_total}), "
                                f"16x16 domains stride 8 ({n_d}), T={args.transforms}, exhaustive, rms 0",
                    "engine": engine_name, "ranges_per_gpu": len(mine), "parallelism": f"ranges/{world}",
                    "env": frac_env(), "ab_run": bool(knobs)},
+        "step": "frame H2D (pinned, 16 MiB per rank) + pool build + search + fit of the rank's shard + 32-byte "
+                "tuples packed on the device + all-gather over ranks (N > 1) + gathered tuples D2H (pinned); "
+                "serial, barrier + synchronisation around the timed steps, slowest rank",
         "roofline": roof,
         "search_form": form,
         "phases_ms": {k: round(float(np.mean(hist["ms_" + k])), 3) for k in ("device", "prep", "search", "finish")},
         "fallback_ranges": st["fallback_ranges"],
         "source_id": lib_sha16(),
         "build": build,  # the loaded library's compiled-in id (frac_build_id): the binary that ran
-    }
+    })
 
-    main_out, _ = eng.fetch()  # the timed steps' records (the SEA engine is checked against them)
-
-    # host boundary (§8(d) end-to-end): frame H2D from pinned memory + search + tuples D2H, per step
-    e2e_steps = args.steps if args.e2e_steps < 0 else args.e2e_steps
-    if e2e_steps > 0:
-        h_frame = torch.from_numpy(frame).pin_memory()
-        h_tuples = torch.empty(len(mine) * TUPLE_BYTES, dtype=torch.uint8).pin_memory()
-        tup = h_tuples.numpy().view(F.TUPLE)
-        eng.set_frame(h_frame.numpy())
-        eng.run()
-        eng.fetch_tuples(tup)
-        if world > 1:
-            dist.barrier()
-        t0 = time.perf_counter()
-        for _ in range(e2e_steps):
-            eng.set_frame(h_frame.numpy())  # same geometry: no re-preparation, the plane is re-uploaded
-            eng.run()
-            eng.fetch_tuples(tup)
-        e2e = time.perf_counter() - t0
-        if world > 1:
-            t = torch.tensor([e2e], dtype=torch.float64, device=dev)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            e2e = float(t.item())
-        line["e2e"] = {"value": round(nr_total / (e2e / e2e_steps), 1), "ms_per_step": round(1e3 * e2e / e2e_steps, 3),
-                       "steps": e2e_steps,
-                       "step": "frame H2D (pinned, 16 MiB) + search + tuples D2H (pinned, 32 B per range)"
-                               + (" per rank; no gather" if world > 1 else "")}
-        # the same through two contexts in turn (a frame stream): frame k+1 uploads on one context's stream
-        # while frame k searches on the other's, and frame k's tuples come back while k+1 searches
+    side_steps = args.steps if args.side_steps < 0 else args.side_steps
+    if side_steps > 0:
+        # the device-only rate: the frame resident in HBM, the gathered tuples left on the device
+        d_frame = torch.from_numpy(frame).to(dev)
+        eng.set_frame(d_frame)
+        dstep = FrameStep(eng, None, plan, rank, dev, device_resident=True)
+        dstep()
+        _, dsec = timed(dstep, side_steps, world, dev)
+        checks["device_leg_equals_e2e"] = dstep.tuples_bytes() == gathered
+        line["device_value"] = {"value": round(nr_total / (dsec / side_steps), 1),
+                                "ms_per_step": round(1e3 * dsec / side_steps, 3), "steps": side_steps,
+                                "step": "the same with the frame resident in HBM before timing and the gathered "
+                                        "tuples left on the device"}
+        # a frame stream: two contexts in turn, frame k+1 uploads on one context's stream while frame k
+        # searches on the other's, and frame k's tuples come back while k+1 searches (per rank, no gather)
+        tup = h_tuples = None
+        if len(mine):
+            h_tuples = [torch.empty(len(mine) * TUPLE_BYTES, dtype=torch.uint8).pin_memory() for _ in range(2)]
+            tup = [h.numpy().view(F.TUPLE) for h in h_tuples]
         with F.Engine(dev.index, args.transforms, False, 0.0, -1.0, engine_id) as eng2:
+            eng.set_frame(h_frame.numpy())
             eng2.set_frame(h_frame.numpy())
             eng2.set_domains(doms)
             eng2.set_ranges(mine)
-            eng2.run()
-            eng2.fetch_tuples(tup)
             ctxs = (eng, eng2)
-            tups = (tup, torch.empty(len(mine) * TUPLE_BYTES, dtype=torch.uint8).pin_memory().numpy().view(F.TUPLE))
-            if world > 1:
-                dist.barrier()
-            t0 = time.perf_counter()
-            for k in range(e2e_steps + 1):
-                if k < e2e_steps:
-                    ctxs[k & 1].set_frame(h_frame.numpy())  # waits for this context's own upload only
-                    ctxs[k & 1].run()
-                if k > 0:
-                    ctxs[(k - 1) & 1].fetch_tuples(tups[(k - 1) & 1])  # frame k−1's winners
-            e2p = time.perf_counter() - t0
-            if world > 1:
-                t = torch.tensor([e2p], dtype=torch.float64, device=dev)
-                dist.all_reduce(t, op=dist.ReduceOp.MAX)
-                e2p = float(t.item())
-            line["e2e"]["pipelined"] = {"value": round(nr_total / (e2p / e2e_steps), 1),
-                                        "ms_per_step": round(1e3 * e2p / e2e_steps, 3),
-                                        "step": "the same per frame, two contexts alternating frames"}
+
+            def stream_steps():
+                for k in range(side_steps + 1):
+                    if k < side_steps:
+                        ctxs[k & 1].set_frame(h_frame.numpy())  # waits for this context's own upload only
+                        ctxs[k & 1].run()
+                    if k > 0 and tup is not None:
+                        ctxs[(k - 1) & 1].fetch_tuples(tup[(k - 1) & 1])  # frame k−1's winners
+
+            stream_steps()
+            _, ssec = timed(stream_steps, 1, world, dev)
+            line["stream_value"] = {"value": round(nr_total / (ssec / side_steps), 1),
+                                    "ms_per_step": round(1e3 * ssec / side_steps, 3), "steps": side_steps,
+                                    "step": "frame H2D + search + tuples D2H per frame, two contexts alternating "
+                                            "frames" + (" (per rank, no gather)" if world > 1 else "")}
         eng.set_frame(d_frame)
         eng.run()
+    line["records"] = {"tuples_sha16": digest(gathered), "n": nr_total, **checks}
 
     if world == 1 and engine_name == "mfma" and args.alt_steps > 0:
-        # the same workload on the other engines, measured the same way: the VALU engine (packed-u16
-        # v_dot2, north_star's no-MFMA formulation, exhaustive) and the SEA engine (successive
-        # elimination: identical records, most candidates skipped by an exact bound, data-dependent)
+        # the same workload on the other engines, frame resident, measured the same way: the VALU engine
+        # (packed-u16 v_dot2, north_star's no-MFMA formulation, exhaustive) and the SEA engine
+        # (successive elimination: identical records, most candidates skipped by an exact bound,
+        # data-dependent)
+        d_frame = torch.from_numpy(frame).to(dev)
         line["alt_engines"] = {}
         for alt_name, alt_id in (("valu", F.ENGINE_VALU), ("sea", F.ENGINE_SEA)):
             with F.Engine(dev.index, args.transforms, False, 0.0, -1.0, alt_id, timing=True) as alt:
@@ -394,7 +479,7 @@ def main(args):
                 alt_out, ast = alt.fetch()
             a_ms = float(np.mean(ah["ms_search"]))
             entry = {"value": round(nr_total / alt_sec, 1), "ms_per_step": round(alt_sec * 1e3, 3),
-                     "steps": args.alt_steps, "dtype": "u16",
+                     "steps": args.alt_steps, "dtype": "u16", "step": "device-resident (as device_value)",
                      "phases_ms": {k: round(float(np.mean(ah["ms_" + k])), 3) for k in ("prep", "search", "finish")}}
             if alt_name == "valu":
                 alt_ach = direct_ops / (a_ms * 1e-3) / 1e12
@@ -418,5 +503,5 @@ def main(args):
 if __name__ == "__main__":
     _args = parse()
     if _args.gpus > 1 and "WORLD_SIZE" not in os.environ:
-        sys.exit(launch_ranks(_args))
+        sys.exit(launch_ranks(_args.gpus))
     main(_args)

@@ -462,7 +462,12 @@ int upload_plane(frac_ctx* c, const uint8_t* p, uint32_t w, uint32_t h, uint32_t
     dstride = (w + 63u) & ~63u;
     // one extra row + column of slack: kernels never read it, but keeps every 2×2 read in-bounds
     FRAC_HIP(c, d.ensure((size_t)dstride * (h + 1)));
-    FRAC_HIP(c, hipMemcpy2DAsync(d.ptr, dstride, p, stride, w, h, hipMemcpyHostToDevice, c->stream));
+    if (h == 0 || w == 0)
+        return FRAC_OK;
+    if (stride == dstride) // rows already at the device pitch: one linear copy (a 2-D copy is a slower path)
+        FRAC_HIP(c, hipMemcpyAsync(d.ptr, p, (size_t)stride * (h - 1) + w, hipMemcpyHostToDevice, c->stream));
+    else
+        FRAC_HIP(c, hipMemcpy2DAsync(d.ptr, dstride, p, stride, w, h, hipMemcpyHostToDevice, c->stream));
     FRAC_HIP(c, hipStreamSynchronize(c->stream));
     return FRAC_OK;
 }
@@ -2297,6 +2302,14 @@ bool qt_device_planned(const frac_ctx* c, const frac_quadtree_params* qp)
 {
     if (c->p.engine != FRAC_ENGINE_AUTO && c->p.engine != FRAC_ENGINE_MFMA)
         return false;
+    // the planner hard-codes the shipped layouts (8-wave Fourier work items, the default direct variants):
+    // a tuning build with an A/B knob set runs the host-planned levels, which honour it
+    if (kTuningBuild)
+        for (const char* k : kAbKnobs) {
+            const char* v = getenv(k);
+            if (v && *v)
+                return false;
+        }
     for (uint32_t n = qp->max_size; n >= qp->min_size; n /= 2)
         if (compute_hit_limit(c->p.rms_threshold, 4 * n * n) >= kExactLimit)
             return false;
@@ -3062,6 +3075,16 @@ int frac_encode_quadtree(frac_ctx* c, const frac_quadtree_params* qp, frac_encod
         return c->fail(FRAC_E_INVALID, "quadtree: sizes must be 2, 4, 8 or 16 with min_size <= max_size");
     if (!c->planes_set)
         return c->fail(FRAC_E_STATE, "quadtree: no frame set");
+    {
+        // the device-planned path never enters frac_run, so it checks the A/B knobs itself (a product
+        // build refuses them here as frac_run does)
+        std::string msg;
+        if (check_ab_knobs(msg) != FRAC_OK)
+            return c->fail(FRAC_E_INVALID, msg);
+    }
+    // every buffer below (ensure(), the pinned counters, the level launches) belongs to this context's
+    // device, whatever device the calling thread has current
+    FRAC_HIP(c, hipSetDevice(c->device));
     const uint32_t W = c->src.w, H = c->src.h;
     if (!c->same_plane && (c->tgt.w != W || c->tgt.h != H))
         return c->fail(FRAC_E_INVALID, "quadtree: source and target planes must have one size");

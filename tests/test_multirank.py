@@ -11,6 +11,7 @@ import pytest
 import torch.multiprocessing as mp
 
 from fractencode_amd.distributed import plan_capacity, range_costs, shard_bounds, shard_capacity, shard_plan
+from oracle_engine import OracleEngine
 
 
 def test_shard_bounds_cover_all_items_once():
@@ -48,46 +49,6 @@ def test_range_costs_are_bucket_sizes():
     r = np.zeros(4, dtype=F.GRID_ITEM)
     r["category"] = [0, 1, 3, -1]
     np.testing.assert_array_equal(range_costs(r, d), [3, 4, 1, 2])
-
-
-class OracleEngine:
-    """Engine-interface stand-in (CPU): set_ranges / run / fetch_tuples / sync."""
-
-    def __init__(self, plane, doms, use_classifier=False):
-        from oracle import oracle as O
-        self.O, self.plane, self.doms = O, plane, doms
-        self.use_classifier = use_classifier
-        self.index = {(int(d["x"]), int(d["y"])): i for i, d in enumerate(doms)}
-
-    def set_ranges(self, r):
-        self.r = r
-
-    def run(self):
-        import fractencode_amd as F
-        out, _, _ = self.O.estimate(self.plane, self.doms, self.r.astype(self.O.ITEM_DTYPE), threads=2,
-                                    use_classifier=self.use_classifier)
-        rec = np.zeros(len(out), dtype=F.ENCODE_ITEM)
-        rec["x"], rec["y"], rec["w"], rec["h"] = self.r["x"], self.r["y"], self.r["w"], self.r["h"]
-        rec["distance"], rec["contrast"], rec["brightness"] = out["dist"], out["s"], out["o"]
-        rec["transform"], rec["dx"], rec["dy"], rec["sw"], rec["sh"] = out["t"], out["dx"], out["dy"], out["dw"], out["dh"]
-        self.rec = rec
-
-    def classify(self, items, target_plane=False):
-        out = items.copy()
-        out["category"] = self.O.classify(self.plane, items.astype(self.O.ITEM_DTYPE))["category"]
-        return out
-
-    def fetch_tuples(self):
-        import fractencode_amd as F
-        t = np.zeros(len(self.rec), dtype=F.TUPLE)
-        for k in ("transform", "contrast", "brightness", "distance"):
-            t[k] = self.rec[k]
-        t["domain"] = [self.index[(int(x), int(y))] if w else F.NO_DOMAIN
-                       for x, y, w in zip(self.rec["dx"], self.rec["dy"], self.rec["sw"])]
-        return t
-
-    def sync(self):
-        pass
 
 
 def _worker(rank, world, port, path):
