@@ -139,6 +139,7 @@ def lib() -> C.CDLL:
         vp, u32, i32, sz = C.c_void_p, C.c_uint32, C.c_int, C.c_size_t
         sig = {
             "frac_abi_version": (i32, []),
+            "frac_device_count": (i32, []),
             "frac_build_id": (C.c_char_p, []),
             "frac_build_flags": (i32, []),
             "frac_create": (vp, [i32, C.POINTER(FracParams)]),

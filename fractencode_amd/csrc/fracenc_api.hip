@@ -2614,6 +2614,17 @@ extern "C" {
 
 int frac_abi_version(void) { return FRAC_ABI_VERSION; }
 
+int frac_device_count(void)
+{
+    int count = 0;
+    const hipError_t e = hipGetDeviceCount(&count);
+    if (e != hipSuccess) {
+        g_last_error = std::string("hipGetDeviceCount: ") + hipGetErrorString(e);
+        return FRAC_E_DEVICE;
+    }
+    return count;
+}
+
 // The source id build() compiles in (-DFRAC_SOURCE_ID="…": the hash fractencode_amd.source_id()
 // computes over csrc/ and include/fracenc.h), so a result can name the binary that produced it.
 #ifndef FRAC_SOURCE_ID

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define FRAC_ABI_VERSION 6
+#define FRAC_ABI_VERSION 7
 
 /* error codes */
 #define FRAC_OK 0
@@ -134,6 +134,10 @@ const char* frac_build_id(void);
 /* FRAC_BUILD_* bits of this library build. */
 #define FRAC_BUILD_TUNING 1 /* -DFRAC_TUNING: ablation variants (wrong results by design) compiled in */
 int frac_build_flags(void);
+/* The number of HIP devices this process sees (ABI 7), or a negative FRAC_E_DEVICE: a caller without
+ * the HIP runtime (the reference's EncodingEngineCore2) registers one engine per device with it
+ * (Multi-GPU). */
+int frac_device_count(void);
 /* NULL on failure (message via frac_last_error(NULL)). */
 frac_ctx* frac_create(int device, const frac_params* params);
 void frac_destroy(frac_ctx* ctx);

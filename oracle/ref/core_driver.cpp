@@ -10,11 +10,15 @@
 // instantiation access idiom (access checks do not apply to explicit instantiations,
 // [temp.spec.general]/6) — the registration itself, nothing else.
 //
-// usage: core_driver PLANE.u8 W H SRC TGT CLASSIFIER(0|1) RMS_THR SMAX OUT.bin [CPU(0|1)]
+// usage: core_driver PLANE.u8 W H SRC TGT CLASSIFIER(0|1) RMS_THR SMAX OUT.bin [CPU(0|1) [DEVICES]]
+//   DEVICES: a comma list of HIP devices, one HipEncodingEngine2 registered per entry (default "0";
+//   "0,0" = two engines, two contexts, on device 0 — the one-GPU box's stand-in for one engine per
+//   device; "all" = one per device frac_device_count() reports).
 //   OUT.bin: the core's result().encoded (encode_item_t, 64 B each) in the core's order, then the
 //   rejected-mapping count of the whole search (u64: the CPU engines' estimator plus the HIP
-//   engine's) and the number of ranges the HIP engine searched (u64).
-//   Exit 6 (message on stderr) when the HIP engine's finalize() failed: rethrowIfFailed() on this
+//   engines'), the number of ranges the HIP engines searched (u64), each HIP engine's own count
+//   (u64 each, in registration order) and the number of HIP engines (u64).
+//   Exit 6 (message on stderr) when a HIP engine's finalize() failed: rethrowIfFailed() on this
 //   thread, after the core's workers have joined — not std::terminate on a worker.
 #include "encode/EncodingEngine2.hpp"
 #include "encode/Classifier2.hpp"
@@ -24,8 +28,11 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <fstream>
 #include <memory>
+#include <sstream>
+#include <string>
 #include <vector>
 
 using namespace Frac2;
@@ -46,8 +53,22 @@ struct NullReporter : ProgressReporter2 {
 
 int main(int argc, char** argv)
 {
-    if (argc != 10 && argc != 11) {
-        std::fprintf(stderr, "usage: %s PLANE W H SRC TGT CLS THR SMAX OUT [CPU]\n", argv[0]);
+    if (argc < 10 || argc > 12) {
+        std::fprintf(stderr, "usage: %s PLANE W H SRC TGT CLS THR SMAX OUT [CPU [DEVICES]]\n", argv[0]);
+        return 2;
+    }
+    std::vector<int> devices;
+    if (argc == 12 && std::strcmp(argv[11], "all") == 0) {
+        const int n = frac_device_count();
+        for (int d = 0; d < n; ++d)
+            devices.push_back(d);
+    } else {
+        std::stringstream ss(argc == 12 ? argv[11] : "0");
+        for (std::string tok; std::getline(ss, tok, ',');)
+            devices.push_back(std::atoi(tok.c_str()));
+    }
+    if (devices.empty()) {
+        std::fprintf(stderr, "no HIP device to register\n");
         return 2;
     }
     const uint32_t W = std::atoi(argv[2]), H = std::atoi(argv[3]);
@@ -57,7 +78,7 @@ int main(int argc, char** argv)
     params.noclassifier = std::atoi(argv[6]) == 0;
     params.rmsThreshold = std::atof(argv[7]);
     params.sMax = std::atof(argv[8]);
-    params.nocpu = argc == 11 ? std::atoi(argv[10]) == 0 : true;
+    params.nocpu = argc >= 11 ? std::atoi(argv[10]) == 0 : true;
     std::vector<uint8_t> buf(size_t(W) * H);
     {
         std::ifstream f(argv[1], std::ios::binary);
@@ -86,30 +107,45 @@ int main(int argc, char** argv)
     NullReporter reporter;
     EncodingEngineCore2 core(params, image, sourceGrid, estimator, &reporter);
     uint64_t rejected = 0;
-    HipEncodingEngine2* hip = nullptr;
-    try { // EncodingEngine2.cpp:21-29, filled in
-        auto engine = std::make_unique<HipEncodingEngine2>(params, image, sourceGrid);
-        engine->setName("HIP");
-        hip = engine.get();
-        engines_of(core).push_back(std::move(engine));
-    } catch (const std::exception& exc) {
-        std::printf("failed to create engine: %s\n", exc.what());
-        return 4;
+    std::vector<HipEncodingEngine2*> hips;
+    // EncodingEngine2.cpp:21-29, filled in: one engine per device; all of them
+    // claim from the core's one queue (EncodingEngine2.hpp:126-168), beside the CPU engines unless --nocpu
+    for (size_t i = 0; i < devices.size(); ++i) {
+        try {
+            auto engine = std::make_unique<HipEncodingEngine2>(params, image, sourceGrid, devices[i]);
+            engine->setName("HIP " + std::to_string(i));
+            hips.push_back(engine.get());
+            engines_of(core).push_back(std::move(engine));
+        } catch (const std::exception& exc) {
+            std::printf("failed to create engine: %s\n", exc.what());
+            return 4;
+        }
     }
     core.encode(targetGrid);
-    try {
-        hip->rethrowIfFailed(); // the failure of finalize(), on this thread
-    } catch (const std::exception& exc) {
-        std::fprintf(stderr, "HIP engine failed: %s (%zu ranges without a record)\n", exc.what(), hip->lostRanges());
-        return 6;
+    for (HipEncodingEngine2* hip : hips) {
+        try {
+            hip->rethrowIfFailed(); // the failure of finalize(), on this thread
+        } catch (const std::exception& exc) {
+            std::fprintf(stderr, "HIP engine failed: %s (%zu ranges without a record)\n", exc.what(), hip->lostRanges());
+            return 6;
+        }
     }
     // the CPU engines' rejected mappings accumulate in the shared estimator (TransformEstimator2.hpp:59)
-    rejected = estimator.rejectedMappings() + hip->rejectedMappings();
-    const uint64_t hip_ranges = hip->searchedRanges();
+    rejected = estimator.rejectedMappings();
+    uint64_t hip_ranges = 0;
+    std::vector<uint64_t> per_engine;
+    for (HipEncodingEngine2* hip : hips) {
+        rejected += hip->rejectedMappings();
+        hip_ranges += hip->searchedRanges();
+        per_engine.push_back(hip->searchedRanges());
+    }
+    const uint64_t n_hip = hips.size();
     const auto data = core.result();
     std::ofstream out(argv[9], std::ios::binary);
     out.write(reinterpret_cast<const char*>(data.encoded.data()), data.encoded.size() * sizeof(Frac::encode_item_t));
     out.write(reinterpret_cast<const char*>(&rejected), sizeof(rejected));
     out.write(reinterpret_cast<const char*>(&hip_ranges), sizeof(hip_ranges));
+    out.write(reinterpret_cast<const char*>(per_engine.data()), per_engine.size() * sizeof(uint64_t));
+    out.write(reinterpret_cast<const char*>(&n_hip), sizeof(n_hip));
     return out ? 0 : 5;
 }

@@ -39,19 +39,24 @@ def test_binding_compiles_against_reference_headers(tmp_path):
     assert os.path.exists(DRIVER), "oracle/_ref/core_driver not built (__graft_entry__.build)"
 
 
-def _run_core(tmp_path, plane_name, W, H, src, tgt, cls, cpu=False, check=True):
+def _run_core(tmp_path, plane_name, W, H, src, tgt, cls, cpu=False, check=True, devices=None, per_engine=False):
     out = tmp_path / f"core_{src}_{tgt}_{cls}_{int(cpu)}.bin"
     plane_path = plane_name if os.path.isabs(plane_name) else os.path.join(GOLD, plane_name + ".u8")
-    r = subprocess.run([DRIVER, plane_path, str(W), str(H), str(src), str(tgt),
-                        str(int(cls)), "0", "-1", str(out), str(int(cpu))], timeout=600, capture_output=True, text=True)
+    r = subprocess.run([DRIVER, plane_path, str(W), str(H), str(src), str(tgt), str(int(cls)), "0", "-1", str(out),
+                        str(int(cpu))] + ([devices] if devices else []), timeout=600, capture_output=True, text=True)
     if not check:
         return r
     assert r.returncode == 0, (r.returncode, r.stdout[-2000:], r.stderr[-2000:])
     raw = out.read_bytes()
-    n = (len(raw) - 16) // 64
+    # trailer: rejected, HIP ranges, one count per HIP engine, the number of HIP engines (u64 each)
+    k = int(np.frombuffer(raw[-8:], dtype=np.uint64)[0])
+    n = (len(raw) - 8 * (3 + k)) // 64
     rec = np.frombuffer(raw[: n * 64], dtype=F.ENCODE_ITEM)
-    rejected, hip_ranges = (int(v) for v in np.frombuffer(raw[n * 64:], dtype=np.uint64))
-    return rec[np.lexsort((rec["x"], rec["y"]))], rejected, hip_ranges
+    tail = [int(v) for v in np.frombuffer(raw[n * 64:], dtype=np.uint64)]
+    rejected, hip_ranges, each = tail[0], tail[1], tail[2:2 + k]
+    assert sum(each) == hip_ranges
+    rec = rec[np.lexsort((rec["x"], rec["y"]))]
+    return (rec, rejected, hip_ranges, each) if per_engine else (rec, rejected, hip_ranges)
 
 
 @pytest.mark.skipif(not os.path.exists(DRIVER), reason="oracle/_ref/core_driver not built")
@@ -101,3 +106,25 @@ def test_hip_engine_failure_comes_back_on_the_callers_thread(tmp_path):
     assert r.returncode == 6, (r.returncode, r.stdout[-2000:], r.stderr[-2000:])
     assert "HIP engine failed" in r.stderr and "range sides must be 2..256" in r.stderr
     assert "4 ranges without a record" in r.stderr
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cpu", [False, True], ids=["hips_only", "cpu_and_hips"])
+@pytest.mark.parametrize("name,cls", [("lenna_t4", False), ("lenna_cls", True)])
+def test_reference_core_with_two_hip_engines_on_one_queue(tmp_path, name, cls, cpu):
+    """Two HipEncodingEngine2 registered in the reference's core (two contexts on device 0 — the one-GPU
+    box's stand-in for one engine per device, INTEGRATION.md §Multi-GPU) claim ranges from the core's
+    one queue (EncodingEngine2.hpp:126-168), with and without the CPU engines beside them: each HIP
+    engine searched ranges, and the records and reject count equal the reference goldens."""
+    assert os.path.exists(DRIVER), "oracle/_ref/core_driver must be built in the build container"
+    rec, meta = golden(name)
+    got, rejected, hip_ranges, each = _run_core(tmp_path, "lenna_y", 512, 512, 16, 8, cls, cpu=cpu, devices="0,0",
+                                                per_engine=True)
+    assert len(each) == 2 and all(c > 0 for c in each), each
+    assert len(got) == len(rec["x"])
+    assert (hip_ranges < len(got)) if cpu else (hip_ranges == len(got))
+    fields = {"x": got["x"], "y": got["y"], "dx": got["dx"], "dy": got["dy"], "dw": got["sw"], "dh": got["sh"],
+              "t": got["transform"], "dist": got["distance"], "s": got["contrast"], "o": got["brightness"]}
+    for k in FIELDS:
+        np.testing.assert_array_equal(fields[k], rec[k], err_msg=f"{name}: {k}")
+    assert rejected == meta["rejected"]
