@@ -37,7 +37,32 @@ TUPLE = np.dtype([("domain", "<u4"), ("transform", "<i4"), ("contrast", "<f8"), 
 # frac_run_timing: per-run device times (frac_timing_history)
 RUN_TIMING = np.dtype([("ms_device", "<f8"), ("ms_prep", "<f8"), ("ms_search", "<f8"), ("ms_finish", "<f8")])
 NO_DOMAIN = 0xFFFFFFFF
-assert GRID_ITEM.itemsize == 20 and ENCODE_ITEM.itemsize == 64 and TUPLE.itemsize == 32
+# frac_qt_leaf: a quadtree leaf in 32 bytes (frac_encode_quadtree_leaves, ABI 7)
+QT_LEAF = np.dtype([("x", "<u2"), ("y", "<u2"), ("code", "<u4"), ("contrast", "<f8"), ("brightness", "<f8"),
+                    ("distance", "<f8")])
+QT_NO_DOMAIN = 0xFFFFFF
+assert GRID_ITEM.itemsize == 20 and ENCODE_ITEM.itemsize == 64 and TUPLE.itemsize == 32 and QT_LEAF.itemsize == 32
+
+
+def records_from_leaves(leaves: np.ndarray, width: int) -> np.ndarray:
+    """encode_item_t records (ENCODE_ITEM) from 32-byte quadtree leaves (QT_LEAF) of a frame `width`
+    pixels wide: the range at (x, y) of size n = 1 << (code >> 28), the winner domain `code & 0xffffff` of
+    that level's grid createUniformGrid(W, H, 2n, n) (cols = (W − 2n)/n + 1), transform (code >> 24) & 15;
+    QT_NO_DOMAIN is the reference's default record (domain (0, 0), size (0, 0))."""
+    code = np.asarray(leaves["code"], np.uint32)
+    n = (np.uint32(1) << (code >> np.uint32(28))).astype(np.uint32)
+    d = (code & np.uint32(QT_NO_DOMAIN)).astype(np.int64)
+    has = d != QT_NO_DOMAIN
+    cols = np.where(width >= 2 * n, (np.int64(width) - 2 * n.astype(np.int64)) // n + 1, 1)
+    rec = np.zeros(len(leaves), dtype=ENCODE_ITEM)
+    rec["x"], rec["y"], rec["w"], rec["h"] = leaves["x"], leaves["y"], n, n
+    for k in ("contrast", "brightness", "distance"):
+        rec[k] = leaves[k]
+    rec["transform"] = ((code >> np.uint32(24)) & np.uint32(15)).astype(np.int32)
+    rec["dx"] = np.where(has, (d % cols) * n, 0)
+    rec["dy"] = np.where(has, (d // cols) * n, 0)
+    rec["sw"] = rec["sh"] = np.where(has, 2 * n, 0)
+    return rec
 
 ENGINE_AUTO, ENGINE_VALU, ENGINE_MFMA, ENGINE_SEA = 0, 1, 2, 3
 FORM_DOT2, FORM_DIRECT, FORM_FOURIER, FORM_SEA, FORM_SEA_MFMA, FORM_SAMPLED = 0, 1, 2, 3, 4, 5
@@ -170,6 +195,8 @@ def lib() -> C.CDLL:
             "frac_classify_items": (i32, [vp, vp, sz, i32]),
             "frac_encode_quadtree": (i32, [vp, C.POINTER(FracQuadtreeParams), vp, sz, C.POINTER(sz),
                                            C.POINTER(FracStats)]),
+            "frac_encode_quadtree_leaves": (i32, [vp, C.POINTER(FracQuadtreeParams), vp, sz, C.POINTER(sz),
+                                                  C.POINTER(FracStats)]),
             "frac_rgb_to_yuv_device": (i32, [vp, vp, u32, u32, u32, vp, u32, vp, u32, vp, u32]),
             "frac_rgb_to_yuv": (i32, [vp, vp, u32, u32, u32, vp, vp, vp]),
             "frac_uniform_grid": (sz, [u32, u32, u32, u32, vp, sz]),
@@ -411,31 +438,38 @@ class Engine:
         return plane, it.value, rms.value
 
     def encode_quadtree(self, max_size: int = 16, min_size: int = 4, split_distance: float = 10.0, out=None,
-                        allow_short: bool = False):
+                        allow_short: bool = False, leaves: bool = False):
         """Quadtree partition of the frame set on this engine (frac_encode_quadtree): ranges of
         max_size split into quadrants while their best distance exceeds split_distance, down to
         min_size.  Returns (encode items of mixed sizes, summed stats dict).  With `out` (an
         ENCODE_ITEM array of at least (W/min_size)·(H/min_size) items, e.g. pinned host memory)
         the items are written there and a view of it is returned, without a copy; pinned host memory is
         written by the device directly (no copy command).  allow_short: `out` may be shorter — the items
-        past it are counted (the stats) but not written, and the returned view is cut to `out`."""
+        past it are counted (the stats) but not written, and the returned view is cut to `out`.
+        leaves=True: 32-byte QT_LEAF items instead (frac_encode_quadtree_leaves; records_from_leaves rebuilds
+        the records), half the bytes across PCIe."""
         qp = FracQuadtreeParams(max_size, min_size, split_distance)
         n = C.c_size_t(0)
         st = FracStats()
         W, H = self._frame_wh
         cap = max((W // min_size) * (H // min_size), 1)
+        dt = QT_LEAF if leaves else ENCODE_ITEM
         if out is not None:
-            if out.dtype != ENCODE_ITEM or not out.flags.c_contiguous or (len(out) < cap and not allow_short):
-                raise ValueError(f"out must be a contiguous ENCODE_ITEM array of at least {cap} items")
+            if out.dtype != dt or not out.flags.c_contiguous or (len(out) < cap and not allow_short):
+                raise ValueError(f"out must be a contiguous {'QT_LEAF' if leaves else 'ENCODE_ITEM'} array of at "
+                                 f"least {cap} items")
             buf = out
             cap = len(out)
         else:
             # one pass with a worst-case capacity (every range at min_size), in a buffer kept across
             # calls: a fresh one costs a page fault per 4 KiB on first touch
-            buf = getattr(self, "_qt_buf", None)
+            attr = "_qt_leaf_buf" if leaves else "_qt_buf"
+            buf = getattr(self, attr, None)
             if buf is None or len(buf) < cap:
-                buf = self._qt_buf = np.empty(cap, dtype=ENCODE_ITEM)
-        self._check(lib().frac_encode_quadtree(self._ctx, C.byref(qp), buf.ctypes.data, cap, C.byref(n), C.byref(st)))
+                buf = np.empty(cap, dtype=dt)
+                setattr(self, attr, buf)
+        fn = lib().frac_encode_quadtree_leaves if leaves else lib().frac_encode_quadtree
+        self._check(fn(self._ctx, C.byref(qp), buf.ctypes.data, cap, C.byref(n), C.byref(st)))
         d = st.as_dict()
         d["items"] = n.value
         return (buf[: min(n.value, cap)] if out is not None else buf[: n.value].copy()), d

@@ -224,6 +224,9 @@ struct frac_ctx {
     DBuf<int32_t> d_dft_trmax; // the six-MFMA fast path's per-tile R6 threshold (kDftFast6)
     DBuf<uint32_t> d_dft_tpool; // pool rows in tile order (resolve_dft)
     DBuf<uint32_t> d_dft_rorb;  // range pixel pairs in orbit order, per slot (resolve_dft)
+    DBuf<frac_qt_leaf> d_qt_leaves32; // frac_encode_quadtree_leaves' device-side leaves (pageable caller buffer)
+    DBuf<uint2> d_dft_tdom;     // each tile row's domain origin (dft_domain_build → resolve_dft's fit)
+    DBuf<unsigned long long> d_dft_slotbest; // per slot the search's merged maximum (search_dft → resolve_dft)
     DBuf<uint4> d_rstat;        // per range: the winner's sums (resolve_dft → fit_rstat)
     DBuf<frac_grid_item> d_cls_items;
     DBuf<uint32_t> d_cls_list;
@@ -1374,6 +1377,8 @@ inline int launch_dft(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool i
     b.pool = c->d_pool.ptr;
     b.negsd2 = c->d_negsd2.ptr;
     b.tpool = c->d_dft_tpool.ptr;
+    FRAC_HIP(c, c->d_dft_tdom.ensure(std::max<size_t>((size_t)c->ntiles * 32, 1)));
+    b.tdom = c->d_dft_tdom.ptr;
     MfmaRangePrepArgs r;
     r.tgt = dtgt;
     r.tstride = tstride;
@@ -1387,6 +1392,12 @@ inline int launch_dft(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool i
     r.plan = c->qplan;
     FRAC_HIP(c, c->d_dft_rorb.ensure(std::max<size_t>((size_t)r.nblocks * 32 * 32, 1)));
     r.rorb = c->d_dft_rorb.ptr;
+    // the search merges its domain splits per slot (64-bit atomicMax; reset by the range prep), so the resolve
+    // reads one word per slot instead of walking the block's entries through the CSR map
+    // (search_dft2, an A/B form of the tuning build, writes entries only)
+    const bool slotbest = !(kTuningBuild && ((form == 6 && var == 23) || (!dft_four_wave(var) && var == 12)));
+    FRAC_HIP(c, c->d_dft_slotbest.ensure(std::max<size_t>((size_t)r.nblocks * 32, 1)));
+    r.slotbest = slotbest ? c->d_dft_slotbest.ptr : nullptr;
     // one launch: domain tiles, range blocks and (inits) the run's resets
     DftPrepInit in;
     if (inits) {
@@ -1434,6 +1445,7 @@ inline int launch_dft(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool i
         da.rguard = c->d_dft_rguard.ptr;
         da.tguard = c->d_dft_tguard.ptr;
         da.trmax = c->d_dft_trmax.ptr;
+        da.slotbest = r.slotbest;
         const unsigned nwg = nwork;
 #ifdef FRAC_CLOCK_STAMP
         da.stamps = clock_stamps_for(nwg);
@@ -1621,6 +1633,8 @@ inline int launch_dft(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool i
         v.flip_slots = c->dft_copies == 2 ? c->nblocks * 32u : 0u;
         v.tpool = c->d_dft_tpool.ptr;
         v.rorb = c->d_dft_rorb.ptr;
+        v.slotbest = r.slotbest;
+        v.tdom = c->d_dft_tdom.ptr;
         v.plan = c->qplan;
         FRAC_HIP(c, c->d_rstat.ensure(std::max<size_t>(nr, 1)));
         v.rstat = c->d_rstat.ptr;
@@ -2329,7 +2343,7 @@ bool qt_device_planned(const frac_ctx* c, const frac_quadtree_params* qp)
 constexpr uint32_t kQtShards = 32, kQtCounters = 9;
 
 int qt_encode_dev(frac_ctx* c, const frac_quadtree_params* qp, LevelGrid& level, frac_encode_item* out, size_t cap,
-                  size_t* n_out, frac_stats* stats)
+                  size_t* n_out, frac_stats* stats, frac_qt_leaf* out32 = nullptr)
 {
     const uint32_t W = c->src.w, H = c->src.h, T = c->p.transforms;
     const int nb = c->p.use_classifier ? 7 : 1;
@@ -2339,7 +2353,10 @@ int qt_encode_dev(frac_ctx* c, const frac_quadtree_params* qp, LevelGrid& level,
     HostTrace tr("quadtree (device-planned)");
     const size_t max_leaves = (size_t)(W / qp->min_size) * (H / qp->min_size);
     constexpr uint32_t kFirst = 2 * (kMaxBuckets + 1); // bucket bounds per level: domains, ranges
-    FRAC_HIP(c, c->d_qt_leaves.ensure(std::max<size_t>(max_leaves, 1)));
+    if (out32)
+        FRAC_HIP(c, c->d_qt_leaves32.ensure(std::max<size_t>(max_leaves, 1)));
+    else
+        FRAC_HIP(c, c->d_qt_leaves.ensure(std::max<size_t>(max_leaves, 1)));
     FRAC_HIP(c, c->d_ranges.ensure(std::max<size_t>(max_leaves, 1)));
     FRAC_HIP(c, c->d_qt_next.ensure(std::max<size_t>(max_leaves, 1)));
     FRAC_HIP(c, c->d_qt_plan.ensure(6));
@@ -2357,14 +2374,19 @@ int qt_encode_dev(frac_ctx* c, const frac_quadtree_params* qp, LevelGrid& level,
     // (the emit kernels write them over PCIe while the later levels run); else into d_qt_leaves and one
     // copy at the end
     frac_encode_item* leaves = c->d_qt_leaves.ptr;
+    frac_qt_leaf* leaves32 = out32 ? c->d_qt_leaves32.ptr : nullptr;
     uint32_t leaf_cap = (uint32_t)std::min<size_t>(max_leaves, 0xffffffffu);
     bool direct = false;
-    if (out && cap) {
+    void* const host_out = out32 ? static_cast<void*>(out32) : static_cast<void*>(out);
+    if (host_out && cap) {
         hipPointerAttribute_t at{};
         void* dp = nullptr;
-        if (hipPointerGetAttributes(&at, out) == hipSuccess && at.type == hipMemoryTypeHost &&
-            hipHostGetDevicePointer(&dp, out, 0) == hipSuccess && dp) {
-            leaves = reinterpret_cast<frac_encode_item*>(dp);
+        if (hipPointerGetAttributes(&at, host_out) == hipSuccess && at.type == hipMemoryTypeHost &&
+            hipHostGetDevicePointer(&dp, host_out, 0) == hipSuccess && dp) {
+            if (out32)
+                leaves32 = reinterpret_cast<frac_qt_leaf*>(dp);
+            else
+                leaves = reinterpret_cast<frac_encode_item*>(dp);
             leaf_cap = (uint32_t)std::min<size_t>(cap, 0xffffffffu);
             direct = true;
         }
@@ -2533,6 +2555,8 @@ int qt_encode_dev(frac_ctx* c, const frac_quadtree_params* qp, LevelGrid& level,
         // (a second stream copying a level's leaves across PCIe while the next level ran measured slower: the
         // copy kernel's PCIe writes stalled the next level's bucket keys 11 → 71 µs)
         sa.leaves = leaves;
+        sa.leaves32 = leaves32;
+        sa.dcols = W >= 2 * n ? (W - 2 * n) / n + 1 : 0u;
         sa.leaf_cap = leaf_cap;
         sa.next_ranges = c->d_qt_next.ptr;
         sa.aux = c->d_aux.ptr;
@@ -2578,6 +2602,9 @@ int qt_encode_dev(frac_ctx* c, const frac_quadtree_params* qp, LevelGrid& level,
     *n_out = n_leaves;
     if (out && n_leaves && !direct)
         FRAC_HIP(c, hipMemcpy(out, c->d_qt_leaves.ptr, std::min<size_t>(cap, n_leaves) * sizeof(frac_encode_item),
+                              hipMemcpyDeviceToHost));
+    if (out32 && n_leaves && !direct)
+        FRAC_HIP(c, hipMemcpy(out32, c->d_qt_leaves32.ptr, std::min<size_t>(cap, n_leaves) * sizeof(frac_qt_leaf),
                               hipMemcpyDeviceToHost));
     tr.mark("leaves D2H");
     if (stats) {
@@ -3074,8 +3101,35 @@ void* frac_get_stream(frac_ctx* c) { return c ? reinterpret_cast<void*>(c->strea
 
 const frac_encode_item* frac_device_results(frac_ctx* c) { return c ? c->d_out.ptr : nullptr; }
 
+static int encode_quadtree_impl(frac_ctx* c, const frac_quadtree_params* qp, frac_encode_item* out,
+                                frac_qt_leaf* out32, size_t cap, size_t* n_out, frac_stats* stats);
+
 int frac_encode_quadtree(frac_ctx* c, const frac_quadtree_params* qp, frac_encode_item* out, size_t cap,
                          size_t* n_out, frac_stats* stats)
+{
+    return encode_quadtree_impl(c, qp, out, nullptr, cap, n_out, stats);
+}
+
+int frac_encode_quadtree_leaves(frac_ctx* c, const frac_quadtree_params* qp, frac_qt_leaf* out, size_t cap,
+                                size_t* n_out, frac_stats* stats)
+{
+    if (!c)
+        return FRAC_E_INVALID;
+    if (!qp || !n_out)
+        return c->fail(FRAC_E_INVALID, "quadtree: params and n_out are required");
+    if (!c->planes_set)
+        return c->fail(FRAC_E_STATE, "quadtree: no frame set");
+    const uint32_t W = c->src.w, H = c->src.h;
+    if (W > 0xffffu || H > 0xffffu)
+        return c->fail(FRAC_E_INVALID, "quadtree leaves: a frame side above 65535 does not fit the 16-bit origins");
+    if (qp->min_size >= 2 && frac_uniform_grid(W, H, 2 * qp->min_size, qp->min_size, nullptr, 0) >= FRAC_QT_NO_DOMAIN)
+        return c->fail(FRAC_E_INVALID, "quadtree leaves: the finest level has more domains than a 24-bit index holds");
+    return encode_quadtree_impl(c, qp, nullptr, out, cap, n_out, stats);
+}
+
+// frac_encode_quadtree (out: 64-byte records) and frac_encode_quadtree_leaves (out32: 32-byte leaves)
+static int encode_quadtree_impl(frac_ctx* c, const frac_quadtree_params* qp, frac_encode_item* out,
+                                frac_qt_leaf* out32, size_t cap, size_t* n_out, frac_stats* stats)
 {
     if (!c)
         return FRAC_E_INVALID;
@@ -3116,9 +3170,20 @@ int frac_encode_quadtree(frac_ctx* c, const frac_quadtree_params* qp, frac_encod
         c->qt_w = W;
         c->qt_h = H;
     }
+    if (out32 && !qt_device_planned(c, qp)) {
+        // the host-planned levels (other engines, tuning knobs): the records, then packed here
+        std::vector<frac_encode_item> rec(cap);
+        FRAC_TRY(encode_quadtree_impl(c, qp, cap ? rec.data() : nullptr, nullptr, cap, n_out, stats));
+        const size_t m = std::min(cap, *n_out);
+        for (size_t i = 0; i < m; ++i) {
+            const uint32_t n = rec[i].w;
+            out32[i] = qt_leaf_of(rec[i], W >= 2 * n ? (W - 2 * n) / n + 1 : 0u);
+        }
+        return FRAC_OK;
+    }
     LevelGrid level{c, c->doms_set};
     if (qt_device_planned(c, qp))
-        return qt_encode_dev(c, qp, level, out, cap, n_out, stats);
+        return qt_encode_dev(c, qp, level, out, cap, n_out, stats, out32);
     // the level-to-level step runs on the device (qt_flags, scan, qt_scatter): each level's leaves are
     // appended to d_qt_leaves and its split ranges' quadrants become the next level's device range list;
     // the host reads one count per level and the leaves once at the end

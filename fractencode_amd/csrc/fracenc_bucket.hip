@@ -611,6 +611,8 @@ struct QtSplitArgs {
     double split;
     uint32_t* tcount;             // [tiles] splits per tile (qt_split_emit sums the earlier ones)
     frac_encode_item* leaves;     // device memory, or the caller's pinned host buffer (written over PCIe)
+    frac_qt_leaf* leaves32 = nullptr; // instead of `leaves`: the 32-byte leaves (frac_encode_quadtree_leaves)
+    uint32_t dcols = 0;           // leaves32: columns of the level's domain grid createUniformGrid(W, H, 2n, n)
     uint32_t leaf_cap;            // leaves past it are not written (the caller's capacity)
     frac_grid_item* next_ranges;
     // the level's frac_stats counters (qt_level_stats), when acc is not null
@@ -622,6 +624,21 @@ struct QtSplitArgs {
     unsigned long long* acc;
     uint32_t shards, stride;
 };
+
+// a leaf record in 32 bytes (frac_qt_leaf): the winner's domain as its index in the level's domain grid
+__host__ __device__ inline frac_qt_leaf qt_leaf_of(const frac_encode_item& r, uint32_t dcols)
+{
+    const uint32_t n = r.w, lg = n ? 31u - (uint32_t)__builtin_clz(n) : 0u;
+    const uint32_t d = r.match.sw ? (r.match.y / n) * dcols + r.match.x / n : FRAC_QT_NO_DOMAIN;
+    frac_qt_leaf l;
+    l.x = (uint16_t)r.x;
+    l.y = (uint16_t)r.y;
+    l.code = (d & 0xffffffu) | (((uint32_t)r.match.score.transform & 15u) << 24) | (lg << 28);
+    l.contrast = r.match.score.contrast;
+    l.brightness = r.match.score.brightness;
+    l.distance = r.match.score.distance;
+    return l;
+}
 
 __device__ inline bool qt_splits(const QtSplitArgs& a, uint32_t i, uint32_t n)
 {
@@ -730,7 +747,11 @@ __global__ void __launch_bounds__(kBkThreads) qt_split_emit(QtSplitArgs a)
                 a.next_ranges[4 * o + 2] = frac_grid_item{r.x, r.y + h, h, h, -1};
                 a.next_ranges[4 * o + 3] = frac_grid_item{r.x + h, r.y + h, h, h, -1};
             } else if (leaf_base + (i - o) < a.leaf_cap) {
-                a.leaves[leaf_base + (i - o)] = a.out[i];
+                if (a.leaves32) {
+                    a.leaves32[leaf_base + (i - o)] = qt_leaf_of(a.out[i], a.dcols);
+                } else {
+                    a.leaves[leaf_base + (i - o)] = a.out[i];
+                }
             }
         }
         __syncthreads();

@@ -191,7 +191,13 @@ struct DftArgs {
     const int32_t* trmax;  // kDftFast6: [ntiles] the largest block R6 whose guard holds against the
                            // tile, (kFast6Limit − max Σb²) / max 2·D6 (−1: none)
     unsigned long long* stamps = nullptr; // FRAC_CLOCK_STAMP builds only: [workgroups][kClockStampWords]
+    // not CHUNKED: per range slot the maximum over every work item, merged here with one 64-bit atomicMax per
+    // (slot, work item) instead of per-work-item entries: fmap(y) << 32 | (kSlotBestTileMax − chunk) << 2 | the
+    // lane halves of that chunk attaining y.  The greatest word names the greatest y and, among equal y, the
+    // earliest chunk — the chunk resolve_dft walked the entries for.  0 = no work item reached the slot.
+    unsigned long long* slotbest = nullptr;
 };
+constexpr uint32_t kSlotBestTileMax = 0x3fffffffu; // chunk tiles below 2^30
 // per workgroup: s_memtime and s_memrealtime before / after the loop, HW_ID | XCC_ID << 32, and the
 // work item's tile range first | end << 32
 constexpr uint32_t kClockStampWords = 6;
@@ -218,6 +224,7 @@ struct DftDomainBuildArgs {
     uint32_t* tpool;            // [ntiles*32][32] the same rows in tile order, orbit order (resolve_dft)
     const uint32_t* row_of = nullptr; // BYPOS: [P] tile row of each pool position (tp_build_tiles)
     uint32_t npos = 0;                // BYPOS: P
+    uint2* tdom = nullptr;            // [ntiles*32] each tile row's domain origin {x, y} (resolve_dft's fit)
 };
 
 // pair_sums: fracenc_kernels.hip (pool_build)
@@ -387,6 +394,8 @@ __device__ __forceinline__ void dft_domain_build_pair_at(uint32_t tid2, const Mf
     int sq = 0;
     if (p >= 0) {
         const frac_grid_item d = s.doms[s.porig[p]];
+        if (hh == 1 && s.tdom) // the row's domain for the resolving wave's record (no porig → doms chain there)
+            s.tdom[gid] = make_uint2(d.x, d.y);
         const uint8_t* base = s.src + (size_t)(d.y + 8 * hh) * s.sstride + d.x;
         if ((((uintptr_t)base | s.sstride) & 7u) == 0) {
 #pragma unroll
@@ -604,6 +613,8 @@ __device__ __forceinline__ void dft_range_prep_at(uint32_t gid, const MfmaRangeP
             a.rfrags[((size_t)b * NBF + f) * 64 + col + 32 * h] = __builtin_bit_cast(uint4, v8);
         }
     a.rconst[gid] = ri >= 0 ? (uint32_t)(16 * sa2) : 0u; // 16Σa² ≤ 2^24
+    if (a.slotbest)
+        a.slotbest[gid] = 0ull; // the run's reset of the search's merged maxima
     if (a.rorb) {
         // raw pixels r = a + 128, orbit o as the pairs (r_{o,0} | r_{o,1} << 16), (r_{o,2} | r_{o,3} << 16)
         uint4* ro = reinterpret_cast<uint4*>(a.rorb + (size_t)gid * 32);
@@ -724,8 +735,11 @@ __device__ __forceinline__ void dft_range_prep_pair_at(uint32_t gid2, const Mfma
         a.rfrags[((size_t)b * NBF + f) * 64 + col + 32 * hh] = __builtin_bit_cast(uint4, comp[f]);
     sa2 += __shfl_xor(sa2, 1, 64);
     r1 += __shfl_xor(r1, 1, 64);
-    if (hh == 0)
+    if (hh == 0) {
         a.rconst[gid] = ri >= 0 ? (uint32_t)(16 * sa2) : 0u; // 16Σa² ≤ 2^24
+        if (a.slotbest)
+            a.slotbest[gid] = 0ull; // the run's reset of the search's merged maxima
+    }
     if (a.rorb) {
         // raw pixels r = a + 128, orbit o as the pairs (r_{o,0} | r_{o,1} << 16), (r_{o,2} | r_{o,3} << 16)
         uint4* ro = reinterpret_cast<uint4*>(a.rorb + (size_t)gid * 32 + 16 * hh);
@@ -1342,8 +1356,31 @@ __global__ void __launch_bounds__(64 * WAVES) search_dft(DftArgs d)
         }
     }
 #endif
-    if (active && !CHUNKED)
-        a.entries[(size_t)(blockIdx.x * WAVES + wv) * 64 + lane] = make_uint2(__float_as_uint(best * kOut), btile);
+    if (active && !CHUNKED) {
+        if (d.slotbest) {
+            // lanes l and l + 32 hold one range slot's two row halves: the greater y, among equal y the earlier
+            // chunk, and which halves attain it there (both: resolve_dft evaluates both halves' rows)
+            const uint32_t y0 = fmap(best * kOut), t0 = btile;
+            const uint32_t y1 = (uint32_t)__shfl_xor((int)y0, 32, 64), t1 = (uint32_t)__shfl_xor((int)t0, 32, 64);
+            const bool first = lane < 32u;
+            const uint32_t ym = first ? y0 : y1, tm = first ? t0 : t1; // this half (lane < 32: half 0)
+            const uint32_t yo = first ? y1 : y0, to = first ? t1 : t0; // the other half
+            if (first) {
+                uint32_t tile = tm, hm = 1u;
+                if (yo > ym || (yo == ym && to < tm)) {
+                    tile = to;
+                    hm = 2u;
+                } else if (yo == ym && to == tm) {
+                    hm = 3u;
+                }
+                const unsigned long long w = ((unsigned long long)max(ym, yo) << 32) |
+                                             ((kSlotBestTileMax - tile) << 2) | hm;
+                atomicMax(d.slotbest + (size_t)blk * 32 + lane, w);
+            }
+        } else {
+            a.entries[(size_t)(blockIdx.x * WAVES + wv) * 64 + lane] = make_uint2(__float_as_uint(best * kOut), btile);
+        }
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1460,6 +1497,7 @@ __global__ void __launch_bounds__(256, F6 ? 2 : 3) search_dft2(DftArgs d)
 struct DftResolved {
     unsigned long long bestk = kKeyNone;
     uint32_t bx = 0, bs1 = 0, bs2 = 0, sr1 = 0, sr2 = 0;
+    uint32_t dx = 0, dy = ~0u; // the winner's domain origin (MfmaResolveArgs::tdom); dy = ~0u: not known
 };
 
 template <bool SORTED>
@@ -1469,18 +1507,21 @@ __device__ inline DftResolved resolve_dft_eval(const MfmaResolveArgs& a, uint32_
     const uint32_t TK = a.T;      // the transforms of the keys (4, or 8 with the flipped copies)
     DftResolved res;
     const int ri = a.slot_range[slot];
+    // the slot-only loads go out with the padding check's (slot < nslots: in bounds either way)
+    const unsigned long long sb = a.slotbest ? a.slotbest[slot] : 0ull;
+    const int64_t sa16 = (int64_t)a.rconst[slot];
+    const int i = lane >> 2, g = lane & 3;
+    const uint4* rp4 = reinterpret_cast<const uint4*>(a.rorb + (size_t)slot * 32 + g * (PG / 2));
+    const uint4 r0 = rp4[0], r1 = rp4[1];
     if (ri < 0)
         return res;
     const uint32_t blk = slot >> 5, col = slot & 31u;
-    const int i = lane >> 2, g = lane & 3;
     // lane (i, g) holds orbits 4g..4g+3 of the range as pixel pairs (dft_range_prep) and meets
     // the same orbits of a domain row (tile-order pool, dft_domain_build). With fwd(t) = g^t,
     //   X_t = Σ_q r(q)·D4(fwd_t q) = Σ_{o,k} r_{o,k}·D_{o,k+t}:
     // t = 0 pairs (A, B) = (D0|D1, D2|D3), t = 2 the swapped pairs (B, A), t = 1 the rotated
     // pairs (D1|D2, D3|D0) = (alignbit(B, A, 16), alignbit(A, B, 16)) and t = 3 those swapped —
     // two v_alignbit per orbit for all four transforms.
-    const uint4* rp4 = reinterpret_cast<const uint4*>(a.rorb + (size_t)slot * 32 + g * (PG / 2));
-    const uint4 r0 = rp4[0], r1 = rp4[1];
     const uint32_t rp[PG / 2] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
     constexpr uint32_t kOnes = 0x00010001u;
     uint32_t sr2u = 0, sr1 = 0;
@@ -1495,145 +1536,177 @@ __device__ inline DftResolved resolve_dft_eval(const MfmaResolveArgs& a, uint32_
     sr2u = (uint32_t)__builtin_amdgcn_readfirstlane((int)quad_sum(sr2u));
     sr1 = (uint32_t)__builtin_amdgcn_readfirstlane((int)quad_sum(sr1));
     const int sr2 = (int)sr2u; // Σr² ≤ 64·255²
-    const uint32_t e0 = a.blk_ptr[blk], e1 = a.blk_ptr[blk + 1];
-    const uint32_t nent = (e1 - e0) * 2u;
-    // the first 64 entries stay in registers for the ballot walk below
-    uint2 en0 = make_uint2(0u, 0u);
-    float vmax = -__builtin_inff();
-    for (uint32_t j = lane; j < nent; j += 64) {
-        const uint2 v = a.entries[(size_t)a.blk_ent[e0 + j / 2] * 64 + col + 32 * (j & 1)];
-        if (j < 64)
-            en0 = v;
-        vmax = __builtin_fmaxf(vmax, __uint_as_float(v.x));
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1)
-        vmax = __builtin_fmaxf(vmax, __uint_as_float(lane_xor(__float_as_uint(vmax), lane, o)));
-    vmax = __uint_as_float((uint32_t)__builtin_amdgcn_readfirstlane((int)__float_as_uint(vmax))); // wave-uniform
-    if (!(vmax > -1.0e29f))
-        return res; // only padding rows: no eligible domain, best_key stays "none"
-    const int64_t sa16 = (int64_t)a.rconst[slot];
-    const bool sentinel = vmax == __builtin_inff();
-    const bool exact = sentinel || vmax > (float)(sa16 - kExactLimit);
-    const int64_t target = exact && !sentinel ? sa16 - (int64_t)vmax : -1;
-    const bool hit = a.hitH >= 0 && (sentinel || (target >= 0 && target <= a.hitH));
+    // the greatest entry y (vmax) over the block's splits and lane halves, and the chunk(s) holding it
     unsigned long long bestk = kKeyNone;
     uint32_t bx = 0, bs1 = 0, bs2 = 0; // X_t, ΣD4, ΣD4² of bestk's candidate (fit_rstat)
-    const uint32_t vbits = __float_as_uint(vmax);
-    // only the entries holding the maximum are re-evaluated (usually one): the lanes test 64
-    // entries at a time and the wave walks the ballot of matches, so the cost does not grow
-    // with the number of domain splits (many splits per block when ranges are sharded)
-    for (uint32_t c0 = 0; c0 < nent; c0 += 64) {
-        const uint32_t jl = c0 + (uint32_t)lane;
-        const uint2 enl = jl >= nent ? make_uint2(0u, 0u)
-                          : c0 == 0  ? en0
-                                     : a.entries[(size_t)a.blk_ent[e0 + jl / 2] * 64 + col + 32 * (jl & 1)];
-        unsigned long long match = __ballot(jl < nent && enl.x == vbits);
-        while (match) {
-            const int src = __ffsll((long long)match) - 1;
-            match &= match - 1;
-            const uint32_t j = c0 + (uint32_t)src;
-            uint2 en = make_uint2(vbits, (uint32_t)__builtin_amdgcn_readlane((int)enl.y, src));
-            // SORTED entries carry the chunk's tile mask in bits 28..31 (search_dft CHUNKED)
-            const uint32_t tmask = SORTED ? (en.y >> 28) : 0xfu;
-            if constexpr (SORTED)
-                en.y &= 0x0fffffffu;
-            const int row = (i & 3) + 8 * (i >> 2) + 4 * (int)(j & 1);
-            if (!exact) {
-                // fp32 fallback regime: every candidate has S16 ≥ 2^24; any valid domain of the
-                // bucket routes the range to fallback_fp32 through fit_winner
-                const int p = a.tile_pos[en.y * 32 + row];
-                const unsigned long long mask = __ballot(p >= 0 && g == 0);
-                if (mask) {
-                    const int pf = __builtin_amdgcn_readlane(p, __ffsll((long long)mask) - 1);
-                    bestk = min(bestk, key_miss((uint64_t)kExactLimit, (uint32_t)pf, 0));
-                }
-                continue;
+    uint32_t bdx = 0, bdy = ~0u; // its domain origin (a.tdom; not SORTED)
+    float vmax = -__builtin_inff();
+    bool exact = false, hit = false;
+    int64_t target = -1;
+    auto set_target = [&]() {
+        const bool sentinel = vmax == __builtin_inff();
+        exact = sentinel || vmax > (float)(sa16 - kExactLimit);
+        target = exact && !sentinel ? sa16 - (int64_t)vmax : -1;
+        hit = a.hitH >= 0 && (sentinel || (target >= 0 && target <= a.hitH));
+    };
+    // re-evaluate chunk `tile0` (4 tiles from there; SORTED: the tiles in tmask) on the rows of lane half h,
+    // keeping the least selection key
+    auto eval_chunk = [&](uint32_t tile0, uint32_t h, uint32_t tmask) {
+        const int row = (i & 3) + 8 * (i >> 2) + 4 * (int)h;
+        if (!exact) {
+            // fp32 fallback regime: every candidate has S16 ≥ 2^24; any valid domain of the
+            // bucket routes the range to fallback_fp32 through fit_winner
+            const int p = a.tile_pos[tile0 * 32 + row];
+            const unsigned long long mask = __ballot(p >= 0 && g == 0);
+            if (mask) {
+                const int pf = __builtin_amdgcn_readlane(p, __ffsll((long long)mask) - 1);
+                bestk = min(bestk, key_miss((uint64_t)kExactLimit, (uint32_t)pf, 0));
             }
-            for (uint32_t tile = en.y; tile < min(en.y + (uint32_t)kTilesPerStage, a.ntiles); ++tile) {
-                if (!((tmask >> (tile - en.y)) & 1u))
-                    continue;
-                // the row's pool position (for the key) and its D4 from the tile-order copy are
-                // independent loads; ΣD4² is summed here rather than loaded through the position.
-                // (Loading the chunk's four tiles up front saved 1 µs at C2 but took 24 more VGPRs:
-                // 4 instead of 6 waves per SIMD cost the C4 quadtree's 65k-range level 21 µs.)
-                const int p = a.tile_pos[tile * 32 + row];
-                const uint4* dp = reinterpret_cast<const uint4*>(a.tpool + ((size_t)tile * 32 + row) * 32 + g * (PG / 2));
-                const uint4 d0 = dp[0], d1 = dp[1];
-                const uint32_t dv[PG / 2] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w};
-                uint32_t sd2 = 0, sd1 = 0;
+            return;
+        }
+        for (uint32_t tile = tile0; tile < min(tile0 + (uint32_t)kTilesPerStage, a.ntiles); ++tile) {
+            if (!((tmask >> (tile - tile0)) & 1u))
+                continue;
+            // the row's pool position (for the key) and its D4 from the tile-order copy are
+            // independent loads; ΣD4² is summed here rather than loaded through the position.
+            // (Loading the chunk's four tiles up front saved 1 µs at C2 but took 24 more VGPRs:
+            // 4 instead of 6 waves per SIMD cost the C4 quadtree's 65k-range level 21 µs.)
+            const int p = a.tile_pos[tile * 32 + row];
+            const uint2 dm = (!SORTED && a.tdom) ? a.tdom[tile * 32 + row] : make_uint2(0u, ~0u);
+            const uint4* dp = reinterpret_cast<const uint4*>(a.tpool + ((size_t)tile * 32 + row) * 32 + g * (PG / 2));
+            const uint4 d0 = dp[0], d1 = dp[1];
+            const uint32_t dv[PG / 2] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w};
+            uint32_t sd2 = 0, sd1 = 0;
+#pragma unroll
+            for (int q = 0; q < PG / 2; ++q) {
+                sd2 = __builtin_amdgcn_udot2(__builtin_bit_cast(ushort2_t, dv[q]), __builtin_bit_cast(ushort2_t, dv[q]),
+                                             sd2, false);
+                sd1 = __builtin_amdgcn_udot2(__builtin_bit_cast(ushort2_t, dv[q]), __builtin_bit_cast(ushort2_t, kOnes),
+                                             sd1, false);
+            }
+            sd2 = quad_sum(sd2);
+            sd1 = quad_sum(sd1);
+            const int nsd2 = -(int)sd2; // ΣD4² ≤ 64·1020² < 2^31
+            unsigned long long tk = kKeyNone;
+            uint32_t tx = 0, ts1 = 0, ts2 = 0;
+            uint32_t tdx = 0, tdy = ~0u;
+#pragma unroll
+            for (int t = 0; t < T; ++t) {
+                uint32_t X = 0;
 #pragma unroll
                 for (int q = 0; q < PG / 2; ++q) {
-                    sd2 = __builtin_amdgcn_udot2(__builtin_bit_cast(ushort2_t, dv[q]), __builtin_bit_cast(ushort2_t, dv[q]),
-                                                 sd2, false);
-                    sd1 = __builtin_amdgcn_udot2(__builtin_bit_cast(ushort2_t, dv[q]), __builtin_bit_cast(ushort2_t, kOnes),
-                                                 sd1, false);
+                    // pair q of orbit q/2 for transform t (see the lane map above)
+                    // t odd: the rotated pairs, rebuilt per transform (a t = 1 copy held across
+                    // the loop would take 8 more VGPRs)
+                    const int qs = q ^ (t >> 1);
+                    const uint32_t dq = (t & 1) ? __builtin_amdgcn_alignbit(dv[qs ^ 1], dv[qs], 16) : dv[qs];
+                    X = __builtin_amdgcn_udot2(__builtin_bit_cast(ushort2_t, rp[q]), __builtin_bit_cast(ushort2_t, dq),
+                                               X, false);
                 }
-                sd2 = quad_sum(sd2);
-                sd1 = quad_sum(sd1);
-                const int nsd2 = -(int)sd2; // ΣD4² ≤ 64·1020² < 2^31
-                unsigned long long tk = kKeyNone;
-                uint32_t tx = 0, ts1 = 0, ts2 = 0;
-#pragma unroll
-                for (int t = 0; t < T; ++t) {
-                    uint32_t X = 0;
-#pragma unroll
-                    for (int q = 0; q < PG / 2; ++q) {
-                        // pair q of orbit q/2 for transform t (see the lane map above)
-                        // t odd: the rotated pairs, rebuilt per transform (a t = 1 copy held across
-                        // the loop would take 8 more VGPRs)
-                        const int qs = q ^ (t >> 1);
-                        const uint32_t dq = (t & 1) ? __builtin_amdgcn_alignbit(dv[qs ^ 1], dv[qs], 16) : dv[qs];
-                        X = __builtin_amdgcn_udot2(__builtin_bit_cast(ushort2_t, rp[q]), __builtin_bit_cast(ushort2_t, dq),
-                                                   X, false);
+                X = quad_sum(X);
+                // S16 = 16Σr² − 8X + ΣD4² ≤ 64·1020² < 2^31: exact in int32
+                const int64_t s16 = p >= 0 ? (int64_t)(16 * sr2 - 8 * (int32_t)X - nsd2) : 0;
+                const bool ok = p >= 0 && g == 0 && (hit ? (s16 <= a.hitH) : (s16 == target));
+                const uint32_t tr = flip ? 4u + ((4u - (uint32_t)t) & 3u) : (uint32_t)t; // the reference's transform
+                if constexpr (SORTED) {
+                    // lane-local least key; one wave reduction per range at the end
+                    const unsigned long long k =
+                        ok ? (hit ? key_hit((uint32_t)p, tr) : key_miss((uint64_t)target, (uint32_t)p, TK - 1 - tr))
+                           : kKeyNone;
+                    if (k < tk) {
+                        tk = k;
+                        tx = X;
                     }
-                    X = quad_sum(X);
-                    // S16 = 16Σr² − 8X + ΣD4² ≤ 64·1020² < 2^31: exact in int32
-                    const int64_t s16 = p >= 0 ? (int64_t)(16 * sr2 - 8 * (int32_t)X - nsd2) : 0;
-                    const bool ok = p >= 0 && g == 0 && (hit ? (s16 <= a.hitH) : (s16 == target));
-                    const uint32_t tr = flip ? 4u + ((4u - (uint32_t)t) & 3u) : (uint32_t)t; // the reference's transform
-                    if constexpr (SORTED) {
-                        // lane-local least key; one wave reduction per range at the end
-                        const unsigned long long k =
-                            ok ? (hit ? key_hit((uint32_t)p, tr) : key_miss((uint64_t)target, (uint32_t)p, TK - 1 - tr))
-                               : kKeyNone;
+                } else {
+                    const unsigned long long mask = __ballot(ok);
+                    if (mask) {
+                        const int first = __ffsll((long long)mask) - 1;
+                        const int pf = __builtin_amdgcn_readlane(p, first);
+                        const unsigned long long k = hit ? key_hit((uint32_t)pf, tr)
+                                                         : key_miss((uint64_t)target, (uint32_t)pf, TK - 1 - tr);
+                        const uint32_t xf = (uint32_t)__builtin_amdgcn_readlane((int)X, first);
+                        const uint32_t s1f = (uint32_t)__builtin_amdgcn_readlane((int)sd1, first);
+                        const uint32_t s2f = (uint32_t)__builtin_amdgcn_readlane((int)sd2, first);
                         if (k < tk) {
                             tk = k;
-                            tx = X;
-                        }
-                    } else {
-                        const unsigned long long mask = __ballot(ok);
-                        if (mask) {
-                            const int first = __ffsll((long long)mask) - 1;
-                            const int pf = __builtin_amdgcn_readlane(p, first);
-                            const unsigned long long k = hit ? key_hit((uint32_t)pf, tr)
-                                                             : key_miss((uint64_t)target, (uint32_t)pf, TK - 1 - tr);
-                            const uint32_t xf = (uint32_t)__builtin_amdgcn_readlane((int)X, first);
-                            const uint32_t s1f = (uint32_t)__builtin_amdgcn_readlane((int)sd1, first);
-                            const uint32_t s2f = (uint32_t)__builtin_amdgcn_readlane((int)sd2, first);
-                            if (k < tk) {
-                                tk = k;
-                                tx = xf;
-                                ts1 = s1f;
-                                ts2 = s2f;
-                            }
+                            tx = xf;
+                            ts1 = s1f;
+                            ts2 = s2f;
+                            tdx = (uint32_t)__builtin_amdgcn_readlane((int)dm.x, first);
+                            tdy = (uint32_t)__builtin_amdgcn_readlane((int)dm.y, first);
                         }
                     }
                 }
-                if constexpr (SORTED) {
-                    ts1 = sd1;
-                    ts2 = sd2;
+            }
+            if constexpr (SORTED) {
+                ts1 = sd1;
+                ts2 = sd2;
+            }
+            if (tk != kKeyNone) {
+                if (tk < bestk) {
+                    bestk = tk;
+                    bx = tx;
+                    bs1 = ts1;
+                    bs2 = ts2;
+                    bdx = tdx;
+                    bdy = tdy;
                 }
-                if (tk != kKeyNone) {
-                    if (tk < bestk) {
-                        bestk = tk;
-                        bx = tx;
-                        bs1 = ts1;
-                        bs2 = ts2;
-                    }
-                    if constexpr (!SORTED)
-                        break;
-                }
+                if constexpr (!SORTED)
+                    break;
+            }
+        }
+    };
+    if (a.slotbest) {
+        // the search merged its splits itself (search_dft, DftArgs::slotbest): the slot's greatest y, the
+        // earliest chunk attaining it and which lane halves of that chunk attain it — one load, no CSR walk
+        if (sb == 0ull)
+            return res; // no work item reached the slot: no eligible domain
+        vmax = funmap((uint32_t)(sb >> 32));
+        if (!(vmax > -1.0e29f))
+            return res; // only padding rows: no eligible domain, best_key stays "none"
+        set_target();
+        const uint32_t tile0 = kSlotBestTileMax - ((uint32_t)sb >> 2), hm = (uint32_t)sb & 3u;
+        for (uint32_t h = 0; h < 2; ++h)
+            if ((hm >> h) & 1u)
+                eval_chunk(tile0, h, 0xfu);
+    } else {
+        const uint32_t e0 = a.blk_ptr[blk], e1 = a.blk_ptr[blk + 1];
+        const uint32_t nent = (e1 - e0) * 2u;
+        // the first 64 entries stay in registers for the ballot walk below
+        uint2 en0 = make_uint2(0u, 0u);
+        for (uint32_t j = lane; j < nent; j += 64) {
+            const uint2 v = a.entries[(size_t)a.blk_ent[e0 + j / 2] * 64 + col + 32 * (j & 1)];
+            if (j < 64)
+                en0 = v;
+            vmax = __builtin_fmaxf(vmax, __uint_as_float(v.x));
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1)
+            vmax = __builtin_fmaxf(vmax, __uint_as_float(lane_xor(__float_as_uint(vmax), lane, o)));
+        vmax = __uint_as_float((uint32_t)__builtin_amdgcn_readfirstlane((int)__float_as_uint(vmax))); // wave-uniform
+        if (!(vmax > -1.0e29f))
+            return res; // only padding rows: no eligible domain, best_key stays "none"
+        set_target();
+        const uint32_t vbits = __float_as_uint(vmax);
+        // only the entries holding the maximum are re-evaluated (usually one): the lanes test 64
+        // entries at a time and the wave walks the ballot of matches, so the cost does not grow
+        // with the number of domain splits (many splits per block when ranges are sharded)
+        for (uint32_t c0 = 0; c0 < nent; c0 += 64) {
+            const uint32_t jl = c0 + (uint32_t)lane;
+            const uint2 enl = jl >= nent ? make_uint2(0u, 0u)
+                              : c0 == 0  ? en0
+                                         : a.entries[(size_t)a.blk_ent[e0 + jl / 2] * 64 + col + 32 * (jl & 1)];
+            unsigned long long match = __ballot(jl < nent && enl.x == vbits);
+            while (match) {
+                const int src = __ffsll((long long)match) - 1;
+                match &= match - 1;
+                const uint32_t j = c0 + (uint32_t)src;
+                uint32_t ey = (uint32_t)__builtin_amdgcn_readlane((int)enl.y, src);
+                // SORTED entries carry the chunk's tile mask in bits 28..31 (search_dft CHUNKED)
+                const uint32_t tmask = SORTED ? (ey >> 28) : 0xfu;
+                if constexpr (SORTED)
+                    ey &= 0x0fffffffu;
+                eval_chunk(ey, j & 1u, tmask);
             }
         }
     }
@@ -1661,11 +1734,15 @@ __device__ inline DftResolved resolve_dft_eval(const MfmaResolveArgs& a, uint32_
     res.bs2 = bs2;
     res.sr1 = sr1;
     res.sr2 = (uint32_t)sr2;
+    res.dx = bdx;
+    res.dy = bdy;
     return res;
 }
 
-// range r's record from its resolved winner w (every lane holds the same after resolve_dft_eval)
-__device__ inline void resolve_dft_record(const MfmaResolveArgs& a, uint32_t r, const DftResolved& w, int lane)
+// range r's record from its resolved winner w (every lane holds the same after resolve_dft_eval); rg: the
+// range's item, loaded by the caller at the start of the resolve
+__device__ inline void resolve_dft_record(const MfmaResolveArgs& a, uint32_t r, const DftResolved& w, int lane,
+                                          const frac_grid_item& rg)
 {
     if (a.fused_fit) { // the range's record right here: one launch less per run (C2: 5 µs of a 43 µs frame)
         if (a.fit.inline_fallback && key_needs_fallback(w.bestk)) { // the fp32 regime, by this wave
@@ -1676,7 +1753,10 @@ __device__ inline void resolve_dft_record(const MfmaResolveArgs& a, uint32_t r, 
         }
         if (lane == 0) {
             a.best_key[r] = w.bestk;
-            fit_rstat_range<8>(a.fit, r, w.bestk, make_uint4(w.bx, w.bs1 | (w.sr1 << 16), w.bs2, w.sr2));
+            // the Fourier path's domains are 16×16 (launch_mfma<8> routes only n = 8, ratio 2 here)
+            const frac_grid_item dk{w.dx, w.dy, 16u, 16u, 0};
+            fit_rstat_range<8>(a.fit, r, w.bestk, make_uint4(w.bx, w.bs1 | (w.sr1 << 16), w.bs2, w.sr2), &rg,
+                               w.dy != ~0u ? &dk : nullptr);
         }
         return;
     }
@@ -1695,13 +1775,14 @@ __device__ inline void resolve_dft_slot(const MfmaResolveArgs& a, uint32_t slot,
     const int ri = a.slot_range[slot];
     if (ri < 0)
         return;
+    const frac_grid_item rg = a.fused_fit ? a.fit.ranges[ri] : frac_grid_item{};
     DftResolved w = resolve_dft_eval<SORTED>(a, slot, lane, false);
     if (!SORTED && a.flip_slots) {
         const DftResolved f = resolve_dft_eval<SORTED>(a, slot + a.flip_slots, lane, true);
         if (f.bestk < w.bestk)
             w = f;
     }
-    resolve_dft_record(a, (uint32_t)ri, w, lane);
+    resolve_dft_record(a, (uint32_t)ri, w, lane, rg);
 }
 
 // T = 8 with the flipped copies (MfmaResolveArgs::paired): a two-wave workgroup per slot, wave 0
@@ -1710,10 +1791,11 @@ __device__ inline void resolve_dft_slot(const MfmaResolveArgs& a, uint32_t slot,
 __device__ inline void resolve_dft_pair(const MfmaResolveArgs& a, uint32_t slot, uint32_t wave, int lane)
 {
     __shared__ unsigned long long fkey;
-    __shared__ uint32_t fsums[5];
+    __shared__ uint32_t fsums[7];
     const int ri = a.slot_range[slot]; // the same for both waves: the barrier below is reached by both or neither
     if (ri < 0)
         return;
+    const frac_grid_item rg = (a.fused_fit && wave == 0) ? a.fit.ranges[ri] : frac_grid_item{};
     const DftResolved w = resolve_dft_eval<false>(a, slot + wave * a.flip_slots, lane, wave == 1);
     if (wave == 1 && lane == 0) {
         fkey = w.bestk;
@@ -1722,6 +1804,8 @@ __device__ inline void resolve_dft_pair(const MfmaResolveArgs& a, uint32_t slot,
         fsums[2] = w.bs2;
         fsums[3] = w.sr1;
         fsums[4] = w.sr2;
+        fsums[5] = w.dx;
+        fsums[6] = w.dy;
     }
     __syncthreads();
     if (wave == 0) {
@@ -1732,7 +1816,9 @@ __device__ inline void resolve_dft_pair(const MfmaResolveArgs& a, uint32_t slot,
         f.bs2 = fsums[2];
         f.sr1 = fsums[3];
         f.sr2 = fsums[4];
-        resolve_dft_record(a, (uint32_t)ri, f.bestk < w.bestk ? f : w, lane);
+        f.dx = fsums[5];
+        f.dy = fsums[6];
+        resolve_dft_record(a, (uint32_t)ri, f.bestk < w.bestk ? f : w, lane, rg);
     }
 }
 

@@ -485,11 +485,14 @@ __device__ inline void fit_sums_range(const FitArgs& a, uint32_t r, unsigned lon
     a.aux[r] = RangeAux{p, hit ? (uint32_t)kAuxHit : 0u};
 }
 
+// rgp / dp: the range's and the winner domain's items when the caller already holds them (resolve_dft),
+// else loaded here
 template <int N>
-__device__ inline void fit_rstat_range(const FitArgs& a, uint32_t r, unsigned long long key, const uint4& st)
+__device__ inline void fit_rstat_range(const FitArgs& a, uint32_t r, unsigned long long key, const uint4& st,
+                                       const frac_grid_item* rgp = nullptr, const frac_grid_item* dp = nullptr)
 {
     constexpr int NN = N * N;
-    const frac_grid_item rg = a.ranges[r];
+    const frac_grid_item rg = rgp ? *rgp : a.ranges[r];
     if (key == kKeyNone) {
         write_default(a.out[r], rg);
         a.aux[r] = RangeAux{0u, (uint32_t)kAuxEmpty};
@@ -504,7 +507,7 @@ __device__ inline void fit_rstat_range(const FitArgs& a, uint32_t r, unsigned lo
         a.fb_list[atomicAdd(a.fb_count, 1u)] = r;
         return;
     }
-    const frac_grid_item d = a.doms[a.porig[p]];
+    const frac_grid_item d = dp ? *dp : a.doms[a.porig[p]];
     const long long X = st.x, sD = st.y & 0xffffu, sA = st.y >> 16, sD2 = st.z, sA2 = st.w;
     const long long S16 = 16 * sA2 - 8 * X + sD2;
     const double dist = ((double)S16 * 0.0625) / (double)(d.w * d.h);

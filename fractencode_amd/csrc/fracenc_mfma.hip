@@ -205,6 +205,7 @@ struct MfmaRangePrepArgs {
     uint32_t flip_from = ~0u;  // dft_range_prep: blocks from here on hold their range read through Flip (T = 8)
     const DevPlan* plan = nullptr; // device-planned search: the block count (and flip_from) from the plan
     int fmode = 0;             // mfma_range_prep, the float-C epilogue: B = 8·(128 − copy_t)
+    unsigned long long* slotbest = nullptr; // dft_range_prep: [nblocks*32] reset to 0 (search_dft's merged maxima)
 };
 
 // the range-block count of a device-planned search (T = 8 Fourier: the originals and their copies)
@@ -849,6 +850,11 @@ struct MfmaResolveArgs {
     const uint4* rfrags = nullptr;
     // resolve_dft, T = 8: two-wave workgroups, one slot and its flipped copy each (flip_slots > 0)
     int paired = 0;
+    // resolve_dft: per slot the search's own merge of its splits (search_dft with DftArgs::slotbest), read
+    // in place of the entries and their CSR map
+    const unsigned long long* slotbest = nullptr;
+    // resolve_dft: each tile row's domain origin (dft_domain_build), so the fused fit needs no porig → doms loads
+    const uint2* tdom = nullptr;
 };
 
 __device__ inline void apply_plan(MfmaResolveArgs& a)

@@ -234,6 +234,22 @@ typedef struct frac_quadtree_params {
 } frac_quadtree_params;
 int frac_encode_quadtree(frac_ctx* ctx, const frac_quadtree_params* qp, frac_encode_item* out, size_t cap,
                          size_t* n_out, frac_stats* stats);
+/* The same partition with each leaf in 32 bytes instead of encode_item_t's 64 (ABI 7): what the frame's
+ * geometry does not already determine.  A leaf of level size n at (x, y) won domain `code & 0xffffff` of
+ * that level's grid createUniformGrid(W, H, 2n, n) — origin ((d % cols)·n, (d / cols)·n) with
+ * cols = (W − 2n)/n + 1, size 2n — under transform (code >> 24) & 15; n = 1 << (code >> 28).
+ * FRAC_QT_NO_DOMAIN: no eligible domain (the reference's default record: domain (0, 0), size (0, 0)).
+ * The doubles are the record's own, bit for bit.  Frames up to 65535 pixels a side whose finest level
+ * has fewer than 2^24 − 1 domains.  Into the caller's pinned host memory the device writes them directly,
+ * half the PCIe bytes of the 64-byte records. */
+#define FRAC_QT_NO_DOMAIN 0xffffffu
+typedef struct frac_qt_leaf {
+    uint16_t x, y;  /* range origin */
+    uint32_t code;  /* domain index (bits 0..23) | transform (24..27) | log2 n (28..31) */
+    double contrast, brightness, distance;
+} frac_qt_leaf;
+int frac_encode_quadtree_leaves(frac_ctx* ctx, const frac_quadtree_params* qp, frac_qt_leaf* out, size_t cap,
+                                size_t* n_out, frac_stats* stats);
 
 /* ---- classifier pre-pass on the device (BrightnessBlocksClassifier2::preclassify,
  * encode/Classifier2.cpp:55-68, as main.cpp:155-162 runs it at grid build) ----

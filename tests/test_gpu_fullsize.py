@@ -77,6 +77,12 @@ def test_c4_quadtree_2048_classifier(oracle, C4_SPLIT):
     with F.Engine(0, 4, True, 0.0, -1.0) as e:
         e.set_frame(p)
         items, st = e.encode_quadtree(16, 4, C4_SPLIT)
+        # the 32-byte leaves (frac_encode_quadtree_leaves) into pinned memory rebuild the same records
+        import torch
+        pinned = torch.empty((W // 4) * (H // 4) * F.QT_LEAF.itemsize, dtype=torch.uint8).pin_memory()
+        lv, lst = e.encode_quadtree(16, 4, C4_SPLIT, out=pinned.numpy().view(F.QT_LEAF), leaves=True)
+        np.testing.assert_array_equal(F.records_from_leaves(lv, W), items)
+        assert lst["rejected_mappings"] == st["rejected_mappings"]
         sizes = items["w"].astype(np.int64)
         assert set(np.unique(sizes)) <= {4, 8, 16} and (items["h"] == items["w"]).all()
         # tiling: every pixel in exactly one leaf, every leaf aligned to its size

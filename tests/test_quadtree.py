@@ -198,3 +198,67 @@ def test_gpu_quadtree_leaves_into_pinned_memory():
         assert sp["items"] == len(want) and len(part) == len(short)
         np.testing.assert_array_equal(part, want[: len(short)])
         assert (pinned[len(short):] == np.zeros(1, dtype=F.ENCODE_ITEM)).all()  # nothing past the capacity
+
+
+def _leaves_from_records(rec, W):
+    """numpy restatement of frac_qt_leaf packing (include/fracenc.h): the test's independent packer."""
+    n = rec["w"].astype(np.int64)
+    cols = (W - 2 * n) // n + 1
+    has = rec["sw"] != 0
+    d = np.where(has, (rec["dy"].astype(np.int64) // n) * cols + rec["dx"].astype(np.int64) // n, F.QT_NO_DOMAIN)
+    lv = np.log2(n).astype(np.int64)
+    out = np.zeros(len(rec), dtype=F.QT_LEAF)
+    out["x"], out["y"] = rec["x"], rec["y"]
+    out["code"] = (d & 0xFFFFFF) | ((rec["transform"].astype(np.int64) & 15) << 24) | (lv << 28)
+    for k in ("contrast", "brightness", "distance"):
+        out[k] = rec[k]
+    return out
+
+
+def test_records_from_leaves_round_trip():
+    # mixed sizes 2..16 on a 96×64 frame, the no-domain default record included
+    rng = np.random.default_rng(9)
+    W, H = 96, 64
+    rec = np.zeros(200, dtype=F.ENCODE_ITEM)
+    n = rng.choice([2, 4, 8, 16], size=len(rec))
+    rec["w"] = rec["h"] = n
+    rec["x"] = rng.integers(0, W // 16, len(rec)) * 16
+    rec["y"] = rng.integers(0, H // 16, len(rec)) * 16
+    cols, rows = (W - 2 * n) // n + 1, (H - 2 * n) // n + 1
+    d = (rng.random(len(rec)) * cols * rows).astype(np.int64)
+    rec["dx"], rec["dy"] = (d % cols) * n, (d // cols) * n
+    rec["sw"] = rec["sh"] = 2 * n
+    rec["transform"] = rng.integers(0, 8, len(rec))
+    rec["distance"], rec["contrast"], rec["brightness"] = rng.random(len(rec)) * 100, rng.normal(size=len(rec)), \
+        rng.normal(size=len(rec)) * 50
+    none = rng.random(len(rec)) < 0.1  # the default record: domain (0, 0), size (0, 0), Id, dist 1e5, s = o = 0
+    rec["dx"][none] = rec["dy"][none] = rec["sw"][none] = rec["sh"][none] = 0
+    rec["transform"][none] = 0
+    rec["distance"][none], rec["contrast"][none], rec["brightness"][none] = 1e5, 0.0, 0.0
+    leaves = _leaves_from_records(rec, W)
+    assert ((leaves["code"][none] & 0xFFFFFF) == F.QT_NO_DOMAIN).all()
+    np.testing.assert_array_equal(F.records_from_leaves(leaves, W), rec)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("engine", [F.ENGINE_AUTO, F.ENGINE_VALU], ids=["device_planned", "host_planned"])
+@pytest.mark.parametrize("cls,T", [(True, 4), (False, 8)])
+def test_gpu_quadtree_32_byte_leaves(engine, cls, T):
+    # frac_encode_quadtree_leaves: the 32-byte leaves are the records' packing (independent numpy packer),
+    # rebuild the records bit for bit, into pageable and pinned buffers, on both the device-planned and the
+    # host-planned levels
+    import torch
+    p = plane("lenna_y")
+    cap = (512 // 4) ** 2
+    pinned = torch.empty(cap * F.QT_LEAF.itemsize, dtype=torch.uint8).pin_memory().numpy().view(F.QT_LEAF)
+    with F.Engine(0, T, cls, 0.0, -1.0, engine) as e:
+        e.set_frame(p)
+        want, sw = e.encode_quadtree(16, 4, 4.0)
+        got, sg = e.encode_quadtree(16, 4, 4.0, leaves=True)
+        pin, sp = e.encode_quadtree(16, 4, 4.0, out=pinned, leaves=True)
+    assert got.dtype == F.QT_LEAF and len(got) == len(want) == sg["items"] == sp["items"]
+    np.testing.assert_array_equal(got, _leaves_from_records(want, 512))
+    np.testing.assert_array_equal(pin, got)
+    assert np.shares_memory(pin, pinned)
+    np.testing.assert_array_equal(F.records_from_leaves(got, 512), want)
+    assert sg["rejected_mappings"] == sw["rejected_mappings"]

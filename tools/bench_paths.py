@@ -175,6 +175,7 @@ def main():
         # the leaves land in pinned host memory owned by the caller (as a C++ caller would pass its buffer)
         cap = (2048 // 4) ** 2
         leaves = torch.empty(cap * F.ENCODE_ITEM.itemsize, dtype=torch.uint8).pin_memory().numpy().view(F.ENCODE_ITEM)
+        leaves32 = torch.empty(cap * F.QT_LEAF.itemsize, dtype=torch.uint8).pin_memory().numpy().view(F.QT_LEAF)
         res = {}
         for split in (0.05, 0.5):
             # the frame rate without timing events (each event record is a marker packet the GPU
@@ -191,8 +192,18 @@ def main():
                 e.set_frame(frame)
                 for _ in range(3):
                     _, st = e.encode_quadtree(16, 4, split, out=leaves)
+            # the same frame with the 32-byte leaves (frac_encode_quadtree_leaves) into pinned memory
+            with F.Engine(0, 4, True) as e:
+                e.set_frame(frame)
+                for _ in range(max(2, args.warmup)):
+                    e.encode_quadtree(16, 4, split, out=leaves32, leaves=True)
+                t0 = time.perf_counter()
+                for _ in range(args.steps):
+                    e.encode_quadtree(16, 4, split, out=leaves32, leaves=True)
+                sec32 = (time.perf_counter() - t0) / args.steps
             sizes, counts = np.unique(items["w"], return_counts=True)
-            res[str(split)] = {"ms_per_frame": round(sec * 1e3, 3), "items": int(len(items)),
+            res[str(split)] = {"ms_per_frame": round(sec * 1e3, 3), "ms_per_frame_leaves32": round(sec32 * 1e3, 3),
+                               "items": int(len(items)),
                                "items_by_size": {int(a): int(b) for a, b in zip(sizes, counts)},
                                "items_per_s": round(len(items) / sec, 1), "ms_search_sum": round(st["ms_search"], 3)}
         print(json.dumps({"path": "c4q", "workload": "C4: S1 2048² crop, classifier on, quadtree 16/8/4 "
