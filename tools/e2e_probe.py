@@ -1,0 +1,57 @@
+#!/usr/bin/env python3
+"""Where the headline's end-to-end step (bench.FrameStep: frame H2D, search, tuples D2H) spends its time
+beside the device-resident step: per leg the step ms (host clock) and the library's per-run event times
+(device / prep / search / finish, median), alternated `rounds` times so drift shows as a pattern.
+usage: tools/e2e_probe.py [steps] [rounds]"""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+import fractencode_amd as F  # noqa: E402
+from fractencode_amd.distributed import shard_plan  # noqa: E402
+from fractencode_amd.synth import value_noise  # noqa: E402
+
+steps = int(sys.argv[1]) if len(sys.argv) > 1 else 20
+rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 2
+S = 4096
+dev = torch.device("cuda", 0)
+torch.cuda.set_device(0)
+stream = torch.cuda.Stream(dev)
+torch.cuda.set_stream(stream)
+frame = value_noise(S, S, 1234)
+rngs = F.create_uniform_grid(S, S, 8, 8)
+plan = shard_plan(len(rngs), 1)
+h_frame = torch.from_numpy(frame).pin_memory()
+d_frame = torch.from_numpy(frame).to(dev)
+with F.Engine(0, 4, False, 0.0, -1.0, F.ENGINE_AUTO, timing=True) as e:
+    e.set_stream(stream.cuda_stream)
+    e.set_frame(h_frame.numpy())
+    e.set_domains(F.create_uniform_grid(S, S, 16, 8))
+    e.set_ranges(rngs)
+    legs = {"e2e": bench.FrameStep(e, h_frame.numpy(), plan, 0, dev),
+            "device": bench.FrameStep(e, None, plan, 0, dev, device_resident=True)}
+    for r in range(rounds):
+        for name, step in legs.items():
+            if name == "device":
+                e.set_frame(d_frame)
+            for _ in range(3):
+                step()
+            torch.cuda.synchronize(dev)
+            e.timing_history()
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                step()
+            torch.cuda.synchronize(dev)
+            sec = (time.perf_counter() - t0) / steps
+            h = e.timing_history()
+            print(json.dumps({"round": r, "leg": name, "ms_per_step": round(sec * 1e3, 3),
+                              **{k: round(float(np.median(h["ms_" + k])), 3) for k in ("device", "prep", "search", "finish")}}),
+                  flush=True)
