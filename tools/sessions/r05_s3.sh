@@ -5,10 +5,10 @@
 set -euo pipefail
 R=$(pwd)
 O=$R/gpurun_out/r05_s3
-mkdir -p $O
+mkdir -p $O; rm -f $O/ab.jsonl
 python3 -c "import torch" > /dev/null
-timeout -k 10 900 python3 -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_quadtree.py tests/test_gpu_parity.py tests/test_gpu_fullsize.py > $O/tests.log 2>&1
-tail -2 $O/tests.log
+[ -n "${SKIP_TESTS:-}" ] || timeout -k 10 900 python3 -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_quadtree.py tests/test_gpu_parity.py tests/test_gpu_fullsize.py > $O/tests.log 2>&1
+[ -n "${SKIP_TESTS:-}" ] || tail -2 $O/tests.log
 for k in 1 2 3; do
   for v in prod notdom prev; do
     lib=$R/fractencode_amd/libfracenc.so
