@@ -225,7 +225,6 @@ struct frac_ctx {
     DBuf<uint32_t> d_dft_tpool; // pool rows in tile order (resolve_dft)
     DBuf<uint32_t> d_dft_rorb;  // range pixel pairs in orbit order, per slot (resolve_dft)
     DBuf<frac_qt_leaf> d_qt_leaves32; // frac_encode_quadtree_leaves' device-side leaves (pageable caller buffer)
-    DBuf<uint2> d_dft_tdom;     // each tile row's domain origin (dft_domain_build → resolve_dft's fit)
     DBuf<unsigned long long> d_dft_slotbest; // per slot the search's merged maximum (search_dft → resolve_dft)
     DBuf<uint4> d_rstat;        // per range: the winner's sums (resolve_dft → fit_rstat)
     DBuf<frac_grid_item> d_cls_items;
@@ -1377,8 +1376,6 @@ inline int launch_dft(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool i
     b.pool = c->d_pool.ptr;
     b.negsd2 = c->d_negsd2.ptr;
     b.tpool = c->d_dft_tpool.ptr;
-    FRAC_HIP(c, c->d_dft_tdom.ensure(std::max<size_t>((size_t)c->ntiles * 32, 1)));
-    b.tdom = c->d_dft_tdom.ptr;
     MfmaRangePrepArgs r;
     r.tgt = dtgt;
     r.tstride = tstride;
@@ -1634,7 +1631,6 @@ inline int launch_dft(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool i
         v.tpool = c->d_dft_tpool.ptr;
         v.rorb = c->d_dft_rorb.ptr;
         v.slotbest = r.slotbest;
-        v.tdom = c->d_dft_tdom.ptr;
         v.plan = c->qplan;
         FRAC_HIP(c, c->d_rstat.ensure(std::max<size_t>(nr, 1)));
         v.rstat = c->d_rstat.ptr;

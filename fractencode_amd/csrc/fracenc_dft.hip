@@ -224,7 +224,6 @@ struct DftDomainBuildArgs {
     uint32_t* tpool;            // [ntiles*32][32] the same rows in tile order, orbit order (resolve_dft)
     const uint32_t* row_of = nullptr; // BYPOS: [P] tile row of each pool position (tp_build_tiles)
     uint32_t npos = 0;                // BYPOS: P
-    uint2* tdom = nullptr;            // [ntiles*32] each tile row's domain origin {x, y} (resolve_dft's fit)
 };
 
 // pair_sums: fracenc_kernels.hip (pool_build)
@@ -394,8 +393,6 @@ __device__ __forceinline__ void dft_domain_build_pair_at(uint32_t tid2, const Mf
     int sq = 0;
     if (p >= 0) {
         const frac_grid_item d = s.doms[s.porig[p]];
-        if (hh == 1 && s.tdom) // the row's domain for the resolving wave's record (no porig → doms chain there)
-            s.tdom[gid] = make_uint2(d.x, d.y);
         const uint8_t* base = s.src + (size_t)(d.y + 8 * hh) * s.sstride + d.x;
         if ((((uintptr_t)base | s.sstride) & 7u) == 0) {
 #pragma unroll
@@ -1497,7 +1494,6 @@ __global__ void __launch_bounds__(256, F6 ? 2 : 3) search_dft2(DftArgs d)
 struct DftResolved {
     unsigned long long bestk = kKeyNone;
     uint32_t bx = 0, bs1 = 0, bs2 = 0, sr1 = 0, sr2 = 0;
-    uint32_t dx = 0, dy = ~0u; // the winner's domain origin (MfmaResolveArgs::tdom); dy = ~0u: not known
 };
 
 template <bool SORTED>
@@ -1539,7 +1535,6 @@ __device__ inline DftResolved resolve_dft_eval(const MfmaResolveArgs& a, uint32_
     // the greatest entry y (vmax) over the block's splits and lane halves, and the chunk(s) holding it
     unsigned long long bestk = kKeyNone;
     uint32_t bx = 0, bs1 = 0, bs2 = 0; // X_t, ΣD4, ΣD4² of bestk's candidate (fit_rstat)
-    uint32_t bdx = 0, bdy = ~0u; // its domain origin (a.tdom; not SORTED)
     float vmax = -__builtin_inff();
     bool exact = false, hit = false;
     int64_t target = -1;
@@ -1572,7 +1567,6 @@ __device__ inline DftResolved resolve_dft_eval(const MfmaResolveArgs& a, uint32_
             // (Loading the chunk's four tiles up front saved 1 µs at C2 but took 24 more VGPRs:
             // 4 instead of 6 waves per SIMD cost the C4 quadtree's 65k-range level 21 µs.)
             const int p = a.tile_pos[tile * 32 + row];
-            const uint2 dm = (!SORTED && a.tdom) ? a.tdom[tile * 32 + row] : make_uint2(0u, ~0u);
             const uint4* dp = reinterpret_cast<const uint4*>(a.tpool + ((size_t)tile * 32 + row) * 32 + g * (PG / 2));
             const uint4 d0 = dp[0], d1 = dp[1];
             const uint32_t dv[PG / 2] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w};
@@ -1589,7 +1583,6 @@ __device__ inline DftResolved resolve_dft_eval(const MfmaResolveArgs& a, uint32_
             const int nsd2 = -(int)sd2; // ΣD4² ≤ 64·1020² < 2^31
             unsigned long long tk = kKeyNone;
             uint32_t tx = 0, ts1 = 0, ts2 = 0;
-            uint32_t tdx = 0, tdy = ~0u;
 #pragma unroll
             for (int t = 0; t < T; ++t) {
                 uint32_t X = 0;
@@ -1632,8 +1625,6 @@ __device__ inline DftResolved resolve_dft_eval(const MfmaResolveArgs& a, uint32_
                             tx = xf;
                             ts1 = s1f;
                             ts2 = s2f;
-                            tdx = (uint32_t)__builtin_amdgcn_readlane((int)dm.x, first);
-                            tdy = (uint32_t)__builtin_amdgcn_readlane((int)dm.y, first);
                         }
                     }
                 }
@@ -1648,8 +1639,6 @@ __device__ inline DftResolved resolve_dft_eval(const MfmaResolveArgs& a, uint32_
                     bx = tx;
                     bs1 = ts1;
                     bs2 = ts2;
-                    bdx = tdx;
-                    bdy = tdy;
                 }
                 if constexpr (!SORTED)
                     break;
@@ -1734,8 +1723,6 @@ __device__ inline DftResolved resolve_dft_eval(const MfmaResolveArgs& a, uint32_
     res.bs2 = bs2;
     res.sr1 = sr1;
     res.sr2 = (uint32_t)sr2;
-    res.dx = bdx;
-    res.dy = bdy;
     return res;
 }
 
@@ -1753,10 +1740,7 @@ __device__ inline void resolve_dft_record(const MfmaResolveArgs& a, uint32_t r, 
         }
         if (lane == 0) {
             a.best_key[r] = w.bestk;
-            // the Fourier path's domains are 16×16 (launch_mfma<8> routes only n = 8, ratio 2 here)
-            const frac_grid_item dk{w.dx, w.dy, 16u, 16u, 0};
-            fit_rstat_range<8>(a.fit, r, w.bestk, make_uint4(w.bx, w.bs1 | (w.sr1 << 16), w.bs2, w.sr2), &rg,
-                               w.dy != ~0u ? &dk : nullptr);
+            fit_rstat_range<8>(a.fit, r, w.bestk, make_uint4(w.bx, w.bs1 | (w.sr1 << 16), w.bs2, w.sr2), &rg);
         }
         return;
     }
@@ -1791,7 +1775,7 @@ __device__ inline void resolve_dft_slot(const MfmaResolveArgs& a, uint32_t slot,
 __device__ inline void resolve_dft_pair(const MfmaResolveArgs& a, uint32_t slot, uint32_t wave, int lane)
 {
     __shared__ unsigned long long fkey;
-    __shared__ uint32_t fsums[7];
+    __shared__ uint32_t fsums[5];
     const int ri = a.slot_range[slot]; // the same for both waves: the barrier below is reached by both or neither
     if (ri < 0)
         return;
@@ -1804,8 +1788,6 @@ __device__ inline void resolve_dft_pair(const MfmaResolveArgs& a, uint32_t slot,
         fsums[2] = w.bs2;
         fsums[3] = w.sr1;
         fsums[4] = w.sr2;
-        fsums[5] = w.dx;
-        fsums[6] = w.dy;
     }
     __syncthreads();
     if (wave == 0) {
@@ -1816,8 +1798,6 @@ __device__ inline void resolve_dft_pair(const MfmaResolveArgs& a, uint32_t slot,
         f.bs2 = fsums[2];
         f.sr1 = fsums[3];
         f.sr2 = fsums[4];
-        f.dx = fsums[5];
-        f.dy = fsums[6];
         resolve_dft_record(a, (uint32_t)ri, f.bestk < w.bestk ? f : w, lane, rg);
     }
 }

@@ -853,8 +853,6 @@ struct MfmaResolveArgs {
     // resolve_dft: per slot the search's own merge of its splits (search_dft with DftArgs::slotbest), read
     // in place of the entries and their CSR map
     const unsigned long long* slotbest = nullptr;
-    // resolve_dft: each tile row's domain origin (dft_domain_build), so the fused fit needs no porig → doms loads
-    const uint2* tdom = nullptr;
 };
 
 __device__ inline void apply_plan(MfmaResolveArgs& a)

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""The fp32-regime cost at C3 size (fallback_wave): a 4096² S1 frame scaled into [0, 150] — so no
+"""The fp32-regime cost at C3 size (fallback_wave): a 4096² S1 frame scaled into [0, 60] — so no
 domain's 2×2 sums come near 1020 — with K isolated white 8×8 ranges, each alone in a black 24×24 patch.  A white
 range's best error is then ≥ 48·1020² > 2^24 (the domain holding it covers a quarter of its cells), the
 fp32 regime the resolving wave emulates in reference order over every candidate of its bucket.  Prints per K
@@ -17,7 +17,7 @@ from fractencode_amd.synth import value_noise  # noqa: E402
 
 
 def frame(k: int, S: int = 4096) -> np.ndarray:
-    p = (value_noise(S, S, 1234).astype(np.float64) * (150.0 / 255.0)).astype(np.uint8)
+    p = (value_noise(S, S, 1234).astype(np.float64) * (60.0 / 255.0)).astype(np.uint8)
     rng = np.random.default_rng(17)
     cells = rng.choice((S // 24) ** 2, size=k, replace=False)
     for c in cells:
