@@ -705,7 +705,6 @@ __global__ void __launch_bounds__(kBkThreads) qt_split_emit(QtSplitArgs a)
 {
     __shared__ uint32_t wcnt[kBkThreads / 64];
     __shared__ uint32_t run;
-    __shared__ uint4 stage[kBkThreads / 64][256]; // per wave up to 64 leaves of 64 bytes
     const uint32_t n = min(a.plan->nr, a.nmax), leaf_base = a.plan->leaf_base;
     const uint32_t base = blockIdx.x * kBkTile, lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     if (wv == 0) { // the splits of the tiles before this one, read from qt_split_count's per-tile counts
@@ -739,46 +738,21 @@ __global__ void __launch_bounds__(kBkThreads) qt_split_emit(QtSplitArgs a)
         uint32_t o = run + (uint32_t)__builtin_popcountll(m & below); // splits before item i
         for (uint32_t w = 0; w < wv; ++w)
             o += wcnt[w];
-        if (i < n && sp) {
-            const frac_grid_item r = a.ranges[i];
-            const uint32_t h = r.w / 2;
-            a.next_ranges[4 * o + 0] = frac_grid_item{r.x, r.y, h, h, -1};
-            a.next_ranges[4 * o + 1] = frac_grid_item{r.x + h, r.y, h, h, -1};
-            a.next_ranges[4 * o + 2] = frac_grid_item{r.x, r.y + h, h, h, -1};
-            a.next_ranges[4 * o + 3] = frac_grid_item{r.x + h, r.y + h, h, h, -1};
-        }
-        // the wave's leaves are consecutive records (leaf_base + i − o): staged in LDS, then written as whole
-        // 1-KiB runs, one 16-byte piece per lane and store — contiguous PCIe writes into a pinned caller buffer
-        // where the record-per-lane stores left each instruction's pieces 32 or 64 bytes apart
-        const bool leaf = i < n && !sp;
-        const unsigned long long lm = __ballot(leaf);
-        if (lm) {
-            const uint32_t W4 = a.leaves32 ? 2u : 4u; // uint4 pieces per leaf
-            const uint32_t rank = (uint32_t)__builtin_popcountll(lm & below), k = (uint32_t)__builtin_popcountll(lm);
-            const uint32_t L0 = (uint32_t)__builtin_amdgcn_readlane((int)(leaf_base + (i - o) - rank),
-                                                                    __ffsll((long long)lm) - 1);
-            uint4* st = stage[wv];
-            if (leaf) {
+        if (i < n) {
+            if (sp) {
+                const frac_grid_item r = a.ranges[i];
+                const uint32_t h = r.w / 2;
+                a.next_ranges[4 * o + 0] = frac_grid_item{r.x, r.y, h, h, -1};
+                a.next_ranges[4 * o + 1] = frac_grid_item{r.x + h, r.y, h, h, -1};
+                a.next_ranges[4 * o + 2] = frac_grid_item{r.x, r.y + h, h, h, -1};
+                a.next_ranges[4 * o + 3] = frac_grid_item{r.x + h, r.y + h, h, h, -1};
+            } else if (leaf_base + (i - o) < a.leaf_cap) {
                 if (a.leaves32) {
-                    const frac_qt_leaf l = qt_leaf_of(a.out[i], a.dcols);
-                    const uint4* q = reinterpret_cast<const uint4*>(&l);
-                    st[2 * rank] = q[0];
-                    st[2 * rank + 1] = q[1];
+                    a.leaves32[leaf_base + (i - o)] = qt_leaf_of(a.out[i], a.dcols);
                 } else {
-                    const uint4* q = reinterpret_cast<const uint4*>(a.out + i);
-#pragma unroll
-                    for (int c = 0; c < 4; ++c)
-                        st[4 * rank + c] = q[c];
+                    a.leaves[leaf_base + (i - o)] = a.out[i];
                 }
             }
-            // the wave's LDS writes above precede its reads below
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            uint4* dst = a.leaves32 ? reinterpret_cast<uint4*>(a.leaves32) : reinterpret_cast<uint4*>(a.leaves);
-            for (uint32_t idx = lane; idx < k * W4; idx += 64)
-                if (L0 + idx / W4 < a.leaf_cap)
-                    dst[(size_t)L0 * W4 + idx] = st[idx];
         }
         __syncthreads();
         if (threadIdx.x == 0)
