@@ -184,6 +184,15 @@ struct frac_ctx {
 
     DBuf<frac_grid_item> d_doms, d_ranges;
     DBuf<uint32_t> d_porig, d_pool, d_fb_list, d_fb_count;
+    // fallback_grid's per-listed-range scratch: the least key so far and the jobs done; all-ones / zero between
+    // runs (the last job of a range resets its pair), set so when (re)allocated
+    DBuf<unsigned long long> d_fb_key;
+    DBuf<uint32_t> d_fb_done;
+    // a fused resolver's fp32-regime ranges are listed, not evaluated: fallback_grid settles them before the
+    // run's records are read (settle_fallback; frac_fetch launches it only when a range was listed)
+    bool fb_pending = false;
+    int fb_n = 0;
+    FallbackArgs fb_args{};
     DBuf<int32_t> d_negsd2, d_slot_range;
     DBuf<uint4> d_work;
     DBuf<uint2> d_rbucket;
@@ -1289,12 +1298,71 @@ inline FitArgs fit_args(const frac_ctx* c, const uint8_t* dtgt, uint32_t tstride
     f.fb_count = c->d_fb_count.ptr;
     f.fb_list = c->d_fb_list.ptr;
     f.plan = c->qplan;
-    // the fused fits evaluate their fp32-regime ranges in the resolving wave (the all-fallback regime
-    // lists every range for fallback_fp32 instead)
-    f.inline_fallback = c->all_fallback ? 0 : 1;
-    f.rbucket = c->d_rbucket.ptr;
-    f.thr = c->p.rms_threshold;
     return f;
+}
+
+// fallback_grid's scratch at the list's capacity: kKeyNone / 0 when (re)allocated, kept so by the kernel
+inline int ensure_fb_scratch(frac_ctx* c)
+{
+    const size_t n = std::max<size_t>(c->d_fb_list.cap, 1);
+    if (c->d_fb_key.cap >= n && c->d_fb_done.cap >= n && c->d_fb_key.ptr && c->d_fb_done.ptr)
+        return FRAC_OK;
+    FRAC_HIP(c, c->d_fb_key.ensure(n));
+    FRAC_HIP(c, c->d_fb_done.ensure(n));
+    FRAC_HIP(c, hipMemsetAsync(c->d_fb_key.ptr, 0xff, c->d_fb_key.cap * sizeof(unsigned long long), c->stream));
+    FRAC_HIP(c, hipMemsetAsync(c->d_fb_done.ptr, 0, c->d_fb_done.cap * sizeof(uint32_t), c->stream));
+    return FRAC_OK;
+}
+
+// the fp32 fallback's arguments for the current run (fallback_grid)
+inline FallbackArgs fallback_args(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride)
+{
+    FallbackArgs b;
+    b.tgt = dtgt;
+    b.tstride = tstride;
+    b.ranges = c->d_ranges.ptr;
+    b.doms = c->d_doms.ptr;
+    b.porig = c->d_porig.ptr;
+    b.pool = c->d_pool.ptr;
+    b.rbucket = c->d_rbucket.ptr;
+    b.fb_count = c->d_fb_count.ptr;
+    b.fb_list = c->d_fb_list.ptr;
+    b.T = c->p.transforms;
+    b.thr = c->p.rms_threshold;
+    b.smax = c->p.s_max;
+    b.out = c->d_out.ptr;
+    b.aux = c->d_aux.ptr;
+    b.fb_key = c->d_fb_key.ptr;
+    b.fb_done = c->d_fb_done.ptr;
+    // jobs per listed range: the largest bucket's domains in chunks of kFbChunk (a planned level: every domain)
+    size_t maxb = 0;
+    for (size_t k = 0; k < c->bucket_begin.size() && k < c->bucket_end.size(); ++k)
+        maxb = std::max<size_t>(maxb, c->bucket_end[k] - c->bucket_begin[k]);
+    if (c->qplan || maxb == 0)
+        maxb = c->doms.size();
+    b.chunks = (uint32_t)std::max<size_t>((maxb + kFbChunk - 1) / kFbChunk, 1);
+    return b;
+}
+
+template <int N>
+void launch_fallback_grid(frac_ctx* c, const FallbackArgs& b)
+{
+    fallback_grid<N><<<kFallbackBlocks, 256, 0, c->stream>>>(b);
+}
+
+// The fused resolvers' listed fp32-regime ranges, settled before anything reads the run's records: one
+// fallback_grid launch (an empty list costs its dispatch).  frac_fetch settles only when a range was listed.
+inline int settle_fallback(frac_ctx* c)
+{
+    if (!c->fb_pending)
+        return FRAC_OK;
+    c->fb_pending = false;
+    if (c->fb_n == 16)
+        launch_fallback_grid<16>(c, c->fb_args);
+    else
+        launch_fallback_grid<8>(c, c->fb_args);
+    FRAC_HIP(c, hipGetLastError());
+    return FRAC_OK;
 }
 
 // work items a search launch covers: the host-built list, or a device-planned level's bound (its
@@ -2232,24 +2300,22 @@ int launch_all(frac_ctx* c)
             fit_winner<N><<<std::max(1u, (nr + 4 * (64 / fit_lanes<N>()) - 1) / (4 * (64 / fit_lanes<N>()))), 256, 0,
                             c->stream>>>(f);
     }
-    // the fused resolvers ran their fp32-regime ranges themselves (FitArgs::inline_fallback): no launch
-    if (nr && !c->virt && !(c->fit_fused && !c->all_fallback)) {
-        FallbackArgs b;
-        b.tgt = dtgt;
-        b.tstride = tstride;
-        b.ranges = c->d_ranges.ptr;
-        b.doms = c->d_doms.ptr;
-        b.porig = c->d_porig.ptr;
-        b.pool = c->d_pool.ptr;
-        b.rbucket = c->d_rbucket.ptr;
-        b.fb_count = c->d_fb_count.ptr;
-        b.fb_list = c->d_fb_list.ptr;
-        b.T = c->p.transforms;
-        b.thr = c->p.rms_threshold;
-        b.smax = c->p.s_max;
-        b.out = c->d_out.ptr;
-        b.aux = c->d_aux.ptr;
-        fallback_fp32<N><<<kFallbackBlocks, 256, 0, c->stream>>>(b);
+    // the fp32 fallback: the fused resolvers (n ≥ 8; below no range leaves the exact regime) list their
+    // fp32-regime ranges and fallback_grid settles them before the records are read (settle_fallback); every
+    // other path runs it here
+    c->fb_pending = false;
+    if (nr && !c->virt) {
+        FRAC_TRY(ensure_fb_scratch(c));
+        const FallbackArgs b = fallback_args(c, dtgt, tstride);
+        if (c->fit_fused && !c->all_fallback) {
+            if constexpr (N >= 8) {
+                c->fb_pending = true;
+                c->fb_n = N;
+                c->fb_args = b;
+            }
+        } else {
+            launch_fallback_grid<N>(c, b);
+        }
     }
     if (timing) {
         FRAC_TRY(mark_event(c, 3));
@@ -2534,6 +2600,7 @@ int qt_encode_dev(frac_ctx* c, const frac_quadtree_params* qp, LevelGrid& level,
         }
         c->qplan = nullptr;
         FRAC_TRY(rc);
+        FRAC_TRY(settle_fallback(c)); // the level's records are complete before its transition reads them
         if (timing)
             runs.push_back(c->hist_runs - 1);
         tr.mark("level launch");
@@ -2777,6 +2844,10 @@ void frac_destroy(frac_ctx* c)
     c->d_dft_trmax.release();
     c->d_dft_tpool.release();
     c->d_dft_rorb.release();
+    c->d_dft_slotbest.release();
+    c->d_qt_leaves32.release();
+    c->d_fb_key.release();
+    c->d_fb_done.release();
     c->d_rstat.release();
     c->d_cls_items.release();
     c->d_cls_list.release();
@@ -2966,6 +3037,8 @@ int frac_sync(frac_ctx* c)
 {
     if (!c)
         return FRAC_E_INVALID;
+    FRAC_HIP(c, hipSetDevice(c->device));
+    FRAC_TRY(settle_fallback(c)); // after the sync the records are complete
     FRAC_HIP(c, hipStreamSynchronize(c->stream));
     return FRAC_OK;
 }
@@ -2992,7 +3065,24 @@ int frac_fetch(frac_ctx* c, frac_encode_item* out, frac_stats* stats)
     if (sea_ran)
         FRAC_HIP(c, hipMemcpyAsync(&sea_count, c->d_sea_count.ptr, sizeof(sea_count), hipMemcpyDeviceToHost,
                                    c->stream));
+    uint32_t listed = 0; // the fused resolvers' fp32-regime ranges (settle_fallback)
+    if (c->fb_pending)
+        FRAC_HIP(c, hipMemcpyAsync(&listed, c->d_fb_count.ptr, sizeof(listed), hipMemcpyDeviceToHost, c->stream));
     FRAC_HIP(c, hipStreamSynchronize(c->stream));
+    if (c->fb_pending) {
+        if (listed) { // rare: their records come from fallback_grid, then the copies again
+            FRAC_HIP(c, hipSetDevice(c->device));
+            FRAC_TRY(settle_fallback(c));
+            if (nr && out)
+                FRAC_HIP(c, hipMemcpyAsync(out, c->d_out.ptr, nr * sizeof(frac_encode_item), hipMemcpyDeviceToHost,
+                                           c->stream));
+            if (nr)
+                FRAC_HIP(c, hipMemcpyAsync(c->h_aux.data(), c->d_aux.ptr, nr * sizeof(RangeAux),
+                                           hipMemcpyDeviceToHost, c->stream));
+            FRAC_HIP(c, hipStreamSynchronize(c->stream));
+        }
+        c->fb_pending = false;
+    }
     if (sea_ran)
         c->evaluated_ran = sea_count;
     if (stats) {
@@ -3095,7 +3185,15 @@ int frac_set_stream(frac_ctx* c, void* s)
 
 void* frac_get_stream(frac_ctx* c) { return c ? reinterpret_cast<void*>(c->stream) : nullptr; }
 
-const frac_encode_item* frac_device_results(frac_ctx* c) { return c ? c->d_out.ptr : nullptr; }
+const frac_encode_item* frac_device_results(frac_ctx* c)
+{
+    if (!c)
+        return nullptr;
+    // work enqueued on the context's stream after this call reads complete records
+    if (c->fb_pending && (hipSetDevice(c->device) != hipSuccess || settle_fallback(c) != FRAC_OK))
+        return nullptr;
+    return c->d_out.ptr;
+}
 
 static int encode_quadtree_impl(frac_ctx* c, const frac_quadtree_params* qp, frac_encode_item* out,
                                 frac_qt_leaf* out32, size_t cap, size_t* n_out, frac_stats* stats);
@@ -3204,6 +3302,7 @@ static int encode_quadtree_impl(frac_ctx* c, const frac_quadtree_params* qp, fra
         c->dirty = true;
         tr.mark("grids");
         FRAC_TRY(frac_run(c));
+        FRAC_TRY(settle_fallback(c)); // the level's records are complete before qt_flags reads them
         tr.mark("run (enqueue)");
         // the level's statistics accumulate on the device (no per-level download or host loop); the
         // counters are read once after the last level, the event times after this level's count
@@ -3577,6 +3676,7 @@ int frac_decode_results(frac_ctx* c, uint32_t w, uint32_t h, int max_iter, doubl
     if (c->src.w > w || c->src.h > h || c->tgt.w > w || c->tgt.h > h)
         return c->fail(FRAC_E_INVALID, "decode: plane smaller than the encoded planes");
     FRAC_HIP(c, hipSetDevice(c->device));
+    FRAC_TRY(settle_fallback(c));
     // the fused form needs every range written: no empty (domain-less) record among the results
     bool fused = covers_exactly(c->ranges, w, h);
     if (fused && !c->ranges.empty()) {
@@ -3604,6 +3704,7 @@ int frac_copy_tuples_device(frac_ctx* c, void* d_dst)
         if (!d_dst)
             return c->fail(FRAC_E_INVALID, "copy_tuples: NULL destination");
         FRAC_HIP(c, hipSetDevice(c->device));
+        FRAC_TRY(settle_fallback(c));
         pack_tuples<<<(nr + 255) / 256, 256, 0, c->stream>>>(c->d_out.ptr, c->d_aux.ptr, c->d_porig.ptr, nr,
                                                              static_cast<frac_tuple*>(d_dst));
         FRAC_HIP(c, hipGetLastError());
@@ -3654,6 +3755,7 @@ int frac_pack_frc1(frac_ctx* c, uint32_t cbits, uint32_t bbits, uint8_t* out, si
     if (!out)
         return FRAC_OK;
     FRAC_HIP(c, hipSetDevice(c->device));
+    FRAC_TRY(settle_fallback(c));
     Frc1MinMax mm{~0ull, 0ull, ~0ull, 0ull};
     std::vector<uint32_t> words(nwords);
     if (nr) {
@@ -3736,6 +3838,8 @@ int frac_copy_results_device(frac_ctx* c, void* d_dst)
     if (!c->ran)
         return c->fail(FRAC_E_STATE, "no results: frac_run has not been called");
     const size_t nr = nranges(c);
+    FRAC_HIP(c, hipSetDevice(c->device));
+    FRAC_TRY(settle_fallback(c));
     if (nr)
         FRAC_HIP(c, hipMemcpyAsync(d_dst, c->d_out.ptr, nr * sizeof(frac_encode_item), hipMemcpyDeviceToDevice,
                                    c->stream));

@@ -208,7 +208,7 @@ constexpr uint32_t kClockStampWords = 6;
 // (SamplerBilinear's integer sum, image/sampler.h:21-38, as pool_build), two cells per
 // 32-bit word — (w & 0x00ff00ff) + ((w >> 8) & 0x00ff00ff) over the word of both rows is
 // the packed u16 pair the pool stores — and the same registers feed the tile fragments.
-// Outputs: the pool and −ΣD4² (read by fit_winner and fallback_fp32), the pool rows again in
+// Outputs: the pool and −ΣD4² (read by fit_winner and fallback_grid), the pool rows again in
 // tile order (resolve_dft); per 32-domain tile the A fragments of the four K-steps
 // [s_b | u_b | γ | δ] (lane l: row l&31, orbit 8(l>>5) + j), −Σb² per row in the [2][16]
 // lane-half layout of the epilogue, and the tile's fast-path guard terms.  Every pool
@@ -1550,7 +1550,7 @@ __device__ inline DftResolved resolve_dft_eval(const MfmaResolveArgs& a, uint32_
         const int row = (i & 3) + 8 * (i >> 2) + 4 * (int)h;
         if (!exact) {
             // fp32 fallback regime: every candidate has S16 ≥ 2^24; any valid domain of the
-            // bucket routes the range to fallback_fp32 through fit_winner
+            // bucket routes the range to fallback_grid through the fit's listing
             const int p = a.tile_pos[tile0 * 32 + row];
             const unsigned long long mask = __ballot(p >= 0 && g == 0);
             if (mask) {
@@ -1732,12 +1732,6 @@ __device__ inline void resolve_dft_record(const MfmaResolveArgs& a, uint32_t r, 
                                           const frac_grid_item& rg)
 {
     if (a.fused_fit) { // the range's record right here: one launch less per run (C2: 5 µs of a 43 µs frame)
-        if (a.fit.inline_fallback && key_needs_fallback(w.bestk)) { // the fp32 regime, by this wave
-            if (lane == 0)
-                a.best_key[r] = w.bestk;
-            fallback_wave<8>(a.fit, r, lane);
-            return;
-        }
         if (lane == 0) {
             a.best_key[r] = w.bestk;
             fit_rstat_range<8>(a.fit, r, w.bestk, make_uint4(w.bx, w.bs1 | (w.sr1 << 16), w.bs2, w.sr2), &rg);

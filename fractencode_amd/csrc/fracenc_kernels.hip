@@ -7,7 +7,7 @@
 //                   broadcast from SGPRs), u64 atomicMin of the selection key per range
 //   fit_winner      per range: re-derive the transform of the winning domain, the reference's
 //                   least-squares contrast/brightness (FP64) and its fp32 error
-//   fallback_fp32   ranges whose best error leaves the exact fp32 regime: sequential fp32
+//   fallback_grid   ranges whose best error leaves the exact fp32 regime: sequential fp32
 //                   emulation of image/metrics.h over all candidates
 #pragma once
 #include "fracenc_common.h"
@@ -292,11 +292,6 @@ struct FitArgs {
     uint32_t* fb_count;
     uint32_t* fb_list;
     const DevPlan* plan = nullptr; // device-planned search: nr from the plan (the grid is a bound)
-    // the resolvers' fused fits: a range whose key leaves the exact regime is evaluated in fp32 by the
-    // resolving wave itself (fallback_wave), and no fallback_fp32 launch follows
-    int inline_fallback = 0;
-    const uint2* rbucket = nullptr; // per range its bucket's pool slice [x, y) (fallback_wave)
-    double thr = 0.0;               // the hit threshold on the fp32 distance (fallback_wave)
 };
 
 __device__ inline void write_fit(frac_encode_item& o, const frac_grid_item& rg, const frac_grid_item& d, int t,
@@ -472,7 +467,7 @@ __device__ inline void fit_sums_range(const FitArgs& a, uint32_t r, unsigned lon
     const bool hit = (key >> 63) == 0;
     const long long err = hit ? 0 : (long long)((key >> 27) & 0xfffffffffull);
     const int t = hit ? (int)(key & 7u) : (int)(a.T - 1 - (uint32_t)(key & 7u));
-    if (!hit && err >= kExactLimit) { // fp32 regime: fallback_fp32 writes the record
+    if (!hit && err >= kExactLimit) { // fp32 regime: listed; fallback_grid writes the record
         a.aux[r] = RangeAux{p, (uint32_t)kAuxFallback};
         a.fb_list[atomicAdd(a.fb_count, 1u)] = r;
         return;
@@ -502,7 +497,7 @@ __device__ inline void fit_rstat_range(const FitArgs& a, uint32_t r, unsigned lo
     const bool hit = (key >> 63) == 0;
     const long long err = hit ? 0 : (long long)((key >> 27) & 0xffffffffull);
     const int t = hit ? (int)(key & 7u) : (int)(a.T - 1 - (uint32_t)(key & 7u));
-    if (!hit && err >= kExactLimit) { // fp32 regime: fallback_fp32 writes the record
+    if (!hit && err >= kExactLimit) { // fp32 regime: listed; fallback_grid writes the record
         a.aux[r] = RangeAux{p, (uint32_t)kAuxFallback};
         a.fb_list[atomicAdd(a.fb_count, 1u)] = r;
         return;
@@ -542,8 +537,7 @@ __global__ void __launch_bounds__(256) fit_winner(FitArgs a)
 }
 
 // ---------------------------------------------------------------------------
-// fallback_fp32<N>: one block per flagged range (grid-stride over the list).
-// Evaluates every candidate of the range's bucket with the reference's exact
+// The fp32 fallback (fallback_grid below): every candidate of a listed range's bucket with the reference's exact
 // arithmetic: fp32 sum over range pixels in row-major order of
 // (float(r) − float(2×2 sum)/4)² (image/metrics.h:37-50).  Selection key:
 //   hit  (dist <= thr): (pos_local << 3) | t
@@ -564,10 +558,16 @@ struct FallbackArgs {
     double smax;
     frac_encode_item* out;
     RangeAux* aux;
+    // fallback_grid: per listed range the least key so far and its jobs done (kKeyNone / 0 between runs), and
+    // the jobs per range (the domain chunks of the largest bucket)
+    unsigned long long* fb_key = nullptr;
+    uint32_t* fb_done = nullptr;
+    uint32_t chunks = 0;
 };
 
 // one block per CU: an empty list (the usual case) costs the dispatch of these blocks only
 constexpr unsigned kFallbackBlocks = 256;
+constexpr uint32_t kFbChunk = 256; // fallback_grid: bucket domains per job (one per thread, every transform)
 
 // one candidate (pool position bk.x + pl, transform t) of a range in the reference's fp32 arithmetic
 // (rpix: the range's pixels as floats), as its selection key
@@ -633,74 +633,135 @@ __device__ inline void fallback_record(const uint32_t* __restrict__ pool, const 
     aux[r] = RangeAux{p, (uint32_t)(kAuxFallback | (hit ? kAuxHit : 0u))};
 }
 
+// The reference's fp32 error of one (domain row, transform TT) (image/metrics.h:37-50): the row in registers,
+// the transform a compile-time permutation, the range's pixels from LDS; every term exact, the sum sequential
+// with one rounding per addition (__fadd_rn), as the reference's loop.
+template <int N, int TT>
+__device__ inline float fp32_error_t(const uint32_t* __restrict__ dp, const float* rpix)
+{
+    constexpr int NN = N * N, W = (NN + 1) / 2;
+    if constexpr (N > 8) { // n = 16: a 128-word row would not stay in registers; the cells load as used
+        float F = 0.0f;
+#pragma unroll 16
+        for (int q = 0; q < NN; ++q) {
+            const int f = fwd_index<N>(TT, q);
+            const uint32_t fw = dp[f >> 1];
+            const float smp = (float)((f & 1) ? (fw >> 16) : (fw & 0xffffu)) / 4.0f;
+            const float val = __fsub_rn(rpix[q], smp);
+            F = __fadd_rn(F, __fmul_rn(val, val));
+        }
+        return F;
+    }
+    uint32_t w[N > 8 ? 1 : W];
+    if constexpr (N > 8) {
+    } else if constexpr (W % 4 == 0) {
+#pragma unroll
+        for (int k = 0; k < W / 4; ++k) {
+            const uint4 v = reinterpret_cast<const uint4*>(dp)[k];
+            w[4 * k] = v.x;
+            w[4 * k + 1] = v.y;
+            w[4 * k + 2] = v.z;
+            w[4 * k + 3] = v.w;
+        }
+    } else { // n = 2: a row of two words
+#pragma unroll
+        for (int k = 0; k < W; ++k)
+            w[k] = dp[k];
+    }
+    float F = 0.0f;
+#pragma unroll
+    for (int q = 0; q < NN; ++q) {
+        const int f = fwd_index<N>(TT, q);
+        const uint32_t fw = w[f >> 1];
+        const float smp = (float)((f & 1) ? (fw >> 16) : (fw & 0xffffu)) / 4.0f;
+        const float val = __fsub_rn(rpix[q], smp);
+        F = __fadd_rn(F, __fmul_rn(val, val));
+    }
+    return F;
+}
+
 template <int N>
-__global__ void __launch_bounds__(256) fallback_fp32(FallbackArgs a)
+__device__ inline float fp32_error(const uint32_t* __restrict__ dp, const float* rpix, int t)
+{
+    switch (t) {
+    case 0: return fp32_error_t<N, 0>(dp, rpix);
+    case 1: return fp32_error_t<N, 1>(dp, rpix);
+    case 2: return fp32_error_t<N, 2>(dp, rpix);
+    case 3: return fp32_error_t<N, 3>(dp, rpix);
+    case 4: return fp32_error_t<N, 4>(dp, rpix);
+    case 5: return fp32_error_t<N, 5>(dp, rpix);
+    case 6: return fp32_error_t<N, 6>(dp, rpix);
+    default: return fp32_error_t<N, 7>(dp, rpix);
+    }
+}
+
+// fallback_grid<N>: every range on the list (the fused resolvers list their fp32-regime ranges — only for n ≥ 8:
+// below, S16 ≤ n²·1020² < 2^24 — and the all-fallback regime of a threshold at or above 2^24 lists them all) evaluated by the whole grid — a job is (listed range, chunk of kFbChunk bucket domains), one
+// domain per thread and every transform; a block minimum of the selection keys (fallback_key's) goes into the
+// range's fb_key with a 64-bit atomicMin, and the job completing the range's count writes its record
+// (fallback_record) and resets the pair.  One wave per range (the resolvers' former in-wave fallback) took
+// 328 ms for one C3 range (1,044,484 candidates); here the list's work spreads over every CU.  An empty list
+// (the usual case) costs the blocks' dispatch.
+template <int N>
+__global__ void __launch_bounds__(256) fallback_grid(FallbackArgs a)
 {
     constexpr int NN = N * N;
     __shared__ float rpix[NN];
-    __shared__ unsigned long long red[256];
+    __shared__ unsigned long long red[4];
+    __shared__ uint32_t last;
     const uint32_t count = *a.fb_count;
-    for (uint32_t e = blockIdx.x; e < count; e += gridDim.x) {
+    const uint64_t jobs = (uint64_t)count * a.chunks;
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    for (uint64_t job = blockIdx.x; job < jobs; job += gridDim.x) {
+        const uint32_t e = (uint32_t)(job / a.chunks), ch = (uint32_t)(job % a.chunks);
         const uint32_t r = a.fb_list[e];
         const frac_grid_item rg = a.ranges[r];
         const uint2 bk = a.rbucket[r];
-        __syncthreads();
+        __syncthreads(); // the previous job's LDS reads are done
         for (int q = threadIdx.x; q < NN; q += blockDim.x)
             rpix[q] = (float)(int16_t)a.tgt[(size_t)(rg.y + q / N) * a.tstride + rg.x + (q % N)];
         __syncthreads();
         unsigned long long best = kKeyNone;
-        const uint32_t ncand = (bk.y - bk.x) * a.T;
-        for (uint32_t c = threadIdx.x; c < ncand; c += blockDim.x) {
-            const unsigned long long key = fallback_key<N>(a.pool, rpix, bk.x + c / a.T, c / a.T, (int)(c % a.T), a.T, a.thr);
-            best = key < best ? key : best;
-        }
-        red[threadIdx.x] = best;
-        __syncthreads();
-        for (int s = blockDim.x / 2; s > 0; s >>= 1) {
-            if ((int)threadIdx.x < s) {
-                const unsigned long long o = red[threadIdx.x + s];
-                if (o < red[threadIdx.x])
-                    red[threadIdx.x] = o;
+        const uint32_t p = bk.x + ch * kFbChunk + threadIdx.x;
+        if (p < bk.y) {
+            const uint32_t* dp = a.pool + (size_t)p * (NN / 2);
+            for (uint32_t t = 0; t < a.T; ++t) {
+                const float F = fp32_error<N>(dp, rpix, (int)t);
+                const double dist = (double)F / (double)(4 * NN);
+                const uint32_t pl = p - bk.x;
+                const unsigned long long key =
+                    dist <= a.thr ? (((unsigned long long)pl << 3) | (unsigned long long)t)
+                                  : (kKeyMiss | ((unsigned long long)__float_as_uint(F) << 27) |
+                                     ((unsigned long long)pl << 3) | (unsigned long long)(a.T - 1 - t));
+                best = key < best ? key : best;
             }
-            __syncthreads();
         }
-        if (threadIdx.x == 0)
-            fallback_record<N>(a.pool, a.doms, a.porig, a.T, a.smax, a.out, a.aux, r, rg, bk, red[0], rpix);
-    }
-}
-
-// fallback_fp32's evaluation of range r by one wave (the resolvers' fused fits, FitArgs::inline_fallback):
-// the range's pixels in this wave's LDS row, the candidates across the lanes, a wave minimum of the keys.
-// Counted in fb_count (the run's fallback_ranges) but not listed: no fallback_fp32 launch follows.
-template <int N>
-__device__ inline void fallback_wave(const FitArgs& a, uint32_t r, int lane)
-{
-    constexpr int NN = N * N;
-    __shared__ float rpix_w[4][NN]; // resolve workgroups have at most 4 waves
-    float* rpix = rpix_w[(threadIdx.x >> 6) & 3u];
-    const frac_grid_item rg = a.ranges[r];
-    const uint2 bk = a.rbucket[r];
-    for (int q = lane; q < NN; q += 64)
-        rpix[q] = (float)(int16_t)a.tgt[(size_t)(rg.y + q / N) * a.tstride + rg.x + (q % N)];
-    // the LDS writes above and the reads below are one wave's, issued in order: keep the compiler's order
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    unsigned long long best = kKeyNone;
-    const uint32_t ncand = (bk.y - bk.x) * a.T;
-    for (uint32_t c = (uint32_t)lane; c < ncand; c += 64) {
-        const unsigned long long key = fallback_key<N>(a.pool, rpix, bk.x + c / a.T, c / a.T, (int)(c % a.T), a.T, a.thr);
-        best = key < best ? key : best;
-    }
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const unsigned long long ob = ((unsigned long long)(uint32_t)__shfl_xor((int)(uint32_t)(best >> 32), o, 64) << 32) |
-                                      (uint32_t)__shfl_xor((int)(uint32_t)best, o, 64);
-        best = ob < best ? ob : best;
-    }
-    if (lane == 0) {
-        atomicAdd(a.fb_count, 1u);
-        fallback_record<N>(a.pool, a.doms, a.porig, a.T, a.smax, a.out, a.aux, r, rg, bk, best, rpix);
+        for (int o = 32; o > 0; o >>= 1) {
+            const unsigned long long ob = ((unsigned long long)(uint32_t)__shfl_xor((int)(uint32_t)(best >> 32), o, 64) << 32) |
+                                          (uint32_t)__shfl_xor((int)(uint32_t)best, o, 64);
+            best = ob < best ? ob : best;
+        }
+        if (lane == 0)
+            red[wv] = best;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            unsigned long long b = red[0];
+            for (uint32_t w = 1; w < blockDim.x / 64; ++w)
+                b = red[w] < b ? red[w] : b;
+            if (b != kKeyNone)
+                atomicMin(a.fb_key + e, b);
+            __threadfence(); // the key lands before the count that may let another job read it
+            last = atomicAdd(a.fb_done + e, 1u) + 1u == a.chunks ? 1u : 0u;
+            __threadfence();
+        }
+        __syncthreads();
+        if (last && threadIdx.x == 0) {
+            const unsigned long long k = atomicMin(a.fb_key + e, kKeyNone); // the final key (kKeyNone changes nothing)
+            fallback_record<N>(a.pool, a.doms, a.porig, a.T, a.smax, a.out, a.aux, r, rg, bk, k, rpix);
+            a.fb_key[e] = kKeyNone; // clean for the next run's list
+            a.fb_done[e] = 0u;
+        }
     }
 }
 

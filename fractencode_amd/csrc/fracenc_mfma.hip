@@ -1084,12 +1084,6 @@ __global__ void __launch_bounds__(256) resolve_mfma(MfmaResolveArgs a)
             }
         }
     }
-    if (a.fused_fit && a.fit.inline_fallback && key_needs_fallback(bestk)) { // the fp32 regime, by this wave
-        if (lane == 0)
-            a.best_key[r] = bestk;
-        fallback_wave<N>(a.fit, r, lane);
-        return;
-    }
     if (lane == 0) {
         a.best_key[r] = bestk;
         if (a.fused_fit) // the record right here: no fit_winner launch
@@ -1252,12 +1246,6 @@ __global__ void __launch_bounds__(256, 6) resolve_small(MfmaResolveArgs a)
                 }
             }
         }
-    }
-    if (a.fused_fit && a.fit.inline_fallback && key_needs_fallback(bestk)) { // the fp32 regime, by this wave
-        if (lane == 0)
-            a.best_key[r] = bestk;
-        fallback_wave<N>(a.fit, r, lane);
-        return;
     }
     if (lane == 0) {
         a.best_key[r] = bestk;

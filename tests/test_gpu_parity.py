@@ -654,11 +654,11 @@ def test_rectangular_ranges_random_planes_match_oracle(oracle, engine):
 
 
 @pytest.mark.parametrize("n,T", [(8, 4), (8, 8), (16, 4), (16, 8)])
-def test_fp32_regime_in_the_resolving_wave(n, T):
+def test_fp32_regime_through_the_fallback_grid(n, T):
     """Ranges whose best exact error is at least 2^24 (S16) take the reference's fp32 arithmetic
-    (image/metrics.h:37-50).  The MFMA engine's fused resolvers (resolve_small / resolve_dft / resolve_mfma)
-    evaluate them in the resolving wave (fallback_wave) and launch no fallback_fp32; the VALU engine lists
-    them for the fallback_fp32 kernel.  Isolated bright n×n blocks 4n apart on a black frame: every
+    (image/metrics.h:37-50).  The MFMA engine's fused resolvers (resolve_dft / resolve_mfma) list them and
+    fallback_grid settles them before the records are read (frac_fetch here); the VALU engine runs
+    fallback_grid at the end of every run.  Isolated bright n×n blocks 4n apart on a black frame: every
     domain is mostly dark (at most a quarter of its cells bright: S16 ≥ 48·1020² at n = 8), so each bright range
     is in the fp32 regime.  Records, fallback counts and reject counts agree, and the fallback count is the
     bright blocks'.  (n ≤ 4 never reaches the regime: 16 cells · 1020² < 2^24.)"""
@@ -681,3 +681,48 @@ def test_fp32_regime_in_the_resolving_wave(n, T):
     assert sa["fallback_ranges"] == sb["fallback_ranges"] == nb, (sa["fallback_ranges"], sb["fallback_ranges"], nb)
     assert a.tobytes() == b.tobytes()
     assert sa["rejected_mappings"] == sb["rejected_mappings"]
+
+
+def _white_ranges_frame(S, k, seed=17):
+    """tools/fallback_probe.py's frame: S1 value noise scaled into [0, 60] with k white 8×8 ranges, each alone in a
+    black 24×24 patch — the white ranges' best error is ≥ 2^24 (fp32 regime), the rest are ordinary."""
+    from fractencode_amd.synth import value_noise
+    p = (value_noise(S, S, 1234).astype(np.float64) * (60.0 / 255.0)).astype(np.uint8)
+    rng = np.random.default_rng(seed)
+    where = []
+    for c in rng.choice((S // 24) ** 2, size=k, replace=False):
+        y0, x0 = (c // (S // 24)) * 24, (c % (S // 24)) * 24
+        p[y0:y0 + 24, x0:x0 + 24] = 0
+        p[y0 + 8:y0 + 16, x0 + 8:x0 + 16] = 255
+        where.append((x0 + 8, y0 + 8))
+    return p, where
+
+
+@pytest.mark.parametrize("T,cls", [(4, False), (8, False), (4, True)])
+def test_fp32_regime_at_scale_every_consumer(oracle, T, cls):
+    """A 1024² frame with 6 fp32-regime ranges among 16,384: every consumer of the run's records — the device
+    tuples (frac_copy_tuples_device → fetch_tuples), frac_fetch, the device decode's input — sees the
+    fp32 winners fallback_grid writes, and those equal the oracle's (the reference's fp32 loop restated)."""
+    S = 1024
+    p, where = _white_ranges_frame(S, 6)
+    doms, rngs = F.create_uniform_grid(S, S, 16, 8), F.create_uniform_grid(S, S, 8, 8)
+    if cls:
+        doms, rngs = F.preclassify(p, doms), F.preclassify(p, rngs)
+    with F.Engine(0, T, cls, 0.0, -1.0, F.ENGINE_MFMA) as e:
+        e.set_frame(p)
+        e.set_domains(doms)
+        e.set_ranges(rngs)
+        e.run()
+        tup = e.fetch_tuples()  # an asynchronous consumer first (the pack runs after the settle)
+        out, st = e.fetch()
+    idx = np.array([(y // 8) * (S // 8) + x // 8 for x, y in where])
+    if not cls:  # with the classifier a white range may meet no domain of its category (the default record)
+        assert st["fallback_ranges"] >= len(where)
+    want, _, _ = oracle.estimate(p, doms.astype(oracle.ITEM_DTYPE), rngs[idx].astype(oracle.ITEM_DTYPE), T=T,
+                                 use_classifier=cls, threads=8)
+    for a, b in (("dx", "dx"), ("dy", "dy"), ("transform", "t"), ("distance", "dist"), ("contrast", "s"),
+                 ("brightness", "o")):
+        np.testing.assert_array_equal(out[a][idx], want[b], err_msg=a)
+    assert (out["distance"][idx] * 16 * 256 >= (1 << 24)).all()  # they are in the fp32 regime
+    for k in ("transform", "contrast", "brightness", "distance"):
+        np.testing.assert_array_equal(tup[k], out[k], err_msg=k)
