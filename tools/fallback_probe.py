@@ -3,11 +3,13 @@
 domain's 2×2 sums come near 1020 — with K isolated white 8×8 ranges, each alone in a black 24×24 patch.  A white
 range's best error is then ≥ 48·1020² > 2^24 (the domain holding it covers a quarter of its cells), the
 fp32 regime the resolving wave emulates in reference order over every candidate of its bucket.  Prints per K
-the per-run device / search / finish ms (library HIP events, median of `reps` runs) and the fallback count.
+the per-run device / search / finish ms (library HIP events, median of `reps` runs: the run's kernels, before
+the fallback settles), the wall clock per run + sync (the fallback included) and the fallback count.
 usage: tools/fallback_probe.py [K ...]"""
 import json
 import os
 import sys
+import time
 
 import numpy as np
 
@@ -39,10 +41,13 @@ if __name__ == "__main__":
             e.run()
             e.sync()
             e.timing_history()
+            t0 = time.perf_counter()
             for _ in range(reps):
                 e.run()
+                e.sync()  # settles the listed fp32-regime ranges (fallback_grid)
+            wall = (time.perf_counter() - t0) / reps
             h = e.timing_history()
             _, st = e.fetch()
-        print(json.dumps({"white_ranges": k, "fallback_ranges": st["fallback_ranges"],
+        print(json.dumps({"white_ranges": k, "fallback_ranges": st["fallback_ranges"], "wall_ms": round(wall * 1e3, 3),
                           **{k2: round(float(np.median(h["ms_" + k2])), 3) for k2 in ("device", "search", "finish")}}),
               flush=True)
