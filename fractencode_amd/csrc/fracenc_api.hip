@@ -220,7 +220,6 @@ struct frac_ctx {
     DBuf<uint4> d_m8_work;
     DBuf<uint32_t> d_m8_blk_ptr, d_m8_blk_ent;
     DBuf<int32_t> d_m_slot_range, d_m_tile_pos;
-    DBuf<uint2> d_m_slot_xy, d_m_tile_xy; // slot / tile-row origins (the Fourier preparation's geometry)
     DBuf<uint32_t> d_m_range_slot, d_m_blk_ptr, d_m_blk_ent, d_m_rconst, d_m_dconst;
     DBuf<uint4> d_m_work, d_m_dtiles, d_m_rfrags;
     DBuf<uint2> d_m_entries;
@@ -1123,8 +1122,6 @@ int prepare(frac_ctx* c)
         FRAC_HIP(c, c->d_m_slot_range.ensure((size_t)c->nblocks * 32 * c->dft_copies));
         FRAC_HIP(c, c->d_m_range_slot.ensure(nr));
         FRAC_HIP(c, c->d_m_tile_pos.ensure((size_t)c->ntiles * 32));
-        FRAC_HIP(c, c->d_m_slot_xy.ensure((size_t)c->nblocks * 32 * c->dft_copies));
-        FRAC_HIP(c, c->d_m_tile_xy.ensure((size_t)c->ntiles * 32));
         FRAC_HIP(c, c->d_m_work.ensure(c->m_work.size()));
         FRAC_HIP(c, c->d_m_blk_ptr.ensure(c->m_blk_ptr.size()));
         FRAC_HIP(c, c->d_m_blk_ent.ensure(c->m_blk_ent.size()));
@@ -1145,21 +1142,15 @@ int prepare(frac_ctx* c)
         }
         if (c->nblocks) {
             fill_range_slots<<<(c->nblocks * 32 + 255) / 256, 256, 0, c->stream>>>(
-                c->mlayout, c->d_rord.ptr, c->nblocks * 32, c->d_m_slot_range.ptr, c->d_m_range_slot.ptr,
-                c->d_ranges.ptr, c->d_m_slot_xy.ptr);
-            if (c->dft_copies == 2) {
+                c->mlayout, c->d_rord.ptr, c->nblocks * 32, c->d_m_slot_range.ptr, c->d_m_range_slot.ptr);
+            if (c->dft_copies == 2)
                 FRAC_HIP(c, hipMemcpyAsync(c->d_m_slot_range.ptr + (size_t)c->nblocks * 32, c->d_m_slot_range.ptr,
                                            (size_t)c->nblocks * 32 * sizeof(int32_t), hipMemcpyDeviceToDevice,
                                            c->stream));
-                FRAC_HIP(c, hipMemcpyAsync(c->d_m_slot_xy.ptr + (size_t)c->nblocks * 32, c->d_m_slot_xy.ptr,
-                                           (size_t)c->nblocks * 32 * sizeof(uint2), hipMemcpyDeviceToDevice,
-                                           c->stream));
-            }
         }
-        if (c->ntiles) // (tile_xy only where a tile row is one domain: not the sampled form's virtual rows)
-            fill_tile_pos<<<(c->ntiles * 32 + 255) / 256, 256, 0, c->stream>>>(
-                c->mlayout, c->ntiles * 32, c->d_m_tile_pos.ptr, c->d_porig.ptr, c->d_doms.ptr,
-                c->virt ? nullptr : c->d_m_tile_xy.ptr);
+        if (c->ntiles)
+            fill_tile_pos<<<(c->ntiles * 32 + 255) / 256, 256, 0, c->stream>>>(c->mlayout, c->ntiles * 32,
+                                                                              c->d_m_tile_pos.ptr);
         FRAC_TRY(up(c->d_m_work.ptr, c->m_work.data(), c->m_work.size() * sizeof(uint4)));
         FRAC_TRY(up(c->d_m_blk_ptr.ptr, c->m_blk_ptr.data(), c->m_blk_ptr.size() * sizeof(uint32_t)));
         FRAC_TRY(up(c->d_m_blk_ent.ptr, c->m_blk_ent.data(), c->m_blk_ent.size() * sizeof(uint32_t)));
@@ -1453,13 +1444,11 @@ inline int launch_dft(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool i
     b.pool = c->d_pool.ptr;
     b.negsd2 = c->d_negsd2.ptr;
     b.tpool = c->d_dft_tpool.ptr;
-    b.tile_xy = c->d_m_tile_xy.ptr;
     MfmaRangePrepArgs r;
     r.tgt = dtgt;
     r.tstride = tstride;
     r.ranges = c->d_ranges.ptr;
     r.slot_range = c->d_m_slot_range.ptr;
-    r.slot_xy = c->d_m_slot_xy.ptr;
     r.nblocks = nbk;
     r.T = 4;
     r.rfrags = c->d_m_rfrags.ptr;
@@ -2589,15 +2578,6 @@ int qt_encode_dev(frac_ctx* c, const frac_quadtree_params* qp, LevelGrid& level,
         fa.rconst = fourier ? nullptr : c->d_m_rconst.ptr;
         fa.best_key = c->d_best_key.ptr;
         fa.fb_count = c->d_fb_count.ptr;
-        if (fourier) { // the Fourier preparation's geometry maps
-            FRAC_HIP(c, c->d_m_slot_xy.ensure((size_t)nblocks_cap * 32 * cp));
-            FRAC_HIP(c, c->d_m_tile_xy.ensure((size_t)ntiles_cap * 32));
-            fa.ranges = c->d_ranges.ptr;
-            fa.doms = c->d_doms.ptr;
-            fa.porig = c->d_porig.ptr;
-            fa.slot_xy = c->d_m_slot_xy.ptr;
-            fa.tile_xy = c->d_m_tile_xy.ptr;
-        }
         // the layout, work lists, CSR map and per-item maps: one launch
         qt_plan<<<std::max(32u, (fa.nthreads + 255) / 256), 256, 0, c->stream>>>(pa);
         // the level's search, on the bounds: launch_all in plan mode
@@ -2810,8 +2790,6 @@ void frac_destroy(frac_ctx* c)
     c->d_aux.release();
     c->d_m_slot_range.release();
     c->d_m_tile_pos.release();
-    c->d_m_slot_xy.release();
-    c->d_m_tile_xy.release();
     c->d_m_range_slot.release();
     c->d_m_blk_ptr.release();
     c->d_m_blk_ent.release();

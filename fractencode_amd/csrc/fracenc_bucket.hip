@@ -424,13 +424,9 @@ __device__ inline uint32_t layout_bucket_of_slot(const BucketLayout& L, uint32_t
 
 // range slots (MFMA: 32 per block, VALU: 64 per wave): slot s of bucket b holds the bucket's
 // k-th range, k = s − slot_first[b], or −1 (padding); range_slot is the inverse map (may be null)
-// slot_xy (optional): each slot's range origin, so the Fourier preparation reads a slot's geometry in the load
-// that gives its range (no slot_range → ranges chain, dft_range_prep_pair_at)
 __global__ void __launch_bounds__(256) fill_range_slots(BucketLayout L, const uint32_t* __restrict__ rord,
                                                         uint32_t nslots, int32_t* __restrict__ slot_range,
-                                                        uint32_t* __restrict__ range_slot,
-                                                        const frac_grid_item* __restrict__ ranges = nullptr,
-                                                        uint2* __restrict__ slot_xy = nullptr)
+                                                        uint32_t* __restrict__ range_slot)
 {
     const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= nslots)
@@ -444,17 +440,10 @@ __global__ void __launch_bounds__(256) fill_range_slots(BucketLayout L, const ui
             range_slot[r] = s;
     }
     slot_range[s] = r;
-    if (slot_xy)
-        slot_xy[s] = r >= 0 ? make_uint2(ranges[r].x, ranges[r].y) : make_uint2(0u, 0u);
 }
 
-// tile rows: row j of bucket b's tiles holds engine pool row VT·dbeg[b] + j, or −1 (padding); tile_xy
-// (optional, VT = 1): the row's domain origin (dft_domain_build_pair_at reads it beside tile_pos instead of the
-// tile_pos → porig → doms chain)
-__global__ void __launch_bounds__(256) fill_tile_pos(BucketLayout L, uint32_t nrows, int32_t* __restrict__ tile_pos,
-                                                     const uint32_t* __restrict__ porig = nullptr,
-                                                     const frac_grid_item* __restrict__ doms = nullptr,
-                                                     uint2* __restrict__ tile_xy = nullptr)
+// tile rows: row j of bucket b's tiles holds engine pool row VT·dbeg[b] + j, or −1 (padding)
+__global__ void __launch_bounds__(256) fill_tile_pos(BucketLayout L, uint32_t nrows, int32_t* __restrict__ tile_pos)
 {
     const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= nrows)
@@ -464,16 +453,7 @@ __global__ void __launch_bounds__(256) fill_tile_pos(BucketLayout L, uint32_t nr
     for (uint32_t k = 1; k < L.nb; ++k)
         b = tile >= L.tile_first[k] ? k : b;
     const uint32_t j = g - 32u * L.tile_first[b];
-    const int32_t p = j < L.VT * L.dcnt[b] ? (int32_t)(L.VT * L.dbeg[b] + j) : -1;
-    tile_pos[g] = p;
-    if (tile_xy) {
-        uint2 xy = make_uint2(0u, 0u);
-        if (p >= 0) {
-            const frac_grid_item d = doms[porig[p]];
-            xy = make_uint2(d.x, d.y);
-        }
-        tile_xy[g] = xy;
-    }
+    tile_pos[g] = j < L.VT * L.dcnt[b] ? (int32_t)(L.VT * L.dbeg[b] + j) : -1;
 }
 
 // per range: the engine pool rows of its bucket [VT·dbeg, VT·(dbeg + dcnt))
@@ -797,12 +777,6 @@ struct QtFillArgs {
     uint32_t* rconst;         // zeroed per slot when not null (the direct form)
     unsigned long long* best_key;
     uint32_t* fb_count;
-    // the Fourier path's geometry maps (fill_range_slots / fill_tile_pos): slot and tile-row origins
-    const frac_grid_item* ranges = nullptr;
-    const frac_grid_item* doms = nullptr;
-    const uint32_t* porig = nullptr;
-    uint2* slot_xy = nullptr;
-    uint2* tile_xy = nullptr;
 };
 
 __device__ inline void qt_fill_item(const QtFillArgs& a, const BucketLayout& L, uint32_t nblocks, uint32_t ntiles,
@@ -820,8 +794,6 @@ __device__ inline void qt_fill_item(const QtFillArgs& a, const BucketLayout& L, 
         a.slot_range[i] = r;
         if (a.rconst)
             a.rconst[i] = 0u;
-        if (a.slot_xy)
-            a.slot_xy[i] = r >= 0 ? make_uint2(a.ranges[r].x, a.ranges[r].y) : make_uint2(0u, 0u);
     }
     if (i < ntiles * 32u) {
         const uint32_t tile = i >> 5;
@@ -829,16 +801,7 @@ __device__ inline void qt_fill_item(const QtFillArgs& a, const BucketLayout& L, 
         for (uint32_t k = 1; k < L.nb; ++k)
             b = tile >= L.tile_first[k] ? k : b;
         const uint32_t j = i - 32u * L.tile_first[b];
-        const int32_t p = j < L.dcnt[b] ? (int32_t)(L.dbeg[b] + j) : -1;
-        a.tile_pos[i] = p;
-        if (a.tile_xy) {
-            uint2 xy = make_uint2(0u, 0u);
-            if (p >= 0) {
-                const frac_grid_item d = a.doms[a.porig[p]];
-                xy = make_uint2(d.x, d.y);
-            }
-            a.tile_xy[i] = xy;
-        }
+        a.tile_pos[i] = j < L.dcnt[b] ? (int32_t)(L.dbeg[b] + j) : -1;
     }
     if (i < nr) {
         const uint32_t b = a.rkey[i];

@@ -224,7 +224,6 @@ struct DftDomainBuildArgs {
     uint32_t* tpool;            // [ntiles*32][32] the same rows in tile order, orbit order (resolve_dft)
     const uint32_t* row_of = nullptr; // BYPOS: [P] tile row of each pool position (tp_build_tiles)
     uint32_t npos = 0;                // BYPOS: P
-    const uint2* tile_xy = nullptr;   // each tile row's domain origin (fill_tile_pos), read beside tile_pos
 };
 
 // pair_sums: fracenc_kernels.hip (pool_build)
@@ -390,17 +389,11 @@ __device__ __forceinline__ void dft_domain_build_pair_at(uint32_t tid2, const Mf
     const uint32_t tile = gid >> 5, row = gid & 31u;
     uint32_t* lrow = rows + ((threadIdx.x >> 1) & 127u) * kDbRowWords;
     const int p = a.tile_pos[gid];
-    const uint2 dxy = s.tile_xy ? s.tile_xy[gid] : make_uint2(0u, 0u);
     uint32_t w[16]; // words 16hh … 16hh + 15 of the row: D4 rows 4hh … 4hh + 3, two cells per word
     int sq = 0;
     if (p >= 0) {
-        uint32_t dx = dxy.x, dy = dxy.y;
-        if (!s.tile_xy) {
-            const frac_grid_item d = s.doms[s.porig[p]];
-            dx = d.x;
-            dy = d.y;
-        }
-        const uint8_t* base = s.src + (size_t)(dy + 8 * hh) * s.sstride + dx;
+        const frac_grid_item d = s.doms[s.porig[p]];
+        const uint8_t* base = s.src + (size_t)(d.y + 8 * hh) * s.sstride + d.x;
         if ((((uintptr_t)base | s.sstride) & 7u) == 0) {
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
@@ -660,17 +653,11 @@ __device__ __forceinline__ void dft_range_prep_pair_at(uint32_t gid2, const Mfma
     const uint32_t b = gid >> 5, col = gid & 31u;
     uint8_t* lp = px + ((threadIdx.x >> 1) & 127u) * kRow;
     const int ri = a.slot_range[gid];
-    const uint2 rxy = a.slot_xy ? a.slot_xy[gid] : make_uint2(0u, 0u);
     uint2 w[4] = {make_uint2(0x80808080u, 0x80808080u), make_uint2(0x80808080u, 0x80808080u),
                   make_uint2(0x80808080u, 0x80808080u), make_uint2(0x80808080u, 0x80808080u)}; // empty: a = 0
     if (ri >= 0) {
-        uint32_t rx = rxy.x, ry = rxy.y;
-        if (!a.slot_xy) {
-            const frac_grid_item rg = a.ranges[ri];
-            rx = rg.x;
-            ry = rg.y;
-        }
-        const uint8_t* base = a.tgt + (size_t)(ry + 4 * hh) * a.tstride + rx;
+        const frac_grid_item rg = a.ranges[ri];
+        const uint8_t* base = a.tgt + (size_t)(rg.y + 4 * hh) * a.tstride + rg.x;
         if ((((uintptr_t)base | a.tstride) & 7u) == 0) {
 #pragma unroll
             for (int y = 0; y < 4; ++y)

@@ -206,7 +206,6 @@ struct MfmaRangePrepArgs {
     const DevPlan* plan = nullptr; // device-planned search: the block count (and flip_from) from the plan
     int fmode = 0;             // mfma_range_prep, the float-C epilogue: B = 8·(128 − copy_t)
     unsigned long long* slotbest = nullptr; // dft_range_prep: [nblocks*32] reset to 0 (search_dft's merged maxima)
-    const uint2* slot_xy = nullptr; // dft_range_prep_pair_at: each slot's range origin (fill_range_slots)
 };
 
 // the range-block count of a device-planned search (T = 8 Fourier: the originals and their copies)
