@@ -1559,30 +1559,16 @@ __device__ inline DftResolved resolve_dft_eval(const MfmaResolveArgs& a, uint32_
             }
             return;
         }
-        // the row's pool position (for the key) and its D4 from the tile-order copy are independent loads;
-        // ΣD4² is summed here rather than loaded through the position.  The next tile's loads are issued
-        // before this tile's evaluation (one tile ahead: 9 VGPRs; all four up front took 24 and cost the C4
-        // quadtree's 65k-range level its occupancy in round 4)
-        const uint32_t tend = min(tile0 + (uint32_t)kTilesPerStage, a.ntiles);
-        auto row_of = [&](uint32_t tile) {
-            return reinterpret_cast<const uint4*>(a.tpool + ((size_t)tile * 32 + row) * 32 + g * (PG / 2));
-        };
-        int pn = tile0 < tend ? a.tile_pos[tile0 * 32 + row] : -1;
-        uint4 d0n = make_uint4(0u, 0u, 0u, 0u), d1n = d0n;
-        if (tile0 < tend) {
-            d0n = row_of(tile0)[0];
-            d1n = row_of(tile0)[1];
-        }
-        for (uint32_t tile = tile0; tile < tend; ++tile) {
-            const int p = pn;
-            const uint4 d0 = d0n, d1 = d1n;
-            if (tile + 1 < tend) {
-                pn = a.tile_pos[(tile + 1) * 32 + row];
-                d0n = row_of(tile + 1)[0];
-                d1n = row_of(tile + 1)[1];
-            }
+        for (uint32_t tile = tile0; tile < min(tile0 + (uint32_t)kTilesPerStage, a.ntiles); ++tile) {
             if (!((tmask >> (tile - tile0)) & 1u))
                 continue;
+            // the row's pool position (for the key) and its D4 from the tile-order copy are
+            // independent loads; ΣD4² is summed here rather than loaded through the position.
+            // (Loading the chunk's four tiles up front saved 1 µs at C2 but took 24 more VGPRs:
+            // 4 instead of 6 waves per SIMD cost the C4 quadtree's 65k-range level 21 µs.)
+            const int p = a.tile_pos[tile * 32 + row];
+            const uint4* dp = reinterpret_cast<const uint4*>(a.tpool + ((size_t)tile * 32 + row) * 32 + g * (PG / 2));
+            const uint4 d0 = dp[0], d1 = dp[1];
             const uint32_t dv[PG / 2] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w};
             uint32_t sd2 = 0, sd1 = 0;
 #pragma unroll
