@@ -10,7 +10,12 @@
 // instantiation access idiom (access checks do not apply to explicit instantiations,
 // [temp.spec.general]/6) — the registration itself, nothing else.
 //
-// usage: core_driver PLANE.u8 W H SRC TGT CLASSIFIER(0|1) RMS_THR SMAX OUT.bin [CPU(0|1) [DEVICES]]
+// usage: core_driver PLANE.u8 W H SRC TGT CLASSIFIER(0|1) RMS_THR SMAX OUT.bin [CPU [DEVICES]]
+//   CPU: 0 = --nocpu (main.cpp:83-84); k > 0 = k of the reference's CpuEncodingEngine2 on the queue, registered
+//   here (the core's constructor would make hardware_concurrency() of them — 256 on the GPU box against a
+//   16-CPU quota — and EncodingEngineCore2::encode's completion wait can lose its last wakeup when that many
+//   engines finish together: it re-waits on the condition variable without a predicate after a yield,
+//   EncodingEngine2.hpp:154-160.  A watchdog turns such a hang into exit 7 instead of a silent stall).
 //   DEVICES: a comma list of HIP devices, one HipEncodingEngine2 registered per entry (default "0";
 //   "0,0" = two engines, two contexts, on device 0 — the one-GPU box's stand-in for one engine per
 //   device; "all" = one per device frac_device_count() reports).
@@ -26,9 +31,12 @@
 #include "image/partition2.hpp"
 #include "HipEncodingEngine2.hpp"
 
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <thread>
+#include <unistd.h>
 #include <fstream>
 #include <memory>
 #include <sstream>
@@ -78,7 +86,8 @@ int main(int argc, char** argv)
     params.noclassifier = std::atoi(argv[6]) == 0;
     params.rmsThreshold = std::atof(argv[7]);
     params.sMax = std::atof(argv[8]);
-    params.nocpu = argc >= 11 ? std::atoi(argv[10]) == 0 : true;
+    const int ncpu = argc >= 11 ? std::atoi(argv[10]) : 0;
+    params.nocpu = true; // the CPU engines, if any, are registered below (see the usage note)
     std::vector<uint8_t> buf(size_t(W) * H);
     {
         std::ifstream f(argv[1], std::ios::binary);
@@ -106,6 +115,11 @@ int main(int argc, char** argv)
                                   std::make_shared<TransformMatcher>(params.rmsThreshold, params.sMax), sourceGrid);
     NullReporter reporter;
     EncodingEngineCore2 core(params, image, sourceGrid, estimator, &reporter);
+    for (int i = 0; i < ncpu; ++i) { // EncodingEngine2.cpp:12-20's engines, k of them
+        auto engine = std::make_unique<CpuEncodingEngine2>(params, image, sourceGrid, estimator);
+        engine->setName("cpu " + std::to_string(i));
+        engines_of(core).push_back(std::move(engine));
+    }
     uint64_t rejected = 0;
     std::vector<HipEncodingEngine2*> hips;
     // EncodingEngine2.cpp:21-29, filled in: one engine per device; all of them
@@ -121,6 +135,11 @@ int main(int argc, char** argv)
             return 4;
         }
     }
+    std::thread([] { // the watchdog (see the usage note): a lost wakeup in the reference's core ends the run
+        std::this_thread::sleep_for(std::chrono::seconds(120));
+        std::fprintf(stderr, "watchdog: EncodingEngineCore2::encode did not return in 120 s\n");
+        _exit(7);
+    }).detach();
     core.encode(targetGrid);
     for (HipEncodingEngine2* hip : hips) {
         try {
