@@ -42,9 +42,9 @@ def test_binding_compiles_against_reference_headers(tmp_path):
 def _run_core(tmp_path, plane_name, W, H, src, tgt, cls, cpu=False, check=True, devices=None, per_engine=False):
     out = tmp_path / f"core_{src}_{tgt}_{cls}_{int(cpu)}.bin"
     plane_path = plane_name if os.path.isabs(plane_name) else os.path.join(GOLD, plane_name + ".u8")
-    # cpu: 8 of the reference's CPU engines beside the HIP engine(s) on the core's queue (core_driver's usage note)
+    # cpu: 2 of the reference's CPU engines beside the HIP engine(s) on the core's queue (core_driver's usage note)
     r = subprocess.run([DRIVER, plane_path, str(W), str(H), str(src), str(tgt), str(int(cls)), "0", "-1", str(out),
-                        str(8 if cpu else 0)] + ([devices] if devices else []), timeout=300, capture_output=True,
+                        str(2 if cpu else 0)] + ([devices] if devices else []), timeout=300, capture_output=True,
                        text=True)
     if not check:
         return r
