@@ -262,3 +262,26 @@ def test_gpu_quadtree_32_byte_leaves(engine, cls, T):
     assert np.shares_memory(pin, pinned)
     np.testing.assert_array_equal(F.records_from_leaves(got, 512), want)
     assert sg["rejected_mappings"] == sw["rejected_mappings"]
+
+
+@pytest.mark.gpu
+def test_device_count_and_quadtree_on_a_context_of_another_device():
+    # frac_device_count (ABI 7) sees the devices torch sees; a quadtree frame on a context of device 1 while the
+    # calling thread's current device is 0 lands every buffer and launch on device 1 (frac_encode_quadtree sets
+    # the context's device first: ADVICE r04) — the same leaves as on device 0
+    import torch
+    n = F.lib().frac_device_count()
+    assert n == torch.cuda.device_count() and n >= 1
+    with pytest.raises(F.FracError):
+        F.Engine(n, 4)  # past the last device: frac_create refuses it
+    if n < 2:
+        pytest.skip("one GPU on this box: the cross-device half needs two")
+    p = plane("lenna_y")
+    with F.Engine(0, 4, True) as e0:
+        e0.set_frame(p)
+        want, _ = e0.encode_quadtree(16, 4, 4.0)
+    with F.Engine(1, 4, True) as e1:
+        e1.set_frame(p)
+        torch.cuda.set_device(0)
+        got, _ = e1.encode_quadtree(16, 4, 4.0)
+    np.testing.assert_array_equal(got, want)
