@@ -285,3 +285,24 @@ def test_device_count_and_quadtree_on_a_context_of_another_device():
         torch.cuda.set_device(0)
         got, _ = e1.encode_quadtree(16, 4, 4.0)
     np.testing.assert_array_equal(got, want)
+
+
+@pytest.mark.gpu
+def test_gpu_quadtree_fp32_regime_levels():
+    # isolated white blocks on a dark frame push ranges of the 16 and 8 levels into the fp32 regime (S16 ≥ 2^24):
+    # the device-planned levels list them and fallback_grid settles each level before its split decision reads
+    # the distances; the leaves equal the host-planned VALU engine's (which runs fallback_grid in every run)
+    from fractencode_amd.synth import value_noise
+    S = 512
+    p = (value_noise(S, S, 1234).astype(np.float64) * (60.0 / 255.0)).astype(np.uint8)
+    for k, (y0, x0) in enumerate([(24, 48), (120, 240), (312, 96), (408, 432), (216, 360)]):
+        p[y0:y0 + 24, x0:x0 + 24] = 0
+        p[y0 + 8:y0 + 16, x0 + 8:x0 + 16] = 255
+    out = {}
+    for eng in (F.ENGINE_AUTO, F.ENGINE_VALU):
+        with F.Engine(0, 4, False, 0.0, -1.0, eng) as e:
+            e.set_frame(p)
+            out[eng] = e.encode_quadtree(16, 4, 2.0)
+    (a, sa), (b, sb) = out[F.ENGINE_AUTO], out[F.ENGINE_VALU]
+    assert sa["fallback_ranges"] == sb["fallback_ranges"] > 0
+    np.testing.assert_array_equal(a, b)
