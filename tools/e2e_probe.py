@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
 """Where the headline's end-to-end step (bench.FrameStep: frame H2D, search, tuples D2H) spends its time
 beside the device-resident step: per leg the step ms (host clock) and the library's per-run event times
-(device / prep / search / finish, median), alternated `rounds` times so drift shows as a pattern.
+(device / prep / search / finish, median), alternated `rounds` times so drift shows as a pattern.  Two more
+legs separate why the search runs slower in the end-to-end step: the device-resident step with the GPU idle
+0.5 ms between steps (clock / power), and with a device-to-device re-copy of the frame instead of the H2D.
 usage: tools/e2e_probe.py [steps] [rounds]"""
 import json
 import os
@@ -36,11 +38,23 @@ with F.Engine(0, 4, False, 0.0, -1.0, F.ENGINE_AUTO, timing=True) as e:
     e.set_frame(h_frame.numpy())
     e.set_domains(F.create_uniform_grid(S, S, 16, 8))
     e.set_ranges(rngs)
-    legs = {"e2e": bench.FrameStep(e, h_frame.numpy(), plan, 0, dev),
-            "device": bench.FrameStep(e, None, plan, 0, dev, device_resident=True)}
+    dstep = bench.FrameStep(e, None, plan, 0, dev, device_resident=True)
+    d_frame2 = d_frame.clone()
+
+    def idle_step():  # the device-resident step with the GPU idle 0.5 ms between steps (no copy)
+        torch.cuda.synchronize(dev)
+        time.sleep(0.0005)
+        dstep()
+
+    def d2d_step():  # a device-to-device re-copy of the frame each step instead of the H2D
+        e.set_frame(d_frame2)
+        dstep()
+
+    legs = {"e2e": bench.FrameStep(e, h_frame.numpy(), plan, 0, dev), "device": dstep, "device_idle": idle_step,
+            "device_d2d": d2d_step}
     for r in range(rounds):
         for name, step in legs.items():
-            if name == "device":
+            if name.startswith("device"):
                 e.set_frame(d_frame)
             for _ in range(3):
                 step()
