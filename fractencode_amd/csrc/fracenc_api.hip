@@ -555,7 +555,7 @@ inline int dft_form(int var)
 {
     if (var == 20 || var == 22)
         return 5;
-    const bool six = var == 21 || var == 23 || (var >= 26 && var <= 28) || (var >= 33 && var <= 36) ||
+    const bool six = var == 21 || var == 23 || (var >= 26 && var <= 28) || (var >= 33 && var <= 37) ||
                      var == 226 || var == 227 || (var >= 240 && var <= 243);
     return six ? 6 : 4;
 }
@@ -573,9 +573,12 @@ inline uint32_t dft_bpw(int var) { return var == 27 || var == 28 ? 16u : kDftBlo
 // form (21) at C3 in two 8-round interleaved A/Bs on two boxes (profiles/r03/session3/r03_ab5.log,
 // r03_ab6.log); 21 was 13.71 vs 15.23 ms for the 8-MFMA form (24) in round 2
 constexpr int kDftDefaultVariant = 35;
+// up to this many domain tiles the product build's search also carries the winning chunk's tile mask
+// (search_dft TMASK; the tuning build's variant 37 always does)
+constexpr uint32_t kDftTmaskTiles = 1024;
 inline int dft_variant(int var)
 {
-    static const int own[] = {1, 3, 5, 6, 12, 20, 21, 22, 23, 24, 26, 27, 28, 33, 34, 35, 36, 9, 17, 41, 65, 73, 105};
+    static const int own[] = {1, 3, 5, 6, 12, 20, 21, 22, 23, 24, 26, 27, 28, 33, 34, 35, 36, 37, 9, 17, 41, 65, 73, 105};
     for (int v : own)
         if (var == v)
             return var;
@@ -1523,12 +1526,26 @@ inline int launch_dft(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool i
         static_assert(kDftDefaultVariant == 35, "the product build's Fourier search is variant 35");
         (void)four;
         constexpr int V35 = 1 | kDftChain | kDft6 | kDftFast6 | kDftUnroll | kDftBufDma;
-        if (hits)
+        // few tiles: the run is a short chain whose resolve weighs as much as its search, and the search also
+        // carries the tiles of the winning chunk that attain its maximum (TMASK) so the resolve evaluates those
+        if (c->ntiles <= kDftTmaskTiles) {
+            if (hits)
+                search_dft<true, V35, W8, kTilesPerStage, false, true><<<nwg, 64 * W8, 0, c->stream>>>(da);
+            else
+                search_dft<false, V35, W8, kTilesPerStage, false, true><<<nwg, 64 * W8, 0, c->stream>>>(da);
+        } else if (hits) {
             search_dft<true, V35, W8><<<nwg, 64 * W8, 0, c->stream>>>(da);
-        else
+        } else {
             search_dft<false, V35, W8><<<nwg, 64 * W8, 0, c->stream>>>(da);
+        }
 #else // the tuning build: every A/B variant and ablation
-        if (!four && var >= 200) {
+        if (form == 6 && var == 37) { // variant 35 carrying the winning chunk's tile mask (TMASK)
+            constexpr int V35 = 1 | kDftChain | kDft6 | kDftFast6 | kDftUnroll | kDftBufDma;
+            if (hits)
+                search_dft<true, V35, W8, kTilesPerStage, false, true><<<nwg, 64 * W8, 0, c->stream>>>(da);
+            else
+                search_dft<false, V35, W8, kTilesPerStage, false, true><<<nwg, 64 * W8, 0, c->stream>>>(da);
+        } else if (!four && var >= 200) {
             // ablations of the 8-wave exact form (wrong results by design)
             switch (var) {
             case 201: search_dft<false, 9, W8><<<nwg, 64 * W8, 0, c->stream>>>(da); break;   // MFMA-only

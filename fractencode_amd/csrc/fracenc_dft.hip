@@ -192,12 +192,13 @@ struct DftArgs {
                            // tile, (kFast6Limit − max Σb²) / max 2·D6 (−1: none)
     unsigned long long* stamps = nullptr; // FRAC_CLOCK_STAMP builds only: [workgroups][kClockStampWords]
     // not CHUNKED: per range slot the maximum over every work item, merged here with one 64-bit atomicMax per
-    // (slot, work item) instead of per-work-item entries: fmap(y) << 32 | (kSlotBestTileMax − chunk) << 2 | the
-    // lane halves of that chunk attaining y.  The greatest word names the greatest y and, among equal y, the
-    // earliest chunk — the chunk resolve_dft walked the entries for.  0 = no work item reached the slot.
+    // (slot, work item) instead of per-work-item entries: fmap(y) << 32 | (kSlotBestTileMax − chunk) << 6 |
+    // the chunk's tiles to re-evaluate << 2 | the lane halves of that chunk attaining y.  The greatest word names
+    // the greatest y and, among equal y, the earliest chunk — the chunk resolve_dft walked the entries for.  The
+    // tile mask is 0xf unless the search tracked the tiles attaining y (TMASK); 0 = no work item reached the slot.
     unsigned long long* slotbest = nullptr;
 };
-constexpr uint32_t kSlotBestTileMax = 0x3fffffffu; // chunk tiles below 2^30
+constexpr uint32_t kSlotBestTileMax = 0x3ffffffu; // chunk tiles below 2^26 (domains < 2^24: tiles < 2^19)
 // per workgroup: s_memtime and s_memrealtime before / after the loop, HW_ID | XCC_ID << 32, and the
 // work item's tile range first | end << 32
 constexpr uint32_t kClockStampWords = 6;
@@ -1155,9 +1156,19 @@ __device__ inline float dft_compute_stage(const uint4* __restrict__ la, uint32_t
 #pragma unroll
         for (int s = 0; s < KS; ++s)
             af[s] = __builtin_bit_cast(half8_t, la[(qq * KS + s) * 64 + lane]);
-        if constexpr (DftForm<VAR>::FAST6 && !MASK) {
-            cm = dft_tile_max6g<VAR & (8 | 16)>(af, bf, la, nt * (uint32_t)KS * 64u + qq * kDftCS, iz, h,
-                                                          (gfast >> (q - q0)) & 1u, cm);
+        if constexpr (DftForm<VAR>::FAST6) {
+            const bool fast = (gfast >> (q - q0)) & 1u;
+            const uint32_t ic = nt * (uint32_t)KS * 64u + qq * kDftCS;
+            if constexpr (MASK) { // TMASK: the tile's own maximum first, then the chunk's tiles attaining it
+                const float tm = dft_tile_max6g<VAR & (8 | 16)>(af, bf, la, ic, iz, h, fast, -__builtin_inff());
+                const uint32_t bit = 1u << (q - q0);
+                masks[0] = tm > cm ? bit : (tm == cm ? masks[0] | bit : masks[0]);
+                if constexpr (HITS)
+                    masks[1] |= tm >= hl ? bit : 0u;
+                cm = __builtin_fmaxf(cm, tm);
+            } else {
+                cm = dft_tile_max6g<VAR & (8 | 16)>(af, bf, la, ic, iz, h, fast, cm);
+            }
             return;
         }
         floatx16_t ny;
@@ -1221,11 +1232,16 @@ constexpr uint32_t kDftBlocksPerWG = 8; // waves (range blocks) sharing one LDS 
 // CHUNKED (the SEA engine's tiled form, fracenc_tp.hip): tiles are in ΣD4 order, not domain
 // order, so instead of the first chunk attaining each lane's maximum every chunk's maximum is
 // written, entry ((choff[work] + chunk)·WAVES + wave)·64 + lane, and resolve_dft keeps all ties.
-template <bool HITS, int VAR, uint32_t WAVES = 4, uint32_t TPS = kTilesPerStage, bool CHUNKED = false>
+// TMASK (not CHUNKED, slotbest): each lane also tracks which tiles of its best chunk attain its maximum (or
+// hold a hit), and the slot word carries them, so resolve_dft re-evaluates those tiles instead of the whole
+// chunk.  Costs the tile-pair epilogue a compare per tile: chosen where the resolve, not the search, dominates.
+template <bool HITS, int VAR, uint32_t WAVES = 4, uint32_t TPS = kTilesPerStage, bool CHUNKED = false,
+          bool TMASK = false>
 __global__ void __launch_bounds__(64 * WAVES) search_dft(DftArgs d)
 {
     static_assert(kTuningBuild || (VAR & (8 | 16 | 32 | 64 | 256 | 512)) == 0,
                   "search_dft ablations exist only in FRAC_TUNING builds");
+    static_assert(!(TMASK && CHUNKED), "CHUNKED entries carry their own tile masks");
     if (past_plan(d.m))
         return;
     const MfmaSearchArgs& a = d.m;
@@ -1262,7 +1278,7 @@ __global__ void __launch_bounds__(64 * WAVES) search_dft(DftArgs d)
     constexpr float kOut = DftForm<VAR>::HALF ? 2.0f : 1.0f;
 
     float best = -__builtin_inff();
-    uint32_t btile = 0;
+    uint32_t btile = 0, bmask = 0xfu;
     uint32_t masks[2] = {0u, 0u};
     auto finish_stage = [&](float cm, uint32_t tb) {
         if constexpr (CHUNKED) {
@@ -1283,12 +1299,20 @@ __global__ void __launch_bounds__(64 * WAVES) search_dft(DftArgs d)
             return;
         }
         // any hit in the chunk: the first-hit chunk wins. (A per-tile mask here, as the CHUNKED
-        // entries carry, cost 4% of this kernel in a 30-sample A/B for 0.1 ms less resolve: not kept.)
+        // entries carry, cost 4% of this kernel in a 30-sample A/B for 0.1 ms less resolve: only TMASK.)
+        uint32_t msk = 0xfu;
+        if constexpr (TMASK) {
+            msk = masks[0];
+            if constexpr (HITS)
+                msk = cm >= hl ? masks[1] : msk;
+            masks[0] = masks[1] = 0u;
+        }
         if constexpr (HITS)
             cm = cm >= hl ? __builtin_inff() : cm;
         if (cm > best) {
             best = cm;
             btile = tb;
+            bmask = msk;
         }
     };
     const uint32_t nstage = (wk.w - wk.z + kTilesPerStage - 1) / kTilesPerStage;
@@ -1323,7 +1347,7 @@ __global__ void __launch_bounds__(64 * WAVES) search_dft(DftArgs d)
             if (st + 1 < nstage && (!SKIPDMA || st == 0))
                 stage(lds1, tb + kTilesPerStage, stage_nt(st + 1));
             for (uint32_t c0 = 0; c0 < stage_nt(st); c0 += 4)
-                finish_stage(dft_compute_stage<VAR, CHUNKED, HITS>(lds0, stage_nt(st), lane, bf, tb, d.tguard, r1, c0,
+                finish_stage(dft_compute_stage<VAR, CHUNKED || TMASK, HITS>(lds0, stage_nt(st), lane, bf, tb, d.tguard, r1, c0,
                                                                    c0 + 4, masks, hl, STAGE, d.trmax),
                              tb + c0);
         }
@@ -1334,7 +1358,7 @@ __global__ void __launch_bounds__(64 * WAVES) search_dft(DftArgs d)
             if (st + 2 < nstage && !SKIPDMA)
                 stage(lds0, tb + kTilesPerStage, stage_nt(st + 2));
             for (uint32_t c0 = 0; c0 < stage_nt(st + 1); c0 += 4)
-                finish_stage(dft_compute_stage<VAR, CHUNKED, HITS>(lds1, stage_nt(st + 1), lane, bf, tb, d.tguard, r1,
+                finish_stage(dft_compute_stage<VAR, CHUNKED || TMASK, HITS>(lds1, stage_nt(st + 1), lane, bf, tb, d.tguard, r1,
                                                                    c0, c0 + 4, masks, hl, STAGE, d.trmax),
                              tb + c0);
         }
@@ -1359,19 +1383,22 @@ __global__ void __launch_bounds__(64 * WAVES) search_dft(DftArgs d)
             // chunk, and which halves attain it there (both: resolve_dft evaluates both halves' rows)
             const uint32_t y0 = fmap(best * kOut), t0 = btile;
             const uint32_t y1 = (uint32_t)__shfl_xor((int)y0, 32, 64), t1 = (uint32_t)__shfl_xor((int)t0, 32, 64);
+            const uint32_t m1 = TMASK ? (uint32_t)__shfl_xor((int)bmask, 32, 64) : 0xfu;
             const bool first = lane < 32u;
             const uint32_t ym = first ? y0 : y1, tm = first ? t0 : t1; // this half (lane < 32: half 0)
             const uint32_t yo = first ? y1 : y0, to = first ? t1 : t0; // the other half
             if (first) {
-                uint32_t tile = tm, hm = 1u;
+                uint32_t tile = tm, hm = 1u, mk = bmask;
                 if (yo > ym || (yo == ym && to < tm)) {
                     tile = to;
                     hm = 2u;
+                    mk = m1;
                 } else if (yo == ym && to == tm) {
                     hm = 3u;
+                    mk |= m1; // both halves' rows are evaluated on every tile of the union
                 }
                 const unsigned long long w = ((unsigned long long)max(ym, yo) << 32) |
-                                             ((kSlotBestTileMax - tile) << 2) | hm;
+                                             ((kSlotBestTileMax - tile) << 6) | (mk << 2) | hm;
                 atomicMax(d.slotbest + (size_t)blk * 32 + lane, w);
             }
         } else {
@@ -1647,17 +1674,19 @@ __device__ inline DftResolved resolve_dft_eval(const MfmaResolveArgs& a, uint32_
     };
     if (a.slotbest) {
         // the search merged its splits itself (search_dft, DftArgs::slotbest): the slot's greatest y, the
-        // earliest chunk attaining it and which lane halves of that chunk attain it — one load, no CSR walk
+        // earliest chunk attaining it, its tiles to evaluate and which lane halves attain it — one load, no
+        // CSR walk
         if (sb == 0ull)
             return res; // no work item reached the slot: no eligible domain
         vmax = funmap((uint32_t)(sb >> 32));
         if (!(vmax > -1.0e29f))
             return res; // only padding rows: no eligible domain, best_key stays "none"
         set_target();
-        const uint32_t tile0 = kSlotBestTileMax - ((uint32_t)sb >> 2), hm = (uint32_t)sb & 3u;
+        const uint32_t tile0 = kSlotBestTileMax - ((uint32_t)sb >> 6), tm = ((uint32_t)sb >> 2) & 0xfu;
+        const uint32_t hm = (uint32_t)sb & 3u;
         for (uint32_t h = 0; h < 2; ++h)
             if ((hm >> h) & 1u)
-                eval_chunk(tile0, h, 0xfu);
+                eval_chunk(tile0, h, tm);
     } else {
         const uint32_t e0 = a.blk_ptr[blk], e1 = a.blk_ptr[blk + 1];
         const uint32_t nent = (e1 - e0) * 2u;

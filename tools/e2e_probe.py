@@ -4,7 +4,9 @@ beside the device-resident step: per leg the step ms (host clock) and the librar
 (device / prep / search / finish, median), alternated `rounds` times so drift shows as a pattern.  Two more
 legs separate why the search runs slower in the end-to-end step: the device-resident step with the GPU idle
 0.5 ms between steps (clock / power), and with a device-to-device re-copy of the frame instead of the H2D.
-usage: tools/e2e_probe.py [steps] [rounds]"""
+Leg e2e_zc packs the tuples straight into the pinned host buffer (the pack kernel's stores cross PCIe) instead
+of packing on the device and copying.  Run it with HSA_ENABLE_SDMA=0 to see the copies done by blit kernels.
+usage: tools/e2e_probe.py [steps] [rounds] [legs,...]"""
 import json
 import os
 import sys
@@ -23,6 +25,7 @@ from fractencode_amd.synth import value_noise  # noqa: E402
 
 steps = int(sys.argv[1]) if len(sys.argv) > 1 else 20
 rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 2
+only = sys.argv[3].split(",") if len(sys.argv) > 3 else None
 S = 4096
 dev = torch.device("cuda", 0)
 torch.cuda.set_device(0)
@@ -50,8 +53,18 @@ with F.Engine(0, 4, False, 0.0, -1.0, F.ENGINE_AUTO, timing=True) as e:
         e.set_frame(d_frame2)
         dstep()
 
+    zstep = bench.FrameStep(e, h_frame.numpy(), plan, 0, dev)
+
+    def zc_step():  # H2D, search, tuples packed by the kernel directly into pinned host memory
+        e.set_frame(h_frame.numpy())
+        e.run()
+        e.copy_tuples_device(zstep.h_out.data_ptr())
+
     legs = {"e2e": bench.FrameStep(e, h_frame.numpy(), plan, 0, dev), "device": dstep, "device_idle": idle_step,
-            "device_d2d": d2d_step}
+            "device_d2d": d2d_step, "e2e_zc": zc_step}
+    if only:
+        legs = {k: v for k, v in legs.items() if k in only}
+    ref = None
     for r in range(rounds):
         for name, step in legs.items():
             if name.startswith("device"):
@@ -66,6 +79,12 @@ with F.Engine(0, 4, False, 0.0, -1.0, F.ENGINE_AUTO, timing=True) as e:
             torch.cuda.synchronize(dev)
             sec = (time.perf_counter() - t0) / steps
             h = e.timing_history()
+            if name == "e2e_zc":  # the zero-copy tuples equal the device-packed ones
+                dstep()
+                torch.cuda.synchronize(dev)
+                zc_step()
+                torch.cuda.synchronize(dev)
+                assert zstep.h_out.numpy().tobytes() == dstep.gathered.cpu().numpy().tobytes()
             print(json.dumps({"round": r, "leg": name, "ms_per_step": round(sec * 1e3, 3),
                               **{k: round(float(np.median(h["ms_" + k])), 3) for k in ("device", "prep", "search", "finish")}}),
                   flush=True)
