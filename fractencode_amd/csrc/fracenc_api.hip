@@ -234,7 +234,8 @@ struct frac_ctx {
     DBuf<uint32_t> d_dft_tpool; // pool rows in tile order (resolve_dft)
     DBuf<uint32_t> d_dft_rorb;  // range pixel pairs in orbit order, per slot (resolve_dft)
     DBuf<frac_qt_leaf> d_qt_leaves32; // frac_encode_quadtree_leaves' device-side leaves (pageable caller buffer)
-    DBuf<unsigned long long> d_dft_slotbest; // per slot the search's merged maximum (search_dft → resolve_dft)
+    DBuf<unsigned long long> d_dft_slotbest; // per slot the search's merged word (search_dft → resolve_dft,
+                                             // search_mfma n ≤ 4 → resolve_small)
     DBuf<uint4> d_rstat;        // per range: the winner's sums (resolve_dft → fit_rstat)
     DBuf<frac_grid_item> d_cls_items;
     DBuf<uint32_t> d_cls_list;
@@ -1743,6 +1744,14 @@ int launch_mfma(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool inits =
     int dvar = 0;
     FRAC_TRY(direct_variant<N>(c, dvar));
     const int fmode = (dvar & 256) ? 1 : 0; // the float-C epilogue: its row constants and B scaling
+    // n ≤ 4 with the transforms merged in the search (resolve_small): the search merges its work items per range
+    // slot itself (one 64-bit atomicMax per slot and work item; reset by mfma_range_prep), so the resolve reads one
+    // word per slot instead of walking the block's entries through the CSR map
+    unsigned long long* slotbest = nullptr;
+    if (N <= 4 && T >= 4 && (dvar & (128 | 256)) && c->nblocks) {
+        FRAC_HIP(c, c->d_dft_slotbest.ensure((size_t)c->nblocks * 32));
+        slotbest = c->d_dft_slotbest.ptr;
+    }
     if (c->ntiles) {
         MfmaDomainPrepArgs d;
         d.fmode = fmode;
@@ -1770,6 +1779,7 @@ int launch_mfma(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool inits =
         r.rconst = c->d_m_rconst.ptr;
         r.plan = c->qplan;
         r.fmode = fmode;
+        r.slotbest = slotbest;
         if constexpr (N == 16) { // one workgroup per range block, the constants written directly
             if (T == 8)
                 mfma_range_prep16<8><<<c->nblocks, 256, 0, c->stream>>>(r);
@@ -1804,6 +1814,7 @@ int launch_mfma(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool inits =
         a.hitH = (uint32_t)std::max<int64_t>(c->hitH, 0);
         a.entries = c->d_m_entries.ptr;
         a.plan = c->qplan;
+        a.slotbest = slotbest;
         if constexpr (N == 16) { // 4-wave workgroups: mfma16_bpw(T) range blocks × their T transforms
             const unsigned nwg = nwork;
             const bool hits = c->hitH > 0;
@@ -1852,6 +1863,7 @@ int launch_mfma(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool inits =
         v.best_key = c->d_best_key.ptr;
         v.merged = (N != 16 && T > 1 && (c->mfma_var_ran & (128 | 256))) ? 1 : 0; // entries merged over t
         v.fmode = (N != 16 && (c->mfma_var_ran & 256)) ? 1 : 0;                  // fmap'd float-C minima
+        v.slotbest = slotbest;
         if constexpr (N == 16)
             v.rfrags = c->d_m_rfrags.ptr; // the range copies from search_mfma16's B fragments
         if (!c->virt) { // the fit in the resolving wave (the sampled form fits at its own points: gen_fit)

@@ -222,14 +222,15 @@ inline void launch_bucket_keys_pair(const KeySeg& d, uint32_t dh, const KeySeg& 
 }
 
 // ---- stable bucket sort of item indices by a 3-bit key (the classifier buckets) ----
-// A counting sort in three launches, for at most kMaxBuckets keys: per 1,024-item tile the bucket
-// counts (bksort_count), per bucket the exclusive prefix over tiles and the bucket starts
-// (bksort_scan: first[b] = the first sorted position of bucket b, first[kMaxBuckets] = the count —
-// what bucket_bounds computed from the sorted keys), then each tile scatters its indices in index
-// order (bksort_scatter: wave ballots per key give the rank among the earlier lanes).  It replaces
-// rocPRIM's Onesweep for these 7 buckets: one third of the launches, no memsets (C4 quadtree: six
-// sorts per frame of ≈33 µs each).  dn (device-planned levels): the item count is *dn ≤ n; the
-// grids cover n.
+// A counting sort in two launches, for at most kMaxBuckets keys: per 1,024-item tile the bucket
+// counts (bksort_count), then each tile sums every tile's counts itself — the bucket starts
+// (first[b] = the first sorted position of bucket b, first[kMaxBuckets] = the count, what
+// bucket_bounds computed from the sorted keys; tile 0 writes them) and its own offset per bucket —
+// and scatters its indices in index order (bksort_scatter: wave ballots per key give the rank among
+// the earlier lanes).  It replaces rocPRIM's Onesweep for these 7 buckets: no memsets, two launches
+// (C4 quadtree: six sorts per frame of ≈33 µs each with Onesweep; round 5 folded the per-bucket scan
+// over tiles, bksort_scan, into the scatter up to kBkSelfTiles tiles per sort).  dn (device-planned
+// levels): the item count is *dn ≤ n; the grids cover n.
 constexpr uint32_t kBkTile = 1024, kBkThreads = 256;
 
 // one sort: keys [n] (or the first *dn of them), per-tile counts scratch, bucket starts, sorted indices
@@ -329,16 +330,65 @@ __global__ void __launch_bounds__(64 * kMaxBuckets) bksort_scan(BkSeg s0, BkSeg 
     }
 }
 
+// SELF: the tile sums every tile's counts itself (above); else bksort_scan turned them into offsets.  The
+// sums read every tile's counts in every tile — quadratic in the tiles, so only for sorts of at most
+// kBkSelfTiles tiles
+constexpr uint32_t kBkSelfTiles = 512;
+template <bool SELF>
 __global__ void __launch_bounds__(kBkThreads) bksort_scatter(BkSeg s0, BkSeg s1)
 {
     __shared__ uint32_t wcnt[kBkThreads / 64][kMaxBuckets];
     __shared__ uint32_t run[kMaxBuckets];
+    __shared__ uint32_t sums[kBkThreads / 64][2 * kMaxBuckets];
     uint32_t blk = blockIdx.x;
     const BkSeg s = bk_seg(s0, s1, blk);
     const uint32_t n = s.dn ? min(*s.dn, s.n) : s.n;
     const uint32_t base = blk * kBkTile, lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-    if (threadIdx.x < (uint32_t)kMaxBuckets)
-        run[threadIdx.x] = s.counts[blk * kMaxBuckets + threadIdx.x];
+    if constexpr (!SELF) {
+        if (threadIdx.x < (uint32_t)kMaxBuckets)
+            run[threadIdx.x] = s.counts[blk * kMaxBuckets + threadIdx.x];
+    } else {
+        // every tile's counts: per bucket the total and the part in the tiles before this one
+        uint32_t tot[kMaxBuckets] = {}, bef[kMaxBuckets] = {};
+        for (uint32_t t = threadIdx.x; t < s.tiles; t += kBkThreads)
+#pragma unroll
+            for (uint32_t b = 0; b < (uint32_t)kMaxBuckets; ++b) {
+                const uint32_t c = s.counts[t * kMaxBuckets + b];
+                tot[b] += c;
+                bef[b] += t < blk ? c : 0u;
+            }
+#pragma unroll
+        for (uint32_t b = 0; b < (uint32_t)kMaxBuckets; ++b)
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) {
+                tot[b] += (uint32_t)__shfl_xor((int)tot[b], o, 64);
+                bef[b] += (uint32_t)__shfl_xor((int)bef[b], o, 64);
+            }
+        if (lane == 0)
+#pragma unroll
+            for (uint32_t b = 0; b < (uint32_t)kMaxBuckets; ++b) {
+                sums[wv][b] = tot[b];
+                sums[wv][kMaxBuckets + b] = bef[b];
+            }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t start = 0;
+            for (uint32_t b = 0; b < (uint32_t)kMaxBuckets; ++b) {
+                uint32_t tb = 0, bb = 0;
+                for (uint32_t w = 0; w < kBkThreads / 64; ++w) {
+                    tb += sums[w][b];
+                    bb += sums[w][kMaxBuckets + b];
+                }
+                if (blk == 0)
+                    s.first[b] = start;
+                run[b] = start + bb;
+                start += tb;
+            }
+            if (blk == 0)
+                s.first[kMaxBuckets] = start;
+        }
+        __syncthreads();
+    }
     const unsigned long long below = lane ? (~0ull >> (64 - lane)) : 0ull;
     for (uint32_t j = 0; j < kBkTile / kBkThreads; ++j) {
         const uint32_t i = base + j * kBkThreads + threadIdx.x;
@@ -373,13 +423,17 @@ inline BkSeg bk_seg_of(const uint32_t* keys, uint32_t n, const uint32_t* dn, uin
     return BkSeg{keys, n, dn, counts, first, out, std::max<uint32_t>((n + kBkTile - 1) / kBkTile, 1u)};
 }
 
-// the three launches for one or two sorts (s1.tiles = 0: one)
+// the launches for one or two sorts (s1.tiles = 0: one): two, or three above kBkSelfTiles tiles per sort
 inline void launch_bucket_sorts(const BkSeg& s0, const BkSeg& s1, hipStream_t st)
 {
     const uint32_t nt = s0.tiles + s1.tiles;
     bksort_count<<<nt, kBkThreads, 0, st>>>(s0, s1);
-    bksort_scan<<<s1.tiles ? 2 : 1, 64 * kMaxBuckets, 0, st>>>(s0, s1);
-    bksort_scatter<<<nt, kBkThreads, 0, st>>>(s0, s1);
+    if (s0.tiles <= kBkSelfTiles && s1.tiles <= kBkSelfTiles) {
+        bksort_scatter<true><<<nt, kBkThreads, 0, st>>>(s0, s1);
+    } else {
+        bksort_scan<<<s1.tiles ? 2 : 1, 64 * kMaxBuckets, 0, st>>>(s0, s1);
+        bksort_scatter<false><<<nt, kBkThreads, 0, st>>>(s0, s1);
+    }
 }
 
 inline void launch_bucket_sort(const uint32_t* keys, uint32_t n, const uint32_t* dn, uint32_t* counts, uint32_t* first,

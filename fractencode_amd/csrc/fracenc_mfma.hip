@@ -205,7 +205,8 @@ struct MfmaRangePrepArgs {
     uint32_t flip_from = ~0u;  // dft_range_prep: blocks from here on hold their range read through Flip (T = 8)
     const DevPlan* plan = nullptr; // device-planned search: the block count (and flip_from) from the plan
     int fmode = 0;             // mfma_range_prep, the float-C epilogue: B = 8·(128 − copy_t)
-    unsigned long long* slotbest = nullptr; // dft_range_prep: [nblocks*32] reset to 0 (search_dft's merged maxima)
+    unsigned long long* slotbest = nullptr; // dft_range_prep / mfma_range_prep: [nblocks*32] reset to 0 (the
+                                            // searches' merged slot words)
 };
 
 // the range-block count of a device-planned search (T = 8 Fourier: the originals and their copies)
@@ -231,6 +232,8 @@ __global__ void __launch_bounds__(256) mfma_range_prep(MfmaRangePrepArgs a)
     const uint32_t t = rem / (KS * 64u), s = (rem / 64u) % KS, lane = rem % 64u;
     const uint32_t col = lane & 31u, h = lane >> 5;
     const int ri = a.slot_range[b * 32 + col];
+    if (a.slotbest && t == 0 && s == 0 && h == 0)
+        a.slotbest[b * 32 + col] = 0ull; // the run's reset of search_mfma's merged slot words
     _Float16 v8[8];
     if (ri >= 0) {
         const frac_grid_item rg = a.ranges[ri];
@@ -364,7 +367,12 @@ struct MfmaSearchArgs {
     uint32_t hitH;         // valid when HITS
     uint2* entries;        // [nwork*4][T][64] {min v (0 = hit), tile}
     const DevPlan* plan = nullptr; // device-planned search: workgroups past plan->nwork leave at once
+    // search_mfma with entries merged over t (VAR 128 / 256): instead of the entries, per range slot one
+    // 64-bit atomicMax per work item, ~v << 32 | (kDirectSlotTileMax − chunk) << 2 | the lane halves of that
+    // chunk attaining v — the least v and, among equal v, the earliest chunk (resolve_small reads it)
+    unsigned long long* slotbest = nullptr;
 };
+constexpr uint32_t kDirectSlotTileMax = 0x3fffffffu; // chunk tiles below 2^30
 
 // a workgroup of a device-planned search's worst-case grid with no work item
 __device__ inline bool past_plan(const MfmaSearchArgs& a)
@@ -451,6 +459,8 @@ __device__ inline void compute_stage(const uint4* __restrict__ la, uint32_t nt, 
     constexpr int KS = MfmaGeom<N>::KS;
     const uint4* lc = la + nt * KS * 64u;
     const uint32_t h = lane >> 5;
+    // the float-C epilogue (VAR 256): the stage's running minimum stays a float (one fmap per stage, not per tile)
+    float fm = __builtin_inff();
     for (uint32_t q = 0; q < nt; ++q) {
         half8_t af[KS];
 #pragma unroll
@@ -479,7 +489,7 @@ __device__ inline void compute_stage(const uint4* __restrict__ la, uint32_t nt, 
 #pragma unroll
             for (int t = 0; t < T; ++t)
                 acc[t] = mfma_tile<N, T>(af, bf[t], c);
-            float m = __builtin_inff();
+            float m = fm;
             if constexpr (T == 1) {
 #pragma unroll
                 for (int i = 0; i < 16; i += 2)
@@ -495,7 +505,7 @@ __device__ inline void compute_stage(const uint4* __restrict__ la, uint32_t nt, 
                     m = __builtin_fminf(__builtin_fminf(m, r), acc[T - 1][i]);
                 }
             }
-            cm[0] = min(cm[0], fmap(m));
+            fm = m;
             continue;
         }
         if constexpr (LATE_E) {
@@ -570,6 +580,9 @@ __device__ inline void compute_stage(const uint4* __restrict__ la, uint32_t nt, 
                 cm[t] = epilogue_min<(VAR & 2) != 0>(mfma_tile<N, T, PRIO>(af, bf[t], cinit), e, cm[t]);
         }
     }
+    if constexpr ((VAR & 256) != 0)
+        if (nt)
+            cm[0] = min(cm[0], fmap(fm));
 }
 
 // Schedule variant bits (A/B'd in one process by tools/ab_mfma.py):
@@ -671,9 +684,30 @@ __global__ void __launch_bounds__(256) search_mfma(MfmaSearchArgs a)
             finish_stage(cm, tb);
         }
     }
+    // merged entries (VAR 128): slot t = 0 only, the one resolve_mfma reads
+    constexpr int TW = ((VAR & (128 | 256)) != 0 && T > 1) ? 1 : T;
+    if constexpr (TW == 1) {
+        if (a.slotbest) {
+            // lanes l and l + 32 hold one range slot's two row halves: the lesser v, among equal v the earlier
+            // chunk, and which halves attain it there (as search_dft's slot words)
+            const uint32_t v0 = best[0], c0 = btile[0];
+            const uint32_t v1 = (uint32_t)__shfl_xor((int)v0, 32, 64), c1 = (uint32_t)__shfl_xor((int)c0, 32, 64);
+            if (active && lane < 32u) {
+                uint32_t tile = c0, hm = 1u;
+                if (v1 < v0 || (v1 == v0 && c1 < c0)) {
+                    tile = c1;
+                    hm = 2u;
+                } else if (v1 == v0 && c1 == c0) {
+                    hm = 3u;
+                }
+                const unsigned long long w = ((unsigned long long)~min(v0, v1) << 32) |
+                                             ((unsigned long long)(kDirectSlotTileMax - tile) << 2) | hm;
+                atomicMax(a.slotbest + (size_t)blk * 32 + lane, w);
+            }
+            return;
+        }
+    }
     if (active) {
-        // merged entries (VAR 128): slot t = 0 only, the one resolve_mfma reads
-        constexpr int TW = ((VAR & (128 | 256)) != 0 && T > 1) ? 1 : T;
 #pragma unroll
         for (int t = 0; t < TW; ++t)
             a.entries[((size_t)(blockIdx.x * 4u + wv) * T + t) * 64 + lane] = make_uint2(best[t], btile[t]);
@@ -850,8 +884,8 @@ struct MfmaResolveArgs {
     const uint4* rfrags = nullptr;
     // resolve_dft, T = 8: two-wave workgroups, one slot and its flipped copy each (flip_slots > 0)
     int paired = 0;
-    // resolve_dft: per slot the search's own merge of its splits (search_dft with DftArgs::slotbest), read
-    // in place of the entries and their CSR map
+    // resolve_dft / resolve_small: per slot the search's own merge of its splits (search_dft with
+    // DftArgs::slotbest, search_mfma with MfmaSearchArgs::slotbest), read in place of the entries and their CSR map
     const unsigned long long* slotbest = nullptr;
 };
 
@@ -1114,19 +1148,26 @@ __global__ void __launch_bounds__(256, 6) resolve_small(MfmaResolveArgs a)
         return;
     const uint32_t slot = a.range_slot[r];
     const uint32_t blk = slot >> 5, col = slot & 31u;
-    const uint32_t e0 = a.blk_ptr[blk], e1 = a.blk_ptr[blk + 1];
+    // search_mfma merged the work items per slot itself (MfmaSearchArgs::slotbest): one word, no CSR walk
+    const unsigned long long sb = a.slotbest ? a.slotbest[slot] : 0ull;
+    uint32_t e0 = 0, nent = 0;
     const uint32_t TE = a.merged ? 1u : a.T;
-    const uint32_t nent = (e1 - e0) * TE * 2u;
     uint32_t vmin = 0xffffffffu;
+    if (a.slotbest) {
+        vmin = sb ? ~(uint32_t)(sb >> 32) : 0xffffffffu;
+    } else {
+        e0 = a.blk_ptr[blk];
+        nent = (a.blk_ptr[blk + 1] - e0) * TE * 2u;
 #pragma nounroll
-    for (uint32_t j = lane; j < nent; j += 64) { // not unrolled, as in resolve_mfma
-        const uint32_t e = e0 + j / (2u * TE), t = (j >> 1) % TE, h = j & 1u;
-        vmin = min(vmin, a.entries[((size_t)a.blk_ent[e] * a.T + t) * 64 + col + 32 * h].x);
-    }
+        for (uint32_t j = lane; j < nent; j += 64) { // not unrolled, as in resolve_mfma
+            const uint32_t e = e0 + j / (2u * TE), t = (j >> 1) % TE, h = j & 1u;
+            vmin = min(vmin, a.entries[((size_t)a.blk_ent[e] * a.T + t) * 64 + col + 32 * h].x);
+        }
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1)
-        vmin = min(vmin, (uint32_t)__shfl_xor((int)vmin, o, 64));
-    vmin = (uint32_t)__builtin_amdgcn_readfirstlane((int)vmin); // wave-uniform: a scalar register
+        for (int o = 32; o > 0; o >>= 1)
+            vmin = min(vmin, (uint32_t)__shfl_xor((int)vmin, o, 64));
+        vmin = (uint32_t)__builtin_amdgcn_readfirstlane((int)vmin); // wave-uniform: a scalar register
+    }
     if (vmin == 0xffffffffu) {
         if (a.fused_fit && lane == 0)
             fit_sums_range<N>(a.fit, r, kKeyNone, 0, 0, 0, 0, 0);
@@ -1163,6 +1204,82 @@ __global__ void __launch_bounds__(256, 6) resolve_small(MfmaResolveArgs a)
     unsigned long long bestk = kKeyNone;
     uint32_t best_tile = 0xffffffffu;
     int64_t bx = 0, bsd = 0, bsd2 = 0;
+    // the rows of lane half h in chunk `ctile`'s tiles, up to the first holding a match
+    auto eval_chunk = [&](uint32_t ctile, uint32_t h) {
+        const int row = (i & 3) + 8 * (i >> 2) + 4 * (int)h;
+        for (uint32_t tile = ctile; tile < min(ctile + (uint32_t)kTilesPerStage, a.ntiles) && tile <= best_tile;
+             ++tile) {
+            const int p = a.tile_pos[tile * 32 + row];
+            uint32_t d[K2];
+            if (p >= 0) {
+                const uint32_t* dp = a.pool + (size_t)p * K2;
+                if constexpr (K2 == 8) {
+                    const uint4 v0 = reinterpret_cast<const uint4*>(dp)[0], v1 = reinterpret_cast<const uint4*>(dp)[1];
+                    d[0] = v0.x, d[1] = v0.y, d[2] = v0.z, d[3] = v0.w, d[4] = v1.x, d[5] = v1.y, d[6] = v1.z, d[7] = v1.w;
+                } else {
+#pragma unroll
+                    for (int k = 0; k < K2; ++k)
+                        d[k] = dp[k];
+                }
+            } else {
+#pragma unroll
+                for (int k = 0; k < K2; ++k)
+                    d[k] = 0u;
+            }
+            uint32_t sd1u = 0;
+#pragma unroll
+            for (int k = 0; k < K2; ++k)
+                sd1u = __builtin_amdgcn_udot2(__builtin_bit_cast(ushort2_t, d[k]), __builtin_bit_cast(ushort2_t, kOnes),
+                                              sd1u, false);
+            const int64_t nsd2 = p >= 0 ? (int64_t)a.negsd2[p] : 0;
+            unsigned long long mk = kKeyNone; // the lane's least key over its transforms
+            int64_t mx = 0;
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                if (c == 1 && !two)
+                    break;
+                uint32_t xu = 0;
+#pragma unroll
+                for (int k = 0; k < K2; ++k)
+                    xu = __builtin_amdgcn_udot2(__builtin_bit_cast(ushort2_t, cp[c][k]),
+                                                __builtin_bit_cast(ushort2_t, d[k]), xu, false);
+                const int64_t s16 = 16 * sr2 - 8 * (int64_t)xu - nsd2;
+                const uint32_t tt = (uint32_t)(t0 + 4 * c);
+                if (p >= 0 && (hit ? (s16 <= a.hitH) : (s16 == target))) {
+                    const unsigned long long k =
+                        hit ? key_hit((uint32_t)p, tt) : key_miss((uint64_t)s16, (uint32_t)p, a.T - 1 - tt);
+                    if (k < mk) {
+                        mk = k;
+                        mx = (int64_t)xu;
+                    }
+                }
+            }
+            unsigned long long wk = mk; // the wave's least key of the tile
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) {
+                const unsigned long long ok2 = ((unsigned long long)lane_xor((uint32_t)(wk >> 32), lane, o) << 32) |
+                                               lane_xor((uint32_t)wk, lane, o);
+                wk = ok2 < wk ? ok2 : wk;
+            }
+            if (wk != kKeyNone) {
+                if (wk < bestk) {
+                    const int src2 = __ffsll((long long)__ballot(mk == wk)) - 1;
+                    bestk = wk;
+                    best_tile = tile;
+                    bx = (int64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)mx, src2);
+                    bsd = (int64_t)(uint32_t)__builtin_amdgcn_readlane((int)sd1u, src2);
+                    bsd2 = -(int64_t)(int32_t)__builtin_amdgcn_readlane((int)(int32_t)nsd2, src2);
+                }
+                break; // later tiles of the chunk hold later pool positions
+            }
+        }
+    };
+    if (a.slotbest) {
+        const uint32_t ctile = kDirectSlotTileMax - ((uint32_t)sb >> 2), hm = (uint32_t)sb & 3u;
+        for (uint32_t h = 0; h < 2; ++h)
+            if ((hm >> h) & 1u)
+                eval_chunk(ctile, h);
+    }
     for (uint32_t c0 = 0; c0 < nent; c0 += 64) {
         const uint32_t jl = c0 + (uint32_t)lane;
         uint2 enl = make_uint2(0xffffffffu, 0u);
@@ -1178,73 +1295,7 @@ __global__ void __launch_bounds__(256, 6) resolve_small(MfmaResolveArgs a)
             const uint32_t ctile = (uint32_t)__builtin_amdgcn_readlane((int)enl.y, src);
             if (ctile > best_tile)
                 continue;
-            const int row = (i & 3) + 8 * (i >> 2) + 4 * (int)h;
-            for (uint32_t tile = ctile; tile < min(ctile + (uint32_t)kTilesPerStage, a.ntiles) && tile <= best_tile;
-                 ++tile) {
-                const int p = a.tile_pos[tile * 32 + row];
-                uint32_t d[K2];
-                if (p >= 0) {
-                    const uint32_t* dp = a.pool + (size_t)p * K2;
-                    if constexpr (K2 == 8) {
-                        const uint4 v0 = reinterpret_cast<const uint4*>(dp)[0], v1 = reinterpret_cast<const uint4*>(dp)[1];
-                        d[0] = v0.x, d[1] = v0.y, d[2] = v0.z, d[3] = v0.w, d[4] = v1.x, d[5] = v1.y, d[6] = v1.z, d[7] = v1.w;
-                    } else {
-#pragma unroll
-                        for (int k = 0; k < K2; ++k)
-                            d[k] = dp[k];
-                    }
-                } else {
-#pragma unroll
-                    for (int k = 0; k < K2; ++k)
-                        d[k] = 0u;
-                }
-                uint32_t sd1u = 0;
-#pragma unroll
-                for (int k = 0; k < K2; ++k)
-                    sd1u = __builtin_amdgcn_udot2(__builtin_bit_cast(ushort2_t, d[k]), __builtin_bit_cast(ushort2_t, kOnes),
-                                                  sd1u, false);
-                const int64_t nsd2 = p >= 0 ? (int64_t)a.negsd2[p] : 0;
-                unsigned long long mk = kKeyNone; // the lane's least key over its transforms
-                int64_t mx = 0;
-#pragma unroll
-                for (int c = 0; c < 2; ++c) {
-                    if (c == 1 && !two)
-                        break;
-                    uint32_t xu = 0;
-#pragma unroll
-                    for (int k = 0; k < K2; ++k)
-                        xu = __builtin_amdgcn_udot2(__builtin_bit_cast(ushort2_t, cp[c][k]),
-                                                    __builtin_bit_cast(ushort2_t, d[k]), xu, false);
-                    const int64_t s16 = 16 * sr2 - 8 * (int64_t)xu - nsd2;
-                    const uint32_t tt = (uint32_t)(t0 + 4 * c);
-                    if (p >= 0 && (hit ? (s16 <= a.hitH) : (s16 == target))) {
-                        const unsigned long long k =
-                            hit ? key_hit((uint32_t)p, tt) : key_miss((uint64_t)s16, (uint32_t)p, a.T - 1 - tt);
-                        if (k < mk) {
-                            mk = k;
-                            mx = (int64_t)xu;
-                        }
-                    }
-                }
-                unsigned long long wk = mk; // the wave's least key of the tile
-#pragma unroll
-                for (int o = 32; o > 0; o >>= 1) {
-                    const unsigned long long ok2 = ((unsigned long long)lane_xor((uint32_t)(wk >> 32), lane, o) << 32) |
-                                                   lane_xor((uint32_t)wk, lane, o);
-                    wk = ok2 < wk ? ok2 : wk;
-                }
-                if (wk != kKeyNone) {
-                    if (wk < bestk) {
-                        const int src2 = __ffsll((long long)__ballot(mk == wk)) - 1;
-                        bestk = wk;
-                        best_tile = tile;
-                        bx = (int64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)mx, src2);
-                        bsd = (int64_t)(uint32_t)__builtin_amdgcn_readlane((int)sd1u, src2);
-                        bsd2 = -(int64_t)(int32_t)__builtin_amdgcn_readlane((int)(int32_t)nsd2, src2);
-                    }
-                    break; // later tiles of the chunk hold later pool positions
-                }
-            }
+            eval_chunk(ctile, h);
         }
     }
     if (lane == 0) {
