@@ -8,7 +8,8 @@ Ranges are sharded contiguously over ranks (fixed total work: strong scaling).
 
 `value` is BASELINE.md's / SURVEY §8(d)'s end-to-end step, the span the reference's own timer
 wraps (main.cpp:164-168, the whole Encoder2): per step the frame H2D from pinned host memory
-(each rank uploads its own copy), domain-pool build, search, winner fit and fp32 fallback of this
+(N > 1: each rank uploads its 1/N stripe of the rows and an RCCL all-gather assembles the frame
+on every rank over xGMI), domain-pool build, search, winner fit and fp32 fallback of this
 rank's shard, its 32-byte (domain, transform, s, o, rms) tuples packed on the device, the RCCL
 all-gather of every rank's tuples (N > 1) and the gathered tuples D2H into pinned host memory —
 serial, one frame after another.  Beside it the line carries:
@@ -239,11 +240,28 @@ class FrameStep:
     pinned host plane, the search of this rank's shard (frame-dependent preparation included), the
     shard's 32-byte tuples into the all-gather buffer, the all-gather (whenever a process group is
     up), and the gathered tuples D2H into pinned host memory.  `device_resident=True`: the frame is
-    not uploaded and the gathered tuples stay on the device (the device-only leg)."""
+    not uploaded and the gathered tuples stay on the device (the device-only leg).
+    `stripes` (default: with more than one rank): each rank uploads only its 1/N stripe of the frame's
+    rows across its own PCIe link and one all-gather assembles the frame on every rank over xGMI,
+    instead of N full 16.8 MB uploads; the frame the engine gets is the same plane."""
 
-    def __init__(self, eng, frame, plan, rank: int, dev, device_resident: bool = False):
+    def __init__(self, eng, frame, plan, rank: int, dev, device_resident: bool = False, stripes=None):
         import torch
 
+        world = len(plan)
+        self.stripes = (world > 1 and not device_resident) if stripes is None else bool(stripes)
+        self.h_stripe = None
+        if self.stripes:
+            ft = frame if isinstance(frame, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(frame))
+            H, W = int(ft.shape[0]), int(ft.shape[1])
+            rows = -(-H // world)  # equal stripes for all_gather_into_tensor; the last rank's is padded
+            r0, r1 = min(H, rank * rows), min(H, (rank + 1) * rows)
+            self.H, self.stripe_rows = H, r1 - r0
+            self.h_stripe = ft[r0:r1]  # a view: pinned when the caller's plane is
+            self.d_stripe = torch.zeros((rows, W), dtype=torch.uint8, device=dev)
+            self.d_full = torch.empty((world * rows, W), dtype=torch.uint8, device=dev)
+        if isinstance(frame, torch.Tensor):
+            frame = frame.numpy()
         self.eng, self.frame, self.plan, self.rank, self.dev = eng, frame, plan, rank, dev
         self.device_resident = device_resident
         a, b = plan[rank]
@@ -258,7 +276,15 @@ class FrameStep:
 
         from fractencode_amd.distributed import gather_tuples
 
-        if not self.device_resident:
+        if self.stripes:
+            import torch.distributed as dist
+
+            if self.stripe_rows:  # this rank's rows H2D (on the engine's = torch's current stream)
+                self.d_stripe[: self.stripe_rows].copy_(self.h_stripe, non_blocking=True)
+            dist.all_gather_into_tensor(self.d_full, self.d_stripe)  # the whole frame on every rank
+            full = self.d_full[: self.H]
+            self.eng.set_frame(full if full.is_cuda else full.numpy())
+        elif not self.device_resident:
             self.eng.set_frame(self.frame)  # H2D (returns once the plane is on the device)
         self.eng.run()
         if self.local.is_cuda:  # packed on the device, on the engine's (= torch's current) stream
@@ -346,7 +372,7 @@ def main(args):
     eng.set_ranges(mine)
 
     # ---- headline: the end-to-end step ----
-    step = FrameStep(eng, h_frame.numpy(), plan, rank, dev)
+    step = FrameStep(eng, h_frame, plan, rank, dev)
     for _ in range(args.warmup):
         step()
     _sync(dev)
@@ -399,7 +425,9 @@ def main(args):
                                f"16x16 domains stride 8 ({n_d}), T={args.transforms}, exhaustive, rms 0",
                    "engine": engine_name, "ranges_per_gpu": len(mine), "parallelism": f"ranges/{world}",
                    "env": frac_env(), "ab_run": bool(knobs)},
-        "step": "frame H2D (pinned, 16 MiB per rank) + pool build + search + fit of the rank's shard + 32-byte "
+        "step": ("frame H2D (pinned, 16 MiB) + " if world == 1 else
+                 "frame H2D of the rank's 1/N stripe of rows (pinned) + RCCL all-gather of the frame + ") +
+                "pool build + search + fit of the rank's shard + 32-byte "
                 "tuples packed on the device + all-gather over ranks (N > 1) + gathered tuples D2H (pinned); "
                 "serial, barrier + synchronisation around the timed steps, slowest rank",
         "roofline": roof,

@@ -1,8 +1,8 @@
 """One rank of bench.py's N > 1 orchestration on the CPU (test infrastructure, launched by
 tests/test_bench_ranks.py through bench.launch_ranks → torch.distributed.run, or run directly for
 world size 1): the oracle stand-in engine behind bench.FrameStep, `gloo` in place of RCCL, the
-same timed() bracket and headline_fields() as the GPU headline.  Rank 0 writes the line, every
-rank's own time and the gathered tuples to OUT.
+same timed() bracket and headline_fields() as the GPU headline (the frame in row stripes assembled by
+the all-gather when N > 1).  Rank 0 writes the line, every rank's own time and the gathered tuples to OUT.
 usage: python tests/bench_rank_cpu.py OUT STEPS [FAIL_RANK]"""
 import json
 import os
@@ -50,7 +50,8 @@ else:
     every = [(0, mine, step.own_slice_ok(own))]
 if rank == 0:
     gathered = step.tuples_bytes()
-    json.dump({"line": line, "ranks": every, "digest": bench.digest(gathered), "tuples": gathered.hex()}, open(out, "w"))
+    json.dump({"line": line, "ranks": every, "digest": bench.digest(gathered), "tuples": gathered.hex(),
+               "stripes": step.stripes}, open(out, "w"))
 if world > 1:
     dist.barrier()
     dist.destroy_process_group()

@@ -38,7 +38,7 @@ def single(tmp_path_factory):
     return json.load(open(out))
 
 
-@pytest.mark.parametrize("world", [2, 4, 8])
+@pytest.mark.parametrize("world", [2, 3, 4, 8])
 def test_bench_orchestration_on_gloo_ranks(tmp_path, single, oracle, world):
     import bench
     import fractencode_amd as F
@@ -48,7 +48,9 @@ def test_bench_orchestration_on_gloo_ranks(tmp_path, single, oracle, world):
     assert rc == 0
     d = json.load(open(out))
     line = d["line"]
-    # the gathered records equal the single-rank run's, byte for byte, and the reference's (oracle)
+    # the gathered records equal the single-rank run's, byte for byte, and the reference's (oracle); the
+    # frame reached every rank as row stripes and one all-gather (64 rows: uneven stripes at world 3)
+    assert d["stripes"] and not single["stripes"]
     assert d["digest"] == single["digest"] and d["tuples"] == single["tuples"]
     tuples = np.frombuffer(bytes.fromhex(d["tuples"]), dtype=F.TUPLE)
     assert len(tuples) == 93

@@ -228,6 +228,62 @@ def test_nccl_device_tuples_world1_match_reference(tmp_path):
         np.testing.assert_array_equal(got[k], rec[k], err_msg=k)
 
 
+def _stripes_worker(rank, world, port, path):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import torch
+    import torch.distributed as dist
+
+    import bench
+    import fractencode_amd as F
+    from fractencode_amd.distributed import records_from_tuples, shard_plan
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    torch.cuda.set_device(rank)
+    dev = torch.device("cuda", rank)
+    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    y = np.fromfile(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "lenna_y.u8"),
+                    dtype=np.uint8).reshape(512, 512)
+    doms = F.create_uniform_grid(512, 512, 16, 8)
+    rngs = F.create_uniform_grid(512, 512, 8, 8)
+    plan = shard_plan(len(rngs), world)
+    a, b = plan[rank]
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
+    h = torch.from_numpy(y).pin_memory()
+    with F.Engine(rank, 4) as e:
+        e.set_stream(stream.cuda_stream)
+        e.set_frame(np.zeros_like(y))  # the step's stripes and all-gather bring the real frame
+        e.set_domains(doms)
+        e.set_ranges(rngs[a:b])
+        step = bench.FrameStep(e, h, plan, rank, dev, stripes=True)
+        step()
+        torch.cuda.synchronize(dev)
+        full = records_from_tuples(np.frombuffer(step.tuples_bytes(), dtype=F.TUPLE), rngs, doms)
+    if rank == 0:
+        np.save(path, full)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_nccl_frame_stripes_world1_match_reference(tmp_path):
+    """bench.FrameStep with the frame in row stripes assembled by an RCCL all-gather (the N > 1 upload), run at
+    world size 1 on the device's nccl group (the collective still runs), against lenna_t4."""
+    from golden_util import FIELDS, golden
+
+    path = str(tmp_path / "full.npy")
+    mp.spawn(_stripes_worker, args=(1, _free_port(), path), nprocs=1, join=True)
+    full = np.load(path)
+    rec, _ = golden("lenna_t4")
+    got = {"x": full["x"], "y": full["y"], "dx": full["dx"], "dy": full["dy"], "dw": full["sw"], "dh": full["sh"],
+           "t": full["transform"], "dist": full["distance"], "s": full["contrast"], "o": full["brightness"]}
+    for k in FIELDS:
+        np.testing.assert_array_equal(got[k], rec[k], err_msg=k)
+
+
 def _gpu_cls_worker(rank, world, port, path):
     import sys
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
