@@ -99,3 +99,35 @@ def test_reference_opencl_classify_test_on_device(oracle):
     np.testing.assert_array_equal(dev["category"], ref["category"])
     np.testing.assert_array_equal(F.preclassify(p, grid)["category"], ref["category"])
     np.testing.assert_array_equal(oracle.classify(p, grid)["category"], ref["category"])
+
+
+def test_classifier_pool_beyond_the_one_pass_sort(oracle):
+    """A classified pool of 1,042,441 domains (8×8 at stride 2 over 2048²): 1,018 sort tiles, above
+    kBkSelfTiles, so the bucket sort runs its three-launch form (count, per-bucket scan, scatter).  A strided
+    sample of the ranges equals the oracle's classified search, and every winner is in its range's bucket."""
+    from fractencode_amd.synth import value_noise
+
+    W = H = 2048
+    p = value_noise(W, H, 77)
+    doms = F.create_uniform_grid(W, H, 8, 2)
+    assert len(doms) > 512 * 1024
+    rngs = F.create_uniform_grid(W, H, 4, 4)[:16384]
+    with F.Engine(0, 4, True, 0.0, -1.0) as e:
+        e.set_frame(p)
+        e.set_domains(doms)
+        e.set_ranges(rngs)
+        e.run()
+        out, st = e.fetch()
+    assert st["rejected_mappings"] > 0
+    pick = np.arange(0, len(rngs), 1024)
+    rg = np.zeros(len(pick), dtype=oracle.ITEM_DTYPE)
+    for k in ("x", "y", "w", "h"):
+        rg[k] = rngs[k][pick]
+    rg = oracle.classify(p, rg)
+    want, _, _ = oracle.estimate(p, oracle.classify(p, oracle.uniform_grid(W, H, 8, 2)), rg, T=4,
+                                 use_classifier=True, threads=16)
+    got = out[pick]
+    g = {"x": got["x"], "y": got["y"], "dx": got["dx"], "dy": got["dy"], "dw": got["sw"], "dh": got["sh"],
+         "t": got["transform"], "dist": got["distance"], "s": got["contrast"], "o": got["brightness"]}
+    for k in FIELDS:
+        np.testing.assert_array_equal(g[k], want[k], err_msg=k)
