@@ -250,16 +250,10 @@ class FrameStep:
 
         world = len(plan)
         self.stripes = (world > 1 and not device_resident) if stripes is None else bool(stripes)
-        self.h_stripe = None
         if self.stripes:
-            ft = frame if isinstance(frame, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(frame))
-            H, W = int(ft.shape[0]), int(ft.shape[1])
-            rows = -(-H // world)  # equal stripes for all_gather_into_tensor; the last rank's is padded
-            r0, r1 = min(H, rank * rows), min(H, (rank + 1) * rows)
-            self.H, self.stripe_rows = H, r1 - r0
-            self.h_stripe = ft[r0:r1]  # a view: pinned when the caller's plane is
-            self.d_stripe = torch.zeros((rows, W), dtype=torch.uint8, device=dev)
-            self.d_full = torch.empty((world * rows, W), dtype=torch.uint8, device=dev)
+            from fractencode_amd.distributed import FrameStripes
+
+            self.frame_stripes = FrameStripes(frame, world, rank, dev)
         if isinstance(frame, torch.Tensor):
             frame = frame.numpy()
         self.eng, self.frame, self.plan, self.rank, self.dev = eng, frame, plan, rank, dev
@@ -276,13 +270,8 @@ class FrameStep:
 
         from fractencode_amd.distributed import gather_tuples
 
-        if self.stripes:
-            import torch.distributed as dist
-
-            if self.stripe_rows:  # this rank's rows H2D (on the engine's = torch's current stream)
-                self.d_stripe[: self.stripe_rows].copy_(self.h_stripe, non_blocking=True)
-            dist.all_gather_into_tensor(self.d_full, self.d_stripe)  # the whole frame on every rank
-            full = self.d_full[: self.H]
+        if self.stripes:  # this rank's rows H2D + the all-gather (on the engine's = torch's current stream)
+            full = self.frame_stripes()
             self.eng.set_frame(full if full.is_cuda else full.numpy())
         elif not self.device_resident:
             self.eng.set_frame(self.frame)  # H2D (returns once the plane is on the device)

@@ -89,6 +89,36 @@ def gather_tuples(local, plan: list[tuple[int, int]], group=None):
     return torch.cat(parts)
 
 
+class FrameStripes:
+    """The frame onto every rank without N full uploads: rank r copies only rows [r·rows, (r+1)·rows) of the
+    caller's host plane across its own PCIe link (rows = ⌈H / world⌉; the last stripe is padded) and one
+    all_gather_into_tensor assembles the whole plane on every rank — over xGMI with RCCL, or on the CPU with
+    gloo.  `frame`: a [H, W] uint8 torch tensor (pinned for an asynchronous copy) or numpy array; calling
+    the object returns the [H, W] plane on `device` (a view of an internal buffer, valid until the next
+    call), ordered on torch's current stream."""
+
+    def __init__(self, frame, world: int, rank: int, device, group=None):
+        import torch
+
+        ft = frame if isinstance(frame, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(frame))
+        self.H, W = int(ft.shape[0]), int(ft.shape[1])
+        rows = -(-self.H // world)
+        r0, r1 = min(self.H, rank * rows), min(self.H, (rank + 1) * rows)
+        self.n = r1 - r0
+        self.host = ft[r0:r1]  # a view: pinned when the caller's plane is
+        self.stripe = torch.zeros((rows, W), dtype=torch.uint8, device=device)
+        self.full = torch.empty((world * rows, W), dtype=torch.uint8, device=device)
+        self.group = group
+
+    def __call__(self):
+        import torch.distributed as dist
+
+        if self.n:
+            self.stripe[: self.n].copy_(self.host, non_blocking=True)
+        dist.all_gather_into_tensor(self.full, self.stripe, group=self.group)
+        return self.full[: self.H]
+
+
 def tuples_from_bytes(buf) -> np.ndarray:
     from . import TUPLE
 
