@@ -79,6 +79,8 @@ CASES = [
     (96, 64, 16, 4, True, 0.0, 0.5, "noise"),
     (256, 256, 16, 4, False, 0.0, -1.0, "flat"),   # n = 16, 8 tiles: ties across tiles, first tile wins
     (256, 192, 16, 4, False, 40.0, -1.0, "flat"),  # n = 16 threshold hits across tiles (T = 4)
+    (256, 256, 4, 4, False, 0.0, -1.0, "flat"),    # n = 4, 125 tiles in splits: ties across tiles and work items
+    (256, 192, 4, 8, False, 40.0, -1.0, "flat"),   # n = 4 threshold hits across tiles and work items (T = 8)
     (64, 64, 8, 4, False, 1e9, -1.0, "noise"),   # every candidate hits: all-fallback mode
     (64, 64, 8, 8, False, 5000.0, -1.0, "uniform"),
 ]
