@@ -6,6 +6,7 @@ legs separate why the search runs slower in the end-to-end step: the device-resi
 0.5 ms between steps (clock / power), and with a device-to-device re-copy of the frame instead of the H2D.
 Leg e2e_zc packs the tuples straight into the pinned host buffer (the pack kernel's stores cross PCIe) instead
 of packing on the device and copying.  Run it with HSA_ENABLE_SDMA=0 to see the copies done by blit kernels.
+Legs idle_<µs>: the device-resident step after that many µs of GPU idle (how the slowdown grows with the idle).
 usage: tools/e2e_probe.py [steps] [rounds] [legs,...]"""
 import json
 import os
@@ -62,12 +63,14 @@ with F.Engine(0, 4, False, 0.0, -1.0, F.ENGINE_AUTO, timing=True) as e:
 
     legs = {"e2e": bench.FrameStep(e, h_frame.numpy(), plan, 0, dev), "device": dstep, "device_idle": idle_step,
             "device_d2d": d2d_step, "e2e_zc": zc_step}
+    for us in (50, 100, 200, 500, 1000, 2000):  # idle_<µs>: the device-resident step after that much GPU idle
+        legs[f"idle_{us}"] = (lambda sec: (lambda: (torch.cuda.synchronize(dev), time.sleep(sec), dstep())))(us * 1e-6)
     if only:
         legs = {k: v for k, v in legs.items() if k in only}
     ref = None
     for r in range(rounds):
         for name, step in legs.items():
-            if name.startswith("device"):
+            if name.startswith(("device", "idle")):
                 e.set_frame(d_frame)
             for _ in range(3):
                 step()
