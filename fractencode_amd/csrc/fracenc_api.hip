@@ -198,6 +198,7 @@ struct frac_ctx {
     DBuf<uint2> d_rbucket;
     DBuf<uint32_t> d_rord, d_rkey;           // bucket-sorted range order; per range bucket
     DBuf<uint32_t> d_bk_keys, d_bk_keys2, d_bk_iota, d_bk_first, d_bk_err, d_bk_cnt;
+    DBuf<uint16_t> d_bsum_s, d_bsum_t; // the source / target plane's block sums (frame_block_sums)
     DBuf<uint8_t> d_bk_tmp;
     size_t bk_tmp_bytes = 0;
     DBuf<unsigned long long> d_best_key;
@@ -484,6 +485,22 @@ int upload_plane(frac_ctx* c, const uint8_t* p, uint32_t w, uint32_t h, uint32_t
     return FRAC_OK;
 }
 
+// The classifier keys of a run or a quadtree level from the planes' block sums (bucket_keys_bs) when every
+// item is at most 32 rows high (q ≤ 16): the source plane's pyramid, and the target's when it is another plane.
+static int plane_block_sums(frac_ctx* c, BlockSums& bs, BlockSums& bt)
+{
+    FRAC_HIP(c, c->d_bsum_s.ensure(std::max<size_t>(bs_words(c->src.w, c->src.h), 1)));
+    launch_block_sums(c->d_src.ptr, c->d_sstride, c->src.w, c->src.h, c->d_bsum_s.ptr, c->stream);
+    bs = bs_layout(c->d_bsum_s.ptr, c->src.w, c->src.h);
+    bt = bs;
+    if (!c->same_plane) {
+        FRAC_HIP(c, c->d_bsum_t.ensure(std::max<size_t>(bs_words(c->tgt.w, c->tgt.h), 1)));
+        launch_block_sums(c->d_tgt.ptr, c->d_tstride, c->tgt.w, c->tgt.h, c->d_bsum_t.ptr, c->stream);
+        bt = bs_layout(c->d_bsum_t.ptr, c->tgt.w, c->tgt.h);
+    }
+    return FRAC_OK;
+}
+
 // The classifier buckets on the device (fracenc_bucket.hip): d_porig (pool position → domain index),
 // d_rord (ranges in bucket order), d_rkey (per range bucket); first[b] / rfirst[b] = the first pool
 // position / bucket-sorted range of bucket b (b = 0..kMaxBuckets).  One small synchronous copy.
@@ -517,9 +534,15 @@ int device_buckets(frac_ctx* c, int nb, uint32_t* dfirst, uint32_t* rfirst)
     // a stored −1 is classified on the item's own plane (Classifier2::compare, Classifier2.cpp:70-81);
     // the pool order porig and the bucket-sorted ranges rord by the stable bucket sort
     // both grids' keys, in one launch for the usual 2n → n geometry
-    launch_bucket_keys_pair(KeySeg{c->d_doms.ptr, nd, c->d_src.ptr, c->d_sstride, c->d_bk_keys.ptr, nullptr, err, nullptr},
-                            c->Sh, KeySeg{c->d_ranges.ptr, nr, tplane, tstride, c->d_rkey.ptr, nullptr, err, nullptr},
-                            c->nh, c->stream);
+    const KeySeg kd{c->d_doms.ptr, nd, c->d_src.ptr, c->d_sstride, c->d_bk_keys.ptr, nullptr, err, nullptr};
+    const KeySeg kr{c->d_ranges.ptr, nr, tplane, tstride, c->d_rkey.ptr, nullptr, err, nullptr};
+    if (c->Sh <= 32 && c->Sw <= 32 && c->nh <= 32 && c->nw <= 32) { // from the planes' block sums
+        BlockSums bs, bt;
+        FRAC_TRY(plane_block_sums(c, bs, bt));
+        launch_bucket_keys_bs(kd, bs, c->Sw, c->Sh, kr, bt, c->nw, c->nh, c->stream);
+    } else {
+        launch_bucket_keys_pair(kd, c->Sh, kr, c->nh, c->stream);
+    }
     const BkSeg sd = bk_seg_of(c->d_bk_keys.ptr, nd, nullptr, c->d_bk_cnt.ptr, first, c->d_porig.ptr);
     const BkSeg sr = bk_seg_of(c->d_rkey.ptr, nr, nullptr, c->d_bk_cnt.ptr + (size_t)sd.tiles * kMaxBuckets,
                                first + kMaxBuckets + 1, c->d_rord.ptr);
@@ -2455,6 +2478,11 @@ int qt_encode_dev(frac_ctx* c, const frac_quadtree_params* qp, LevelGrid& level,
     FRAC_HIP(c, c->d_qt_stats.ensure(kQtShards * kQtCounters));
     FRAC_HIP(c, c->d_bk_first.ensure(2 * (kMaxBuckets + 1) + 1));
     FRAC_HIP(c, hipMemsetAsync(c->d_qt_stats.ptr, 0, kQtShards * kQtCounters * sizeof(unsigned long long), c->stream));
+    // the classifier keys of every level from the frame's block sums, summed once here (domains 2n ≤ 32 rows)
+    BlockSums bs_src, bs_tgt;
+    const bool use_bs = nb > 1 && qp->max_size <= 16;
+    if (use_bs)
+        FRAC_TRY(plane_block_sums(c, bs_src, bs_tgt));
     // the first level's ranges: createUniformGrid(W, H, max, max), generated on the device
     const uint32_t m0 = qp->max_size;
     const uint32_t nr0 = W >= m0 && H >= m0 ? ((W - m0) / m0 + 1) * ((H - m0) / m0 + 1) : 0u;
@@ -2562,9 +2590,12 @@ int qt_encode_dev(frac_ctx* c, const frac_quadtree_params* qp, LevelGrid& level,
             // domains: keys + stable bucket sort (the pool order porig) + bounds; ranges: the same over the
             // worst case, counting only the level's *dn (the grids' categories are −1, computed here:
             // no invalid category can occur, so no error word)
-            launch_bucket_keys_pair(
-                KeySeg{c->d_doms.ptr, nd, c->d_src.ptr, c->d_sstride, c->d_bk_keys.ptr, nullptr, nullptr, nullptr}, 2 * n,
-                KeySeg{c->d_ranges.ptr, nr_max, tplane, tstride, c->d_rkey.ptr, nullptr, nullptr, dn}, n, c->stream);
+            const KeySeg kd{c->d_doms.ptr, nd, c->d_src.ptr, c->d_sstride, c->d_bk_keys.ptr, nullptr, nullptr, nullptr};
+            const KeySeg kr{c->d_ranges.ptr, nr_max, tplane, tstride, c->d_rkey.ptr, nullptr, nullptr, dn};
+            if (use_bs) // the frame's block sums, summed once before the first level
+                launch_bucket_keys_bs(kd, bs_src, 2 * n, 2 * n, kr, bs_tgt, n, n, c->stream);
+            else
+                launch_bucket_keys_pair(kd, 2 * n, kr, n, c->stream);
             // both sorts in one set of launches (the range counts after the domain counts in the scratch)
             const BkSeg sd = bk_seg_of(c->d_bk_keys.ptr, nd, nullptr, c->d_bk_cnt.ptr, first, c->d_porig.ptr);
             const BkSeg sr = bk_seg_of(c->d_rkey.ptr, nr_max, dn, c->d_bk_cnt.ptr + (size_t)sd.tiles * kMaxBuckets,
@@ -2896,6 +2927,8 @@ void frac_destroy(frac_ctx* c)
     c->d_rkey.release();
     c->d_bk_keys.release();
     c->d_bk_cnt.release();
+    c->d_bsum_s.release();
+    c->d_bsum_t.release();
     c->d_bk_keys2.release();
     c->d_bk_iota.release();
     c->d_bk_first.release();

@@ -196,6 +196,201 @@ inline void launch_bucket_keys(const frac_grid_item* items, uint32_t cnt, uint32
         bucket_keys<<<(cnt + 3) / 4, 256, 0, s>>>(items, cnt, plane, stride, key, iota, err);
 }
 
+// ---- classifier keys from the plane's block sums (round 5) ----
+// Classifier2's categories depend on an item's four quadrant sums only (Classifier2.cpp:55-68).  The grids
+// the engine classifies on every frame — the C4 run's domains and ranges, the quadtree levels' — are
+// q-aligned squares of side 2q, q ∈ {2, 4, 8, 16}, whose quadrants are whole q×q blocks of the plane at
+// q-aligned positions.  frame_block_sums sums every such block of a plane once (one thread per 4×4 block,
+// 8×8 blocks per wave: 2×2 sums from the bytes, 4×4 from those, 8×8 and 16×16 over lane shuffles), and
+// bucket_keys_bs classifies an item with four loads from the pyramid instead of re-reading its 4q² pixels
+// (each plane pixel was read 4× by the overlapping stride-q domains).  Items that are not such squares are
+// summed from the plane by their own thread.  Sums ≤ 16²·255 < 2^16: u16, exact.
+// Rows are padded to an even pitch (4-byte aligned rows).
+struct BlockSums {
+    uint16_t* s[4] = {nullptr, nullptr, nullptr, nullptr}; // q = 2, 4, 8, 16: [⌊H/q⌋][pitch]
+    uint32_t cols[4] = {0, 0, 0, 0};                        // ⌊W/q⌋
+    uint32_t rows[4] = {0, 0, 0, 0};                        // ⌊H/q⌋
+    uint32_t pitch[4] = {0, 0, 0, 0};                       // cols rounded up to even
+};
+
+// the pyramid's layout in one buffer of bs_words(W, H) u16 (+ 2 words of slack)
+inline size_t bs_words(uint32_t W, uint32_t H)
+{
+    size_t n = 2;
+    for (uint32_t q = 2; q <= 16; q *= 2)
+        n += (size_t)(((W / q) + 1) & ~1u) * (H / q);
+    return n;
+}
+inline BlockSums bs_layout(uint16_t* base, uint32_t W, uint32_t H)
+{
+    BlockSums b;
+    size_t off = 0;
+    for (int l = 0; l < 4; ++l) {
+        const uint32_t q = 2u << l;
+        b.s[l] = base + off;
+        b.cols[l] = W / q;
+        b.rows[l] = H / q;
+        b.pitch[l] = (b.cols[l] + 1) & ~1u;
+        off += (size_t)b.pitch[l] * b.rows[l];
+    }
+    return b;
+}
+
+__global__ void __launch_bounds__(256) frame_block_sums(const uint8_t* __restrict__ plane, uint32_t stride, uint32_t W,
+                                                        uint32_t H, BlockSums b)
+{
+    const uint32_t W4c = (W + 3) / 4, H4c = (H + 3) / 4; // 4×4 blocks, the last column / row possibly partial
+    const uint32_t nwx = (W4c + 7) / 8;
+    const uint32_t wid = blockIdx.x * 4u + (threadIdx.x >> 6), lane = threadIdx.x & 63u;
+    const uint32_t bx = (wid % nwx) * 8 + (lane & 7u), by = (wid / nwx) * 8 + (lane >> 3);
+    if (wid >= nwx * ((H4c + 7) / 8))
+        return; // whole waves: the shuffles below see only live lanes
+    const uint32_t x0 = 4 * bx, y0 = 4 * by;
+    uint32_t r[4] = {0u, 0u, 0u, 0u}; // the block's rows, four pixels each (zero outside the plane)
+    if (bx < W4c && by < H4c) {
+        const uint8_t* p = plane + (size_t)y0 * stride + x0;
+        const bool full = x0 + 4 <= W && y0 + 4 <= H && ((((uintptr_t)p) | stride) & 3u) == 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            if (full) {
+                r[i] = *reinterpret_cast<const uint32_t*>(p + (size_t)i * stride);
+            } else if (y0 + i < H) {
+                for (uint32_t j = 0; j < 4; ++j)
+                    if (x0 + j < W)
+                        r[i] |= (uint32_t)p[(size_t)i * stride + j] << (8 * j);
+            }
+        }
+    }
+    // q = 2: pixel columns (0, 1) and (2, 3) of row pairs (0, 1) and (2, 3)
+    uint32_t s2[4], s4 = 0;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const uint32_t m = j ? 0x01010000u : 0x00000101u;
+            s2[2 * i + j] = __builtin_amdgcn_udot4(r[2 * i], m, __builtin_amdgcn_udot4(r[2 * i + 1], m, 0u, false), false);
+            s4 += s2[2 * i + j];
+        }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const uint32_t cx = 2 * bx + j, cy = 2 * by + i;
+            if (cx < b.cols[0] && cy < b.rows[0])
+                b.s[0][(size_t)cy * b.pitch[0] + cx] = (uint16_t)s2[2 * i + j];
+        }
+    if (bx < b.cols[1] && by < b.rows[1])
+        b.s[1][(size_t)by * b.pitch[1] + bx] = (uint16_t)s4;
+    // q = 8, 16: sums over 2×2 and 4×4 lanes (lane = 8·(by mod 8) + (bx mod 8))
+    uint32_t s8 = s4 + (uint32_t)__shfl_xor((int)s4, 1, 64);
+    s8 += (uint32_t)__shfl_xor((int)s8, 8, 64);
+    uint32_t s16 = s8 + (uint32_t)__shfl_xor((int)s8, 2, 64);
+    s16 += (uint32_t)__shfl_xor((int)s16, 16, 64);
+    if ((lane & 9u) == 0 && bx / 2 < b.cols[2] && by / 2 < b.rows[2])
+        b.s[2][(size_t)(by / 2) * b.pitch[2] + bx / 2] = (uint16_t)s8;
+    if ((lane & 27u) == 0 && bx / 4 < b.cols[3] && by / 4 < b.rows[3])
+        b.s[3][(size_t)(by / 4) * b.pitch[3] + bx / 4] = (uint16_t)s16;
+}
+
+inline void launch_block_sums(const uint8_t* plane, uint32_t stride, uint32_t W, uint32_t H, uint16_t* out,
+                              hipStream_t st)
+{
+    const uint32_t W4c = (W + 3) / 4, H4c = (H + 3) / 4;
+    const uint32_t waves = ((W4c + 7) / 8) * ((H4c + 7) / 8);
+    if (waves)
+        frame_block_sums<<<(waves + 3) / 4, 256, 0, st>>>(plane, stride, W, H, bs_layout(out, W, H));
+}
+
+// the pyramid level a grid of w × h items reads (every item of a grid has one size): q = w / 2 = 2^sh
+struct BsLevel {
+    const uint16_t* s = nullptr; // nullptr: the grid's items are summed from the plane
+    uint32_t pitch = 0, sh = 0;
+};
+inline BsLevel bs_level(const BlockSums& b, uint32_t w, uint32_t h)
+{
+    BsLevel v;
+    const uint32_t q = w / 2;
+    const int l = q == 2 ? 0 : q == 4 ? 1 : q == 8 ? 2 : q == 16 ? 3 : -1;
+    if (w == h && l >= 0 && b.s[l]) {
+        v.s = b.s[l];
+        v.pitch = b.pitch[l];
+        v.sh = (uint32_t)l + 1u;
+    }
+    return v;
+}
+
+// one item's key from the grid's pyramid level (or, for an item that is not a q-aligned 2q square of that
+// level, from the plane by this thread alone); the padding and error rules of keys_rows_item
+__device__ __forceinline__ void keys_bs_item(const KeySeg& sg, const BsLevel& lv, uint32_t k)
+{
+    if (sg.dn && k >= min(*sg.dn, sg.n)) {
+        if (k < sg.n) {
+            sg.key[k] = kPadKey;
+            if (sg.iota)
+                sg.iota[k] = k;
+        }
+        return;
+    }
+    if (k >= sg.n)
+        return;
+    const frac_grid_item it = sg.items[k];
+    int cat = it.category;
+    if (cat == -1) {
+        const uint32_t q = 1u << lv.sh;
+        uint32_t qs[4] = {0u, 0u, 0u, 0u};
+        if (lv.s && it.w == 2 * q && it.h == 2 * q && ((it.x | it.y) & (q - 1)) == 0) {
+            const uint16_t* sp = lv.s + (size_t)(it.y >> lv.sh) * lv.pitch + (it.x >> lv.sh);
+            qs[0] = sp[0];
+            qs[1] = sp[1];
+            qs[2] = sp[lv.pitch];
+            qs[3] = sp[lv.pitch + 1];
+        } else {
+            const uint32_t hw = it.w / 2, hh = it.h / 2;
+#pragma unroll
+            for (int qd = 0; qd < 4; ++qd) { // quadrant by quadrant (constant indices: no private array)
+                const uint8_t* p0 = sg.plane + (size_t)(it.y + (qd >> 1) * hh) * sg.stride + it.x + (qd & 1) * hw;
+                uint32_t t = 0;
+                for (uint32_t py = 0; py < hh; ++py)
+                    for (uint32_t px = 0; px < hw; ++px)
+                        t += p0[(size_t)py * sg.stride + px];
+                qs[qd] = t;
+            }
+            if (hw <= 16)
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    qs[i] &= 0xffffu;
+        }
+        cat = category4_dev(qs[0], qs[1], qs[2], qs[3]);
+    }
+    if (cat < -1 || cat > 5) {
+        if (sg.err)
+            atomicOr(sg.err, 1u);
+        cat = -1;
+    }
+    sg.key[k] = (uint32_t)(cat + 1);
+    if (sg.iota)
+        sg.iota[k] = k;
+}
+
+// both grids' keys from block sums, one thread per item: threads [0, s0.n) take s0, the rest s1
+__global__ void __launch_bounds__(256) bucket_keys_bs(KeySeg s0, BsLevel l0, KeySeg s1, BsLevel l1)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < s0.n)
+        keys_bs_item(s0, l0, i);
+    else
+        keys_bs_item(s1, l1, i - s0.n);
+}
+
+// d: items dw × dh, r: items rw × rh
+inline void launch_bucket_keys_bs(const KeySeg& d, const BlockSums& bd, uint32_t dw, uint32_t dh, const KeySeg& r,
+                                  const BlockSums& br, uint32_t rw, uint32_t rh, hipStream_t st)
+{
+    const uint64_t n = (uint64_t)d.n + r.n;
+    if (n)
+        bucket_keys_bs<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(d, bs_level(bd, dw, dh), r, bs_level(br, rw, rh));
+}
+
 // a level's domain keys (items 2h rows high) and range keys (h rows) in one launch when h ∈ {4, 8, 16}
 // (the C4 frame and the quadtree's levels), else the two launches of launch_bucket_keys
 inline void launch_bucket_keys_pair(const KeySeg& d, uint32_t dh, const KeySeg& r, uint32_t rh, hipStream_t s)

@@ -81,6 +81,8 @@ CASES = [
     (256, 192, 16, 4, False, 40.0, -1.0, "flat"),  # n = 16 threshold hits across tiles (T = 4)
     (256, 256, 4, 4, False, 0.0, -1.0, "flat"),    # n = 4, 125 tiles in splits: ties across tiles and work items
     (256, 192, 4, 8, False, 40.0, -1.0, "flat"),   # n = 4 threshold hits across tiles and work items (T = 8)
+    (70, 58, 4, 4, True, 0.0, -1.0, "noise"),      # classifier keys from block sums: plane sides not multiples of 4
+    (98, 74, 8, 4, True, 0.0, -1.0, "uniform"),    # ... nor of 8 (partial blocks at the right and bottom edges)
     (64, 64, 8, 4, False, 1e9, -1.0, "noise"),   # every candidate hits: all-fallback mode
     (64, 64, 8, 8, False, 5000.0, -1.0, "uniform"),
 ]
@@ -101,6 +103,26 @@ def test_engine_matches_oracle_random(oracle, case, engine):
         rngs = oracle.classify(p, rngs)
     want, rej, _ = oracle.estimate(p, doms, rngs, T=T, thr=thr, smax=smax, use_classifier=cls)
     assert_same(out, {k: want[k] for k in FIELDS}, f"case {CASES[case]}")
+    assert st["rejected_mappings"] == rej
+
+
+@pytest.mark.parametrize("engine", ENGINES)
+def test_distinct_planes_with_the_classifier(oracle, engine):
+    """Source and target planes differ and the classifier is on: the domains' keys come from the source
+    plane's block sums, the ranges' from the target's (bucket_keys_bs), against the oracle."""
+    rng = np.random.default_rng(77)
+    src = _random_plane(rng, 96, 80, "noise")
+    tgt = _random_plane(rng, 48, 40, "uniform")
+    with F.Engine(0, 4, True, 0.0, -1.0, engine) as e:
+        e.set_planes(src, tgt)
+        e.set_domains(F.create_uniform_grid(96, 80, 8, 4))
+        e.set_ranges(F.create_uniform_grid(48, 40, 4, 4))
+        e.run()
+        out, st = e.fetch()
+    doms = oracle.classify(src, oracle.uniform_grid(96, 80, 8, 4))
+    rngs = oracle.classify(tgt, oracle.uniform_grid(48, 40, 4, 4))
+    want, rej, _ = oracle.estimate(src, doms, rngs, T=4, use_classifier=True, tgt=tgt)
+    assert_same(out, {k: want[k] for k in FIELDS}, "distinct planes, classifier")
     assert st["rejected_mappings"] == rej
 
 
