@@ -1775,48 +1775,50 @@ int launch_mfma(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool inits =
         FRAC_HIP(c, c->d_dft_slotbest.ensure((size_t)c->nblocks * 32));
         slotbest = c->d_dft_slotbest.ptr;
     }
-    if (c->ntiles) {
-        MfmaDomainPrepArgs d;
-        d.fmode = fmode;
-        d.pool = c->d_pool.ptr;
-        d.negsd2 = c->d_negsd2.ptr;
-        d.tile_pos = c->d_m_tile_pos.ptr;
-        d.ntiles = c->ntiles;
-        d.dtiles = c->d_m_dtiles.ptr;
-        d.dconst = c->d_m_dconst.ptr;
-        d.plan = c->qplan;
-        if constexpr (N == 16)
-            mfma_domain_prep16<<<(c->ntiles * 32 * MfmaGeom<16>::KS + 255) / 256, 256, 0, c->stream>>>(d);
-        else
-            mfma_domain_prep<N><<<(c->ntiles * 32 + 255) / 256, 256, 0, c->stream>>>(d);
-    }
-    if (c->nblocks) {
-        MfmaRangePrepArgs r;
-        r.tgt = dtgt;
-        r.tstride = tstride;
-        r.ranges = c->d_ranges.ptr;
-        r.slot_range = c->d_m_slot_range.ptr;
-        r.nblocks = c->nblocks;
-        r.T = T;
-        r.rfrags = c->d_m_rfrags.ptr;
-        r.rconst = c->d_m_rconst.ptr;
-        r.plan = c->qplan;
-        r.fmode = fmode;
-        r.slotbest = slotbest;
-        if constexpr (N == 16) { // one workgroup per range block, the constants written directly
+    // the domain tiles and the range blocks' fragments in one launch (mfma_prep)
+    MfmaDomainPrepArgs d;
+    d.fmode = fmode;
+    d.pool = c->d_pool.ptr;
+    d.negsd2 = c->d_negsd2.ptr;
+    d.tile_pos = c->d_m_tile_pos.ptr;
+    d.ntiles = c->ntiles;
+    d.dtiles = c->d_m_dtiles.ptr;
+    d.dconst = c->d_m_dconst.ptr;
+    d.plan = c->qplan;
+    MfmaRangePrepArgs r;
+    r.tgt = dtgt;
+    r.tstride = tstride;
+    r.ranges = c->d_ranges.ptr;
+    r.slot_range = c->d_m_slot_range.ptr;
+    r.nblocks = c->nblocks;
+    r.T = T;
+    r.rfrags = c->d_m_rfrags.ptr;
+    r.rconst = c->d_m_rconst.ptr;
+    r.plan = c->qplan;
+    r.fmode = fmode;
+    r.slotbest = slotbest;
+    // n = 16: 16 lanes per tile row and one workgroup per range block; else a thread per tile row and per
+    // (block, transform, K-step, lane)
+    const uint32_t dblocks = !c->ntiles ? 0u
+                             : N == 16  ? (c->ntiles * 32 * MfmaGeom<16>::KS + 255) / 256
+                                        : (c->ntiles * 32 + 255) / 256;
+    const uint32_t rblocks = !c->nblocks ? 0u
+                             : N == 16   ? c->nblocks
+                                         : (uint32_t)(((size_t)c->nblocks * T * MfmaGeom<N>::KS * 64 + 255) / 256);
+    // rconst is a sum of per-pixel terms, accumulated by the transform-0 threads (n < 16; a planned level's
+    // qt_fill_maps zeroed it)
+    if (N != 16 && c->nblocks && !c->qplan)
+        FRAC_HIP(c, hipMemsetAsync(c->d_m_rconst.ptr, 0, (size_t)c->nblocks * 32 * sizeof(uint32_t), c->stream));
+    if (dblocks + rblocks) {
+        if constexpr (N == 16) {
             if (T == 8)
-                mfma_range_prep16<8><<<c->nblocks, 256, 0, c->stream>>>(r);
+                mfma_prep<16, 8><<<dblocks + rblocks, 256, 0, c->stream>>>(d, r, dblocks);
             else if (T == 1)
-                mfma_range_prep16<1><<<c->nblocks, 256, 0, c->stream>>>(r);
+                mfma_prep<16, 1><<<dblocks + rblocks, 256, 0, c->stream>>>(d, r, dblocks);
             else
-                mfma_range_prep16<4><<<c->nblocks, 256, 0, c->stream>>>(r);
+                mfma_prep<16, 4><<<dblocks + rblocks, 256, 0, c->stream>>>(d, r, dblocks);
         } else {
-            const size_t threads = (size_t)c->nblocks * T * MfmaGeom<N>::KS * 64;
-            // rconst is a sum of per-pixel terms, accumulated by the transform-0 threads (a planned level's
-            // qt_fill_maps zeroed it)
-            if (!c->qplan)
-                FRAC_HIP(c, hipMemsetAsync(c->d_m_rconst.ptr, 0, (size_t)c->nblocks * 32 * sizeof(uint32_t), c->stream));
-            mfma_range_prep<N><<<(unsigned)((threads + 255) / 256), 256, 0, c->stream>>>(r);
+            mfma_prep<N><<<dblocks + rblocks, 256, 0, c->stream>>>(d, r, dblocks);
         }
     }
     if (c->p.flags & FRAC_FLAG_TIMING)
@@ -2477,7 +2479,6 @@ int qt_encode_dev(frac_ctx* c, const frac_quadtree_params* qp, LevelGrid& level,
     FRAC_HIP(c, c->d_qt_first.ensure(5 * kFirst));
     FRAC_HIP(c, c->d_qt_stats.ensure(kQtShards * kQtCounters));
     FRAC_HIP(c, c->d_bk_first.ensure(2 * (kMaxBuckets + 1) + 1));
-    FRAC_HIP(c, hipMemsetAsync(c->d_qt_stats.ptr, 0, kQtShards * kQtCounters * sizeof(unsigned long long), c->stream));
     // the classifier keys of every level from the frame's block sums, summed once here (domains 2n ≤ 32 rows)
     BlockSums bs_src, bs_tgt;
     const bool use_bs = nb > 1 && qp->max_size <= 16;
@@ -2486,9 +2487,11 @@ int qt_encode_dev(frac_ctx* c, const frac_quadtree_params* qp, LevelGrid& level,
     // the first level's ranges: createUniformGrid(W, H, max, max), generated on the device
     const uint32_t m0 = qp->max_size;
     const uint32_t nr0 = W >= m0 && H >= m0 ? ((W - m0) / m0 + 1) * ((H - m0) / m0 + 1) : 0u;
-    if (nr0)
-        qt_uniform_grid<<<(nr0 + 255) / 256, 256, 0, c->stream>>>((W - qp->max_size) / qp->max_size + 1, nr0,
-                                                                  qp->max_size, qp->max_size, c->d_ranges.ptr);
+    // (the same launch zeroes the frame's counters)
+    constexpr uint32_t kQtZero = kQtShards * kQtCounters;
+    qt_uniform_grid<<<(std::max(nr0, kQtZero) + 255) / 256, 256, 0, c->stream>>>(
+        nr0 ? (W - qp->max_size) / qp->max_size + 1 : 1u, nr0, qp->max_size, qp->max_size, c->d_ranges.ptr,
+        c->d_qt_stats.ptr, kQtZero);
     // the leaves go straight into the caller's buffer when it is pinned host memory the device can write
     // (the emit kernels write them over PCIe while the later levels run); else into d_qt_leaves and one
     // copy at the end

@@ -1261,12 +1261,16 @@ __global__ void __launch_bounds__(256) qt_plan(QtPlanArgs a)
 
 // createUniformGrid(W, H, size, off) on the device (image/partition2.hpp:123-133, frac_uniform_grid2):
 // the first quadtree level's ranges, kept on the device across frames like the domain grids
+// (also the frame's reset of `nz` counters, in place of a memset launch)
 __global__ void __launch_bounds__(256) qt_uniform_grid(uint32_t nx, uint32_t n, uint32_t size, uint32_t off,
-                                                       frac_grid_item* __restrict__ out)
+                                                       frac_grid_item* __restrict__ out,
+                                                       unsigned long long* __restrict__ zero = nullptr, uint32_t nz = 0)
 {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n)
         out[i] = frac_grid_item{(i % nx) * off, (i / nx) * off, size, size, -1};
+    if (i < nz)
+        zero[i] = 0ull;
 }
 
 } // namespace fracenc

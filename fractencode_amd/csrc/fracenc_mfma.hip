@@ -86,12 +86,11 @@ struct MfmaDomainPrepArgs {
 // n = 16: 16 K-steps per row, one lane each (16-lane groups per tile row): the row's 128 pool words and
 // 32 fragment stores split 16 ways (one thread per row was a 128-load chain on 63 workgroups: 39 µs at
 // the C4 quadtree's first level); the row sum ΣD4 of the epilogue constant by a 16-lane reduction
-__global__ void __launch_bounds__(256) mfma_domain_prep16(MfmaDomainPrepArgs a)
+__device__ __forceinline__ void mfma_domain_prep16_at(MfmaDomainPrepArgs a, uint32_t gid)
 {
     constexpr int N = 16, NN = N * N, KS = MfmaGeom<N>::KS;
     if (a.plan)
         a.ntiles = a.plan->ntiles;
-    const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
     if (gid >= a.ntiles * 32u * KS) // whole 16-lane row groups leave together
         return;
     const uint32_t rg = gid / KS, s = gid % KS, tile = rg >> 5, row = rg & 31u;
@@ -125,12 +124,11 @@ __global__ void __launch_bounds__(256) mfma_domain_prep16(MfmaDomainPrepArgs a)
 }
 
 template <int N>
-__global__ void __launch_bounds__(256) mfma_domain_prep(MfmaDomainPrepArgs a)
+__device__ __forceinline__ void mfma_domain_prep_at(MfmaDomainPrepArgs a, uint32_t gid)
 {
     constexpr int NN = N * N, KS = MfmaGeom<N>::KS;
     if (a.plan)
         a.ntiles = a.plan->ntiles;
-    const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
     if (gid >= a.ntiles * 32u)
         return;
     const uint32_t tile = gid >> 5, row = gid & 31u;
@@ -220,11 +218,10 @@ __device__ inline void apply_plan(MfmaRangePrepArgs& a, uint32_t copies)
 }
 
 template <int N>
-__global__ void __launch_bounds__(256) mfma_range_prep(MfmaRangePrepArgs a)
+__device__ __forceinline__ void mfma_range_prep_at(MfmaRangePrepArgs a, uint32_t gid)
 {
     constexpr int NN = N * N, KS = MfmaGeom<N>::KS;
     apply_plan(a, 1);
-    const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t per_block = a.T * KS * 64u;
     if (gid >= a.nblocks * per_block)
         return;
@@ -273,11 +270,10 @@ __global__ void __launch_bounds__(256) mfma_range_prep(MfmaRangePrepArgs a)
 constexpr uint32_t kRp16Row = 260;
 
 template <int T>
-__global__ void __launch_bounds__(256) mfma_range_prep16(MfmaRangePrepArgs a)
+__device__ __forceinline__ void mfma_range_prep16_at(MfmaRangePrepArgs a, uint32_t b)
 {
     constexpr int N = 16, NN = 256, KS = MfmaGeom<16>::KS;
     apply_plan(a, 1);
-    const uint32_t b = blockIdx.x;
     if (b >= a.nblocks)
         return;
     __shared__ uint8_t px[32 * kRp16Row];
@@ -350,6 +346,26 @@ __global__ void __launch_bounds__(256) mfma_range_prep16(MfmaRangePrepArgs a)
             v8[j] = (_Float16)(a.fmode ? 8 * (128 - rv) : 128 - rv);
         }
         a.rfrags[((size_t)b * T * KS) * 64 + o] = __builtin_bit_cast(uint4, v8);
+    }
+}
+
+// The direct form's preparation in one launch (dft_prep's arrangement): blocks [0, dblocks) build the domain
+// tiles (mfma_domain_prep), the rest the range blocks' fragments (mfma_range_prep; n = 16: one block per
+// range block), so the two run side by side instead of one after the other.  T: n = 16's transforms (the
+// range half's template); the smaller sides read a.T.
+template <int N, int T = 0>
+__global__ void __launch_bounds__(256) mfma_prep(MfmaDomainPrepArgs d, MfmaRangePrepArgs r, uint32_t dblocks)
+{
+    if (blockIdx.x < dblocks) {
+        if constexpr (N == 16)
+            mfma_domain_prep16_at(d, blockIdx.x * blockDim.x + threadIdx.x);
+        else
+            mfma_domain_prep_at<N>(d, blockIdx.x * blockDim.x + threadIdx.x);
+    } else {
+        if constexpr (N == 16)
+            mfma_range_prep16_at<T>(r, blockIdx.x - dblocks);
+        else
+            mfma_range_prep_at<N>(r, (blockIdx.x - dblocks) * blockDim.x + threadIdx.x);
     }
 }
 
