@@ -1785,6 +1785,14 @@ int launch_mfma(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool inits =
     d.dtiles = c->d_m_dtiles.ptr;
     d.dconst = c->d_m_dconst.ptr;
     d.plan = c->qplan;
+    if ((N == 4 || N == 16) && !c->virt) { // the pool rows built here (launch_all skips pool_build)
+        d.src = c->d_src.ptr;
+        d.sstride = c->d_sstride;
+        d.doms = c->d_doms.ptr;
+        d.porig = c->d_porig.ptr;
+        d.pool_out = c->d_pool.ptr;
+        d.negsd2_out = c->d_negsd2.ptr;
+    }
     MfmaRangePrepArgs r;
     r.tgt = dtgt;
     r.tstride = tstride;
@@ -2281,9 +2289,11 @@ int launch_all(frac_ctx* c)
     }
     // the Fourier path and the SEA engine's tiled form build the pool in their fused domain pass
     // (dft_domain_build)
-    const bool fused_pool = N == 8 && !c->virt &&
-                            ((use_mfma && (c->p.transforms == 4 || c->dft_copies == 2) && mfma_dft_enabled(c)) ||
-                             (c->engine == FRAC_ENGINE_SEA && !c->all_fallback && c->tp));
+    // (and the direct form at n = 4 / 16 in mfma_prep's domain half)
+    const bool fused_pool = !c->virt &&
+                            ((N == 8 && ((use_mfma && (c->p.transforms == 4 || c->dft_copies == 2) && mfma_dft_enabled(c)) ||
+                                         (c->engine == FRAC_ENGINE_SEA && !c->all_fallback && c->tp))) ||
+                             ((N == 4 || N == 16) && use_mfma));
     const GenArgs g = gen_args(c, dtgt, tstride);
     if (P && c->virt) // the sampled form: one row per (domain, transform), fracenc_gen.hip
         gen_pool_build<<<(P + 255) / 256, 256, 0, c->stream>>>(g);

@@ -81,7 +81,44 @@ struct MfmaDomainPrepArgs {
     uint32_t* dconst;           // [ntiles][2][16]
     const DevPlan* plan = nullptr; // device-planned search: ntiles from the plan (the grid is a bound)
     int fmode = 0;              // the float-C epilogue (VAR 256): dconst = float e_d, padding kFltPadE
+    // n = 4 / 16 (mfma_prep): the pool rows and −ΣD4² are built here from the source plane (pool_build's
+    // sums per tile row) and written beside the fragments, instead of a pool_build launch before; else read
+    const uint8_t* src = nullptr;
+    uint32_t sstride = 0;
+    const frac_grid_item* doms = nullptr;
+    const uint32_t* porig = nullptr;
+    uint32_t* pool_out = nullptr;
+    int32_t* negsd2_out = nullptr;
 };
+
+// D4 row k of pool position p (its domain's plane rows 2k and 2k + 1, 2·n columns) as n/2 words of two u16
+// pair sums (pool_build<n>); returns Σ of the row's squares
+template <int N>
+__device__ inline int build_pool_row(const MfmaDomainPrepArgs& a, const frac_grid_item& d, int k, uint32_t* w)
+{
+    const uint8_t* r0 = a.src + (size_t)(d.y + 2u * (uint32_t)k) * a.sstride + d.x;
+    const uint8_t* r1 = r0 + a.sstride;
+    int sq = 0;
+    if ((((uintptr_t)r0 | a.sstride) & 3u) == 0) {
+#pragma unroll
+        for (int q = 0; q < N / 2; ++q) {
+            const uint32_t v = pair_sums(reinterpret_cast<const uint32_t*>(r0)[q], reinterpret_cast<const uint32_t*>(r1)[q]);
+            const int lo = (int)(v & 0xffffu), hi = (int)(v >> 16);
+            sq += lo * lo + hi * hi;
+            w[q] = v;
+        }
+    } else {
+#pragma unroll
+        for (int q = 0; q < N / 2; ++q) {
+            const uint8_t* x = r0 + 4 * q;
+            const uint8_t* y = r1 + 4 * q;
+            const int lo = (int)x[0] + x[1] + y[0] + y[1], hi = (int)x[2] + x[3] + y[2] + y[3];
+            sq += lo * lo + hi * hi;
+            w[q] = (uint32_t)lo | ((uint32_t)hi << 16);
+        }
+    }
+    return sq;
+}
 
 // n = 16: 16 K-steps per row, one lane each (16-lane groups per tile row): the row's 128 pool words and
 // 32 fragment stores split 16 ways (one thread per row was a 128-load chain on 63 workgroups: 39 µs at
@@ -95,13 +132,21 @@ __device__ __forceinline__ void mfma_domain_prep16_at(MfmaDomainPrepArgs a, uint
         return;
     const uint32_t rg = gid / KS, s = gid % KS, tile = rg >> 5, row = rg & 31u;
     const int p = a.tile_pos[rg];
-    int sumd = 0;
+    int sumd = 0, sq = 0;
+    uint32_t bw[8]; // a.src: this lane's D4 row s, built from the plane (and written to the pool)
+    if (a.src && p >= 0) {
+        sq = build_pool_row<16>(a, a.doms[a.porig[p]], (int)s, bw);
+        uint4* pw = reinterpret_cast<uint4*>(a.pool_out + (size_t)p * (NN / 2) + 8 * s);
+        pw[0] = make_uint4(bw[0], bw[1], bw[2], bw[3]);
+        pw[1] = make_uint4(bw[4], bw[5], bw[6], bw[7]);
+    }
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
         _Float16 v8[8];
         uint4 w = make_uint4(0x01fe01feu, 0x01fe01feu, 0x01fe01feu, 0x01fe01feu); // padding rows: 510 (0)
         if (p >= 0)
-            w = *reinterpret_cast<const uint4*>(a.pool + (size_t)p * (NN / 2) + 8 * s + 4 * h);
+            w = a.src ? make_uint4(bw[4 * h], bw[4 * h + 1], bw[4 * h + 2], bw[4 * h + 3])
+                      : *reinterpret_cast<const uint4*>(a.pool + (size_t)p * (NN / 2) + 8 * s + 4 * h);
         const uint32_t ww[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
@@ -113,10 +158,14 @@ __device__ __forceinline__ void mfma_domain_prep16_at(MfmaDomainPrepArgs a, uint
         a.dtiles[((size_t)tile * KS + s) * 64 + row + 32 * h] = __builtin_bit_cast(uint4, v8);
     }
 #pragma unroll
-    for (int o = 8; o > 0; o >>= 1)
+    for (int o = 8; o > 0; o >>= 1) {
         sumd += __shfl_xor(sumd, o, 64);
+        sq += __shfl_xor(sq, o, 64);
+    }
     if (s == 0) {
-        const int sd2 = p >= 0 ? -a.negsd2[p] : 0;
+        if (a.src && p >= 0)
+            a.negsd2_out[p] = -sq;
+        const int sd2 = p >= 0 ? (a.src ? sq : -a.negsd2[p]) : 0;
         const uint32_t e = p >= 0 ? (uint32_t)(sd2 - 1024 * sumd) + (1u << 28) : kMfmaPadConst;
         const uint32_t hh = (row >> 2) & 1u, i = (row & 3u) + 4u * (row >> 3);
         a.dconst[(size_t)tile * 32 + hh * 16 + i] = e;
@@ -137,7 +186,19 @@ __device__ __forceinline__ void mfma_domain_prep_at(MfmaDomainPrepArgs a, uint32
     constexpr int K2 = NN / 2, K2R = (K2 + 3) / 4 * 4;
     uint32_t w[K2R];
     int sd2 = 0;
-    if (p >= 0) {
+    if (p >= 0 && a.src) { // the pool row from the plane, written to the pool (N ≥ 4: N rows of N/2 words)
+        if constexpr (N >= 4) {
+            const frac_grid_item d = a.doms[a.porig[p]];
+#pragma unroll
+            for (int k = 0; k < N; ++k)
+                sd2 += build_pool_row<N>(a, d, k, w + k * (N / 2));
+            uint32_t* pw = a.pool_out + (size_t)p * K2;
+#pragma unroll
+            for (int q = 0; q < K2; ++q)
+                pw[q] = w[q];
+            a.negsd2_out[p] = -sd2;
+        }
+    } else if (p >= 0) {
         if constexpr (K2 % 4 == 0) {
             const uint4* pr = reinterpret_cast<const uint4*>(a.pool + (size_t)p * K2);
 #pragma unroll
