@@ -186,8 +186,8 @@ __device__ __forceinline__ void mfma_domain_prep_at(MfmaDomainPrepArgs a, uint32
     constexpr int K2 = NN / 2, K2R = (K2 + 3) / 4 * 4;
     uint32_t w[K2R];
     int sd2 = 0;
-    if (p >= 0 && a.src) { // the pool row from the plane, written to the pool (N ≥ 4: N rows of N/2 words)
-        if constexpr (N >= 4) {
+    if (N >= 4 && p >= 0 && a.src) { // the pool row from the plane, written to the pool: N rows of N/2 words
+        if constexpr (N >= 4) { // (n = 2 rows are read from pool_build's pool: the host sets src for 4 and 16 only)
             const frac_grid_item d = a.doms[a.porig[p]];
 #pragma unroll
             for (int k = 0; k < N; ++k)
