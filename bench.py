@@ -243,7 +243,10 @@ class FrameStep:
     not uploaded and the gathered tuples stay on the device (the device-only leg).
     `stripes` (default: with more than one rank): each rank uploads only its 1/N stripe of the frame's
     rows across its own PCIe link and one all-gather assembles the frame on every rank over xGMI,
-    instead of N full 16.8 MB uploads; the frame the engine gets is the same plane."""
+    instead of N full 16.8 MB uploads; the frame the engine gets is the same plane.
+    On the GPU the run writes its tuples itself (frac_set_tuple_sink): without a process group straight
+    into the pinned output (they cross PCIe while the resolve writes them: no pack kernel and no D2H
+    copy after it), with one into the all-gather buffer."""
 
     def __init__(self, eng, frame, plan, rank: int, dev, device_resident: bool = False, stripes=None):
         import torch
@@ -258,6 +261,7 @@ class FrameStep:
             frame = frame.numpy()
         self.eng, self.frame, self.plan, self.rank, self.dev = eng, frame, plan, rank, dev
         self.device_resident = device_resident
+        self.sink = hasattr(eng, "set_tuple_sink") and dev.type == "cuda"
         a, b = plan[rank]
         self.n_mine = b - a
         cap = max((q - p for p, q in plan), default=0)
@@ -275,9 +279,19 @@ class FrameStep:
             self.eng.set_frame(full if full.is_cuda else full.numpy())
         elif not self.device_resident:
             self.eng.set_frame(self.frame)  # H2D (returns once the plane is on the device)
+        import torch.distributed as dist
+
+        direct = self.sink and not self.device_resident and not dist.is_initialized() and self.n_mine > 0
+        if self.sink and self.n_mine:  # the run writes the tuples: into the pinned output, or the gather buffer
+            self.eng.set_tuple_sink(self.h_out.data_ptr() if direct else self.local.data_ptr())
         self.eng.run()
+        if self.sink and self.n_mine:
+            self.eng.set_tuple_sink(None)
+        if direct:  # one rank, no group: the tuples are already on their way into h_out
+            self.gathered = None
+            return
         if self.local.is_cuda:  # packed on the device, on the engine's (= torch's current) stream
-            if self.n_mine:
+            if self.n_mine and not self.sink:
                 self.eng.copy_tuples_device(self.local.data_ptr())
         elif self.n_mine:  # CPU backend: the engine hands back host tuples
             t = np.ascontiguousarray(self.eng.fetch_tuples())

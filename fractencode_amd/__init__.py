@@ -186,6 +186,7 @@ def lib() -> C.CDLL:
             "frac_device_results": (vp, [vp]),
             "frac_copy_results_device": (i32, [vp, vp]),
             "frac_copy_tuples_device": (i32, [vp, vp]),
+            "frac_set_tuple_sink": (i32, [vp, vp]),
             "frac_pack_frc1": (i32, [vp, u32, u32, vp, sz, C.POINTER(C.c_size_t)]),
             "frac_fetch_tuples": (i32, [vp, vp]),
             "frac_decode": (i32, [vp, vp, sz, u32, u32, i32, C.c_double, vp, C.POINTER(C.c_int),
@@ -400,6 +401,11 @@ class Engine:
     def copy_tuples_device(self, dst_ptr: int) -> None:
         """Async pack of the last run's 32-byte (domain, transform, s, o, rms) tuples into a device buffer."""
         self._check(lib().frac_copy_tuples_device(self._ctx, C.c_void_p(dst_ptr)))
+
+    def set_tuple_sink(self, dst_ptr: int | None) -> None:
+        """Every later run also writes its 32-byte tuples to dst_ptr (device memory, or pinned host memory
+        the device can write: they then cross PCIe while the resolve writes them); None clears it (ABI 8)."""
+        self._check(lib().frac_set_tuple_sink(self._ctx, C.c_void_p(dst_ptr) if dst_ptr else None))
 
     def pack_frc1(self, contrast_bits: int = 5, brightness_bits: int = 7) -> bytes:
         """The last run's results as an FRC1 stream (codec.py layout), quantized and packed on the

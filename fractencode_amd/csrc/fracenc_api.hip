@@ -248,6 +248,7 @@ struct frac_ctx {
     DBuf<SeaEntry> d_sea_ent;
     DBuf<int32_t> d_sea_snegsd2;
     DBuf<frac_tuple> d_tuples; // frac_fetch_tuples staging
+    frac_tuple* tuple_sink = nullptr; // frac_set_tuple_sink: every frac_run's tuples also go here
     // SEA engine, tiled form (fracenc_tp.hip)
     bool tp = false;
     TpBuckets tp_bk{};
@@ -1359,6 +1360,7 @@ inline FallbackArgs fallback_args(frac_ctx* c, const uint8_t* dtgt, uint32_t tst
     b.smax = c->p.s_max;
     b.out = c->d_out.ptr;
     b.aux = c->d_aux.ptr;
+    b.tuples = c->fit_fused && !c->qplan ? c->tuple_sink : nullptr; // the fused resolvers' sink, if any
     b.fb_key = c->d_fb_key.ptr;
     b.fb_done = c->d_fb_done.ptr;
     // jobs per listed range: the largest bucket's domains in chunks of kFbChunk (a planned level: every domain)
@@ -1745,6 +1747,7 @@ inline int launch_dft(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool i
         v.rstat = c->d_rstat.ptr;
         v.fused_fit = 1; // the fit in the resolving wave (launch_all skips fit_rstat)
         v.fit = fit_args(c, dtgt, tstride, nr);
+        v.fit.tuples = c->qplan ? nullptr : c->tuple_sink;
         c->fit_fused = true;
         // one-wave workgroups: a finished range frees its slot at once (0.254 vs 0.271 ms finish
         // against 4-wave workgroups, 30-sample A/B, profiles/r01/ab_fourier_variants.log); T = 8: two
@@ -1902,6 +1905,7 @@ int launch_mfma(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool inits =
         if (!c->virt) { // the fit in the resolving wave (the sampled form fits at its own points: gen_fit)
             v.fused_fit = 1;
             v.fit = fit_args(c, dtgt, tstride, nr);
+            v.fit.tuples = c->qplan ? nullptr : c->tuple_sink;
             c->fit_fused = true;
         }
         v.plan = c->qplan;
@@ -2086,6 +2090,7 @@ int launch_tp(frac_ctx* c, const uint8_t* dtgt, uint32_t tstride, bool timing)
     v.rstat = c->d_rstat.ptr;
     v.fused_fit = 1;
     v.fit = fit_args(c, dtgt, tstride, nr);
+    v.fit.tuples = c->qplan ? nullptr : c->tuple_sink;
     c->fit_fused = true;
     // resolve_dft<true> (SORTED) keeps every tie of the ΣD4-ordered chunks but does not merge T = 8's
     // flipped copies (that is the !SORTED path): the tiled form exists for T = 4 only (prepare)
@@ -3103,9 +3108,25 @@ int frac_run(frac_ctx* c)
     case 16: rc = launch_all<16>(c); break;
     default: rc = launch_all<8>(c); break;
     }
+    const uint32_t nr = (uint32_t)nranges(c);
+    if (rc == FRAC_OK && c->tuple_sink && nr) {
+        if (c->fit_fused) // the resolvers wrote the tuples; the fp32-regime ranges' come with their records
+            rc = settle_fallback(c);
+        else // records by a separate fit: packed from them
+            pack_tuples<<<(nr + 255) / 256, 256, 0, c->stream>>>(c->d_out.ptr, c->d_aux.ptr, c->d_porig.ptr, nr,
+                                                                 c->tuple_sink);
+    }
     if (rc == FRAC_OK)
         c->ran = true;
     return rc;
+}
+
+int frac_set_tuple_sink(frac_ctx* c, void* dst)
+{
+    if (!c)
+        return FRAC_E_INVALID;
+    c->tuple_sink = static_cast<frac_tuple*>(dst);
+    return FRAC_OK;
 }
 
 int frac_sync(frac_ctx* c)
@@ -3302,6 +3323,13 @@ static int encode_quadtree_impl(frac_ctx* c, const frac_quadtree_params* qp, fra
 {
     if (!c)
         return FRAC_E_INVALID;
+    // the levels' runs write no tuples into a frac_run sink (it is sized for the context's own ranges)
+    struct SinkAside {
+        frac_ctx* c;
+        frac_tuple* saved;
+        ~SinkAside() { c->tuple_sink = saved; }
+    } aside{c, c->tuple_sink};
+    c->tuple_sink = nullptr;
     if (!qp || !n_out)
         return c->fail(FRAC_E_INVALID, "quadtree: params and n_out are required");
     auto valid = [](uint32_t v) { return v == 2 || v == 4 || v == 8 || v == 16; };

@@ -292,11 +292,15 @@ struct FitArgs {
     uint32_t* fb_count;
     uint32_t* fb_list;
     const DevPlan* plan = nullptr; // device-planned search: nr from the plan (the grid is a bound)
+    // frac_set_tuple_sink: the fused resolvers (and fallback_grid) also write each range's 32-byte tuple here —
+    // device memory or the caller's pinned host buffer, so the tuples cross PCIe while the resolve runs
+    frac_tuple* tuples = nullptr;
 };
 
+// tp (a tuple sink): the same record as the (domain index, transform, s, o, rms) tuple
 __device__ inline void write_fit(frac_encode_item& o, const frac_grid_item& rg, const frac_grid_item& d, int t,
                                  double sumA, double sumA2, double sumB, double sumAB, double N, double smax,
-                                 double dist)
+                                 double dist, frac_tuple* tp = nullptr, uint32_t dom = 0)
 {
     const double tmp = (N * sumA2 - (sumA - 1) * sumA);
     double s = fabs(tmp) < 0.00001 ? 0.0 : (N * sumAB - sumA * sumB) / tmp;
@@ -316,9 +320,18 @@ __device__ inline void write_fit(frac_encode_item& o, const frac_grid_item& rg, 
     o.match.y = d.y;
     o.match.sw = d.w;
     o.match.sh = d.h;
+    if (tp) {
+        frac_tuple u;
+        u.domain = dom;
+        u.transform = t;
+        u.contrast = s;
+        u.brightness = br;
+        u.distance = dist;
+        *tp = u;
+    }
 }
 
-__device__ inline void write_default(frac_encode_item& o, const frac_grid_item& rg)
+__device__ inline void write_default(frac_encode_item& o, const frac_grid_item& rg, frac_tuple* tp = nullptr)
 {
     // item_match_t{} defaults (encode/datatypes.h:8-19): distance 1e5, s = o = 0, Id, (0,0), size (0,0)
     o.x = rg.x;
@@ -334,6 +347,15 @@ __device__ inline void write_default(frac_encode_item& o, const frac_grid_item& 
     o.match.y = 0;
     o.match.sw = 0;
     o.match.sh = 0;
+    if (tp) {
+        frac_tuple u;
+        u.domain = FRAC_NO_DOMAIN;
+        u.transform = 0;
+        u.contrast = 0.0;
+        u.brightness = 0.0;
+        u.distance = 100000.0;
+        *tp = u;
+    }
 }
 
 // lane groups of L: ranges per wave = 64 / L, 4 pixels per lane (n = 2: one lane per range)
@@ -457,8 +479,9 @@ __device__ inline void fit_sums_range(const FitArgs& a, uint32_t r, unsigned lon
 {
     constexpr int NN = N * N;
     const frac_grid_item rg = a.ranges[r];
+    frac_tuple* tp = a.tuples ? a.tuples + r : nullptr;
     if (key == kKeyNone) {
-        write_default(a.out[r], rg);
+        write_default(a.out[r], rg, tp);
         a.aux[r] = RangeAux{0u, (uint32_t)kAuxEmpty};
         return;
     }
@@ -472,11 +495,12 @@ __device__ inline void fit_sums_range(const FitArgs& a, uint32_t r, unsigned lon
         a.fb_list[atomicAdd(a.fb_count, 1u)] = r;
         return;
     }
-    const frac_grid_item d = a.doms[a.porig[p]];
+    const uint32_t dom = a.porig[p];
+    const frac_grid_item d = a.doms[dom];
     const long long S16 = 16 * sA2 - 8 * X + sD2;
     const double dist = ((double)S16 * 0.0625) / (double)(d.w * d.h);
     write_fit(a.out[r], rg, d, t, (double)sA, (double)sA2, (double)sD * 0.25, (double)X * 0.25, (double)NN, a.smax,
-              dist);
+              dist, tp, dom);
     a.aux[r] = RangeAux{p, hit ? (uint32_t)kAuxHit : 0u};
 }
 
@@ -488,8 +512,9 @@ __device__ inline void fit_rstat_range(const FitArgs& a, uint32_t r, unsigned lo
 {
     constexpr int NN = N * N;
     const frac_grid_item rg = rgp ? *rgp : a.ranges[r];
+    frac_tuple* tp = a.tuples ? a.tuples + r : nullptr;
     if (key == kKeyNone) {
-        write_default(a.out[r], rg);
+        write_default(a.out[r], rg, tp);
         a.aux[r] = RangeAux{0u, (uint32_t)kAuxEmpty};
         return;
     }
@@ -502,12 +527,13 @@ __device__ inline void fit_rstat_range(const FitArgs& a, uint32_t r, unsigned lo
         a.fb_list[atomicAdd(a.fb_count, 1u)] = r;
         return;
     }
-    const frac_grid_item d = dp ? *dp : a.doms[a.porig[p]];
+    const uint32_t dom = (!dp || tp) ? a.porig[p] : 0u; // the domain index (a tuple's, or to load the item)
+    const frac_grid_item d = dp ? *dp : a.doms[dom];
     const long long X = st.x, sD = st.y & 0xffffu, sA = st.y >> 16, sD2 = st.z, sA2 = st.w;
     const long long S16 = 16 * sA2 - 8 * X + sD2;
     const double dist = ((double)S16 * 0.0625) / (double)(d.w * d.h);
     write_fit(a.out[r], rg, d, t, (double)sA, (double)sA2, (double)sD * 0.25, (double)X * 0.25, (double)NN, a.smax,
-              dist);
+              dist, tp, dom);
     a.aux[r] = RangeAux{p, hit ? (uint32_t)kAuxHit : 0u};
 }
 
@@ -558,6 +584,7 @@ struct FallbackArgs {
     double smax;
     frac_encode_item* out;
     RangeAux* aux;
+    frac_tuple* tuples = nullptr; // the run's tuple sink when its resolvers write one (FitArgs::tuples)
     // fallback_grid: per listed range the least key so far and its jobs done (kKeyNone / 0 between runs), and
     // the jobs per range (the domain chunks of the largest bucket)
     unsigned long long* fb_key = nullptr;
@@ -597,11 +624,12 @@ template <int N>
 __device__ inline void fallback_record(const uint32_t* __restrict__ pool, const frac_grid_item* doms,
                                        const uint32_t* porig, uint32_t T, double smax, frac_encode_item* out,
                                        RangeAux* aux, uint32_t r, const frac_grid_item& rg, const uint2& bk,
-                                       unsigned long long k, const float* rpix)
+                                       unsigned long long k, const float* rpix, frac_tuple* tuples = nullptr)
 {
     constexpr int NN = N * N;
+    frac_tuple* tp = tuples ? tuples + r : nullptr;
     if (k == kKeyNone) {
-        write_default(out[r], rg);
+        write_default(out[r], rg, tp);
         aux[r] = RangeAux{0u, (uint32_t)kAuxEmpty};
         return;
     }
@@ -609,7 +637,8 @@ __device__ inline void fallback_record(const uint32_t* __restrict__ pool, const 
     const uint32_t pl = (uint32_t)((k >> 3) & 0xffffffu);
     const int t = hit ? (int)(k & 7u) : (int)(T - 1 - (uint32_t)(k & 7u));
     const uint32_t p = bk.x + pl;
-    const frac_grid_item d = doms[porig[p]];
+    const uint32_t dom = porig[p];
+    const frac_grid_item d = doms[dom];
     const uint32_t* dp = pool + (size_t)p * (NN / 2);
     long long sA = 0, sA2 = 0, sD = 0, X = 0;
     float Fh = 0.0f;
@@ -629,7 +658,7 @@ __device__ inline void fallback_record(const uint32_t* __restrict__ pool, const 
     }
     const double dist = (double)Fh / (double)(d.w * d.h);
     write_fit(out[r], rg, d, t, (double)sA, (double)sA2, (double)sD * 0.25, (double)X * 0.25, (double)NN, smax,
-              dist);
+              dist, tp, dom);
     aux[r] = RangeAux{p, (uint32_t)(kAuxFallback | (hit ? kAuxHit : 0u))};
 }
 
@@ -758,7 +787,7 @@ __global__ void __launch_bounds__(256) fallback_grid(FallbackArgs a)
         __syncthreads();
         if (last && threadIdx.x == 0) {
             const unsigned long long k = atomicMin(a.fb_key + e, kKeyNone); // the final key (kKeyNone changes nothing)
-            fallback_record<N>(a.pool, a.doms, a.porig, a.T, a.smax, a.out, a.aux, r, rg, bk, k, rpix);
+            fallback_record<N>(a.pool, a.doms, a.porig, a.T, a.smax, a.out, a.aux, r, rg, bk, k, rpix, a.tuples);
             a.fb_key[e] = kKeyNone; // clean for the next run's list
             a.fb_done[e] = 0u;
         }

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define FRAC_ABI_VERSION 7
+#define FRAC_ABI_VERSION 8
 
 /* error codes */
 #define FRAC_OK 0
@@ -204,6 +204,11 @@ typedef struct frac_tuple {
 int frac_copy_tuples_device(frac_ctx* ctx, void* d_dst);
 /* Synchronous: the last run's nr tuples into host memory. */
 int frac_fetch_tuples(frac_ctx* ctx, frac_tuple* out);
+/* ABI 8: every later frac_run also writes its nr tuples into dst (32·nr bytes; device memory, or pinned host
+ * memory the device can write — then they cross PCIe while the run's resolve kernels write them, with no
+ * separate pack or copy), ordered on the context's stream: complete once that stream's work is.  The records
+ * (frac_fetch, …) are unchanged.  NULL clears it.  The quadtree entry points ignore it. */
+int frac_set_tuple_sink(frac_ctx* ctx, void* dst);
 
 /* Decoder2::decode (encode/Encoder2.hpp:67-99) on the device.  `plane` (w×h, row
  * stride w) holds the decoder's initial target (main.cpp:171-173 zero-fills it) and

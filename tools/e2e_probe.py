@@ -7,6 +7,7 @@ legs separate why the search runs slower in the end-to-end step: the device-resi
 Leg e2e_zc packs the tuples straight into the pinned host buffer (the pack kernel's stores cross PCIe) instead
 of packing on the device and copying.  Run it with HSA_ENABLE_SDMA=0 to see the copies done by blit kernels.
 Legs idle_<µs>: the device-resident step after that many µs of GPU idle (how the slowdown grows with the idle).
+Leg e2e_nosink: the end-to-end step without the tuple sink (pack + D2H after the run).
 usage: tools/e2e_probe.py [steps] [rounds] [legs,...]"""
 import json
 import os
@@ -61,8 +62,10 @@ with F.Engine(0, 4, False, 0.0, -1.0, F.ENGINE_AUTO, timing=True) as e:
         e.run()
         e.copy_tuples_device(zstep.h_out.data_ptr())
 
+    nosink = bench.FrameStep(e, h_frame.numpy(), plan, 0, dev)
+    nosink.sink = False  # the pack kernel and the D2H copy after the run (the step before frac_set_tuple_sink)
     legs = {"e2e": bench.FrameStep(e, h_frame.numpy(), plan, 0, dev), "device": dstep, "device_idle": idle_step,
-            "device_d2d": d2d_step, "e2e_zc": zc_step}
+            "device_d2d": d2d_step, "e2e_zc": zc_step, "e2e_nosink": nosink}
     for us in (50, 100, 200, 500, 1000, 2000):  # idle_<µs>: the device-resident step after that much GPU idle
         legs[f"idle_{us}"] = (lambda sec: (lambda: (torch.cuda.synchronize(dev), time.sleep(sec), dstep())))(us * 1e-6)
     if only:
