@@ -78,6 +78,9 @@ def parse(argv=None):
                     help="steps of the VALU engine (north_star's no-MFMA formulation) reported beside (0 = skip)")
     ap.add_argument("--side-steps", type=int, default=-1,
                     help="steps of the device-resident and stream legs (-1 = --steps, 0 = skip)")
+    ap.add_argument("--tuples", default="node", choices=["node", "gather"],
+                    help="N > 1 on one host: the ranks' tuples into one shared host buffer (node), or the "
+                         "all-gather + every rank's download (gather; always with ranks on several hosts)")
     ap.add_argument("--ab", action="store_true",
                     help="allow FRAC_LIB / A/B knobs in the environment (the line is then marked, not a headline)")
     return ap.parse_args(argv)
@@ -246,12 +249,18 @@ class FrameStep:
     instead of N full 16.8 MB uploads; the frame the engine gets is the same plane.
     On the GPU the run writes its tuples itself (frac_set_tuple_sink): without a process group straight
     into the pinned output (they cross PCIe while the resolve writes them: no pack kernel and no D2H
-    copy after it), with one into the all-gather buffer."""
+    copy after it), with one into the all-gather buffer.
+    `node_tuples` (a distributed.NodeTuples; bench.py passes one when every rank is on one host): every rank's
+    run writes its shard's tuples into the node's one shared host buffer (each PCIe link carries only its own
+    shard's tuples, no tuple all-gather, no download of every rank's tuples by every rank), then one
+    completion token per frame."""
 
-    def __init__(self, eng, frame, plan, rank: int, dev, device_resident: bool = False, stripes=None):
+    def __init__(self, eng, frame, plan, rank: int, dev, device_resident: bool = False, stripes=None,
+                 node_tuples=None):
         import torch
 
         world = len(plan)
+        self.node = None if device_resident else node_tuples
         self.stripes = (world > 1 and not device_resident) if stripes is None else bool(stripes)
         if self.stripes:
             from fractencode_amd.distributed import FrameStripes
@@ -268,6 +277,12 @@ class FrameStep:
         self.local = torch.zeros(cap * TUPLE_BYTES, dtype=torch.uint8, device=dev)
         self.h_out = torch.empty(plan[-1][1] * TUPLE_BYTES, dtype=torch.uint8, pin_memory=dev.type == "cuda")
         self.gathered = None
+        if self.node is not None:
+            import torch.distributed as dist
+
+            self.h_out = self.node.host
+            self.nccl = dist.get_backend() == "nccl"
+            self.token = torch.zeros(1, dtype=torch.int32, device=dev if self.nccl else "cpu")
 
     def __call__(self) -> None:
         import torch
@@ -281,6 +296,9 @@ class FrameStep:
             self.eng.set_frame(self.frame)  # H2D (returns once the plane is on the device)
         import torch.distributed as dist
 
+        if self.node is not None:
+            self._node_step()
+            return
         direct = self.sink and not self.device_resident and not dist.is_initialized() and self.n_mine > 0
         if self.sink and self.n_mine:  # the run writes the tuples: into the pinned output, or the gather buffer
             self.eng.set_tuple_sink(self.h_out.data_ptr() if direct else self.local.data_ptr())
@@ -299,6 +317,27 @@ class FrameStep:
         self.gathered = gather_tuples(self.local, self.plan)
         if not self.device_resident:
             self.h_out.copy_(self.gathered, non_blocking=True)  # D2H into pinned memory
+
+    def _node_step(self) -> None:
+        """The run writes its shard's tuples into the node's shared host buffer (NodeTuples): on the GPU
+        through the tuple sink, else copied in from the engine's host tuples; then one completion token
+        per frame — a 4-byte RCCL all-reduce on the stream after the run (nccl), or a synchronisation and
+        a barrier (gloo)."""
+        import torch.distributed as dist
+
+        if self.n_mine and self.sink:
+            self.eng.set_tuple_sink(self.node.sink_ptr())
+            self.eng.run()
+            self.eng.set_tuple_sink(None)
+        else:
+            self.eng.run()
+            if self.n_mine:
+                self.node.put(np.ascontiguousarray(self.eng.fetch_tuples()).tobytes())
+        if self.nccl:
+            dist.all_reduce(self.token)
+        else:
+            _sync(self.dev)
+            dist.barrier()
 
     def tuples_bytes(self) -> bytes:
         """The last step's gathered tuples (after a synchronisation)."""
@@ -348,6 +387,7 @@ def main(args):
         dist.all_gather_object(where, (socket.gethostname(), local, torch.cuda.get_device_name(local)))
         if len({(h, d) for h, d, _ in where}) != world:
             raise SystemExit(f"bench.py: ranks share a GPU: {where}")
+        one_host = len({h for h, _, _ in where}) == 1
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", local if world > 1 else 0)
@@ -375,7 +415,12 @@ def main(args):
     eng.set_ranges(mine)
 
     # ---- headline: the end-to-end step ----
-    step = FrameStep(eng, h_frame, plan, rank, dev)
+    node = None
+    if world > 1 and one_host and args.tuples == "node":
+        from fractencode_amd.distributed import NodeTuples
+
+        node = NodeTuples(plan, rank, dev)
+    step = FrameStep(eng, h_frame, plan, rank, dev, node_tuples=node)
     for _ in range(args.warmup):
         step()
     _sync(dev)
@@ -428,11 +473,15 @@ def main(args):
                                f"16x16 domains stride 8 ({n_d}), T={args.transforms}, exhaustive, rms 0",
                    "engine": engine_name, "ranges_per_gpu": len(mine), "parallelism": f"ranges/{world}",
                    "env": frac_env(), "ab_run": bool(knobs)},
-        "step": ("frame H2D (pinned, 16 MiB) + " if world == 1 else
-                 "frame H2D of the rank's 1/N stripe of rows (pinned) + RCCL all-gather of the frame + ") +
-                "pool build + search + fit of the rank's shard + 32-byte "
-                "tuples packed on the device + all-gather over ranks (N > 1) + gathered tuples D2H (pinned); "
-                "serial, barrier + synchronisation around the timed steps, slowest rank",
+        "step": ("frame H2D (pinned, 16 MiB) + pool build + search + fit + 32-byte tuples written by the resolve "
+                 "into pinned host memory" if world == 1 else
+                 "frame H2D of the rank's 1/N stripe of rows (pinned) + RCCL all-gather of the frame + pool build "
+                 "+ search + fit of the rank's shard + " +
+                 ("its 32-byte tuples written by the resolve into the node's shared pinned tuple buffer + a "
+                  "4-byte RCCL all-reduce per frame" if node is not None else
+                  "32-byte tuples into the all-gather buffer + RCCL all-gather + gathered tuples D2H (pinned)")) +
+                "; serial, barrier + synchronisation around the timed steps, slowest rank",
+        "tuples_out": "node" if node is not None else ("gather" if world > 1 else "sink"),
         "roofline": roof,
         "search_form": form,
         "phases_ms": {k: round(float(np.mean(hist["ms_" + k])), 3) for k in ("device", "prep", "search", "finish")},
@@ -525,6 +574,9 @@ def main(args):
         threads, host = host_cores()
         line["cpu_baseline"] = cpu_baseline(frame, args.cpu_budget, args.cpu_threads or threads, host)
     eng.close()
+    if node is not None:
+        del step
+        node.close()
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:

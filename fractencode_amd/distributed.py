@@ -119,6 +119,105 @@ class FrameStripes:
         return self.full[: self.H]
 
 
+def _hip_runtime():
+    """The process's HIP runtime (the one PyTorch loaded: dlopen by soname returns it)."""
+    import ctypes as C
+
+    import torch  # noqa: F401  (loads the runtime first)
+
+    L = C.CDLL("libamdhip64.so.7")
+    L.hipHostRegister.restype = C.c_int
+    L.hipHostRegister.argtypes = [C.c_void_p, C.c_size_t, C.c_uint]
+    L.hipHostUnregister.restype = C.c_int
+    L.hipHostUnregister.argtypes = [C.c_void_p]
+    L.hipHostGetDevicePointer.restype = C.c_int
+    L.hipHostGetDevicePointer.argtypes = [C.POINTER(C.c_void_p), C.c_void_p, C.c_uint]
+    return L
+
+
+class NodeTuples:
+    """One host buffer of every range's 32-byte tuple, shared by all ranks of one node: rank 0 creates a
+    file in /dev/shm, every rank maps it (MAP_SHARED) and, on a GPU, registers the mapping with HIP, so a
+    rank's resolve writes its shard's tuples (frac_set_tuple_sink at `sink_ptr()`) straight into the one
+    output every rank sees — no tuple all-gather and no N full downloads, each PCIe link carries only its
+    own shard's tuples.  The file is unlinked once every rank holds its mapping (nothing is left behind
+    however the job ends).  Only for ranks that share one host (the caller checks); with ranks on several
+    hosts the all-gather path (gather_tuples) stays."""
+
+    def __init__(self, plan: list[tuple[int, int]], rank: int, device, group=None):
+        import mmap
+        import os
+        import secrets
+
+        import torch
+        import torch.distributed as dist
+
+        self.plan, self.rank, self.device = plan, rank, device
+        self.n = plan[-1][1] if plan else 0
+        self.bytes = max(1, self.n * TUPLE_BYTES)
+        size = -(-self.bytes // mmap.PAGESIZE) * mmap.PAGESIZE
+        name = [f"/dev/shm/fracenc_tuples_{os.getpid()}_{secrets.token_hex(6)}" if rank == 0 else None]
+        if rank == 0:
+            fd = os.open(name[0], os.O_CREAT | os.O_EXCL | os.O_RDWR, 0o600)
+            os.ftruncate(fd, size)
+            os.close(fd)
+        dist.broadcast_object_list(name, src=0, group=group)
+        try:
+            fd = os.open(name[0], os.O_RDWR)
+            try:
+                self._mm = mmap.mmap(fd, size, mmap.MAP_SHARED, mmap.PROT_READ | mmap.PROT_WRITE)
+            finally:
+                os.close(fd)
+        finally:
+            dist.barrier(group=group)  # every rank mapped (or failed) before the name goes
+            if rank == 0:
+                os.unlink(name[0])
+        self.host = torch.frombuffer(self._mm, dtype=torch.uint8)[: self.n * TUPLE_BYTES]
+        self._addr = self.host.data_ptr()
+        self._size = size
+        self._dptr = None
+        if device.type == "cuda":
+            import ctypes as C
+
+            hip = _hip_runtime()
+            err = hip.hipHostRegister(self._addr, size, 0x1 | 0x2)  # portable | mapped
+            if err:
+                raise RuntimeError(f"hipHostRegister of the node tuple buffer failed ({err})")
+            p = C.c_void_p()
+            err = hip.hipHostGetDevicePointer(C.byref(p), self._addr, 0)
+            if err:
+                hip.hipHostUnregister(self._addr)
+                raise RuntimeError(f"hipHostGetDevicePointer failed ({err})")
+            self._hip, self._dptr = hip, p.value
+
+    def sink_ptr(self) -> int:
+        """The device address of this rank's shard within the buffer (the tuple sink)."""
+        assert self._dptr is not None, "a GPU rank's buffer"
+        return self._dptr + self.plan[self.rank][0] * TUPLE_BYTES
+
+    def put(self, tuples: bytes) -> None:
+        """This rank's shard's tuples written by the host (an engine that hands back host tuples)."""
+        a, b = self.plan[self.rank]
+        assert len(tuples) == (b - a) * TUPLE_BYTES
+        self.host[a * TUPLE_BYTES: b * TUPLE_BYTES] = torch_bytes(tuples)
+
+    def close(self) -> None:
+        if self._dptr is not None:
+            self._hip.hipHostUnregister(self._addr)
+            self._dptr = None
+        self.host = None
+        try:
+            self._mm.close()
+        except BufferError:  # a caller still holds a view: the mapping goes with the process
+            pass
+
+
+def torch_bytes(b: bytes):
+    import torch
+
+    return torch.frombuffer(bytearray(b), dtype=torch.uint8) if b else torch.empty(0, dtype=torch.uint8)
+
+
 def tuples_from_bytes(buf) -> np.ndarray:
     from . import TUPLE
 

@@ -2,8 +2,9 @@
 tests/test_bench_ranks.py through bench.launch_ranks → torch.distributed.run, or run directly for
 world size 1): the oracle stand-in engine behind bench.FrameStep, `gloo` in place of RCCL, the
 same timed() bracket and headline_fields() as the GPU headline (the frame in row stripes assembled by
-the all-gather when N > 1).  Rank 0 writes the line, every rank's own time and the gathered tuples to OUT.
-usage: python tests/bench_rank_cpu.py OUT STEPS [FAIL_RANK]"""
+the all-gather when N > 1; the tuples into the node's shared buffer, or with BENCH_TUPLES=gather the
+all-gather).  Rank 0 writes the line, every rank's own time and the gathered tuples to OUT.
+usage: [BENCH_TUPLES=node|gather] python tests/bench_rank_cpu.py OUT STEPS [FAIL_RANK]"""
 import json
 import os
 import sys
@@ -38,7 +39,12 @@ a, b = plan[rank]
 eng = OracleEngine(np.zeros_like(plane), doms)
 eng.set_ranges(rngs[a:b])
 dev = torch.device("cpu")
-step = bench.FrameStep(eng, plane, plan, rank, dev)
+node = None
+if world > 1 and os.environ.get("BENCH_TUPLES", "node") == "node":
+    from fractencode_amd.distributed import NodeTuples
+
+    node = NodeTuples(plan, rank, dev)
+step = bench.FrameStep(eng, plane, plan, rank, dev, node_tuples=node)
 step()  # warmup
 mine, mx = bench.timed(step, steps, world, dev)
 line = bench.headline_fields(len(rngs), world, steps, 1, mx)
@@ -51,7 +57,10 @@ else:
 if rank == 0:
     gathered = step.tuples_bytes()
     json.dump({"line": line, "ranks": every, "digest": bench.digest(gathered), "tuples": gathered.hex(),
-               "stripes": step.stripes}, open(out, "w"))
+               "stripes": step.stripes, "node": node is not None}, open(out, "w"))
 if world > 1:
     dist.barrier()
+    if node is not None:
+        del step
+        node.close()
     dist.destroy_process_group()

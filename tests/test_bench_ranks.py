@@ -1,6 +1,6 @@
 """bench.py's N > 1 orchestration, executed on the CPU: bench.launch_ranks
 starts `gloo` ranks under torch.distributed.run; each runs bench.FrameStep (frame upload, search of
-its shard, tuples into the all-gather buffer, all-gather, gathered tuples out) with the oracle
+its shard, tuples into the node's shared buffer or the all-gather buffer + all-gather, tuples out) with the oracle
 stand-in engine, the same timed() bracket and headline_fields() the GPU headline uses.  No scaling
 curve is measured here: only the orchestration's correctness (records, MAX over ranks, exit
 status).  Reference parallelism being replaced: EncodingEngineCore2's thread pool over range items
@@ -18,12 +18,12 @@ SCRIPT = os.path.join(HERE, "bench_rank_cpu.py")
 STEPS = 2
 
 
-def _run(tmp_path, world, fail_rank=None):
+def _run(tmp_path, world, fail_rank=None, tuples="node"):
     import bench
 
     out = str(tmp_path / f"line_{world}.json")
     argv = [out, str(STEPS)] + ([] if fail_rank is None else [str(fail_rank)])
-    env = dict(os.environ, OMP_NUM_THREADS="1")
+    env = dict(os.environ, OMP_NUM_THREADS="1", BENCH_TUPLES=tuples)
     if world == 1:  # a single rank without a process group, as bench.py runs at N = 1
         rc = subprocess.call([sys.executable, SCRIPT, *argv], env=env)
     else:
@@ -38,19 +38,28 @@ def single(tmp_path_factory):
     return json.load(open(out))
 
 
-@pytest.mark.parametrize("world", [2, 3, 4, 8])
-def test_bench_orchestration_on_gloo_ranks(tmp_path, single, oracle, world):
+def _node_files():
+    return {f for f in os.listdir("/dev/shm") if f.startswith("fracenc_tuples_")}
+
+
+@pytest.mark.parametrize("world,tuples", [(2, "node"), (3, "node"), (4, "node"), (8, "node"), (3, "gather"),
+                                          (8, "gather")])
+def test_bench_orchestration_on_gloo_ranks(tmp_path, single, oracle, world, tuples):
     import bench
     import fractencode_amd as F
     from fractencode_amd.distributed import records_from_tuples
 
-    rc, out = _run(tmp_path, world)
+    before = _node_files()
+    rc, out = _run(tmp_path, world, tuples=tuples)
     assert rc == 0
+    assert _node_files() == before  # the shared tuple buffer's file is gone once every rank mapped it
     d = json.load(open(out))
     line = d["line"]
     # the gathered records equal the single-rank run's, byte for byte, and the reference's (oracle); the
-    # frame reached every rank as row stripes and one all-gather (64 rows: uneven stripes at world 3)
+    # frame reached every rank as row stripes and one all-gather (64 rows: uneven stripes at world 3); the
+    # tuples met in the node's shared host buffer, or through the all-gather
     assert d["stripes"] and not single["stripes"]
+    assert d["node"] == (tuples == "node") and not single["node"]
     assert d["digest"] == single["digest"] and d["tuples"] == single["tuples"]
     tuples = np.frombuffer(bytes.fromhex(d["tuples"]), dtype=F.TUPLE)
     assert len(tuples) == 93

@@ -284,6 +284,76 @@ def test_nccl_frame_stripes_world1_match_reference(tmp_path):
         np.testing.assert_array_equal(got[k], rec[k], err_msg=k)
 
 
+def _node_worker(rank, world, port, path, backend):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import torch
+    import torch.distributed as dist
+
+    import bench
+    import fractencode_amd as F
+    from fractencode_amd.distributed import NodeTuples, records_from_tuples, shard_plan
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)  # one-GPU box: with gloo every rank's engine is on GPU 0
+    if backend == "nccl":
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    else:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    y = np.fromfile(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "lenna_y.u8"),
+                    dtype=np.uint8).reshape(512, 512)
+    doms = F.create_uniform_grid(512, 512, 16, 8)
+    rngs = F.create_uniform_grid(512, 512, 8, 8)
+    plan = shard_plan(len(rngs), world)
+    a, b = plan[rank]
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
+    h = torch.from_numpy(y).pin_memory()
+    node = NodeTuples(plan, rank, dev)
+    with F.Engine(0, 4) as e:
+        e.set_stream(stream.cuda_stream)
+        e.set_frame(np.zeros_like(y))  # the step brings the real frame
+        e.set_domains(doms)
+        e.set_ranges(rngs[a:b])
+        step = bench.FrameStep(e, h, plan, rank, dev, stripes=backend == "nccl", node_tuples=node)
+        for _ in range(3):  # the buffer is rewritten by every frame
+            step()
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        full = records_from_tuples(np.frombuffer(step.tuples_bytes(), dtype=F.TUPLE), rngs, doms)
+        own_ok = step.own_slice_ok(e.fetch_tuples().tobytes())
+    if rank == 0:
+        np.save(path, full)
+    assert own_ok
+    dist.barrier()
+    del step
+    node.close()
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("backend,world", [("nccl", 1), ("gloo", 2)])
+def test_node_tuple_buffer_match_reference(tmp_path, backend, world):
+    """bench.FrameStep at N > 1 on one host: every rank's resolve writes its shard's tuples through the sink
+    into the node's one shared, HIP-registered host buffer (distributed.NodeTuples) — at world 1 on the nccl
+    group (stripes, the per-frame RCCL token), and at world 2 over gloo with both ranks' engines on GPU 0 (two
+    processes writing into one mapping) — against lenna_t4."""
+    from golden_util import FIELDS, golden
+
+    path = str(tmp_path / "full.npy")
+    mp.spawn(_node_worker, args=(world, _free_port(), path, backend), nprocs=world, join=True)
+    assert not [f for f in os.listdir("/dev/shm") if f.startswith("fracenc_tuples_")]
+    full = np.load(path)
+    rec, _ = golden("lenna_t4")
+    got = {"x": full["x"], "y": full["y"], "dx": full["dx"], "dy": full["dy"], "dw": full["sw"], "dh": full["sh"],
+           "t": full["transform"], "dist": full["distance"], "s": full["contrast"], "o": full["brightness"]}
+    for k in FIELDS:
+        np.testing.assert_array_equal(got[k], rec[k], err_msg=k)
+
+
 def _gpu_cls_worker(rank, world, port, path):
     import sys
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
