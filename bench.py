@@ -10,33 +10,46 @@ Ranges are sharded contiguously over ranks (fixed total work: strong scaling).
 wraps (main.cpp:164-168, the whole Encoder2): per step the frame H2D from pinned host memory
 (N > 1: each rank uploads its 1/N stripe of the rows and an RCCL all-gather assembles the frame
 on every rank over xGMI), domain-pool build, search, winner fit and fp32 fallback of this
-rank's shard, its 32-byte (domain, transform, s, o, rms) tuples packed on the device, the RCCL
-all-gather of every rank's tuples (N > 1) and the gathered tuples D2H into pinned host memory —
-serial, one frame after another.  Beside it the line carries:
+rank's shard, its 32-byte (domain, transform, s, o, rms) tuples written by the resolve, the RCCL
+all-gather of every rank's tuples (N > 1, north_star's exchange) and the gathered tuples D2H into
+pinned host memory — serial, one frame after another.  Beside it the line carries:
+  phases_ms     per phase (frame H2D, frame all-gather, run = prep + search + finish, tuple exchange)
+                the mean over the timed steps, MAX over ranks (phases_ms_by_rank: every rank's)
+  rank_ms_per_step  every rank's own step time (ms_per_step / value are the slowest rank's)
+  node_value    N > 1 on one host: the same step with every rank's resolve writing its shard's tuples
+                into one node-shared pinned host buffer instead of the tuple all-gather (--tuples node
+                makes that the headline and the all-gather `gather_value`)
   device_value  the same search with the frame already resident in HBM and the tuples left there
                 (the all-gather still runs for N > 1): the device-only rate
   stream_value  the end-to-end step through two contexts alternating frames, so frame k+1's
                 upload and frame k−1's download overlap frame k's search
+  c5            BASELINE configs[4]: the S1 RGB 4096² frame H2D (N > 1: row stripes + all-gather),
+                rgb2yuv on the device, every plane's shard searched, one all-gather of the three
+                planes' tuples, D2H — range-blocks/s over Y + U + V
   roofline      the search kernel against the dense f16 MFMA peak: `achieved` = the matrix flops
                 the search issues per launch (its algorithm's count) ÷ the kernel's mean duration
                 over exactly the headline's timed steps (library HIP events on the kernel's stream,
-                frac_timing_history); `direct_form` = the §8(d) direct-form op count over the same
-                time (an algorithmic-equivalent rate, not a hardware fraction); `traffic` = HBM
-                bytes per launch from the committed rocprofv3 PMC passes of THIS library build
-                (null when profiles/pmc_search.json was taken from another build)
+                frac_timing_history); `frac_device` the same over the device-resident leg's steps;
+                `direct_form` = the §8(d) direct-form op count over the same time (an
+                algorithmic-equivalent rate, not a hardware fraction); `traffic` = HBM bytes per launch
+                from the committed rocprofv3 PMC passes of THIS library build (null when
+                profiles/pmc_search.json was taken from another build)
   arith         what `dtype` "f16" means here: exact integer arithmetic in f16 containers
   records       a digest of the gathered tuples (equal across N = 1/2/4/8 iff the shards' gathered
                 records equal the single-rank run's), and the checks that each rank's slice of the
-                gathered tuples is its own shard and that the end-to-end and device legs agree
+                gathered tuples is its own shard and that the legs agree
   cpu_baseline  the unmodified reference (oracle/_ref) on a bounded sample, all the host cores this
                 process may use (affinity, capped by the cgroup CPU quota), CPU model recorded
+  drop_in       (N = 1) the same C3 frame through the reference's own EncodingEngineCore2 with the HIP
+                engine registered (oracle/ref/core_driver): the rate a reference user gets through
+                its API, alone and beside its CPU engines, and with the batch-claim patch
 
 Run:  python bench.py [--gpus N] [--steps K] [--warmup W] [--engine valu|mfma|auto]
 --gpus N > 1 without WORLD_SIZE in the environment: this process launches N ranks itself
 (torch.distributed.run as a child process, before anything touches the GPU) and exits with its
 status; under torch.distributed.run (WORLD_SIZE set) it runs one rank per GPU over RCCL.
-The step, the all-gather and the line's core fields (FrameStep, timed, headline_fields) take any
-engine object and process-group backend: tests/test_bench_ranks.py runs them on `gloo` ranks.
+main() takes an engine factory, a process-group backend and the device kind: tests/bench_main_cpu.py
+runs this same main() on `gloo` ranks with the oracle stand-in engine.
 """
 from __future__ import annotations
 
@@ -47,6 +60,7 @@ import os
 import socket
 import subprocess
 import sys
+import tempfile
 import time
 
 import numpy as np
@@ -61,6 +75,7 @@ HBM_PEAK_GBS = 8000.0
 ARITH = ("exact integer: f16 operands are integers |x| <= 2048 (exact in f16), fp32 accumulation with every "
          "partial sum < 2^24 (guarded per tile pair), winners re-resolved in integer arithmetic, fit in fp64")
 TUPLE_BYTES = 32
+PHASES = ("frame_h2d", "frame_allgather", "run", "tuples")
 
 
 def parse(argv=None):
@@ -77,10 +92,13 @@ def parse(argv=None):
     ap.add_argument("--alt-steps", type=int, default=2,
                     help="steps of the VALU engine (north_star's no-MFMA formulation) reported beside (0 = skip)")
     ap.add_argument("--side-steps", type=int, default=-1,
-                    help="steps of the device-resident and stream legs (-1 = --steps, 0 = skip)")
-    ap.add_argument("--tuples", default="node", choices=["node", "gather"],
-                    help="N > 1 on one host: the ranks' tuples into one shared host buffer (node), or the "
-                         "all-gather + every rank's download (gather; always with ranks on several hosts)")
+                    help="steps of the device-resident, stream, other-tuples and C5 legs (-1 = --steps, 0 = skip)")
+    ap.add_argument("--tuples", default="gather", choices=["gather", "node"],
+                    help="N > 1: the headline's tuple exchange — the RCCL all-gather + download (gather, north_star's "
+                         "design) or, ranks on one host, one node-shared host buffer (node); the other is a side leg")
+    ap.add_argument("--drop-in", type=int, default=1,
+                    help="N = 1: time the frame through the reference's own core (oracle/_ref/core_driver; 0 = skip)")
+    ap.add_argument("--out", default=None, help="also write the line to this file (rank 0)")
     ap.add_argument("--ab", action="store_true",
                     help="allow FRAC_LIB / A/B knobs in the environment (the line is then marked, not a headline)")
     return ap.parse_args(argv)
@@ -170,6 +188,53 @@ def cpu_baseline(frame: np.ndarray, budget: float, threads: int, host: dict):
                       f"{threads} threads, {dt:.1f} s"}
 
 
+CORE_DRIVER = os.path.join(ROOT, "oracle", "_ref", "core_driver")
+# (name, CPU engines beside the HIP engine, core mode): the reference's core as compiled, and the batch-claim
+# patch INTEGRATION.md §Drop-in rate proposes (HIP engines claim 4,096 ranges per lock, CPU engines one)
+DROP_IN_RUNS = (("hip_only", 0, "ref"), ("cpu2_and_hip", 2, "ref"), ("cpu16_and_hip", 16, "ref"),
+                ("batched_hip_only", 0, "batch:4096"), ("batched_cpu16_and_hip", 16, "batch:4096"))
+
+
+def drop_in(frame: np.ndarray, timeout_s: float = 240.0) -> dict:
+    """The C3 frame through the reference's own EncodingEngineCore2 (compiled unmodified, oracle/ref/Makefile)
+    with one HipEncodingEngine2 registered (integration/, oracle/ref/core_driver.cpp): core.encode()'s time,
+    which is what a reference user times (main.cpp:164-167), alone (--nocpu) and beside k of the reference's
+    CPU engines on the one claim queue (EncodingEngine2.hpp:126-152, EncodingEngine2.cpp:12-20), and with
+    the batch-claim patch.  After the timed region, in child processes (the reference never runs in this one)."""
+    if not os.path.exists(CORE_DRIVER):
+        return {"skipped": "oracle/_ref/core_driver not built"}
+    H, W = frame.shape
+    out = {"workload": f"C3 {W}x{H} S1 frame, 16x16 domains stride 8, 8x8 ranges, T=4, exhaustive, through "
+                       "EncodingEngineCore2::encode with HipEncodingEngine2 on device 0",
+           "timer": "core.encode() (main.cpp:164-167 times Encoder2, whose search is this call) minus the "
+                    "lost-wakeup guard's hold (core_driver's tail engine)", "runs": {}}
+    with tempfile.TemporaryDirectory() as td:
+        plane = os.path.join(td, "c3.u8")
+        frame.tofile(plane)
+        for name, ncpu, mode in DROP_IN_RUNS:
+            res = os.path.join(td, f"{name}.bin")
+            cmd = [CORE_DRIVER, plane, str(W), str(H), "16", "8", "0", "0", "-1", res, str(ncpu), "0", mode]
+            try:
+                r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout_s)
+            except subprocess.TimeoutExpired:
+                out["runs"][name] = {"error": f"timeout {timeout_s} s"}
+                continue
+            rec = next((json.loads(ln) for ln in r.stdout.splitlines() if ln.startswith("{")), None)
+            if r.returncode != 0 or rec is None:
+                out["runs"][name] = {"error": f"exit {r.returncode}: {r.stderr[-300:]}"}
+                continue
+            n = rec["ranges"]
+            raw = open(res, "rb").read()
+            k = int(np.frombuffer(raw[-8:], dtype=np.uint64)[0])
+            hip_ranges = int(np.frombuffer(raw[-8 * (2 + k): -8 * (1 + k)], dtype=np.uint64)[0])
+            out["runs"][name] = {"value": round(n / rec["drop_in_s"], 1), "unit": "range-blocks/s",
+                                 "drop_in_s": rec["drop_in_s"], "encode_s": rec["encode_s"],
+                                 "tail_hold_s": rec["tail_hold_s"], "records_s": rec["records_s"],
+                                 "cpu_engines": ncpu, "mode": mode, "hip_ranges": hip_ranges,
+                                 "records": int((len(raw) - 8 * (3 + k)) // 64)}
+    return out
+
+
 def lib_sha16() -> str:
     import fractencode_amd as F
 
@@ -208,14 +273,32 @@ def _sync(dev) -> None:
 
 def max_over_ranks(x: float, world: int, dev) -> float:
     """The largest of every rank's `x` (the slowest rank's time)."""
+    return max_vector([x], world, dev)[0]
+
+
+def max_vector(xs: list, world: int, dev) -> list:
+    """Element-wise maximum over ranks of a list of floats."""
     if world == 1:
-        return x
+        return list(xs)
     import torch
     import torch.distributed as dist
 
-    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    t = torch.tensor(xs, dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return float(t.item())
+    return [float(v) for v in t.cpu()]
+
+
+def gather_floats(xs: list, world: int, dev) -> list:
+    """Every rank's list of floats (rank order)."""
+    if world == 1:
+        return [list(xs)]
+    import torch
+    import torch.distributed as dist
+
+    t = torch.tensor(xs, dtype=torch.float64, device=dev)
+    out = torch.empty(world * len(xs), dtype=torch.float64, device=dev)
+    dist.all_gather_into_tensor(out, t)
+    return out.cpu().view(world, len(xs)).tolist()
 
 
 def timed(fn, steps: int, world: int, dev) -> tuple[float, float]:
@@ -238,6 +321,46 @@ def timed(fn, steps: int, world: int, dev) -> tuple[float, float]:
     return mine, max_over_ranks(mine, world, dev)
 
 
+class PhaseClock:
+    """Per-step phase marks: HIP events on torch's current stream (the engine's) on the GPU, the host clock
+    on the CPU (where every step's operations are synchronous).  A phase's time is the span from the
+    previous mark to its own; `means()` averages over the recorded steps (after a synchronisation)."""
+
+    def __init__(self, dev):
+        self.cuda = dev.type == "cuda"
+        self.rows = []
+        self._cur = None
+
+    def _now(self):
+        if self.cuda:
+            import torch
+
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            return e
+        return time.perf_counter()
+
+    def begin(self) -> None:
+        self._cur = [("", self._now())]
+
+    def mark(self, name: str) -> None:
+        if self._cur is not None:
+            self._cur.append((name, self._now()))
+
+    def end(self) -> None:
+        if self._cur is not None:
+            self.rows.append(self._cur)
+        self._cur = None
+
+    def means(self) -> dict:
+        acc = {k: 0.0 for k in PHASES}
+        for row in self.rows:
+            for (_, a), (name, b) in zip(row, row[1:]):
+                acc[name] += a.elapsed_time(b) if self.cuda else (b - a) * 1e3
+        n = max(1, len(self.rows))
+        return {k: v / n for k, v in acc.items()}
+
+
 class FrameStep:
     """The headline step (BASELINE.md "Metric"): the frame H2D from the caller's
     pinned host plane, the search of this rank's shard (frame-dependent preparation included), the
@@ -250,13 +373,13 @@ class FrameStep:
     On the GPU the run writes its tuples itself (frac_set_tuple_sink): without a process group straight
     into the pinned output (they cross PCIe while the resolve writes them: no pack kernel and no D2H
     copy after it), with one into the all-gather buffer.
-    `node_tuples` (a distributed.NodeTuples; bench.py passes one when every rank is on one host): every rank's
-    run writes its shard's tuples into the node's one shared host buffer (each PCIe link carries only its own
-    shard's tuples, no tuple all-gather, no download of every rank's tuples by every rank), then one
-    completion token per frame."""
+    `node_tuples` (a distributed.NodeTuples, ranks on one host): every rank's run writes its shard's tuples
+    into the node's one shared host buffer (each PCIe link carries only its own shard's tuples, no tuple
+    all-gather, no download of every rank's tuples by every rank), then one completion token per frame.
+    `clock` (a PhaseClock): marks frame_h2d / frame_allgather / run / tuples per step."""
 
     def __init__(self, eng, frame, plan, rank: int, dev, device_resident: bool = False, stripes=None,
-                 node_tuples=None):
+                 node_tuples=None, clock=None):
         import torch
 
         world = len(plan)
@@ -270,6 +393,7 @@ class FrameStep:
             frame = frame.numpy()
         self.eng, self.frame, self.plan, self.rank, self.dev = eng, frame, plan, rank, dev
         self.device_resident = device_resident
+        self.clock = clock
         self.sink = hasattr(eng, "set_tuple_sink") and dev.type == "cuda"
         a, b = plan[rank]
         self.n_mine = b - a
@@ -284,18 +408,28 @@ class FrameStep:
             self.nccl = dist.get_backend() == "nccl"
             self.token = torch.zeros(1, dtype=torch.int32, device=dev if self.nccl else "cpu")
 
+    def _mark(self, name: str) -> None:
+        if self.clock is not None:
+            self.clock.mark(name)
+
     def __call__(self) -> None:
-        import torch
+        if self.clock is not None:
+            self.clock.begin()
+        self._step()
+        if self.clock is not None:
+            self.clock.end()
+
+    def _step(self) -> None:
+        import torch.distributed as dist
 
         from fractencode_amd.distributed import gather_tuples
 
         if self.stripes:  # this rank's rows H2D + the all-gather (on the engine's = torch's current stream)
-            full = self.frame_stripes()
+            full = self.frame_stripes(self._mark)
             self.eng.set_frame(full if full.is_cuda else full.numpy())
         elif not self.device_resident:
             self.eng.set_frame(self.frame)  # H2D (returns once the plane is on the device)
-        import torch.distributed as dist
-
+            self._mark("frame_h2d")
         if self.node is not None:
             self._node_step()
             return
@@ -303,20 +437,25 @@ class FrameStep:
         if self.sink and self.n_mine:  # the run writes the tuples: into the pinned output, or the gather buffer
             self.eng.set_tuple_sink(self.h_out.data_ptr() if direct else self.local.data_ptr())
         self.eng.run()
+        self._mark("run")
         if self.sink and self.n_mine:
             self.eng.set_tuple_sink(None)
         if direct:  # one rank, no group: the tuples are already on their way into h_out
             self.gathered = None
+            self._mark("tuples")
             return
         if self.local.is_cuda:  # packed on the device, on the engine's (= torch's current) stream
             if self.n_mine and not self.sink:
                 self.eng.copy_tuples_device(self.local.data_ptr())
         elif self.n_mine:  # CPU backend: the engine hands back host tuples
+            import torch
+
             t = np.ascontiguousarray(self.eng.fetch_tuples())
             self.local[: self.n_mine * TUPLE_BYTES] = torch.from_numpy(t.view(np.uint8))
         self.gathered = gather_tuples(self.local, self.plan)
         if not self.device_resident:
             self.h_out.copy_(self.gathered, non_blocking=True)  # D2H into pinned memory
+        self._mark("tuples")
 
     def _node_step(self) -> None:
         """The run writes its shard's tuples into the node's shared host buffer (NodeTuples): on the GPU
@@ -328,9 +467,11 @@ class FrameStep:
         if self.n_mine and self.sink:
             self.eng.set_tuple_sink(self.node.sink_ptr())
             self.eng.run()
+            self._mark("run")
             self.eng.set_tuple_sink(None)
         else:
             self.eng.run()
+            self._mark("run")
             if self.n_mine:
                 self.node.put(np.ascontiguousarray(self.eng.fetch_tuples()).tobytes())
         if self.nccl:
@@ -338,6 +479,7 @@ class FrameStep:
         else:
             _sync(self.dev)
             dist.barrier()
+        self._mark("tuples")
 
     def tuples_bytes(self) -> bytes:
         """The last step's gathered tuples (after a synchronisation)."""
@@ -348,6 +490,83 @@ class FrameStep:
         """This rank's slice of the gathered tuples is its own shard's."""
         a, b = self.plan[self.rank]
         return self.tuples_bytes()[a * TUPLE_BYTES: b * TUPLE_BYTES] == own
+
+
+class ColorStep:
+    """C5 (BASELINE configs[4]): one RGB frame per step — its H2D from pinned host
+    memory (N > 1: this rank's stripe of rows + one all-gather), ImageIO::rgb2yuv on the device
+    (image/ImageIO.cpp:43-58), every plane's shard of its ranges searched on the three engines (one stream;
+    the resolvers write the tuples into one buffer, plane after plane), one all-gather of the three planes'
+    tuples (N > 1) and the D2H into pinned memory.  CPU engines take the host frame and hand back host tuples."""
+
+    def __init__(self, engines, rgb, plans, rank: int, dev):
+        import torch
+
+        self.engines, self.plans, self.rank, self.dev = engines, plans, rank, dev
+        self.world = len(plans[0])
+        self.cuda = dev.type == "cuda"
+        H, W = rgb.shape[:2]
+        self.H, self.W = H, W
+        self.rgb_np = rgb if isinstance(rgb, np.ndarray) else None
+        if self.cuda:
+            self.rgb = rgb  # pinned host tensor [H, W, 3]
+            if self.world > 1:
+                from fractencode_amd.distributed import FrameStripes
+
+                self.stripes = FrameStripes(rgb.view(H, W * 3), self.world, rank, dev)
+            else:
+                self.d_rgb = torch.empty((H, W, 3), dtype=torch.uint8, device=dev)
+        self.caps = [max(b - a for a, b in p) for p in plans]
+        self.offs = np.concatenate([[0], np.cumsum(self.caps)]).astype(int)
+        cap = int(self.offs[-1])
+        self.local = torch.zeros(cap * TUPLE_BYTES, dtype=torch.uint8, device=dev)
+        self.h_out = torch.empty(self.world * cap * TUPLE_BYTES, dtype=torch.uint8, pin_memory=self.cuda)
+        self.out = None
+
+    def __call__(self) -> None:
+        import torch
+        import torch.distributed as dist
+
+        if self.cuda:
+            if self.world > 1:
+                d_rgb = self.stripes().view(self.H, self.W, 3)
+            else:
+                self.d_rgb.copy_(self.rgb, non_blocking=True)
+                d_rgb = self.d_rgb
+            planes = self.engines[0].rgb_to_yuv(d_rgb)
+        else:
+            planes = self.engines[0].rgb_to_yuv(self.rgb_np)
+        for e, p in zip(self.engines, planes):
+            e.set_frame(p)
+        for k, (e, plan) in enumerate(zip(self.engines, self.plans)):
+            a, b = plan[self.rank]
+            off = int(self.offs[k]) * TUPLE_BYTES
+            if self.cuda and b > a:
+                e.set_tuple_sink(self.local.data_ptr() + off)
+            e.run()
+            if self.cuda and b > a:
+                e.set_tuple_sink(None)
+            elif b > a:
+                t = np.ascontiguousarray(e.fetch_tuples())
+                self.local[off: off + (b - a) * TUPLE_BYTES] = torch.from_numpy(t.view(np.uint8))
+        if dist.is_initialized():
+            out = torch.empty(self.world * self.local.numel(), dtype=torch.uint8, device=self.dev)
+            dist.all_gather_into_tensor(out, self.local)
+        else:
+            out = self.local
+        self.h_out[: out.numel()].copy_(out, non_blocking=True)
+        self.out = out
+
+    def tuples_bytes(self) -> bytes:
+        """The last step's tuples in plane order (Y's ranges, then U's, then V's), rank shards concatenated."""
+        raw = self.h_out.numpy().tobytes() if not self.cuda else self.h_out.cpu().numpy().tobytes()
+        cap = int(self.offs[-1]) * TUPLE_BYTES
+        parts = []
+        for k, plan in enumerate(self.plans):
+            for r, (a, b) in enumerate(plan):
+                base = r * cap + int(self.offs[k]) * TUPLE_BYTES
+                parts.append(raw[base: base + (b - a) * TUPLE_BYTES])
+        return b"".join(parts)
 
 
 def headline_fields(nr_total: int, world: int, steps: int, warmup: int, elapsed_max: float) -> dict:
@@ -361,7 +580,76 @@ def digest(b: bytes) -> str:
     return hashlib.sha256(b).hexdigest()[:16]
 
 
-def main(args):
+def hip_engine(dev, transforms: int, engine_id: int, timing: bool = False):
+    """The product engine factory: one fracenc context on `dev` (exhaustive, no classifier, rms 0, sMax −1)."""
+    import fractencode_amd as F
+
+    return F.Engine(dev.index, transforms, False, 0.0, -1.0, engine_id, timing=timing)
+
+
+def _setup(args, backend: str, cuda: bool):
+    """The process group (N > 1) and this rank's device: (world, rank, dev, ranks on one host)."""
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    one_host = True
+    if cuda:
+        dev = torch.device("cuda", local if world > 1 else 0)
+        torch.cuda.set_device(dev)
+    else:
+        dev = torch.device("cpu")
+    if world > 1:
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
+        where = [None] * world
+        name = torch.cuda.get_device_name(dev) if cuda else "cpu"
+        dist.all_gather_object(where, (socket.gethostname(), local, name))
+        if cuda and len({(h, d) for h, d, _ in where}) != world:
+            raise SystemExit(f"bench.py: ranks share a GPU: {where}")
+        one_host = len({h for h, _, _ in where}) == 1
+    return world, rank, dev, one_host
+
+
+def _node_buffer(plan, rank, dev, world):
+    """A NodeTuples on every rank, or None on every rank when any rank could not map or register it (a
+    Python error on one rank must not leave the others waiting in a collective)."""
+    import torch
+    import torch.distributed as dist
+
+    from fractencode_amd.distributed import NodeTuples
+
+    node, err = None, ""
+    try:
+        node = NodeTuples(plan, rank, dev)
+    except (OSError, RuntimeError) as exc:
+        err = str(exc)
+    ok = torch.tensor([0 if node is None else 1], dtype=torch.int32, device=dev)
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    if int(ok.item()) == 0:
+        if node is not None:
+            node.close()
+        return None, err or "another rank could not map the node buffer"
+    return node, ""
+
+
+def _run_leg(step, steps: int, warmup: int, world: int, dev):
+    for _ in range(warmup):
+        step()
+    return timed(step, steps, world, dev)
+
+
+def main(args, engine_factory=None, backend: str = "nccl", cuda: bool = True) -> dict:
+    """The bench on this rank.  `engine_factory(dev, transforms, engine_id, timing)` builds an engine (default:
+    the HIP library's), `backend` the process group's (nccl = RCCL), `cuda` whether ranks own a GPU; the
+    CPU tests pass the oracle stand-in, gloo and False.  Rank 0 prints the line and returns it."""
     import torch
     import torch.distributed as dist
 
@@ -369,28 +657,14 @@ def main(args):
     from fractencode_amd.distributed import shard_plan
     from fractencode_amd.synth import value_noise
 
+    product = engine_factory is None
+    engine_factory = engine_factory or hip_engine
     knobs = check_headline_env(args)
     build = F.build_info()
-    if not build["matches_sources"] and not args.ab:
+    if product and not build["matches_sources"] and not args.ab:
         raise SystemExit(f"bench.py: the library was built from sources {build['build_id']}, these are "
                          f"{F.source_id()}: rebuild (__graft_entry__.build())")
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
-    if world > 1:
-        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        where = [None] * world
-        dist.all_gather_object(where, (socket.gethostname(), local, torch.cuda.get_device_name(local)))
-        if len({(h, d) for h, d, _ in where}) != world:
-            raise SystemExit(f"bench.py: ranks share a GPU: {where}")
-        one_host = len({h for h, _, _ in where}) == 1
-    else:
-        torch.cuda.set_device(0)
-    dev = torch.device("cuda", local if world > 1 else 0)
+    world, rank, dev, one_host = _setup(args, backend, cuda)
 
     S = args.size
     frame = value_noise(S, S, 1234)
@@ -401,31 +675,41 @@ def main(args):
     start, stop = plan[rank]
     mine = rngs[start:stop]
     engine_id = {"auto": F.ENGINE_AUTO, "valu": F.ENGINE_VALU, "mfma": F.ENGINE_MFMA}[args.engine]
+    side_steps = args.steps if args.side_steps < 0 else args.side_steps
 
-    # one dedicated stream for the engine, the tuple copies and the RCCL gather, so every copy and the
-    # all-gather are ordered after the kernels (the legacy null stream cannot be handed to the
-    # library: NULL = its own stream)
-    stream = torch.cuda.Stream(dev)
-    torch.cuda.set_stream(stream)
-    eng = F.Engine(dev.index, args.transforms, False, 0.0, -1.0, engine_id, timing=True)
-    eng.set_stream(stream.cuda_stream)
-    h_frame = torch.from_numpy(frame).pin_memory()  # the caller's plane, in pinned host memory
+    # one dedicated stream for the engine, the tuple copies and the RCCL collectives, so every copy and the
+    # all-gathers are ordered after the kernels (the legacy null stream cannot be handed to the library:
+    # NULL = its own stream)
+    stream = None
+    if cuda:
+        stream = torch.cuda.Stream(dev)
+        torch.cuda.set_stream(stream)
+
+    def new_engine(timing=False):
+        e = engine_factory(dev, args.transforms, engine_id, timing)
+        if stream is not None:
+            e.set_stream(stream.cuda_stream)
+        return e
+
+    eng = new_engine(timing=True)
+    h_frame = torch.from_numpy(frame)
+    if cuda:
+        h_frame = h_frame.pin_memory()  # the caller's plane, in pinned host memory
     eng.set_frame(h_frame.numpy())
     eng.set_domains(doms)
     eng.set_ranges(mine)
 
     # ---- headline: the end-to-end step ----
-    node = None
-    if world > 1 and one_host and args.tuples == "node":
-        from fractencode_amd.distributed import NodeTuples
-
-        node = NodeTuples(plan, rank, dev)
-    step = FrameStep(eng, h_frame, plan, rank, dev, node_tuples=node)
+    use_node = world > 1 and one_host and args.tuples == "node"
+    node, node_err = (_node_buffer(plan, rank, dev, world) if use_node else (None, ""))
+    clock = PhaseClock(dev)
+    step = FrameStep(eng, h_frame, plan, rank, dev, node_tuples=node, clock=clock)
     for _ in range(args.warmup):
         step()
     _sync(dev)
+    clock.rows = []
     eng.timing_history()  # drop the warmup runs: the history now covers exactly the timed steps
-    _, elapsed = timed(step, args.steps, world, dev)
+    mine_s, elapsed = timed(step, args.steps, world, dev)
     hist = eng.timing_history()  # per-run HIP events of the K timed steps (on the kernel's stream)
     # the library keeps the last 256 runs: with more steps the mean is over the last 256 of them
     assert len(hist) == min(args.steps, 256), (len(hist), args.steps)
@@ -433,13 +717,22 @@ def main(args):
     gathered = step.tuples_bytes()
     own = eng.fetch_tuples().tobytes() if len(mine) else b""
     checks = {"own_slice_in_gather": step.own_slice_ok(own)}
+    phases = clock.means()
+    phases.update({k: float(np.mean(hist["ms_" + k])) if len(hist) else 0.0 for k in ("prep", "search", "finish")})
+    keys = list(PHASES) + ["prep", "search", "finish"]
+    by_rank = gather_floats([phases[k] for k in keys], world, dev)
+    rank_s = [r[0] for r in gather_floats([mine_s], world, dev)]
+    if node is not None:
+        del step
+        node.close()
+        node = None
 
     kernel_ms = float(np.mean(hist["ms_search"]))
     engine_name = {1: "valu", 2: "mfma"}.get(st["engine"], "valu")
     form = F.FORM_NAMES.get(st["search_form"], engine_name)
     n_d = len(doms)
     direct_ops = 2 * 64 * args.transforms * n_d * len(mine)  # one MAC per pixel per candidate
-    traffic, traffic_src = load_traffic(form)
+    traffic, traffic_src = load_traffic(form) if product else (None, "stand-in engine")
     if engine_name == "mfma":
         # the matrix flops the search issues: the Fourier form's own count (6 MFMA 32x32x16 per
         # 32-range × 32-domain tile pair), fewer than the direct form's §8(d) count for the same result
@@ -448,14 +741,14 @@ def main(args):
     else:
         work = direct_ops
         bound, peak, unit = "valu", VALU_PEAK_TOPS, "TOP/s"
-    achieved = work / (kernel_ms * 1e-3) / 1e12
+    achieved = work / (kernel_ms * 1e-3) / 1e12 if kernel_ms > 0 else 0.0
     roof = {"bound": bound, "achieved": round(achieved, 2), "peak": peak, "unit": unit,
             "frac": round(achieved / peak, 4), "traffic": traffic,
             "kernel": {"fourier": "search_dft", "direct": "search_mfma"}.get(form, "search_valu"),
             "kernel_ms": round(kernel_ms, 3), "kernel_ms_timed_steps": [round(float(x), 3) for x in hist["ms_search"]],
             "flops_per_launch": int(work),
             "direct_form": {"ops_per_launch": direct_ops,
-                            "rate": round(direct_ops / (kernel_ms * 1e-3) / 1e12, 2),
+                            "rate": round(direct_ops / (kernel_ms * 1e-3) / 1e12, 2) if kernel_ms > 0 else 0.0,
                             "note": "SURVEY §8(d) direct-form count over the same kernel time: an "
                                     "algorithmic-equivalent rate, not a hardware fraction"}}
     if traffic:
@@ -464,6 +757,7 @@ def main(args):
         roof["traffic_source"] = traffic_src
     else:
         roof["traffic_note"] = traffic_src
+    tuples_out = "node" if use_node and not node_err else ("gather" if world > 1 else "sink")
     line = headline_fields(nr_total, world, args.steps, args.warmup, elapsed)
     line.update({
         "dtype": "u16" if engine_name == "valu" else "f16",
@@ -478,38 +772,74 @@ def main(args):
                  "frame H2D of the rank's 1/N stripe of rows (pinned) + RCCL all-gather of the frame + pool build "
                  "+ search + fit of the rank's shard + " +
                  ("its 32-byte tuples written by the resolve into the node's shared pinned tuple buffer + a "
-                  "4-byte RCCL all-reduce per frame" if node is not None else
-                  "32-byte tuples into the all-gather buffer + RCCL all-gather + gathered tuples D2H (pinned)")) +
+                  "4-byte RCCL all-reduce per frame" if tuples_out == "node" else
+                  "32-byte tuples written by the resolve into the all-gather buffer + RCCL all-gather + gathered "
+                  "tuples D2H (pinned)")) +
                 "; serial, barrier + synchronisation around the timed steps, slowest rank",
-        "tuples_out": "node" if node is not None else ("gather" if world > 1 else "sink"),
+        "tuples_out": tuples_out,
+        "rank_ms_per_step": [round(1e3 * s / args.steps, 3) for s in rank_s],
         "roofline": roof,
         "search_form": form,
-        "phases_ms": {k: round(float(np.mean(hist["ms_" + k])), 3) for k in ("device", "prep", "search", "finish")},
+        "phases_ms": {k: round(v, 3) for k, v in zip(keys, max_vector([phases[k] for k in keys], world, dev))},
+        "phases_ms_by_rank": [{k: round(v, 3) for k, v in zip(keys, row)} for row in by_rank],
+        "phases_note": "frame_h2d / frame_allgather / run / tuples: spans between marks on the engine's stream "
+                       "(the tuple exchange includes the D2H); prep / search / finish: the library's events "
+                       "inside run; each the mean over the timed steps, phases_ms the maximum over ranks",
         "fallback_ranges": st["fallback_ranges"],
         "source_id": lib_sha16(),
         "build": build,  # the loaded library's compiled-in id (frac_build_id): the binary that ran
     })
+    if node_err:
+        line["node_error"] = node_err
 
-    side_steps = args.steps if args.side_steps < 0 else args.side_steps
+    if side_steps > 0 and world > 1:
+        # the other tuple exchange, timed the same way (north_star's all-gather beside the node buffer)
+        other = "gather" if tuples_out == "node" else "node"
+        onode, oerr = (None, "")
+        if other == "node":
+            onode, oerr = (_node_buffer(plan, rank, dev, world) if one_host else (None, "ranks on several hosts"))
+        if other == "gather" or onode is not None:
+            ostep = FrameStep(eng, h_frame, plan, rank, dev, node_tuples=onode)
+            _, osec = _run_leg(ostep, side_steps, 1, world, dev)
+            checks[f"{other}_equals_headline"] = ostep.tuples_bytes() == gathered
+            line[f"{other}_value"] = {"value": round(nr_total / (osec / side_steps), 1),
+                                      "ms_per_step": round(1e3 * osec / side_steps, 3), "steps": side_steps,
+                                      "tuples_out": other}
+            del ostep
+            if onode is not None:
+                onode.close()
+        else:
+            line[f"{other}_value"] = {"skipped": oerr}
+
     if side_steps > 0:
         # the device-only rate: the frame resident in HBM, the gathered tuples left on the device
         d_frame = torch.from_numpy(frame).to(dev)
-        eng.set_frame(d_frame)
+        eng.set_frame(d_frame if cuda else frame)
         dstep = FrameStep(eng, None, plan, rank, dev, device_resident=True)
         dstep()
+        eng.timing_history()
         _, dsec = timed(dstep, side_steps, world, dev)
+        dhist = eng.timing_history()
         checks["device_leg_equals_e2e"] = dstep.tuples_bytes() == gathered
         line["device_value"] = {"value": round(nr_total / (dsec / side_steps), 1),
                                 "ms_per_step": round(1e3 * dsec / side_steps, 3), "steps": side_steps,
                                 "step": "the same with the frame resident in HBM before timing and the gathered "
                                         "tuples left on the device"}
+        if len(dhist):
+            dk = float(np.mean(dhist["ms_search"]))
+            if dk > 0:
+                roof["kernel_ms_device"] = round(dk, 3)
+                roof["frac_device"] = round(work / (dk * 1e-3) / 1e12 / peak, 4)
         # a frame stream: two contexts in turn, frame k+1 uploads on one context's stream while frame k
         # searches on the other's, and frame k's tuples come back while k+1 searches (per rank, no gather)
-        tup = h_tuples = None
+        tup = None
         if len(mine):
-            h_tuples = [torch.empty(len(mine) * TUPLE_BYTES, dtype=torch.uint8).pin_memory() for _ in range(2)]
-            tup = [h.numpy().view(F.TUPLE) for h in h_tuples]
-        with F.Engine(dev.index, args.transforms, False, 0.0, -1.0, engine_id) as eng2:
+            if cuda:
+                h_tuples = [torch.empty(len(mine) * TUPLE_BYTES, dtype=torch.uint8).pin_memory() for _ in range(2)]
+                tup = [h.numpy().view(F.TUPLE) for h in h_tuples]
+            else:
+                tup = [np.zeros(len(mine), dtype=F.TUPLE) for _ in range(2)]
+        with new_engine() as eng2:
             eng.set_frame(h_frame.numpy())
             eng2.set_frame(h_frame.numpy())
             eng2.set_domains(doms)
@@ -530,11 +860,39 @@ def main(args):
                                     "ms_per_step": round(1e3 * ssec / side_steps, 3), "steps": side_steps,
                                     "step": "frame H2D + search + tuples D2H per frame, two contexts alternating "
                                             "frames" + (" (per rank, no gather)" if world > 1 else "")}
-        eng.set_frame(d_frame)
+        eng.set_frame(d_frame if cuda else frame)
         eng.run()
+
+        # C5 (BASELINE configs[4]): three planes of an S1 RGB frame, sharded the same way
+        rgb = np.stack([value_noise(S, S, 1234 + k) for k in range(3)], -1)
+        h_rgb = torch.from_numpy(rgb)
+        if cuda:
+            h_rgb = h_rgb.pin_memory()
+        sizes = [(S, S), (S // 2, S // 2), (S // 2, S // 2)]
+        c5_rngs = [F.create_uniform_grid(w, h, 8, 8) for w, h in sizes]
+        c5_plans = [shard_plan(len(r), world) for r in c5_rngs]
+        c5_eng = [new_engine() for _ in range(3)]
+        for e, (w, h), r, p in zip(c5_eng, sizes, c5_rngs, c5_plans):
+            a, b = p[rank]
+            e.set_frame(np.zeros((h, w), np.uint8))
+            e.set_domains(F.create_uniform_grid(w, h, 16, 8))
+            e.set_ranges(r[a:b])
+        cstep = ColorStep(c5_eng, h_rgb if cuda else rgb, c5_plans, rank, dev)
+        _, csec = _run_leg(cstep, side_steps, 1, world, dev)
+        c5_bytes = cstep.tuples_bytes()
+        n5 = sum(len(r) for r in c5_rngs)
+        line["c5"] = {"value": round(n5 / (csec / side_steps), 1), "unit": "range-blocks/s",
+                      "ms_per_step": round(1e3 * csec / side_steps, 3), "steps": side_steps,
+                      "workload": f"C5: S1 RGB {S}x{S} (seeds 1234/1235/1236) -> Y {S}x{S}, U/V {S // 2}x{S // 2}, "
+                                  f"8x8 ranges ({n5}), 16x16 domains stride 8, T={args.transforms}, exhaustive",
+                      "step": "RGB H2D (N > 1: row stripes + RCCL all-gather) + rgb2yuv on the device + the three "
+                              "planes' shards searched on one stream + one all-gather of their tuples + D2H",
+                      "records": {"tuples_sha16": digest(c5_bytes), "n": n5}}
+        for e in c5_eng:
+            e.close()
     line["records"] = {"tuples_sha16": digest(gathered), "n": nr_total, **checks}
 
-    if world == 1 and engine_name == "mfma" and args.alt_steps > 0:
+    if world == 1 and engine_name == "mfma" and args.alt_steps > 0 and product:
         # the same workload on the other engines, frame resident, measured the same way: the VALU engine
         # (packed-u16 v_dot2, north_star's no-MFMA formulation, exhaustive) and the SEA engine
         # (successive elimination: identical records, most candidates skipped by an exact bound,
@@ -573,14 +931,18 @@ def main(args):
     if rank == 0 and world == 1 and args.cpu_budget > 0:
         threads, host = host_cores()
         line["cpu_baseline"] = cpu_baseline(frame, args.cpu_budget, args.cpu_threads or threads, host)
+    if rank == 0 and world == 1 and cuda and product and args.drop_in:
+        line["drop_in"] = drop_in(frame)
     eng.close()
-    if node is not None:
-        del step
-        node.close()
     if rank == 0:
         print(json.dumps(line), flush=True)
+        if args.out:
+            with open(args.out, "w") as f:
+                json.dump(line, f)
     if world > 1:
+        dist.barrier()
         dist.destroy_process_group()
+    return line
 
 
 if __name__ == "__main__":

@@ -2230,6 +2230,8 @@ int launch_generic(frac_ctx* c)
     }
     if (timing)
         FRAC_TRY(mark_event(c, 0));
+    c->fit_fused = false; // gen_fit writes the records; frac_run packs the sink's tuples from them
+    c->fb_pending = false;
     if (nr)
         FRAC_HIP(c, hipMemsetAsync(c->d_best_key.ptr, 0xff, nr * sizeof(unsigned long long), c->stream));
     FRAC_HIP(c, hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(c->d_fb_count.ptr), (int)(c->all_fallback ? nr : 0u),
@@ -3098,6 +3100,10 @@ int frac_run(frac_ctx* c)
             c->dirty = true;
         c->prep_knobs = knobs;
     }
+    // a new run owns the records: the previous run's fused-resolver state and its unsettled fallback
+    // (whose saved args may name buffers prepare() is about to reallocate) go, whichever path runs next
+    c->fit_fused = false;
+    c->fb_pending = false;
     if (c->dirty)
         FRAC_TRY(prepare(c));
     int rc;
@@ -3275,6 +3281,10 @@ int frac_set_stream(frac_ctx* c, void* s)
 {
     if (!c)
         return FRAC_E_INVALID;
+    if (c->fb_pending) { // the last run's fallback goes on the stream its search and resolve ran on
+        FRAC_HIP(c, hipSetDevice(c->device));
+        FRAC_TRY(settle_fallback(c));
+    }
     c->stream = s ? reinterpret_cast<hipStream_t>(s) : c->own_stream;
     return FRAC_OK;
 }

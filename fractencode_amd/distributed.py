@@ -110,12 +110,18 @@ class FrameStripes:
         self.full = torch.empty((world * rows, W), dtype=torch.uint8, device=device)
         self.group = group
 
-    def __call__(self):
+    def __call__(self, mark=None):
+        """`mark` (optional): called with "frame_h2d" after the stripe's copy is enqueued and with
+        "frame_allgather" after the all-gather (a phase clock's marks)."""
         import torch.distributed as dist
 
         if self.n:
             self.stripe[: self.n].copy_(self.host, non_blocking=True)
+        if mark:
+            mark("frame_h2d")
         dist.all_gather_into_tensor(self.full, self.stripe, group=self.group)
+        if mark:
+            mark("frame_allgather")
         return self.full[: self.H]
 
 
@@ -158,10 +164,21 @@ class NodeTuples:
         size = -(-self.bytes // mmap.PAGESIZE) * mmap.PAGESIZE
         name = [f"/dev/shm/fracenc_tuples_{os.getpid()}_{secrets.token_hex(6)}" if rank == 0 else None]
         if rank == 0:
-            fd = os.open(name[0], os.O_CREAT | os.O_EXCL | os.O_RDWR, 0o600)
-            os.ftruncate(fd, size)
-            os.close(fd)
+            try:
+                fd = os.open(name[0], os.O_CREAT | os.O_EXCL | os.O_RDWR, 0o600)
+                try:
+                    os.ftruncate(fd, size)
+                finally:
+                    os.close(fd)
+            except OSError as exc:  # every rank learns of it from the broadcast, none waits forever
+                try:
+                    os.unlink(name[0])
+                except OSError:
+                    pass
+                name = [f"error: {exc}"]
         dist.broadcast_object_list(name, src=0, group=group)
+        if name[0].startswith("error: "):
+            raise RuntimeError(f"node tuple buffer: rank 0 could not create its file ({name[0][7:]})")
         try:
             fd = os.open(name[0], os.O_RDWR)
             try:

@@ -33,16 +33,55 @@ def _sink_bytes(e, nr, where):
 @pytest.mark.parametrize("where", ["device", "pinned"])
 @pytest.mark.parametrize("engine", ENGINES)
 @pytest.mark.parametrize("T,cls,thr", [(4, False, 0.0), (8, False, 0.0), (4, True, 0.0), (8, True, 2.0)])
-def test_sink_equals_fetch_tuples(engine, where, T, cls, thr):
+@pytest.mark.parametrize("n", [2, 4, 8, 16])
+def test_sink_equals_fetch_tuples(engine, where, T, cls, thr, n):
+    # every range size with a templated engine (the fused resolvers at n = 2/4/8/16, the SEA paths, the
+    # separate fits), domains 2n at stride n; n = 2 on a 128² crop to keep the pool small
     y = plane("lenna_y")
-    rngs = F.create_uniform_grid(512, 512, 8, 8)
+    if n == 2:
+        y = np.ascontiguousarray(y[192:320, 192:320])
+    H, W = y.shape
+    rngs = F.create_uniform_grid(W, H, n, n)
     with F.Engine(0, T, cls, thr, -1.0, engine) as e:
         e.set_frame(y)
-        e.set_domains(F.create_uniform_grid(512, 512, 16, 8))
+        e.set_domains(F.create_uniform_grid(W, H, 2 * n, n))
         e.set_ranges(rngs)
         got = _sink_bytes(e, len(rngs), where)
         want = e.fetch_tuples().tobytes()
     assert got == want
+
+
+def test_sampled_run_after_a_fused_run_on_one_context():
+    """A context that ran the fused n = 8 Fourier search (its resolvers write the records and the sink, and
+    list fp32-regime ranges for a deferred fallback) and then gets 6×6 ranges (the sampled form: a separate
+    fit, tuples packed after the run): the second run's sink, tuples and records are its own — no stale
+    fused state or deferred fallback of the first run leaks into them."""
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    from fallback_probe import frame
+
+    p = frame(6, 512)  # fp32-regime ranges: the first run leaves a deferred fallback behind
+    doms = F.create_uniform_grid(512, 512, 16, 8)
+    r8 = F.create_uniform_grid(512, 512, 8, 8)
+    r6 = F.create_uniform_grid(512, 512, 6, 6)
+    with F.Engine(0, 4, False, 0.0, -1.0, F.ENGINE_MFMA) as fresh:
+        fresh.set_frame(p)
+        fresh.set_domains(doms)
+        want, _ = fresh.search(r6)
+        want_t = fresh.fetch_tuples().tobytes()
+    with F.Engine(0, 4, False, 0.0, -1.0, F.ENGINE_MFMA) as e:
+        e.set_frame(p)
+        e.set_domains(doms)
+        e.set_ranges(r8)
+        _sink_bytes(e, len(r8), "device")  # the fused run, settled by sync()
+        e.set_ranges(r8)
+        e.run()  # a second fused run whose fallback stays pending (nothing read its records)
+        e.set_ranges(r6)
+        got_sink = _sink_bytes(e, len(r6), "pinned")
+        got, st = e.fetch()
+        got_t = e.fetch_tuples().tobytes()
+    assert st["search_form"] == F.FORM_SAMPLED
+    assert got_sink == want_t and got_t == want_t
+    assert got.tobytes() == want.tobytes()
 
 
 def test_sink_with_fp32_regime_and_empty_ranges():

@@ -12,6 +12,7 @@ A geometry the engine refuses fails its finalize(); the failure comes back on th
 (rethrowIfFailed), not as std::terminate on the core's worker.  Without a device the engine's
 constructor throws where EncodingEngine2.cpp:27-29 catches ("failed to create engine").
 """
+import json
 import os
 import subprocess
 
@@ -39,16 +40,23 @@ def test_binding_compiles_against_reference_headers(tmp_path):
     assert os.path.exists(DRIVER), "oracle/_ref/core_driver not built (__graft_entry__.build)"
 
 
-def _run_core(tmp_path, plane_name, W, H, src, tgt, cls, cpu=False, check=True, devices=None, per_engine=False):
+def _run_core(tmp_path, plane_name, W, H, src, tgt, cls, cpu=False, check=True, devices=None, per_engine=False,
+              mode=None):
     out = tmp_path / f"core_{src}_{tgt}_{cls}_{int(cpu)}.bin"
     plane_path = plane_name if os.path.isabs(plane_name) else os.path.join(GOLD, plane_name + ".u8")
     # cpu: 2 of the reference's CPU engines beside the HIP engine(s) on the core's queue (core_driver's usage note)
     r = subprocess.run([DRIVER, plane_path, str(W), str(H), str(src), str(tgt), str(int(cls)), "0", "-1", str(out),
-                        str(2 if cpu else 0)] + ([devices] if devices else []), timeout=300, capture_output=True,
-                       text=True)
+                        str(2 if cpu else 0)] + ([devices or "0"] if devices or mode else []) + ([mode] if mode else []),
+                       timeout=300, capture_output=True, text=True)
     if not check:
         return r
     assert r.returncode == 0, (r.returncode, r.stdout[-2000:], r.stderr[-2000:])
+    # the timing line (bench.py's drop_in reads it): core.encode()'s time, and the tail engine's hold that
+    # closes the reference core's lost-wakeup window (0 in the batch-claim mode, which has no tail)
+    timing = next(json.loads(ln) for ln in r.stdout.splitlines() if ln.startswith("{"))
+    assert timing["mode"] == (mode or "ref").split(":")[0]
+    assert 0 < timing["records_s"] <= timing["encode_s"] and timing["drop_in_s"] > 0
+    assert (timing["tail_hold_s"] >= 0.02) if timing["mode"] == "ref" else timing["tail_hold_s"] == 0
     raw = out.read_bytes()
     # trailer: rejected, HIP ranges, one count per HIP engine, the number of HIP engines (u64 each)
     k = int(np.frombuffer(raw[-8:], dtype=np.uint64)[0])
@@ -129,4 +137,21 @@ def test_reference_core_with_two_hip_engines_on_one_queue(tmp_path, name, cls, c
               "t": got["transform"], "dist": got["distance"], "s": got["contrast"], "o": got["brightness"]}
     for k in FIELDS:
         np.testing.assert_array_equal(fields[k], rec[k], err_msg=f"{name}: {k}")
+    assert rejected == meta["rejected"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cpu", [False, True], ids=["hip_only", "cpu_and_hip"])
+def test_batch_claim_core_matches_goldens(tmp_path, cpu):
+    """The maintainer patch INTEGRATION.md §Drop-in rate proposes (core_driver MODE batch:K: HIP engines claim
+    K ranges per lock, CPU engines one, a join instead of the predicate-less wait), over the same engines:
+    the records and reject counts are the reference goldens', like the reference's own core."""
+    rec, meta = golden("lenna_t4")
+    got, rejected, hip_ranges = _run_core(tmp_path, "lenna_y", 512, 512, 16, 8, False, cpu=cpu, mode="batch:256")
+    assert len(got) == len(rec["x"])
+    assert (0 < hip_ranges < len(got)) if cpu else (hip_ranges == len(got))
+    fields = {"x": got["x"], "y": got["y"], "dx": got["dx"], "dy": got["dy"], "dw": got["sw"], "dh": got["sh"],
+              "t": got["transform"], "dist": got["distance"], "s": got["contrast"], "o": got["brightness"]}
+    for k in FIELDS:
+        np.testing.assert_array_equal(fields[k], rec[k], err_msg=k)
     assert rejected == meta["rejected"]
