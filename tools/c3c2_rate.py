@@ -3,7 +3,7 @@
 FRAC_LIB names (or the product): C3 (4096² S1, T = 4) per-run device / search / finish ms (library HIP
 events, median of `--c3` runs after 2 warm-ups) and C2 (Lenna 512², T = 8 and 4) µs per frame enqueued back
 to back and event-timed (median).  Run it alternately per library for an interleaved A/B
-(tools/sessions/r05_*.sh).  usage: tools/c3c2_rate.py [--c3 K] [--c2 K]"""
+(tools/session.sh paths).  usage: tools/c3c2_rate.py [--c3 K] [--c2 K]"""
 import argparse
 import json
 import os
