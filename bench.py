@@ -99,6 +99,10 @@ def parse(argv=None):
     ap.add_argument("--drop-in", type=int, default=1,
                     help="N = 1: time the frame through the reference's own core (oracle/_ref/core_driver; 0 = skip)")
     ap.add_argument("--out", default=None, help="also write the line to this file (rank 0)")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="N > 1: the process group's backend (nccl = RCCL; gloo only for tests)")
+    ap.add_argument("--share-gpu", action="store_true",
+                    help="test only: every rank on GPU 0 (a one-GPU box; with --backend gloo)")
     ap.add_argument("--ab", action="store_true",
                     help="allow FRAC_LIB / A/B knobs in the environment (the line is then marked, not a headline)")
     return ap.parse_args(argv)
@@ -230,6 +234,7 @@ def drop_in(frame: np.ndarray, timeout_s: float = 240.0) -> dict:
             out["runs"][name] = {"value": round(n / rec["drop_in_s"], 1), "unit": "range-blocks/s",
                                  "drop_in_s": rec["drop_in_s"], "encode_s": rec["encode_s"],
                                  "tail_hold_s": rec["tail_hold_s"], "records_s": rec["records_s"],
+                                 "hip_search_s": rec["hip_search_s"], "hip_handback_s": rec["hip_handback_s"],
                                  "cpu_engines": ncpu, "mode": mode, "hip_ranges": hip_ranges,
                                  "records": int((len(raw) - 8 * (3 + k)) // 64)}
     return out
@@ -598,8 +603,11 @@ def _setup(args, backend: str, cuda: bool):
     if world != args.gpus:
         raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     one_host = True
+    share = cuda and getattr(args, "share_gpu", False)
+    if share and backend == "nccl" and world > 1:
+        raise SystemExit("bench.py: --share-gpu needs --backend gloo (RCCL takes one rank per GPU)")
     if cuda:
-        dev = torch.device("cuda", local if world > 1 else 0)
+        dev = torch.device("cuda", local if world > 1 and not share else 0)
         torch.cuda.set_device(dev)
     else:
         dev = torch.device("cpu")
@@ -612,7 +620,7 @@ def _setup(args, backend: str, cuda: bool):
         where = [None] * world
         name = torch.cuda.get_device_name(dev) if cuda else "cpu"
         dist.all_gather_object(where, (socket.gethostname(), local, name))
-        if cuda and len({(h, d) for h, d, _ in where}) != world:
+        if cuda and not share and len({(h, d) for h, d, _ in where}) != world:
             raise SystemExit(f"bench.py: ranks share a GPU: {where}")
         one_host = len({h for h, _, _ in where}) == 1
     return world, rank, dev, one_host
@@ -646,7 +654,7 @@ def _run_leg(step, steps: int, warmup: int, world: int, dev):
     return timed(step, steps, world, dev)
 
 
-def main(args, engine_factory=None, backend: str = "nccl", cuda: bool = True) -> dict:
+def main(args, engine_factory=None, backend: str | None = None, cuda: bool = True) -> dict:
     """The bench on this rank.  `engine_factory(dev, transforms, engine_id, timing)` builds an engine (default:
     the HIP library's), `backend` the process group's (nccl = RCCL), `cuda` whether ranks own a GPU; the
     CPU tests pass the oracle stand-in, gloo and False.  Rank 0 prints the line and returns it."""
@@ -659,6 +667,7 @@ def main(args, engine_factory=None, backend: str = "nccl", cuda: bool = True) ->
 
     product = engine_factory is None
     engine_factory = engine_factory or hip_engine
+    backend = backend or args.backend
     knobs = check_headline_env(args)
     build = F.build_info()
     if product and not build["matches_sources"] and not args.ab:

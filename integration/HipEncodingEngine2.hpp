@@ -36,6 +36,7 @@
 #include "encode/EncodingEngine2.hpp"
 #include "fracenc.h"
 
+#include <chrono>
 #include <cstddef>
 #include <exception>
 #include <stdexcept>
@@ -101,15 +102,20 @@ public:
     void finalize() noexcept override
     {
         try {
+            using Clock = std::chrono::steady_clock;
+            const auto t0 = Clock::now();
             _records.resize(_pending.size());
             frac_stats st{};
             check(frac_search(_ctx, reinterpret_cast<const frac_grid_item*>(_pending.data()), _pending.size(),
                               reinterpret_cast<frac_encode_item*>(_records.data()), &st));
+            const auto t1 = Clock::now();
             _rejected += st.rejected_mappings;
             _next = 0;
             for (const auto& item : _pending)
                 AbstractEncodingEngine2::encode(item); // → encode_impl → _records[_next++]
             _searched += _pending.size();
+            _searchSeconds += std::chrono::duration<double>(t1 - t0).count();
+            _handbackSeconds += std::chrono::duration<double>(Clock::now() - t1).count();
         } catch (...) {
             _failed = std::current_exception();
             _lost += _pending.size();
@@ -132,6 +138,10 @@ public:
     // ranges searched by this engine / claimed but lost to a failure
     size_t searchedRanges() const noexcept { return _searched; }
     size_t lostRanges() const noexcept { return _lost; }
+    // seconds finalize() spent in frac_search (upload of the claims, search, records back) and handing the
+    // records to the base class's encode() (the core's per-item result list)
+    double searchSeconds() const noexcept { return _searchSeconds; }
+    double handbackSeconds() const noexcept { return _handbackSeconds; }
 
 protected:
     encode_item_t encode_impl(const UniformGridItem& targetItem) const override
@@ -156,6 +166,7 @@ private:
     mutable size_t _next = 0;
     uint64_t _rejected = 0;
     size_t _searched = 0, _lost = 0;
+    double _searchSeconds = 0.0, _handbackSeconds = 0.0;
     std::exception_ptr _failed;
 };
 

@@ -283,10 +283,16 @@ int main(int argc, char** argv)
         auto sec = [&](Clock::time_point t) { return std::chrono::duration<double>(t - t0).count(); };
         const double encode_s = sec(t1), records_s = sec(line.last);
         const double hold_s = tail ? std::chrono::duration<double>(tail->released - line.last).count() : 0.0;
+        double search_s = 0.0, handback_s = 0.0; // summed over the HIP engines (they run concurrently)
+        for (auto* hip : hips) {
+            search_s += hip->searchSeconds();
+            handback_s += hip->handbackSeconds();
+        }
         std::printf("{\"mode\": \"%s\", \"batch\": %zu, \"ranges\": %zu, \"cpu_engines\": %d, \"hip_engines\": %zu, "
-                    "\"encode_s\": %.6f, \"records_s\": %.6f, \"tail_hold_s\": %.6f, \"drop_in_s\": %.6f}\n",
+                    "\"encode_s\": %.6f, \"records_s\": %.6f, \"tail_hold_s\": %.6f, \"drop_in_s\": %.6f, "
+                    "\"hip_search_s\": %.6f, \"hip_handback_s\": %.6f}\n",
                     batch ? "batch" : "ref", batch, targetGrid.items().size(), ncpu, hips.size(), encode_s, records_s,
-                    hold_s, encode_s - hold_s);
+                    hold_s, encode_s - hold_s, search_s, handback_s);
         std::fflush(stdout);
     }
     for (auto* hip : hips) {
