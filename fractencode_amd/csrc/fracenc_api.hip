@@ -722,8 +722,10 @@ int prepare(frac_ctx* c)
         if ((uint64_t)r.x + r.w > c->tgt.w || (uint64_t)r.y + r.h > c->tgt.h)
             return c->fail(FRAC_E_INVALID, "range outside the target plane");
     }
-    if (nw < 2 || nw > kGenMaxN || nh < 2 || nh > kGenMaxN)
-        return c->fail(FRAC_E_INVALID, "range sides must be 2..256");
+    if (nw < 2 || nh < 2)
+        return c->fail(FRAC_E_INVALID, "range sides must be at least 2");
+    if ((uint64_t)nw * nh > (1ull << 26))
+        return c->fail(FRAC_E_INVALID, "ranges of more than 2^26 pixels");
     // domains: validated by frac_set_domains (one size, inside the plane); re-checked against the
     // current plane, which may have changed since
     const uint32_t Sw = c->doms.empty() ? 2u * nw : c->doms[0].w;
@@ -834,7 +836,10 @@ int prepare(frac_ctx* c)
     for (int b = 0; b < nb; ++b)
         c->eligible_pairs += (uint64_t)L.rcnt[b] * L.dcnt[b];
     c->hitH = compute_hit_limit(c->p.rms_threshold, Sw * Sh); // the domain's area (image/metrics.h:49)
-    c->all_fallback = c->hitH >= kExactLimit;
+    // every candidate in the reference's fp32 arithmetic (gen_fallback): with a threshold no exact error can
+    // meet, and for range sides above kGenMaxN, whose S16 outgrows the search keys' error field — there the
+    // exact search could not order the candidates, and S16 ≥ 2^24 is the fp32 regime anyway for almost all
+    c->all_fallback = c->hitH >= kExactLimit || nw > kGenMaxN || nh > kGenMaxN;
 
     // engine.  MFMA: exact for every templated n (n = 16 through search_mfma16's integer epilogue).
     // SEA covers n ≤ 8 (its exact evaluation holds a candidate in one wave's VGPRs): larger ranges run

@@ -130,9 +130,10 @@ struct GenSearchArgs {
     unsigned long long* best_key;
 };
 
-// Range sides up to 256 (match_generic takes any size, transformmatcher.h:80-111; the CLI any
+// Range sides up to 256 search exactly (match_generic takes any size, transformmatcher.h:80-111; the CLI any
 // 2 ≤ target < source, main.cpp:99): the largest S16 of a 256×256 range, 65,536 · 1020², stays below
-// 2^36, the key's error field (fracenc_common.h key_miss).
+// 2^36, the key's error field (fracenc_common.h key_miss).  Larger ranges run every candidate through
+// gen_fallback's fp32 replay of the reference (prepare() sets all_fallback).
 constexpr uint32_t kGenMaxN = 256;
 // gen_search holds the range in LDS (as 4r) in chunks of kGenChunk pixels per wave
 constexpr uint32_t kGenChunk = 4096;

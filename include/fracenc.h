@@ -14,9 +14,10 @@
  *    to the later transform; the first candidate with distance <= rms_threshold
  *    wins (early exit); distance is the reference's unfitted fp32 error;
  *  - contrast / brightness follow TransformMatcher::match_generic bit-for-bit;
- *  - geometry: n x n ranges (2 <= n <= 256) and S x S domains with S > n, the pairs the reference
- *    CLI accepts (main.cpp:99); S = 2n is the decimate-then-permute path, any other pair — the
- *    CLI default 16 -> 4 (match_16to4) included — samples as RootMeanSquare does;
+ *  - geometry: n x n ranges (n >= 2; Size32u rectangles too) and S x S domains with S > n, the pairs
+ *    the reference CLI accepts (main.cpp:99); S = 2n is the decimate-then-permute path, any other
+ *    pair — the CLI default 16 -> 4 (match_16to4) included — samples as RootMeanSquare does; range
+ *    sides above 256 run every candidate in the reference's fp32 arithmetic (slower, same records);
  *  - results are returned in the order the ranges were given.
  * All entry points return 0 on success and a negative FRAC_E* code on error;
  * frac_last_error() gives the message.  Not thread-safe per context.

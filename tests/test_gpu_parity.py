@@ -211,10 +211,37 @@ def test_invalid_geometry_is_an_error(engine):
     with F.Engine(0, 4, engine=engine) as e:
         e.set_frame(np.zeros((512, 512), np.uint8))
         e.set_domains(F.create_uniform_grid(512, 512, 512, 256))
-        with pytest.raises(F.FracError, match="2..256"):  # ranges above the 256×256 limit (the key's S16 field)
-            e.search(np.array([(0, 0, 300, 300, -1)], dtype=F.GRID_ITEM))
-        out, _ = e.search(np.array([(0, 0, 256, 256, -1)], dtype=F.GRID_ITEM))  # the largest accepted
+        with pytest.raises(F.FracError, match="at least 2"):
+            e.search(np.array([(0, 0, 1, 1, -1)], dtype=F.GRID_ITEM))
+        out, _ = e.search(np.array([(0, 0, 256, 256, -1)], dtype=F.GRID_ITEM))  # the largest exact-search side
         assert out["sw"][0] == 512 and out["distance"][0] == 0.0
+
+
+@pytest.mark.parametrize("cls", [False, True])
+@pytest.mark.parametrize("engine", ENGINES)
+def test_range_sides_above_256(oracle, engine, cls):
+    """Range sides above 256 (the CLI accepts any 2 <= target < source, main.cpp:99; match_generic any size,
+    transformmatcher.h:80-111): every candidate in the reference's fp32 arithmetic (gen_fallback), records
+    equal to the oracle's — 320×320 ranges against 640×640 domains at stride 320 on a 1024² S1 frame, and
+    rectangles of 272×300 against 544×600 at stride (272, 300)."""
+    from fractencode_amd.synth import value_noise
+
+    p = value_noise(1024, 1024, 77)
+    for (rw, rh) in ((320, 320), (272, 300)):
+        doms = F.create_uniform_grid(1024, 1024, (2 * rw, 2 * rh), (rw, rh))
+        rngs = F.create_uniform_grid(1024, 1024, (rw, rh), (rw, rh))
+        if cls:
+            doms, rngs = F.preclassify(p, doms), F.preclassify(p, rngs)
+        with F.Engine(0, 4, cls, 0.0, -1.0, engine) as e:
+            e.set_frame(p)
+            e.set_domains(doms)
+            out, st = e.search(rngs)
+        want, rej, _ = oracle.estimate(p, doms.astype(oracle.ITEM_DTYPE), rngs.astype(oracle.ITEM_DTYPE),
+                                       use_classifier=cls)
+        assert_same(out, {k: want[k] for k in FIELDS}, f"{rw}x{rh}")
+        assert st["fallback_ranges"] == len(rngs) - st["empty_ranges"]
+        if cls:
+            assert st["rejected_mappings"] == rej
 
 
 def _recompute_s16(p, out, n=8):

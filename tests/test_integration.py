@@ -105,17 +105,15 @@ def test_reference_core_with_hip_engine_matches_goldens(tmp_path, name, src, tgt
 
 @pytest.mark.gpu
 def test_hip_engine_failure_comes_back_on_the_callers_thread(tmp_path):
-    # 512×512 ranges against 1024×1024 domains (the CLI accepts them, main.cpp:99; the grids are aligned,
-    # image/partition2.hpp:119) are beyond the engine's range sides (2..256, the largest whose S16 fits the
-    # key): frac_search fails inside finalize() on the core's worker thread; the binding keeps the error and
-    # the driver's rethrowIfFailed() reports it after the workers joined (exit 6), where a throw on the
+    # 16×16 ranges against 8×8 domains (the CLI refuses them, main.cpp:99; the driver does not check): the
+    # engine's constructor accepts the domain grid, frac_search fails inside finalize() on the core's worker
+    # thread ("domains must be wider than the ranges", metrics.h:39's FRAC_ASSERT); the binding keeps the error
+    # and the driver's rethrowIfFailed() reports it after the workers joined (exit 6), where a throw on the
     # worker would have been std::terminate (SIGABRT)
-    plane = tmp_path / "flat1024.u8"
-    np.full((1024, 1024), 77, np.uint8).tofile(plane)
-    r = _run_core(tmp_path, str(plane), 1024, 1024, 1024, 512, False, check=False)
+    r = _run_core(tmp_path, "lenna_y", 512, 512, 8, 16, False, check=False)
     assert r.returncode == 6, (r.returncode, r.stdout[-2000:], r.stderr[-2000:])
-    assert "HIP engine failed" in r.stderr and "range sides must be 2..256" in r.stderr
-    assert "4 ranges without a record" in r.stderr
+    assert "HIP engine failed" in r.stderr and "domains must be wider than the ranges" in r.stderr
+    assert "1024 ranges without a record" in r.stderr
 
 
 @pytest.mark.gpu
