@@ -23,9 +23,10 @@
 //   patch INTEGRATION.md §Drop-in rate proposes, restated here over the same engines (one lock claims up to K
 //   items, no yield per item, a predicate wait) — for timing the patch, never for parity.
 //   A tail engine (below) is registered last in "ref" mode: the core's lost final wakeup cannot happen.
-//   stdout: one JSON line {"encode_s", "records_s", "tail_hold_s", "drop_in_s", ...} — core.encode()'s wall
-//   time, the time the last real engine's finalize() returned, the tail's hold, and encode_s − tail_hold_s
-//   (the core's time with a wait that loses nothing).
+//   stdout: one JSON line {"encode_s", "records_s", "tail_hold_s", "drop_in_s", "construct_s", ...} —
+//   core.encode()'s wall time, the time the last real engine's finalize() returned, the tail's hold,
+//   encode_s − tail_hold_s (the core's time with a wait that loses nothing), and the construction of the core
+//   and its engines before it (HIP runtime start, frame and domain upload: inside Encoder2's timer too).
 //   OUT.bin: the core's result().encoded (encode_item_t, 64 B each) in the core's order, then the
 //   rejected-mapping count of the whole search (u64: the CPU engines' estimator plus the HIP
 //   engines'), the number of ranges the HIP engines searched (u64), each HIP engine's own count
@@ -236,6 +237,8 @@ int main(int argc, char** argv)
     TransformEstimator2 estimator(image, image, std::move(classifier),
                                   std::make_shared<TransformMatcher>(params.rmsThreshold, params.sMax), sourceGrid);
     NullReporter reporter;
+    // Encoder2's timer (main.cpp:164-167) starts before the core and its engines are constructed
+    const auto tc = std::chrono::steady_clock::now();
     EncodingEngineCore2 core(params, image, sourceGrid, estimator, &reporter);
     FinishLine line;
     for (int i = 0; i < ncpu; ++i) { // EncodingEngine2.cpp:12-20's engines, k of them
@@ -282,6 +285,7 @@ int main(int argc, char** argv)
     {
         auto sec = [&](Clock::time_point t) { return std::chrono::duration<double>(t - t0).count(); };
         const double encode_s = sec(t1), records_s = sec(line.last);
+        const double construct_s = std::chrono::duration<double>(t0 - tc).count(); // the core + every engine
         const double hold_s = tail ? std::chrono::duration<double>(tail->released - line.last).count() : 0.0;
         double search_s = 0.0, handback_s = 0.0; // summed over the HIP engines (they run concurrently)
         for (auto* hip : hips) {
@@ -290,9 +294,9 @@ int main(int argc, char** argv)
         }
         std::printf("{\"mode\": \"%s\", \"batch\": %zu, \"ranges\": %zu, \"cpu_engines\": %d, \"hip_engines\": %zu, "
                     "\"encode_s\": %.6f, \"records_s\": %.6f, \"tail_hold_s\": %.6f, \"drop_in_s\": %.6f, "
-                    "\"hip_search_s\": %.6f, \"hip_handback_s\": %.6f}\n",
+                    "\"hip_search_s\": %.6f, \"hip_handback_s\": %.6f, \"construct_s\": %.6f}\n",
                     batch ? "batch" : "ref", batch, targetGrid.items().size(), ncpu, hips.size(), encode_s, records_s,
-                    hold_s, encode_s - hold_s, search_s, handback_s);
+                    hold_s, encode_s - hold_s, search_s, handback_s, construct_s);
         std::fflush(stdout);
     }
     for (auto* hip : hips) {
