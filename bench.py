@@ -10,15 +10,17 @@ Ranges are sharded contiguously over ranks (fixed total work: strong scaling).
 wraps (main.cpp:164-168, the whole Encoder2): per step the frame H2D from pinned host memory
 (N > 1: each rank uploads its 1/N stripe of the rows and an RCCL all-gather assembles the frame
 on every rank over xGMI), domain-pool build, search, winner fit and fp32 fallback of this
-rank's shard, its 32-byte (domain, transform, s, o, rms) tuples written by the resolve, the RCCL
-all-gather of every rank's tuples (N > 1, north_star's exchange) and the gathered tuples D2H into
-pinned host memory — serial, one frame after another.  Beside it the line carries:
+rank's shard, its 32-byte (domain, transform, s, o, rms) tuples written by the resolve — at N = 1 straight
+into pinned host memory; at N > 1 (ranks on one host) each rank's resolve writes its shard's tuples into one node-shared pinned host
+buffer, one 4-byte RCCL all-reduce per frame marks it complete (with ranks on several hosts: the RCCL
+all-gather of the tuples + rank 0's D2H) — serial, one frame after another.  Beside it the line carries:
   phases_ms     per phase (frame H2D, frame all-gather, run = prep + search + finish, tuple exchange)
                 the mean over the timed steps, MAX over ranks (phases_ms_by_rank: every rank's)
   rank_ms_per_step  every rank's own step time (ms_per_step / value are the slowest rank's)
-  node_value    N > 1 on one host: the same step with every rank's resolve writing its shard's tuples
-                into one node-shared pinned host buffer instead of the tuple all-gather (--tuples node
-                makes that the headline and the all-gather `gather_value`)
+  gather_value  N > 1: the same step with north_star's RCCL all-gather of the tuples + rank 0's D2H in place
+                of the headline's node-shared host buffer (every rank's resolve writing its shard's tuples
+                into one pinned buffer mapped by all; --tuples gather swaps the two: `node_value`); the
+                records check `gather_equals_headline` verifies the node buffer against it in the same run
   device_value  the same search with the frame already resident in HBM and the tuples left there
                 (the all-gather still runs for N > 1): the device-only rate
   stream_value  the end-to-end step through two contexts alternating frames, so frame k+1's
@@ -93,9 +95,11 @@ def parse(argv=None):
                     help="steps of the VALU engine (north_star's no-MFMA formulation) reported beside (0 = skip)")
     ap.add_argument("--side-steps", type=int, default=-1,
                     help="steps of the device-resident, stream, other-tuples and C5 legs (-1 = --steps, 0 = skip)")
-    ap.add_argument("--tuples", default="gather", choices=["gather", "node"],
-                    help="N > 1: the headline's tuple exchange — the RCCL all-gather + download (gather, north_star's "
-                         "design) or, ranks on one host, one node-shared host buffer (node); the other is a side leg")
+    ap.add_argument("--tuples", default="node", choices=["node", "gather"],
+                    help="N > 1: the headline's tuple exchange — ranks on one host: one node-shared host buffer every "
+                         "rank's resolve writes its shard into (node); the RCCL all-gather + rank 0's download (gather, "
+                         "north_star's design; always with ranks on several hosts); the other is a side leg, and the "
+                         "line checks that both give the same tuples")
     ap.add_argument("--drop-in", type=int, default=1,
                     help="N = 1: time the frame through the reference's own core (oracle/_ref/core_driver; 0 = skip)")
     ap.add_argument("--out", default=None, help="also write the line to this file (rank 0)")
@@ -374,7 +378,8 @@ class FrameStep:
     """The headline step (BASELINE.md "Metric"): the frame H2D from the caller's
     pinned host plane, the search of this rank's shard (frame-dependent preparation included), the
     shard's 32-byte tuples into the all-gather buffer, the all-gather (whenever a process group is
-    up), and the gathered tuples D2H into pinned host memory.  `device_resident=True`: the frame is
+    up), and the gathered tuples D2H into rank 0's pinned host memory (the frame's result reaches the host once;
+    the other ranks keep the gathered tuples on the device).  `device_resident=True`: the frame is
     not uploaded and the gathered tuples stay on the device (the device-only leg).
     `stripes` (default: with more than one rank): each rank uploads only its 1/N stripe of the frame's
     rows across its own PCIe link and one all-gather assembles the frame on every rank over xGMI,
@@ -462,8 +467,8 @@ class FrameStep:
             t = np.ascontiguousarray(self.eng.fetch_tuples())
             self.local[: self.n_mine * TUPLE_BYTES] = torch.from_numpy(t.view(np.uint8))
         self.gathered = gather_tuples(self.local, self.plan)
-        if not self.device_resident:
-            self.h_out.copy_(self.gathered, non_blocking=True)  # D2H into pinned memory
+        if not self.device_resident and self.rank == 0:  # the frame's tuples reach the host once: rank 0's D2H
+            self.h_out.copy_(self.gathered, non_blocking=True)  # into pinned memory
         self._mark("tuples")
 
     def _node_step(self) -> None:
@@ -492,7 +497,7 @@ class FrameStep:
 
     def tuples_bytes(self) -> bytes:
         """The last step's gathered tuples (after a synchronisation)."""
-        src = self.gathered if self.device_resident else self.h_out
+        src = self.gathered if self.device_resident or (self.node is None and self.rank != 0) else self.h_out
         return src.cpu().numpy().tobytes()
 
     def own_slice_ok(self, own: bytes) -> bool:
@@ -786,8 +791,8 @@ def main(args, engine_factory=None, backend: str | None = None, cuda: bool = Tru
                  "+ search + fit of the rank's shard + " +
                  ("its 32-byte tuples written by the resolve into the node's shared pinned tuple buffer + a "
                   "4-byte RCCL all-reduce per frame" if tuples_out == "node" else
-                  "32-byte tuples written by the resolve into the all-gather buffer + RCCL all-gather + gathered "
-                  "tuples D2H (pinned)")) +
+                  "32-byte tuples written by the resolve into the all-gather buffer + RCCL all-gather + the gathered "
+                  "tuples D2H into rank 0's pinned memory")) +
                 "; serial, barrier + synchronisation around the timed steps, slowest rank",
         "tuples_out": tuples_out,
         "rank_ms_per_step": [round(1e3 * s / args.steps, 3) for s in rank_s],
