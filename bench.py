@@ -23,8 +23,8 @@ all-gather of the tuples + rank 0's D2H) — serial, one frame after another.  B
                 records check `gather_equals_headline` verifies the node buffer against it in the same run
   device_value  the same search with the frame already resident in HBM and the tuples left there
                 (the all-gather still runs for N > 1): the device-only rate
-  stream_value  the end-to-end step through two contexts alternating frames, so frame k+1's
-                upload and frame k−1's download overlap frame k's search
+  stream_value  a frame stream: frame k+1's H2D on a copy stream overlaps frame k's search on the
+                compute stream (one context; frac_set_frame_device_async), tuples into pinned memory
   c5            BASELINE configs[4]: the S1 RGB 4096² frame H2D (N > 1: row stripes + all-gather),
                 rgb2yuv on the device, every plane's shard searched, one all-gather of the three
                 planes' tuples, D2H — range-blocks/s over Y + U + V
@@ -848,36 +848,51 @@ def main(args, engine_factory=None, backend: str | None = None, cuda: bool = Tru
             if dk > 0:
                 roof["kernel_ms_device"] = round(dk, 3)
                 roof["frac_device"] = round(work / (dk * 1e-3) / 1e12 / peak, 4)
-        # a frame stream: two contexts in turn, frame k+1 uploads on one context's stream while frame k
-        # searches on the other's, and frame k's tuples come back while k+1 searches (per rank, no gather)
-        tup = None
-        if len(mine):
-            if cuda:
-                h_tuples = [torch.empty(len(mine) * TUPLE_BYTES, dtype=torch.uint8).pin_memory() for _ in range(2)]
-                tup = [h.numpy().view(F.TUPLE) for h in h_tuples]
-            else:
-                tup = [np.zeros(len(mine), dtype=F.TUPLE) for _ in range(2)]
-        with new_engine() as eng2:
-            eng.set_frame(h_frame.numpy())
-            eng2.set_frame(h_frame.numpy())
-            eng2.set_domains(doms)
-            eng2.set_ranges(mine)
-            ctxs = (eng, eng2)
+        # a frame stream on one context and one compute stream: frame k+1's H2D runs on a copy stream of its own
+        # while frame k searches; the context's stream waits for that upload (an event), copies the plane
+        # device-to-device (frac_set_frame_device_async, ABI 9) and runs, the resolve writing the frame's tuples
+        # into one of two pinned buffers (per rank, no gather).  CPU stand-in engines: the same frames in turn.
+        if cuda:
+            up = torch.cuda.Stream(dev)
+            d_bufs = [torch.empty((S, S), dtype=torch.uint8, device=dev) for _ in range(2)]
+            up_ev = [torch.cuda.Event() for _ in range(2)]
+            free_ev = [torch.cuda.Event() for _ in range(2)]
+            for ev in free_ev:
+                ev.record(stream)
+            h_tup = [torch.zeros(max(1, len(mine)) * TUPLE_BYTES, dtype=torch.uint8).pin_memory() for _ in range(2)]
 
             def stream_steps():
-                for k in range(side_steps + 1):
-                    if k < side_steps:
-                        ctxs[k & 1].set_frame(h_frame.numpy())  # waits for this context's own upload only
-                        ctxs[k & 1].run()
-                    if k > 0 and tup is not None:
-                        ctxs[(k - 1) & 1].fetch_tuples(tup[(k - 1) & 1])  # frame k−1's winners
+                for k in range(side_steps):
+                    j = k & 1
+                    up.wait_event(free_ev[j])  # the buffer's previous frame has been copied out of it
+                    with torch.cuda.stream(up):
+                        d_bufs[j].copy_(h_frame, non_blocking=True)
+                    up_ev[j].record(up)
+                    stream.wait_event(up_ev[j])
+                    eng.set_frame_device_async(d_bufs[j])
+                    free_ev[j].record(stream)
+                    if len(mine):
+                        eng.set_tuple_sink(h_tup[j].data_ptr())
+                    eng.run()
+                eng.set_tuple_sink(None)
+        else:
+            h_tup = [torch.zeros(max(1, len(mine)) * TUPLE_BYTES, dtype=torch.uint8) for _ in range(2)]
 
-            stream_steps()
-            _, ssec = timed(stream_steps, 1, world, dev)
-            line["stream_value"] = {"value": round(nr_total / (ssec / side_steps), 1),
-                                    "ms_per_step": round(1e3 * ssec / side_steps, 3), "steps": side_steps,
-                                    "step": "frame H2D + search + tuples D2H per frame, two contexts alternating "
-                                            "frames" + (" (per rank, no gather)" if world > 1 else "")}
+            def stream_steps():
+                for k in range(side_steps):
+                    eng.set_frame(frame)
+                    eng.run()
+                    if len(mine):
+                        eng.fetch_tuples(h_tup[k & 1].numpy().view(F.TUPLE))
+
+        stream_steps()
+        _, ssec = timed(stream_steps, 1, world, dev)
+        checks["stream_leg_equals_e2e"] = h_tup[(side_steps - 1) & 1].numpy().tobytes()[: len(own)] == own
+        line["stream_value"] = {"value": round(nr_total / (ssec / side_steps), 1),
+                                "ms_per_step": round(1e3 * ssec / side_steps, 3), "steps": side_steps,
+                                "step": "per frame: H2D on a copy stream overlapped with the previous frame's search, "
+                                        "device-to-device copy + search + tuples written by the resolve into pinned "
+                                        "memory on the compute stream" + (" (per rank, no gather)" if world > 1 else "")}
         eng.set_frame(d_frame if cuda else frame)
         eng.run()
 

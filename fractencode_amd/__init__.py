@@ -174,6 +174,7 @@ def lib() -> C.CDLL:
             "frac_set_frame": (i32, [vp, vp, u32, u32, u32]),
             "frac_set_planes": (i32, [vp, vp, u32, u32, u32, vp, u32, u32, u32]),
             "frac_set_frame_device": (i32, [vp, vp, u32, u32, u32]),
+            "frac_set_frame_device_async": (i32, [vp, vp, u32, u32, u32]),
             "frac_set_domains": (i32, [vp, vp, sz]),
             "frac_set_ranges": (i32, [vp, vp, sz]),
             "frac_run": (i32, [vp]),
@@ -347,6 +348,16 @@ class Engine:
         plane = np.ascontiguousarray(plane, dtype=np.uint8)
         self._check(lib().frac_set_frame(self._ctx, plane.ctypes.data, plane.shape[1], plane.shape[0],
                                          plane.shape[1]))
+
+    def set_frame_device_async(self, plane) -> None:
+        """ABI 9: a CUDA uint8 [H, W] plane copied on this engine's stream without waiting (frame streaming).
+        The caller orders the plane's producer before this engine's stream (e.g. an event the stream waits on)
+        and keeps the plane unchanged until the stream has passed the copy."""
+        if not (hasattr(plane, "is_cuda") and plane.is_cuda) or plane.dim() != 2 or plane.stride(1) != 1:
+            raise FracError("set_frame_device_async: a 2-D CUDA uint8 plane with contiguous rows")
+        self._frame_wh = (int(plane.shape[1]), int(plane.shape[0]))
+        self._check(lib().frac_set_frame_device_async(self._ctx, C.c_void_p(plane.data_ptr()), plane.shape[1],
+                                                      plane.shape[0], plane.stride(0)))
 
     def set_planes(self, source: np.ndarray, target: np.ndarray) -> None:
         self._frame_wh = (int(source.shape[1]), int(source.shape[0]))

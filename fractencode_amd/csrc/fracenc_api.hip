@@ -3029,6 +3029,7 @@ int frac_set_planes(frac_ctx* c, const uint8_t* src, uint32_t sw, uint32_t sh, u
     const bool same = tgt == nullptr || tgt == src;
     if (!same && (tw == 0 || th == 0 || tstride < tw))
         return c->fail(FRAC_E_INVALID, "invalid target plane");
+    FRAC_TRY(settle_fallback(c)); // the last run's fp32-regime ranges read the planes the uploads overwrite
     FRAC_TRY(upload_plane(c, src, sw, sh, sstride, c->d_src, c->d_sstride));
     if (!same)
         FRAC_TRY(upload_plane(c, tgt, tw, th, tstride, c->d_tgt, c->d_tstride));
@@ -3041,20 +3042,37 @@ int frac_set_frame(frac_ctx* c, const uint8_t* plane, uint32_t w, uint32_t h, ui
     return frac_set_planes(c, plane, w, h, stride, nullptr, 0, 0, 0);
 }
 
-int frac_set_frame_device(frac_ctx* c, const void* d_plane, uint32_t w, uint32_t h, uint32_t stride)
+static int set_frame_device(frac_ctx* c, const void* d_plane, uint32_t w, uint32_t h, uint32_t stride, bool wait)
 {
     if (!c)
         return FRAC_E_INVALID;
     if (!d_plane || w == 0 || h == 0 || stride < w)
         return c->fail(FRAC_E_INVALID, "invalid device plane");
     FRAC_HIP(c, hipSetDevice(c->device));
+    FRAC_TRY(settle_fallback(c)); // the last run's fp32-regime ranges read the plane this copy overwrites
     // the frame stays on the device: the classifier pre-pass runs there too
     c->d_sstride = (w + 63u) & ~63u;
     FRAC_HIP(c, c->d_src.ensure((size_t)c->d_sstride * (h + 1)));
-    FRAC_HIP(c, hipMemcpy2DAsync(c->d_src.ptr, c->d_sstride, d_plane, stride, w, h, hipMemcpyDeviceToDevice, c->stream));
-    FRAC_HIP(c, hipStreamSynchronize(c->stream));
+    if (stride == c->d_sstride) // rows already at the device pitch: one linear copy (the 2-D path is slower)
+        FRAC_HIP(c, hipMemcpyAsync(c->d_src.ptr, d_plane, (size_t)stride * (h - 1) + w, hipMemcpyDeviceToDevice,
+                                   c->stream));
+    else
+        FRAC_HIP(c, hipMemcpy2DAsync(c->d_src.ptr, c->d_sstride, d_plane, stride, w, h, hipMemcpyDeviceToDevice,
+                                     c->stream));
+    if (wait)
+        FRAC_HIP(c, hipStreamSynchronize(c->stream));
     planes_changed(c, w, h, w, h, true);
     return FRAC_OK;
+}
+
+int frac_set_frame_device(frac_ctx* c, const void* d_plane, uint32_t w, uint32_t h, uint32_t stride)
+{
+    return set_frame_device(c, d_plane, w, h, stride, true);
+}
+
+int frac_set_frame_device_async(frac_ctx* c, const void* d_plane, uint32_t w, uint32_t h, uint32_t stride)
+{
+    return set_frame_device(c, d_plane, w, h, stride, false);
 }
 
 int frac_set_domains(frac_ctx* c, const frac_grid_item* d, size_t nd)

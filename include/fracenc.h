@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define FRAC_ABI_VERSION 8
+#define FRAC_ABI_VERSION 9
 
 /* error codes */
 #define FRAC_OK 0
@@ -154,6 +154,12 @@ int frac_set_planes(frac_ctx* ctx, const uint8_t* src, uint32_t sw, uint32_t sh,
                     const uint8_t* tgt, uint32_t tw, uint32_t th, uint32_t tstride);
 /* Planes already in device memory (e.g. a torch tensor in HBM): copied device-to-device. */
 int frac_set_frame_device(frac_ctx* ctx, const void* d_plane, uint32_t w, uint32_t h, uint32_t stride);
+/* ABI 9: the same copy enqueued on the context's stream without waiting for it, so a caller can stream
+ * frames: upload frame k+1 on a stream of its own while frame k searches, make the context's stream wait
+ * for that upload (an event), then call this and frac_run.  d_plane must stay unchanged until the
+ * context's stream has passed the copy (an event recorded on it after this call).  The first frame of a
+ * geometry, or any frame with the classifier on, re-prepares on the host in the next frac_run. */
+int frac_set_frame_device_async(frac_ctx* ctx, const void* d_plane, uint32_t w, uint32_t h, uint32_t stride);
 
 /* The domain pool (TransformEstimator2's sourceGrid) and the range list. */
 int frac_set_domains(frac_ctx* ctx, const frac_grid_item* domains, size_t nd);

@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol():
     assert len(names) >= 20
     missing = [n for n in names if not hasattr(lib, n)]
     assert not missing, missing
-    assert lib.frac_abi_version() == 8
+    assert lib.frac_abi_version() == 9
 
 
 def test_library_carries_the_source_id():

@@ -5,7 +5,7 @@
 # usage: tools/session.sh TAG STEP...
 # steps:
 #   suite         the whole GPU test suite (pytest -m gpu tests), one process
-#   tests:EXPR    the GPU tests pytest -k EXPR selects
+#   tests:A,B,..  the GPU tests pytest -k "A or B or ..." selects
 #   smoke         __graft_entry__.smoke()
 #   bench         python bench.py --steps 20 --warmup 5 (the headline line) -> bench.json
 #   pmc           the search's HBM-traffic passes (tools/pmc_search_r04.sh), re-keying profiles/pmc_search.json
@@ -38,7 +38,7 @@ run() { # SECONDS LOGNAME COMMAND...: one step, stop the session on failure
 for step in "$@"; do
   case $step in
   suite) run 1500 suite.log python3 -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests ;;
-  tests:*) run 900 "tests_${step#tests:}.log" python3 -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests -k "${step#tests:}" ;;
+  tests:*) k=${step#tests:}; run 900 "tests_${k//,/_}.log" python3 -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests -k "${k//,/ or }" ;;
   smoke) run 300 smoke.log python3 -c "import __graft_entry__ as G; G.smoke()" ;;
   bench) run 500 bench.log python3 -u bench.py --steps 20 --warmup 5 --out "$O/bench.json" ;;
   pmc) run 600 pmc.log bash tools/pmc_search_r04.sh "$O/pmc" && cp profiles/pmc_search.json "$O/pmc_search.json" ;;
