@@ -809,6 +809,9 @@ def main(args, engine_factory=None, backend: str | None = None, cuda: bool = Tru
     })
     if node_err:
         line["node_error"] = node_err
+    if tuples_out == "node":
+        line["tuples_note"] = ("the node-shared buffer had run only on one GPU before this line (ADVICE r05): "
+                               "records.gather_equals_headline checks it here against the RCCL all-gather leg")
 
     if side_steps > 0 and world > 1:
         # the other tuple exchange, timed the same way (north_star's all-gather beside the node buffer)
