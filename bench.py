@@ -409,6 +409,11 @@ class FrameStep:
         self.device_resident = device_resident
         self.clock = clock
         self.sink = hasattr(eng, "set_tuple_sink") and dev.type == "cuda"
+        # the assembled frame goes to the engine without a host synchronisation when the engine enqueues on
+        # torch's current stream (where the all-gather leaves it): frac_set_frame_device_async (ABI 9)
+        self.async_frame = False
+        if self.stripes and dev.type == "cuda" and hasattr(eng, "set_frame_device_async"):
+            self.async_frame = eng.stream_handle() == torch.cuda.current_stream(dev).cuda_stream
         a, b = plan[rank]
         self.n_mine = b - a
         cap = max((q - p for p, q in plan), default=0)
@@ -440,7 +445,10 @@ class FrameStep:
 
         if self.stripes:  # this rank's rows H2D + the all-gather (on the engine's = torch's current stream)
             full = self.frame_stripes(self._mark)
-            self.eng.set_frame(full if full.is_cuda else full.numpy())
+            if self.async_frame:  # the device-to-device copy ordered after the all-gather: no host wait
+                self.eng.set_frame_device_async(full)
+            else:
+                self.eng.set_frame(full if full.is_cuda else full.numpy())
         elif not self.device_resident:
             self.eng.set_frame(self.frame)  # H2D (returns once the plane is on the device)
             self._mark("frame_h2d")

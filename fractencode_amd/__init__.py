@@ -405,6 +405,10 @@ class Engine:
     def set_stream(self, stream_handle: int | None) -> None:
         self._check(lib().frac_set_stream(self._ctx, C.c_void_p(stream_handle) if stream_handle else None))
 
+    def stream_handle(self) -> int:
+        """The hipStream_t this context enqueues on (frac_get_stream), as an integer."""
+        return lib().frac_get_stream(self._ctx) or 0
+
     def copy_results_device(self, dst_ptr: int) -> None:
         """Async D2D copy of the last run's results (64 B each) to a device buffer."""
         self._check(lib().frac_copy_results_device(self._ctx, C.c_void_p(dst_ptr)))
