@@ -671,201 +671,222 @@ def _run_leg(step, steps: int, warmup: int, world: int, dev):
     return timed(step, steps, world, dev)
 
 
-def main(args, engine_factory=None, backend: str | None = None, cuda: bool = True) -> dict:
-    """The bench on this rank.  `engine_factory(dev, transforms, engine_id, timing)` builds an engine (default:
-    the HIP library's), `backend` the process group's (nccl = RCCL), `cuda` whether ranks own a GPU; the
-    CPU tests pass the oracle stand-in, gloo and False.  Rank 0 prints the line and returns it."""
-    import torch
-    import torch.distributed as dist
+class Bench:
+    """One rank's bench: the process group, the C3 grids and this rank's shard, the engine on its dedicated
+    stream, and the line that the headline and each side leg (methods below) add to."""
 
-    import fractencode_amd as F
-    from fractencode_amd.distributed import shard_plan
-    from fractencode_amd.synth import value_noise
+    def __init__(self, args, engine_factory=None, backend: str | None = None, cuda: bool = True):
+        import torch
 
-    product = engine_factory is None
-    engine_factory = engine_factory or hip_engine
-    backend = backend or args.backend
-    knobs = check_headline_env(args)
-    build = F.build_info()
-    if product and not build["matches_sources"] and not args.ab:
-        raise SystemExit(f"bench.py: the library was built from sources {build['build_id']}, these are "
-                         f"{F.source_id()}: rebuild (__graft_entry__.build())")
-    world, rank, dev, one_host = _setup(args, backend, cuda)
+        import fractencode_amd as F
+        from fractencode_amd.distributed import shard_plan
+        from fractencode_amd.synth import value_noise
 
-    S = args.size
-    frame = value_noise(S, S, 1234)
-    doms = F.create_uniform_grid(S, S, 16, 8)
-    rngs = F.create_uniform_grid(S, S, 8, 8)
-    nr_total = len(rngs)
-    plan = shard_plan(nr_total, world)
-    start, stop = plan[rank]
-    mine = rngs[start:stop]
-    engine_id = {"auto": F.ENGINE_AUTO, "valu": F.ENGINE_VALU, "mfma": F.ENGINE_MFMA}[args.engine]
-    side_steps = args.steps if args.side_steps < 0 else args.side_steps
+        self.args, self.cuda, self.F = args, cuda, F
+        self.product = engine_factory is None
+        self.engine_factory = engine_factory or hip_engine
+        self.knobs = check_headline_env(args)
+        self.build = F.build_info()
+        if self.product and not self.build["matches_sources"] and not args.ab:
+            raise SystemExit(f"bench.py: the library was built from sources {self.build['build_id']}, these are "
+                             f"{F.source_id()}: rebuild (__graft_entry__.build())")
+        self.world, self.rank, self.dev, self.one_host = _setup(args, backend or args.backend, cuda)
+        S = self.S = args.size
+        self.frame = value_noise(S, S, 1234)
+        self.doms = F.create_uniform_grid(S, S, 16, 8)
+        rngs = F.create_uniform_grid(S, S, 8, 8)
+        self.nr_total = len(rngs)
+        self.plan = shard_plan(self.nr_total, self.world)
+        start, stop = self.plan[self.rank]
+        self.mine = rngs[start:stop]
+        self.engine_id = {"auto": F.ENGINE_AUTO, "valu": F.ENGINE_VALU, "mfma": F.ENGINE_MFMA}[args.engine]
+        self.side_steps = args.steps if args.side_steps < 0 else args.side_steps
+        # one dedicated stream for the engine, the tuple copies and the RCCL collectives, so every copy and the
+        # all-gathers are ordered after the kernels (the legacy null stream cannot be handed to the library:
+        # NULL = its own stream)
+        self.stream = None
+        if cuda:
+            self.stream = torch.cuda.Stream(self.dev)
+            torch.cuda.set_stream(self.stream)
+        self.eng = self.new_engine(timing=True)
+        self.h_frame = torch.from_numpy(self.frame)
+        if cuda:
+            self.h_frame = self.h_frame.pin_memory()  # the caller's plane, in pinned host memory
+        self.eng.set_frame(self.h_frame.numpy())
+        self.eng.set_domains(self.doms)
+        self.eng.set_ranges(self.mine)
+        self.checks = {}
+        self.line = {}
 
-    # one dedicated stream for the engine, the tuple copies and the RCCL collectives, so every copy and the
-    # all-gathers are ordered after the kernels (the legacy null stream cannot be handed to the library:
-    # NULL = its own stream)
-    stream = None
-    if cuda:
-        stream = torch.cuda.Stream(dev)
-        torch.cuda.set_stream(stream)
-
-    def new_engine(timing=False):
-        e = engine_factory(dev, args.transforms, engine_id, timing)
-        if stream is not None:
-            e.set_stream(stream.cuda_stream)
+    def new_engine(self, timing: bool = False):
+        e = self.engine_factory(self.dev, self.args.transforms, self.engine_id, timing)
+        if self.stream is not None:
+            e.set_stream(self.stream.cuda_stream)
         return e
 
-    eng = new_engine(timing=True)
-    h_frame = torch.from_numpy(frame)
-    if cuda:
-        h_frame = h_frame.pin_memory()  # the caller's plane, in pinned host memory
-    eng.set_frame(h_frame.numpy())
-    eng.set_domains(doms)
-    eng.set_ranges(mine)
+    def per_step(self, seconds: float, steps: int, n: int | None = None) -> dict:
+        n = self.nr_total if n is None else n
+        return {"value": round(n / (seconds / steps), 1), "ms_per_step": round(1e3 * seconds / steps, 3),
+                "steps": steps}
 
-    # ---- headline: the end-to-end step ----
-    use_node = world > 1 and one_host and args.tuples == "node"
-    node, node_err = (_node_buffer(plan, rank, dev, world) if use_node else (None, ""))
-    clock = PhaseClock(dev)
-    step = FrameStep(eng, h_frame, plan, rank, dev, node_tuples=node, clock=clock)
-    for _ in range(args.warmup):
-        step()
-    _sync(dev)
-    clock.rows = []
-    eng.timing_history()  # drop the warmup runs: the history now covers exactly the timed steps
-    mine_s, elapsed = timed(step, args.steps, world, dev)
-    hist = eng.timing_history()  # per-run HIP events of the K timed steps (on the kernel's stream)
-    # the library keeps the last 256 runs: with more steps the mean is over the last 256 of them
-    assert len(hist) == min(args.steps, 256), (len(hist), args.steps)
-    main_out, st = eng.fetch()  # the timed steps' records (the SEA engine is checked against them)
-    gathered = step.tuples_bytes()
-    own = eng.fetch_tuples().tobytes() if len(mine) else b""
-    checks = {"own_slice_in_gather": step.own_slice_ok(own)}
-    phases = clock.means()
-    phases.update({k: float(np.mean(hist["ms_" + k])) if len(hist) else 0.0 for k in ("prep", "search", "finish")})
-    keys = list(PHASES) + ["prep", "search", "finish"]
-    by_rank = gather_floats([phases[k] for k in keys], world, dev)
-    rank_s = [r[0] for r in gather_floats([mine_s], world, dev)]
-    if node is not None:
-        del step
-        node.close()
-        node = None
+    # ---- the headline: the end-to-end step ----
+    def headline(self) -> None:
+        args, world, rank, dev, eng = self.args, self.world, self.rank, self.dev, self.eng
+        use_node = world > 1 and self.one_host and args.tuples == "node"
+        node, node_err = (_node_buffer(self.plan, rank, dev, world) if use_node else (None, ""))
+        clock = PhaseClock(dev)
+        step = FrameStep(eng, self.h_frame, self.plan, rank, dev, node_tuples=node, clock=clock)
+        for _ in range(args.warmup):
+            step()
+        _sync(dev)
+        clock.rows = []
+        eng.timing_history()  # drop the warmup runs: the history now covers exactly the timed steps
+        mine_s, elapsed = timed(step, args.steps, world, dev)
+        hist = eng.timing_history()  # per-run HIP events of the K timed steps (on the kernel's stream)
+        # the library keeps the last 256 runs: with more steps the mean is over the last 256 of them
+        assert len(hist) == min(args.steps, 256), (len(hist), args.steps)
+        self.main_out, st = eng.fetch()  # the timed steps' records (the SEA engine is checked against them)
+        self.gathered = step.tuples_bytes()
+        self.own = eng.fetch_tuples().tobytes() if len(self.mine) else b""
+        self.checks["own_slice_in_gather"] = step.own_slice_ok(self.own)
+        phases = clock.means()
+        phases.update({k: float(np.mean(hist["ms_" + k])) if len(hist) else 0.0 for k in ("prep", "search", "finish")})
+        keys = list(PHASES) + ["prep", "search", "finish"]
+        by_rank = gather_floats([phases[k] for k in keys], world, dev)
+        rank_s = [r[0] for r in gather_floats([mine_s], world, dev)]
+        if node is not None:
+            del step
+            node.close()
+        self.engine_name = {1: "valu", 2: "mfma"}.get(st["engine"], "valu")
+        self.form = self.F.FORM_NAMES.get(st["search_form"], self.engine_name)
+        self.tuples_out = "node" if use_node and not node_err else ("gather" if world > 1 else "sink")
+        S, nr_total, n_d = self.S, self.nr_total, len(self.doms)
+        line = self.line
+        line.update(headline_fields(nr_total, world, args.steps, args.warmup, elapsed))
+        line.update({
+            "dtype": "u16" if self.engine_name == "valu" else "f16",
+            "arith": ARITH if self.engine_name == "mfma" else "exact integer (u16 x u16 -> u32 dot products), fit in "
+                                                             "fp64",
+            "data": "synthetic",
+            "config": {"workload": f"C3: {S}x{S} S1 value-noise frame (seed 1234), 8x8 ranges ({nr_total}), "
+                                   f"16x16 domains stride 8 ({n_d}), T={args.transforms}, exhaustive, rms 0",
+                       "engine": self.engine_name, "ranges_per_gpu": len(self.mine), "parallelism": f"ranges/{world}",
+                       "env": frac_env(), "ab_run": bool(self.knobs)},
+            "step": ("frame H2D (pinned, 16 MiB) + pool build + search + fit + 32-byte tuples written by the resolve "
+                     "into pinned host memory" if world == 1 else
+                     "frame H2D of the rank's 1/N stripe of rows (pinned) + RCCL all-gather of the frame + pool build "
+                     "+ search + fit of the rank's shard + " +
+                     ("its 32-byte tuples written by the resolve into the node's shared pinned tuple buffer + a "
+                      "4-byte RCCL all-reduce per frame" if self.tuples_out == "node" else
+                      "32-byte tuples written by the resolve into the all-gather buffer + RCCL all-gather + the "
+                      "gathered tuples D2H into rank 0's pinned memory")) +
+                    "; serial, barrier + synchronisation around the timed steps, slowest rank",
+            "tuples_out": self.tuples_out,
+            "rank_ms_per_step": [round(1e3 * s / args.steps, 3) for s in rank_s],
+            "roofline": self.roofline(hist, st),
+            "search_form": self.form,
+            "phases_ms": {k: round(v, 3) for k, v in zip(keys, max_vector([phases[k] for k in keys], world, dev))},
+            "phases_ms_by_rank": [{k: round(v, 3) for k, v in zip(keys, row)} for row in by_rank],
+            "phases_note": "frame_h2d / frame_allgather / run / tuples: spans between marks on the engine's stream "
+                           "(the tuple exchange includes the D2H); prep / search / finish: the library's events "
+                           "inside run; each the mean over the timed steps, phases_ms the maximum over ranks",
+            "fallback_ranges": st["fallback_ranges"],
+            "source_id": lib_sha16(),
+            "build": self.build,  # the loaded library's compiled-in id (frac_build_id): the binary that ran
+        })
+        if node_err:
+            line["node_error"] = node_err
+        if self.tuples_out == "node":
+            line["tuples_note"] = ("the node-shared buffer had run only on one GPU before this line (ADVICE r05): "
+                                   "records.gather_equals_headline checks it here against the RCCL all-gather leg")
 
-    kernel_ms = float(np.mean(hist["ms_search"]))
-    engine_name = {1: "valu", 2: "mfma"}.get(st["engine"], "valu")
-    form = F.FORM_NAMES.get(st["search_form"], engine_name)
-    n_d = len(doms)
-    direct_ops = 2 * 64 * args.transforms * n_d * len(mine)  # SURVEY.md §8(d): one MAC per pixel per candidate
-    traffic, traffic_src = load_traffic(form) if product else (None, "stand-in engine")
-    if engine_name == "mfma":
-        # the matrix flops the search issues: the Fourier form's own count (6 MFMA 32x32x16 per
-        # 32-range × 32-domain tile pair), fewer than the direct form's §8(d) count for the same result
-        work = st["matrix_flops"]
-        bound, peak, unit = "mfma", MFMA_F16_PEAK_TFLOPS, "TFLOP/s"
-    else:
-        work = direct_ops
-        bound, peak, unit = "valu", VALU_PEAK_TOPS, "TOP/s"
-    achieved = work / (kernel_ms * 1e-3) / 1e12 if kernel_ms > 0 else 0.0
-    roof = {"bound": bound, "achieved": round(achieved, 2), "peak": peak, "unit": unit,
-            "frac": round(achieved / peak, 4), "traffic": traffic,
-            "kernel": {"fourier": "search_dft", "direct": "search_mfma"}.get(form, "search_valu"),
-            "kernel_ms": round(kernel_ms, 3), "kernel_ms_timed_steps": [round(float(x), 3) for x in hist["ms_search"]],
-            "flops_per_launch": int(work),
-            "direct_form": {"ops_per_launch": direct_ops,
-                            "rate": round(direct_ops / (kernel_ms * 1e-3) / 1e12, 2) if kernel_ms > 0 else 0.0,
-                            "note": "SURVEY §8(d) direct-form count over the same kernel time: an "
-                                    "algorithmic-equivalent rate, not a hardware fraction"}}
-    if traffic:
-        roof["hbm_gbs"] = round(traffic / (kernel_ms * 1e-3) / 1e9, 3)
-        roof["hbm_frac"] = round(roof["hbm_gbs"] / HBM_PEAK_GBS, 6)
-        roof["traffic_source"] = traffic_src
-    else:
-        roof["traffic_note"] = traffic_src
-    tuples_out = "node" if use_node and not node_err else ("gather" if world > 1 else "sink")
-    line = headline_fields(nr_total, world, args.steps, args.warmup, elapsed)
-    line.update({
-        "dtype": "u16" if engine_name == "valu" else "f16",
-        "arith": ARITH if engine_name == "mfma" else "exact integer (u16 x u16 -> u32 dot products), fit in fp64",
-        "data": "synthetic",
-        "config": {"workload": f"C3: {S}x{S} S1 value-noise frame (seed 1234), 8x8 ranges ({nr_total}), "
-                               f"16x16 domains stride 8 ({n_d}), T={args.transforms}, exhaustive, rms 0",
-                   "engine": engine_name, "ranges_per_gpu": len(mine), "parallelism": f"ranges/{world}",
-                   "env": frac_env(), "ab_run": bool(knobs)},
-        "step": ("frame H2D (pinned, 16 MiB) + pool build + search + fit + 32-byte tuples written by the resolve "
-                 "into pinned host memory" if world == 1 else
-                 "frame H2D of the rank's 1/N stripe of rows (pinned) + RCCL all-gather of the frame + pool build "
-                 "+ search + fit of the rank's shard + " +
-                 ("its 32-byte tuples written by the resolve into the node's shared pinned tuple buffer + a "
-                  "4-byte RCCL all-reduce per frame" if tuples_out == "node" else
-                  "32-byte tuples written by the resolve into the all-gather buffer + RCCL all-gather + the gathered "
-                  "tuples D2H into rank 0's pinned memory")) +
-                "; serial, barrier + synchronisation around the timed steps, slowest rank",
-        "tuples_out": tuples_out,
-        "rank_ms_per_step": [round(1e3 * s / args.steps, 3) for s in rank_s],
-        "roofline": roof,
-        "search_form": form,
-        "phases_ms": {k: round(v, 3) for k, v in zip(keys, max_vector([phases[k] for k in keys], world, dev))},
-        "phases_ms_by_rank": [{k: round(v, 3) for k, v in zip(keys, row)} for row in by_rank],
-        "phases_note": "frame_h2d / frame_allgather / run / tuples: spans between marks on the engine's stream "
-                       "(the tuple exchange includes the D2H); prep / search / finish: the library's events "
-                       "inside run; each the mean over the timed steps, phases_ms the maximum over ranks",
-        "fallback_ranges": st["fallback_ranges"],
-        "source_id": lib_sha16(),
-        "build": build,  # the loaded library's compiled-in id (frac_build_id): the binary that ran
-    })
-    if node_err:
-        line["node_error"] = node_err
-    if tuples_out == "node":
-        line["tuples_note"] = ("the node-shared buffer had run only on one GPU before this line (ADVICE r05): "
-                               "records.gather_equals_headline checks it here against the RCCL all-gather leg")
+    def roofline(self, hist, st) -> dict:
+        """The search kernel against its roofline: the work one launch issues ÷ its mean duration over the
+        timed steps (library HIP events on the kernel's stream)."""
+        kernel_ms = float(np.mean(hist["ms_search"]))
+        self.direct_ops = 2 * 64 * self.args.transforms * len(self.doms) * len(self.mine)  # SURVEY.md §8(d)
+        traffic, traffic_src = load_traffic(self.form) if self.product else (None, "stand-in engine")
+        if self.engine_name == "mfma":
+            # the matrix flops the search issues: the Fourier form's own count (6 MFMA 32x32x16 per
+            # 32-range × 32-domain tile pair), fewer than the direct form's §8(d) count for the same result
+            self.work = st["matrix_flops"]
+            bound, self.peak, unit = "mfma", MFMA_F16_PEAK_TFLOPS, "TFLOP/s"
+        else:
+            self.work = self.direct_ops
+            bound, self.peak, unit = "valu", VALU_PEAK_TOPS, "TOP/s"
+        achieved = self.work / (kernel_ms * 1e-3) / 1e12 if kernel_ms > 0 else 0.0
+        roof = {"bound": bound, "achieved": round(achieved, 2), "peak": self.peak, "unit": unit,
+                "frac": round(achieved / self.peak, 4), "traffic": traffic,
+                "kernel": {"fourier": "search_dft", "direct": "search_mfma"}.get(self.form, "search_valu"),
+                "kernel_ms": round(kernel_ms, 3),
+                "kernel_ms_timed_steps": [round(float(x), 3) for x in hist["ms_search"]],
+                "flops_per_launch": int(self.work),
+                "direct_form": {"ops_per_launch": self.direct_ops,
+                                "rate": round(self.direct_ops / (kernel_ms * 1e-3) / 1e12, 2) if kernel_ms > 0 else 0.0,
+                                "note": "SURVEY §8(d) direct-form count over the same kernel time: an "
+                                        "algorithmic-equivalent rate, not a hardware fraction"}}
+        if traffic:
+            roof["hbm_gbs"] = round(traffic / (kernel_ms * 1e-3) / 1e9, 3)
+            roof["hbm_frac"] = round(roof["hbm_gbs"] / HBM_PEAK_GBS, 6)
+            roof["traffic_source"] = traffic_src
+        else:
+            roof["traffic_note"] = traffic_src
+        return roof
 
-    if side_steps > 0 and world > 1:
-        # the other tuple exchange, timed the same way (north_star's all-gather beside the node buffer)
-        other = "gather" if tuples_out == "node" else "node"
+    # ---- side legs ----
+    def other_tuples_leg(self) -> None:
+        """N > 1: the other tuple exchange, timed the same way (north_star's all-gather beside the node buffer)."""
+        world, rank, dev = self.world, self.rank, self.dev
+        other = "gather" if self.tuples_out == "node" else "node"
         onode, oerr = (None, "")
         if other == "node":
-            onode, oerr = (_node_buffer(plan, rank, dev, world) if one_host else (None, "ranks on several hosts"))
+            onode, oerr = (_node_buffer(self.plan, rank, dev, world) if self.one_host else
+                           (None, "ranks on several hosts"))
         if other == "gather" or onode is not None:
-            ostep = FrameStep(eng, h_frame, plan, rank, dev, node_tuples=onode)
-            _, osec = _run_leg(ostep, side_steps, 1, world, dev)
-            checks[f"{other}_equals_headline"] = ostep.tuples_bytes() == gathered
-            line[f"{other}_value"] = {"value": round(nr_total / (osec / side_steps), 1),
-                                      "ms_per_step": round(1e3 * osec / side_steps, 3), "steps": side_steps,
-                                      "tuples_out": other}
+            ostep = FrameStep(self.eng, self.h_frame, self.plan, rank, dev, node_tuples=onode)
+            _, osec = _run_leg(ostep, self.side_steps, 1, world, dev)
+            self.checks[f"{other}_equals_headline"] = ostep.tuples_bytes() == self.gathered
+            self.line[f"{other}_value"] = {**self.per_step(osec, self.side_steps), "tuples_out": other}
             del ostep
             if onode is not None:
                 onode.close()
         else:
-            line[f"{other}_value"] = {"skipped": oerr}
+            self.line[f"{other}_value"] = {"skipped": oerr}
 
-    if side_steps > 0:
-        # the device-only rate: the frame resident in HBM, the gathered tuples left on the device
-        d_frame = torch.from_numpy(frame).to(dev)
-        eng.set_frame(d_frame if cuda else frame)
-        dstep = FrameStep(eng, None, plan, rank, dev, device_resident=True)
+    def device_leg(self) -> None:
+        """The device-only rate: the frame resident in HBM, the gathered tuples left on the device."""
+        import torch
+
+        eng, ss = self.eng, self.side_steps
+        self.d_frame = torch.from_numpy(self.frame).to(self.dev)
+        eng.set_frame(self.d_frame if self.cuda else self.frame)
+        dstep = FrameStep(eng, None, self.plan, self.rank, self.dev, device_resident=True)
         dstep()
         eng.timing_history()
-        _, dsec = timed(dstep, side_steps, world, dev)
+        _, dsec = timed(dstep, ss, self.world, self.dev)
         dhist = eng.timing_history()
-        checks["device_leg_equals_e2e"] = dstep.tuples_bytes() == gathered
-        line["device_value"] = {"value": round(nr_total / (dsec / side_steps), 1),
-                                "ms_per_step": round(1e3 * dsec / side_steps, 3), "steps": side_steps,
-                                "step": "the same with the frame resident in HBM before timing and the gathered "
-                                        "tuples left on the device"}
+        self.checks["device_leg_equals_e2e"] = dstep.tuples_bytes() == self.gathered
+        self.line["device_value"] = {**self.per_step(dsec, ss),
+                                     "step": "the same with the frame resident in HBM before timing and the gathered "
+                                             "tuples left on the device"}
         if len(dhist):
             dk = float(np.mean(dhist["ms_search"]))
             if dk > 0:
+                roof = self.line["roofline"]
                 roof["kernel_ms_device"] = round(dk, 3)
-                roof["frac_device"] = round(work / (dk * 1e-3) / 1e12 / peak, 4)
-        # a frame stream on one context and one compute stream: frame k+1's H2D runs on a copy stream of its own
-        # while frame k searches; the context's stream waits for that upload (an event), copies the plane
-        # device-to-device (frac_set_frame_device_async, ABI 9) and runs, the resolve writing the frame's tuples
-        # into one of two pinned buffers (per rank, no gather).  CPU stand-in engines: the same frames in turn.
-        if cuda:
-            up = torch.cuda.Stream(dev)
-            d_bufs = [torch.empty((S, S), dtype=torch.uint8, device=dev) for _ in range(2)]
+                roof["frac_device"] = round(self.work / (dk * 1e-3) / 1e12 / self.peak, 4)
+
+    def stream_leg(self) -> None:
+        """A frame stream on one context and one compute stream: frame k+1's H2D runs on a copy stream of its own
+        while frame k searches; the context's stream waits for that upload (an event), copies the plane
+        device-to-device (frac_set_frame_device_async, ABI 9) and runs, the resolve writing the frame's tuples
+        into one of two pinned buffers (per rank, no gather).  CPU stand-in engines: the same frames in turn."""
+        import torch
+
+        eng, ss, S, mine = self.eng, self.side_steps, self.S, self.mine
+        if self.cuda:
+            up, stream, h_frame = torch.cuda.Stream(self.dev), self.stream, self.h_frame
+            d_bufs = [torch.empty((S, S), dtype=torch.uint8, device=self.dev) for _ in range(2)]
             up_ev = [torch.cuda.Event() for _ in range(2)]
             free_ev = [torch.cuda.Event() for _ in range(2)]
             for ev in free_ev:
@@ -873,7 +894,7 @@ def main(args, engine_factory=None, backend: str | None = None, cuda: bool = Tru
             h_tup = [torch.zeros(max(1, len(mine)) * TUPLE_BYTES, dtype=torch.uint8).pin_memory() for _ in range(2)]
 
             def stream_steps():
-                for k in range(side_steps):
+                for k in range(ss):
                     j = k & 1
                     up.wait_event(free_ev[j])  # the buffer's previous frame has been copied out of it
                     with torch.cuda.stream(up):
@@ -890,65 +911,72 @@ def main(args, engine_factory=None, backend: str | None = None, cuda: bool = Tru
             h_tup = [torch.zeros(max(1, len(mine)) * TUPLE_BYTES, dtype=torch.uint8) for _ in range(2)]
 
             def stream_steps():
-                for k in range(side_steps):
-                    eng.set_frame(frame)
+                for k in range(ss):
+                    eng.set_frame(self.frame)
                     eng.run()
                     if len(mine):
-                        eng.fetch_tuples(h_tup[k & 1].numpy().view(F.TUPLE))
+                        eng.fetch_tuples(h_tup[k & 1].numpy().view(self.F.TUPLE))
 
         stream_steps()
-        _, ssec = timed(stream_steps, 1, world, dev)
-        checks["stream_leg_equals_e2e"] = h_tup[(side_steps - 1) & 1].numpy().tobytes()[: len(own)] == own
-        line["stream_value"] = {"value": round(nr_total / (ssec / side_steps), 1),
-                                "ms_per_step": round(1e3 * ssec / side_steps, 3), "steps": side_steps,
-                                "step": "per frame: H2D on a copy stream overlapped with the previous frame's search, "
-                                        "device-to-device copy + search + tuples written by the resolve into pinned "
-                                        "memory on the compute stream" + (" (per rank, no gather)" if world > 1 else "")}
-        eng.set_frame(d_frame if cuda else frame)
+        _, ssec = timed(stream_steps, 1, self.world, self.dev)
+        self.checks["stream_leg_equals_e2e"] = h_tup[(ss - 1) & 1].numpy().tobytes()[: len(self.own)] == self.own
+        self.line["stream_value"] = {
+            **self.per_step(ssec, ss),
+            "step": "per frame: H2D on a copy stream overlapped with the previous frame's search, device-to-device "
+                    "copy + search + tuples written by the resolve into pinned memory on the compute stream" +
+                    (" (per rank, no gather)" if self.world > 1 else "")}
+        eng.set_frame(self.d_frame if self.cuda else self.frame)
         eng.run()
 
-        # C5 (BASELINE configs[4]): three planes of an S1 RGB frame, sharded the same way
+    def c5_leg(self) -> None:
+        """C5 (BASELINE configs[4]): three planes of an S1 RGB frame, each plane's ranges sharded the same way."""
+        import torch
+
+        from fractencode_amd.distributed import shard_plan
+        from fractencode_amd.synth import value_noise
+
+        F, S, ss, rank = self.F, self.S, self.side_steps, self.rank
         rgb = np.stack([value_noise(S, S, 1234 + k) for k in range(3)], -1)
         h_rgb = torch.from_numpy(rgb)
-        if cuda:
+        if self.cuda:
             h_rgb = h_rgb.pin_memory()
         sizes = [(S, S), (S // 2, S // 2), (S // 2, S // 2)]
         c5_rngs = [F.create_uniform_grid(w, h, 8, 8) for w, h in sizes]
-        c5_plans = [shard_plan(len(r), world) for r in c5_rngs]
-        c5_eng = [new_engine() for _ in range(3)]
+        c5_plans = [shard_plan(len(r), self.world) for r in c5_rngs]
+        c5_eng = [self.new_engine() for _ in range(3)]
         for e, (w, h), r, p in zip(c5_eng, sizes, c5_rngs, c5_plans):
             a, b = p[rank]
             e.set_frame(np.zeros((h, w), np.uint8))
             e.set_domains(F.create_uniform_grid(w, h, 16, 8))
             e.set_ranges(r[a:b])
-        cstep = ColorStep(c5_eng, h_rgb if cuda else rgb, c5_plans, rank, dev)
-        _, csec = _run_leg(cstep, side_steps, 1, world, dev)
-        c5_bytes = cstep.tuples_bytes()
+        cstep = ColorStep(c5_eng, h_rgb if self.cuda else rgb, c5_plans, rank, self.dev)
+        _, csec = _run_leg(cstep, ss, 1, self.world, self.dev)
         n5 = sum(len(r) for r in c5_rngs)
-        line["c5"] = {"value": round(n5 / (csec / side_steps), 1), "unit": "range-blocks/s",
-                      "ms_per_step": round(1e3 * csec / side_steps, 3), "steps": side_steps,
-                      "workload": f"C5: S1 RGB {S}x{S} (seeds 1234/1235/1236) -> Y {S}x{S}, U/V {S // 2}x{S // 2}, "
-                                  f"8x8 ranges ({n5}), 16x16 domains stride 8, T={args.transforms}, exhaustive",
-                      "step": "RGB H2D (N > 1: row stripes + RCCL all-gather) + rgb2yuv on the device + the three "
-                              "planes' shards searched on one stream + one all-gather of their tuples + D2H",
-                      "records": {"tuples_sha16": digest(c5_bytes), "n": n5}}
+        self.line["c5"] = {
+            **self.per_step(csec, ss, n5), "unit": "range-blocks/s",
+            "workload": f"C5: S1 RGB {S}x{S} (seeds 1234/1235/1236) -> Y {S}x{S}, U/V {S // 2}x{S // 2}, 8x8 ranges "
+                        f"({n5}), 16x16 domains stride 8, T={self.args.transforms}, exhaustive",
+            "step": "RGB H2D (N > 1: row stripes + RCCL all-gather) + rgb2yuv on the device + the three planes' shards "
+                    "searched on one stream + one all-gather of their tuples + D2H",
+            "records": {"tuples_sha16": digest(cstep.tuples_bytes()), "n": n5}}
         for e in c5_eng:
             e.close()
-    line["records"] = {"tuples_sha16": digest(gathered), "n": nr_total, **checks}
 
-    if world == 1 and engine_name == "mfma" and args.alt_steps > 0 and product:
-        # the same workload on the other engines, frame resident, measured the same way: the VALU engine
-        # (packed-u16 v_dot2, north_star's no-MFMA formulation, exhaustive) and the SEA engine
-        # (successive elimination: identical records, most candidates skipped by an exact bound,
-        # data-dependent)
-        d_frame = torch.from_numpy(frame).to(dev)
-        line["alt_engines"] = {}
+    def alt_engines(self) -> None:
+        """The same workload on the other engines, frame resident, measured the same way: the VALU engine
+        (packed-u16 v_dot2, north_star's no-MFMA formulation, exhaustive) and the SEA engine (successive
+        elimination: identical records, most candidates skipped by an exact bound, data-dependent)."""
+        import torch
+
+        F, dev, args = self.F, self.dev, self.args
+        d_frame = torch.from_numpy(self.frame).to(dev)
+        out = self.line["alt_engines"] = {}
         for alt_name, alt_id in (("valu", F.ENGINE_VALU), ("sea", F.ENGINE_SEA)):
             with F.Engine(dev.index, args.transforms, False, 0.0, -1.0, alt_id, timing=True) as alt:
-                alt.set_stream(stream.cuda_stream)
+                alt.set_stream(self.stream.cuda_stream)
                 alt.set_frame(d_frame)
-                alt.set_domains(doms)
-                alt.set_ranges(mine)
+                alt.set_domains(self.doms)
+                alt.set_ranges(self.mine)
                 alt.run()
                 torch.cuda.synchronize(dev)
                 alt.timing_history()
@@ -960,33 +988,55 @@ def main(args, engine_factory=None, backend: str | None = None, cuda: bool = Tru
                 ah = alt.timing_history()
                 alt_out, ast = alt.fetch()
             a_ms = float(np.mean(ah["ms_search"]))
-            entry = {"value": round(nr_total / alt_sec, 1), "ms_per_step": round(alt_sec * 1e3, 3),
+            entry = {"value": round(self.nr_total / alt_sec, 1), "ms_per_step": round(alt_sec * 1e3, 3),
                      "steps": args.alt_steps, "dtype": "u16", "step": "device-resident (as device_value)",
                      "phases_ms": {k: round(float(np.mean(ah["ms_" + k])), 3) for k in ("prep", "search", "finish")}}
             if alt_name == "valu":
-                alt_ach = direct_ops / (a_ms * 1e-3) / 1e12
+                alt_ach = self.direct_ops / (a_ms * 1e-3) / 1e12
                 entry["roofline"] = {"bound": "valu", "achieved": round(alt_ach, 2), "peak": VALU_PEAK_TOPS,
                                      "unit": "TOP/s", "frac": round(alt_ach / VALU_PEAK_TOPS, 4),
                                      "kernel_ms": round(a_ms, 3)}
             else:
-                entry["records_identical_to_exhaustive"] = bool(alt_out.tobytes() == main_out.tobytes())
-                entry["evaluated_frac"] = round(ast["evaluated_mappings"] / (len(mine) * n_d), 6)
-            line["alt_engines"][alt_name] = entry
-    if rank == 0 and world == 1 and args.cpu_budget > 0:
-        threads, host = host_cores()
-        line["cpu_baseline"] = cpu_baseline(frame, args.cpu_budget, args.cpu_threads or threads, host)
-    if rank == 0 and world == 1 and cuda and product and args.drop_in:
-        line["drop_in"] = drop_in(frame)
-    eng.close()
-    if rank == 0:
-        print(json.dumps(line), flush=True)
-        if args.out:
-            with open(args.out, "w") as f:
-                json.dump(line, f)
-    if world > 1:
-        dist.barrier()
-        dist.destroy_process_group()
-    return line
+                entry["records_identical_to_exhaustive"] = bool(alt_out.tobytes() == self.main_out.tobytes())
+                entry["evaluated_frac"] = round(ast["evaluated_mappings"] / (len(self.mine) * len(self.doms)), 6)
+            out[alt_name] = entry
+
+    def run(self) -> dict:
+        import torch.distributed as dist
+
+        args, world, rank = self.args, self.world, self.rank
+        self.headline()
+        if self.side_steps > 0:
+            if world > 1:
+                self.other_tuples_leg()
+            self.device_leg()
+            self.stream_leg()
+            self.c5_leg()
+        self.line["records"] = {"tuples_sha16": digest(self.gathered), "n": self.nr_total, **self.checks}
+        if world == 1 and self.engine_name == "mfma" and args.alt_steps > 0 and self.product:
+            self.alt_engines()
+        if rank == 0 and world == 1 and args.cpu_budget > 0:
+            threads, host = host_cores()
+            self.line["cpu_baseline"] = cpu_baseline(self.frame, args.cpu_budget, args.cpu_threads or threads, host)
+        if rank == 0 and world == 1 and self.cuda and self.product and args.drop_in:
+            self.line["drop_in"] = drop_in(self.frame)
+        self.eng.close()
+        if rank == 0:
+            print(json.dumps(self.line), flush=True)
+            if args.out:
+                with open(args.out, "w") as f:
+                    json.dump(self.line, f)
+        if world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+        return self.line
+
+
+def main(args, engine_factory=None, backend: str | None = None, cuda: bool = True) -> dict:
+    """The bench on this rank.  `engine_factory(dev, transforms, engine_id, timing)` builds an engine (default:
+    the HIP library's), `backend` the process group's (default --backend: nccl = RCCL), `cuda` whether ranks own a
+    GPU; the CPU tests pass the oracle stand-in, gloo and False.  Rank 0 prints the line and returns it."""
+    return Bench(args, engine_factory, backend, cuda).run()
 
 
 if __name__ == "__main__":
