@@ -297,6 +297,7 @@ struct frac_ctx {
 
     std::vector<RangeAux> h_aux;
     hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+    hipEvent_t handoff = nullptr; // frac_set_stream: the new stream waits for the old one's work (created on use)
     // FRAC_FLAG_TIMING: the same four boundaries (start | prep | search | finish) of every run
     // since the last frac_timing_history call, a ring of kHistRuns runs (created on first use)
     std::vector<hipEvent_t> hist;
@@ -2968,6 +2969,8 @@ void frac_destroy(frac_ctx* c)
     for (auto& ev : c->ev)
         if (ev)
             (void)hipEventDestroy(ev);
+    if (c->handoff)
+        (void)hipEventDestroy(c->handoff);
     for (auto& ev : c->hist)
         if (ev)
             (void)hipEventDestroy(ev);
@@ -3304,11 +3307,18 @@ int frac_set_stream(frac_ctx* c, void* s)
 {
     if (!c)
         return FRAC_E_INVALID;
-    if (c->fb_pending) { // the last run's fallback goes on the stream its search and resolve ran on
-        FRAC_HIP(c, hipSetDevice(c->device));
-        FRAC_TRY(settle_fallback(c));
-    }
-    c->stream = s ? reinterpret_cast<hipStream_t>(s) : c->own_stream;
+    hipStream_t next = s ? reinterpret_cast<hipStream_t>(s) : c->own_stream;
+    if (next == c->stream)
+        return FRAC_OK;
+    FRAC_HIP(c, hipSetDevice(c->device));
+    // the last run's fallback goes on the stream its search and resolve ran on, and everything enqueued on
+    // that stream so far comes before what is enqueued on the new one: a switch keeps the context's order
+    FRAC_TRY(settle_fallback(c));
+    if (!c->handoff)
+        FRAC_HIP(c, hipEventCreateWithFlags(&c->handoff, hipEventDisableTiming));
+    FRAC_HIP(c, hipEventRecord(c->handoff, c->stream));
+    FRAC_HIP(c, hipStreamWaitEvent(next, c->handoff, 0));
+    c->stream = next;
     return FRAC_OK;
 }
 

@@ -185,7 +185,8 @@ int frac_timing_history(frac_ctx* ctx, frac_run_timing* out, size_t cap, size_t*
  * applied to a batch of range items). */
 int frac_search(frac_ctx* ctx, const frac_grid_item* ranges, size_t nr, frac_encode_item* out, frac_stats* stats);
 
-/* Use an external hipStream_t (passed as void*); NULL restores the context's own. */
+/* Use an external hipStream_t (passed as void*); NULL restores the context's own.  Work the context
+ * enqueued on its previous stream comes before anything it enqueues on the new one (an event). */
 int frac_set_stream(frac_ctx* ctx, void* hip_stream);
 void* frac_get_stream(frac_ctx* ctx);
 /* Device pointer to the nr frac_encode_item results of the last run (valid until

@@ -83,7 +83,7 @@ def test_set_frame_device_async_rejects_host_planes():
 def test_stream_switch_settles_the_pending_fp32_fallback():
     """A run whose fp32-regime ranges wait for the deferred fallback_grid, then frac_set_stream to another
     stream before anything reads the records: the fallback runs on the stream the search and
-    resolve ran on, and the records fetched on the new stream equal a fresh context's."""
+    resolve ran on, the new stream waits for that work, and the records fetched on it equal a fresh context's."""
     import torch
 
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
@@ -92,7 +92,7 @@ def test_stream_switch_settles_the_pending_fp32_fallback():
     p = fp32_frame(6, 512)
     doms = F.create_uniform_grid(512, 512, 16, 8)
     rngs = F.create_uniform_grid(512, 512, 8, 8)
-    want, wst = _sync_search(p, False, doms, rngs)[0], None
+    want = _sync_search(p, False, doms, rngs)[0]
     s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
     with F.Engine(0, 4) as e:
         e.set_stream(s1.cuda_stream)
