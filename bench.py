@@ -242,6 +242,7 @@ def drop_in(frame: np.ndarray, timeout_s: float = 240.0) -> dict:
                                  "tail_hold_s": rec["tail_hold_s"], "records_s": rec["records_s"],
                                  "hip_search_s": rec["hip_search_s"], "hip_handback_s": rec["hip_handback_s"],
                                  "construct_s": rec["construct_s"],
+                                 "hip_search_parts_s": {k: rec["hip_" + k + "_s"] for k in ("prepare", "device", "fetch")},
                                  "encoder2_value": round(n / (rec["drop_in_s"] + rec["construct_s"]), 1),
                                  "cpu_engines": ncpu, "mode": mode, "hip_ranges": hip_ranges,
                                  "records": int((len(raw) - 8 * (3 + k)) // 64)}

@@ -106,9 +106,17 @@ public:
             const auto t0 = Clock::now();
             _records.resize(_pending.size());
             frac_stats st{};
-            check(frac_search(_ctx, reinterpret_cast<const frac_grid_item*>(_pending.data()), _pending.size(),
-                              reinterpret_cast<frac_encode_item*>(_records.data()), &st));
+            // frac_search's three steps, timed apart (the drop-in measurement's breakdown)
+            check(frac_set_ranges(_ctx, reinterpret_cast<const frac_grid_item*>(_pending.data()), _pending.size()));
+            check(frac_run(_ctx)); // preparation for these ranges (host), then every launch (asynchronous)
+            const auto tr = Clock::now();
+            check(frac_sync(_ctx));
+            const auto ts = Clock::now();
+            check(frac_fetch(_ctx, reinterpret_cast<frac_encode_item*>(_records.data()), &st));
             const auto t1 = Clock::now();
+            _prepareSeconds += std::chrono::duration<double>(tr - t0).count();
+            _deviceSeconds += std::chrono::duration<double>(ts - tr).count();
+            _fetchSeconds += std::chrono::duration<double>(t1 - ts).count();
             _rejected += st.rejected_mappings;
             _next = 0;
             for (const auto& item : _pending)
@@ -142,6 +150,11 @@ public:
     // records to the base class's encode() (the core's per-item result list)
     double searchSeconds() const noexcept { return _searchSeconds; }
     double handbackSeconds() const noexcept { return _handbackSeconds; }
+    // the search's parts: claims up + preparation + launches (host), the device work after them, the records
+    // and statistics back
+    double prepareSeconds() const noexcept { return _prepareSeconds; }
+    double deviceSeconds() const noexcept { return _deviceSeconds; }
+    double fetchSeconds() const noexcept { return _fetchSeconds; }
 
 protected:
     encode_item_t encode_impl(const UniformGridItem& targetItem) const override
@@ -166,7 +179,8 @@ private:
     mutable size_t _next = 0;
     uint64_t _rejected = 0;
     size_t _searched = 0, _lost = 0;
-    double _searchSeconds = 0.0, _handbackSeconds = 0.0;
+    double _searchSeconds = 0.0, _handbackSeconds = 0.0, _prepareSeconds = 0.0, _deviceSeconds = 0.0,
+           _fetchSeconds = 0.0;
     std::exception_ptr _failed;
 };
 

@@ -287,16 +287,20 @@ int main(int argc, char** argv)
         const double encode_s = sec(t1), records_s = sec(line.last);
         const double construct_s = std::chrono::duration<double>(t0 - tc).count(); // the core + every engine
         const double hold_s = tail ? std::chrono::duration<double>(tail->released - line.last).count() : 0.0;
-        double search_s = 0.0, handback_s = 0.0; // summed over the HIP engines (they run concurrently)
-        for (auto* hip : hips) {
+        double search_s = 0.0, handback_s = 0.0, prep_s = 0.0, dev_s = 0.0, fetch_s = 0.0; // summed over the HIP
+        for (auto* hip : hips) {                                                          // engines (concurrent)
             search_s += hip->searchSeconds();
             handback_s += hip->handbackSeconds();
+            prep_s += hip->prepareSeconds();
+            dev_s += hip->deviceSeconds();
+            fetch_s += hip->fetchSeconds();
         }
         std::printf("{\"mode\": \"%s\", \"batch\": %zu, \"ranges\": %zu, \"cpu_engines\": %d, \"hip_engines\": %zu, "
                     "\"encode_s\": %.6f, \"records_s\": %.6f, \"tail_hold_s\": %.6f, \"drop_in_s\": %.6f, "
-                    "\"hip_search_s\": %.6f, \"hip_handback_s\": %.6f, \"construct_s\": %.6f}\n",
+                    "\"hip_search_s\": %.6f, \"hip_handback_s\": %.6f, \"construct_s\": %.6f, "
+                    "\"hip_prepare_s\": %.6f, \"hip_device_s\": %.6f, \"hip_fetch_s\": %.6f}\n",
                     batch ? "batch" : "ref", batch, targetGrid.items().size(), ncpu, hips.size(), encode_s, records_s,
-                    hold_s, encode_s - hold_s, search_s, handback_s, construct_s);
+                    hold_s, encode_s - hold_s, search_s, handback_s, construct_s, prep_s, dev_s, fetch_s);
         std::fflush(stdout);
     }
     for (auto* hip : hips) {
