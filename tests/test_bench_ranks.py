@@ -136,3 +136,19 @@ def test_node_buffer_creation_failure_reaches_every_rank(tmp_path):
     rc = bench.launch_ranks(2, script=str(script), argv=[], env=dict(os.environ, OMP_NUM_THREADS="1"))
     assert rc == 0
     assert _node_files() == before
+
+
+def test_drop_in_leg_reports_a_failed_core_run_instead_of_raising():
+    """bench.drop_in runs oracle/_ref/core_driver (the reference's core with the HIP engine) in child processes
+    after the timed region; without a device every run fails at engine creation (exit 4), and the leg records
+    each failure in the line instead of ending the bench."""
+    import bench
+    import torch
+
+    if not os.path.exists(bench.CORE_DRIVER):
+        pytest.skip("oracle/_ref/core_driver not built")
+    if torch.cuda.is_available():
+        pytest.skip("device present: the GPU bench runs the real leg")
+    out = bench.drop_in(np.zeros((64, 64), np.uint8), timeout_s=60)
+    assert set(out["runs"]) == {name for name, _, _ in bench.DROP_IN_RUNS}
+    assert all("exit 4" in r["error"] for r in out["runs"].values())
