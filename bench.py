@@ -233,20 +233,28 @@ def drop_in(frame: np.ndarray, timeout_s: float = 240.0) -> dict:
             if r.returncode != 0 or rec is None:
                 out["runs"][name] = {"error": f"exit {r.returncode}: {r.stderr[-300:]}"}
                 continue
-            n = rec["ranges"]
-            raw = open(res, "rb").read()
-            k = int(np.frombuffer(raw[-8:], dtype=np.uint64)[0])
-            hip_ranges = int(np.frombuffer(raw[-8 * (2 + k): -8 * (1 + k)], dtype=np.uint64)[0])
-            out["runs"][name] = {"value": round(n / rec["drop_in_s"], 1), "unit": "range-blocks/s",
-                                 "drop_in_s": rec["drop_in_s"], "encode_s": rec["encode_s"],
-                                 "tail_hold_s": rec["tail_hold_s"], "records_s": rec["records_s"],
-                                 "hip_search_s": rec["hip_search_s"], "hip_handback_s": rec["hip_handback_s"],
-                                 "construct_s": rec["construct_s"],
-                                 "hip_search_parts_s": {k: rec["hip_" + k + "_s"] for k in ("prepare", "device", "fetch")},
-                                 "encoder2_value": round(n / (rec["drop_in_s"] + rec["construct_s"]), 1),
-                                 "cpu_engines": ncpu, "mode": mode, "hip_ranges": hip_ranges,
-                                 "records": int((len(raw) - 8 * (3 + k)) // 64)}
+            try:
+                out["runs"][name] = _drop_in_run(rec, res, ncpu, mode)
+            except (KeyError, ValueError, OSError, IndexError) as exc:  # a driver of another build: recorded
+                out["runs"][name] = {"error": f"unreadable result: {exc!r}"}
     return out
+
+
+def _drop_in_run(rec: dict, res: str, ncpu: int, mode: str) -> dict:
+    """One core_driver run's entry: its timing line `rec` and its output file `res` (records, then the trailer
+    rejected, HIP ranges, one count per HIP engine, the number of HIP engines)."""
+    n = rec["ranges"]
+    raw = open(res, "rb").read()
+    n_hip = int(np.frombuffer(raw[-8:], dtype=np.uint64)[0])
+    hip_ranges = int(np.frombuffer(raw[-8 * (2 + n_hip): -8 * (1 + n_hip)], dtype=np.uint64)[0])
+    return {"value": round(n / rec["drop_in_s"], 1), "unit": "range-blocks/s",
+            "drop_in_s": rec["drop_in_s"], "encode_s": rec["encode_s"], "tail_hold_s": rec["tail_hold_s"],
+            "records_s": rec["records_s"], "hip_search_s": rec["hip_search_s"],
+            "hip_handback_s": rec["hip_handback_s"], "construct_s": rec["construct_s"],
+            "hip_search_parts_s": {part: rec[f"hip_{part}_s"] for part in ("prepare", "device", "fetch")},
+            "encoder2_value": round(n / (rec["drop_in_s"] + rec["construct_s"]), 1),
+            "cpu_engines": ncpu, "mode": mode, "hip_ranges": hip_ranges,
+            "records": int((len(raw) - 8 * (3 + n_hip)) // 64)}
 
 
 def lib_sha16() -> str:
