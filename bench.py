@@ -23,8 +23,8 @@ all-gather of the tuples + rank 0's D2H) — serial, one frame after another.  B
                 records check `gather_equals_headline` verifies the node buffer against it in the same run
   device_value  the same search with the frame already resident in HBM and the tuples left there
                 (the all-gather still runs for N > 1): the device-only rate
-  stream_value  a frame stream: frame k+1's H2D on a copy stream overlaps frame k's search on the
-                compute stream (one context; frac_set_frame_device_async), tuples into pinned memory
+  stream_value  a frame stream: frame k+1's H2D on the context's copy stream overlaps frame k's search
+                (one context, two plane buffers; frac_set_frame_async), tuples into pinned memory
   c5            BASELINE configs[4]: the S1 RGB 4096² frame H2D (N > 1: row stripes + all-gather),
                 rgb2yuv on the device, every plane's shard searched, one all-gather of the three
                 planes' tuples, D2H — range-blocks/s over Y + U + V
@@ -886,39 +886,27 @@ class Bench:
                 roof["frac_device"] = round(self.work / (dk * 1e-3) / 1e12 / self.peak, 4)
 
     def stream_leg(self) -> None:
-        """A frame stream on one context and one compute stream: frame k+1's H2D runs on a copy stream of its own
-        while frame k searches; the context's stream waits for that upload (an event), copies the plane
-        device-to-device (frac_set_frame_device_async, ABI 9) and runs, the resolve writing the frame's tuples
-        into one of two pinned buffers (per rank, no gather).  CPU stand-in engines: the same frames in turn."""
+        """A frame stream on one context: each frame's H2D runs on the context's own copy stream into its second
+        plane buffer while the previous frame searches (frac_set_frame_async, ABI 9); the context's stream waits
+        for the upload and runs, the resolve writing the frame's tuples into one of two pinned buffers (per rank,
+        no gather).  CPU stand-in engines: the same frames in turn."""
         import torch
 
-        eng, ss, S, mine = self.eng, self.side_steps, self.S, self.mine
-        if self.cuda:
-            up, stream, h_frame = torch.cuda.Stream(self.dev), self.stream, self.h_frame
-            d_bufs = [torch.empty((S, S), dtype=torch.uint8, device=self.dev) for _ in range(2)]
-            up_ev = [torch.cuda.Event() for _ in range(2)]
-            free_ev = [torch.cuda.Event() for _ in range(2)]
-            for ev in free_ev:
-                ev.record(stream)
-            h_tup = [torch.zeros(max(1, len(mine)) * TUPLE_BYTES, dtype=torch.uint8).pin_memory() for _ in range(2)]
+        eng, ss, mine = self.eng, self.side_steps, self.mine
+        pin = self.cuda
+        h_tup = [torch.zeros(max(1, len(mine)) * TUPLE_BYTES, dtype=torch.uint8) for _ in range(2)]
+        if pin:
+            h_tup = [t.pin_memory() for t in h_tup]
+            h_frame = self.h_frame.numpy()  # pinned: the upload is asynchronous
 
             def stream_steps():
                 for k in range(ss):
-                    j = k & 1
-                    up.wait_event(free_ev[j])  # the buffer's previous frame has been copied out of it
-                    with torch.cuda.stream(up):
-                        d_bufs[j].copy_(h_frame, non_blocking=True)
-                    up_ev[j].record(up)
-                    stream.wait_event(up_ev[j])
-                    eng.set_frame_device_async(d_bufs[j])
-                    free_ev[j].record(stream)
+                    eng.set_frame_async(h_frame)
                     if len(mine):
-                        eng.set_tuple_sink(h_tup[j].data_ptr())
+                        eng.set_tuple_sink(h_tup[k & 1].data_ptr())
                     eng.run()
                 eng.set_tuple_sink(None)
         else:
-            h_tup = [torch.zeros(max(1, len(mine)) * TUPLE_BYTES, dtype=torch.uint8) for _ in range(2)]
-
             def stream_steps():
                 for k in range(ss):
                     eng.set_frame(self.frame)
@@ -931,8 +919,8 @@ class Bench:
         self.checks["stream_leg_equals_e2e"] = h_tup[(ss - 1) & 1].numpy().tobytes()[: len(self.own)] == self.own
         self.line["stream_value"] = {
             **self.per_step(ssec, ss),
-            "step": "per frame: H2D on a copy stream overlapped with the previous frame's search, device-to-device "
-                    "copy + search + tuples written by the resolve into pinned memory on the compute stream" +
+            "step": "per frame: H2D on the context's copy stream into its second plane buffer, overlapped with the "
+                    "previous frame's search + search + tuples written by the resolve into pinned memory" +
                     (" (per rank, no gather)" if self.world > 1 else "")}
         eng.set_frame(self.d_frame if self.cuda else self.frame)
         eng.run()

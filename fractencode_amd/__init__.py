@@ -175,6 +175,7 @@ def lib() -> C.CDLL:
             "frac_set_planes": (i32, [vp, vp, u32, u32, u32, vp, u32, u32, u32]),
             "frac_set_frame_device": (i32, [vp, vp, u32, u32, u32]),
             "frac_set_frame_device_async": (i32, [vp, vp, u32, u32, u32]),
+            "frac_set_frame_async": (i32, [vp, vp, u32, u32, u32]),
             "frac_set_domains": (i32, [vp, vp, sz]),
             "frac_set_ranges": (i32, [vp, vp, sz]),
             "frac_run": (i32, [vp]),
@@ -358,6 +359,22 @@ class Engine:
         self._frame_wh = (int(plane.shape[1]), int(plane.shape[0]))
         self._check(lib().frac_set_frame_device_async(self._ctx, C.c_void_p(plane.data_ptr()), plane.shape[1],
                                                       plane.shape[0], plane.stride(0)))
+
+    def set_frame_async(self, plane) -> None:
+        """ABI 9: frame streaming from host memory — a uint8 [H, W] plane (a pinned torch tensor or a numpy view
+        of one, for an asynchronous copy) uploaded on the context's copy stream while the runs already enqueued
+        search the previous frame; the next run() searches this one.  The plane must stay unchanged until the
+        upload is done (a later sync() / fetch(), or an event on this engine's stream)."""
+        if hasattr(plane, "is_cuda"):
+            if plane.is_cuda:
+                raise FracError("set_frame_async: a host plane (set_frame_device_async takes device planes)")
+            plane = plane.numpy()
+        if plane.dtype != np.uint8 or plane.ndim != 2 or plane.strides[1] != 1:
+            raise FracError("set_frame_async: a 2-D uint8 host plane with contiguous rows")
+        self._frame_wh = (int(plane.shape[1]), int(plane.shape[0]))
+        self._keep_async = plane  # the memory stays referenced while the upload may run
+        self._check(lib().frac_set_frame_async(self._ctx, C.c_void_p(plane.ctypes.data), plane.shape[1],
+                                               plane.shape[0], plane.strides[0]))
 
     def set_planes(self, source: np.ndarray, target: np.ndarray) -> None:
         self._frame_wh = (int(source.shape[1]), int(source.shape[0]))

@@ -152,6 +152,12 @@ struct frac_ctx {
     bool same_plane = true;
     bool planes_set = false;
     DBuf<uint8_t> d_src, d_tgt;
+    // frac_set_frame_async (ABI 9): the frame after the current one is uploaded into d_src_next on copy_stream
+    // while the context's stream still reads d_src; the two swap at the call (created on first use)
+    DBuf<uint8_t> d_src_next;
+    hipStream_t copy_stream = nullptr;
+    hipEvent_t up_done = nullptr, next_free = nullptr;
+    bool next_free_recorded = false;
     uint32_t d_sstride = 0, d_tstride = 0;
 
     std::vector<frac_grid_item> doms, ranges;
@@ -2861,6 +2867,9 @@ void frac_destroy(frac_ctx* c)
         (void)hipStreamSynchronize(c->stream);
     c->d_src.release();
     c->d_tgt.release();
+    if (c->copy_stream)
+        (void)hipStreamSynchronize(c->copy_stream);
+    c->d_src_next.release();
     c->d_doms.release();
     c->d_ranges.release();
     c->d_porig.release();
@@ -2976,6 +2985,12 @@ void frac_destroy(frac_ctx* c)
             (void)hipEventDestroy(ev);
     if (c->own_stream)
         (void)hipStreamDestroy(c->own_stream);
+    if (c->copy_stream)
+        (void)hipStreamDestroy(c->copy_stream);
+    if (c->up_done)
+        (void)hipEventDestroy(c->up_done);
+    if (c->next_free)
+        (void)hipEventDestroy(c->next_free);
     delete c;
 }
 
@@ -3071,6 +3086,46 @@ static int set_frame_device(frac_ctx* c, const void* d_plane, uint32_t w, uint32
 int frac_set_frame_device(frac_ctx* c, const void* d_plane, uint32_t w, uint32_t h, uint32_t stride)
 {
     return set_frame_device(c, d_plane, w, h, stride, true);
+}
+
+// Frame streaming from host memory: the upload runs on the context's copy stream into the plane buffer the
+// current runs do not read, after the runs that last read that buffer (next_free); the context's stream waits
+// for the upload (up_done) and the buffers swap, so frame k+1 crosses PCIe while frame k searches.
+int frac_set_frame_async(frac_ctx* c, const uint8_t* plane, uint32_t w, uint32_t h, uint32_t stride)
+{
+    if (!c)
+        return FRAC_E_INVALID;
+    if (!plane || w == 0 || h == 0 || stride < w)
+        return c->fail(FRAC_E_INVALID, "invalid plane");
+    FRAC_HIP(c, hipSetDevice(c->device));
+    FRAC_TRY(settle_fallback(c)); // the last run's fp32-regime ranges read the current plane
+    if (!c->copy_stream) {
+        FRAC_HIP(c, hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
+        FRAC_HIP(c, hipEventCreateWithFlags(&c->up_done, hipEventDisableTiming));
+        FRAC_HIP(c, hipEventCreateWithFlags(&c->next_free, hipEventDisableTiming));
+    }
+    const uint32_t dstride = (w + 63u) & ~63u;
+    if (c->d_src_next.cap < (size_t)dstride * (h + 1)) { // a (re)allocation: nothing may still read the buffer
+        FRAC_HIP(c, hipStreamSynchronize(c->stream));
+        FRAC_HIP(c, c->d_src_next.ensure((size_t)dstride * (h + 1)));
+    }
+    if (c->next_free_recorded) // the runs that read this buffer before the last swap are done
+        FRAC_HIP(c, hipStreamWaitEvent(c->copy_stream, c->next_free, 0));
+    if (stride == dstride)
+        FRAC_HIP(c, hipMemcpyAsync(c->d_src_next.ptr, plane, (size_t)stride * (h - 1) + w, hipMemcpyHostToDevice,
+                                   c->copy_stream));
+    else
+        FRAC_HIP(c, hipMemcpy2DAsync(c->d_src_next.ptr, dstride, plane, stride, w, h, hipMemcpyHostToDevice,
+                                     c->copy_stream));
+    FRAC_HIP(c, hipEventRecord(c->up_done, c->copy_stream));
+    FRAC_HIP(c, hipStreamWaitEvent(c->stream, c->up_done, 0));
+    std::swap(c->d_src, c->d_src_next);
+    c->d_sstride = dstride;
+    // the plane now in d_src_next is free once everything the context enqueued so far has run
+    FRAC_HIP(c, hipEventRecord(c->next_free, c->stream));
+    c->next_free_recorded = true;
+    planes_changed(c, w, h, w, h, true);
+    return FRAC_OK;
 }
 
 int frac_set_frame_device_async(frac_ctx* c, const void* d_plane, uint32_t w, uint32_t h, uint32_t stride)

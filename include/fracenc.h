@@ -160,6 +160,13 @@ int frac_set_frame_device(frac_ctx* ctx, const void* d_plane, uint32_t w, uint32
  * context's stream has passed the copy (an event recorded on it after this call).  The first frame of a
  * geometry, or any frame with the classifier on, re-prepares on the host in the next frac_run. */
 int frac_set_frame_device_async(frac_ctx* ctx, const void* d_plane, uint32_t w, uint32_t h, uint32_t stride);
+/* ABI 9: frame streaming from host memory.  The plane (pinned host memory for an asynchronous copy) is uploaded
+ * on the context's own copy stream into a second plane buffer while the runs already enqueued still read the
+ * current one; the context's stream waits for the upload and the buffers swap.  frac_run right after it
+ * searches the new frame, so frame k+1 crosses PCIe while frame k searches.  The host plane must stay unchanged
+ * until the upload is done: until a later frac_sync / frac_fetch, or an event recorded on the context's stream
+ * after this call. */
+int frac_set_frame_async(frac_ctx* ctx, const uint8_t* plane, uint32_t w, uint32_t h, uint32_t stride);
 
 /* The domain pool (TransformEstimator2's sourceGrid) and the range list. */
 int frac_set_domains(frac_ctx* ctx, const frac_grid_item* domains, size_t nd);

@@ -24,6 +24,41 @@ def _sync_search(p, cls, doms, rngs):
 
 
 @pytest.mark.parametrize("cls", [False, True])
+def test_host_streamed_frames_equal_synchronous_searches(cls):
+    """frac_set_frame_async: frames from pinned host memory uploaded on the context's copy stream into its second
+    plane buffer while the previous frame searches; every frame's tuples (sink) and the last records equal a
+    synchronous search of that frame."""
+    import torch
+
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    from fallback_probe import frame as fp32_frame
+
+    y = plane("lenna_y")
+    frames = [y, np.ascontiguousarray(y[::-1]), fp32_frame(6, 512), np.ascontiguousarray(y[:, ::-1])] * 2
+    doms = F.create_uniform_grid(512, 512, 16, 8)
+    rngs = F.create_uniform_grid(512, 512, 8, 8)
+    want = [_sync_search(p, cls, doms, rngs) for p in frames[:4]]
+    hosts = [torch.from_numpy(p).pin_memory() for p in frames]
+    sinks = [torch.zeros(len(rngs) * F.TUPLE.itemsize, dtype=torch.uint8).pin_memory() for _ in frames]
+    with F.Engine(0, 4, cls) as e:
+        e.set_frame(frames[0])
+        e.set_domains(doms)
+        e.set_ranges(rngs)
+        for k, h in enumerate(hosts):
+            e.set_frame_async(h)
+            e.set_tuple_sink(sinks[k].data_ptr())
+            e.run()
+        e.set_tuple_sink(None)
+        last, _ = e.fetch()
+        e.set_frame(frames[1])  # a synchronous frame after the streamed ones
+        again, _ = e.search(rngs)
+    for k, s in enumerate(sinks):
+        assert s.numpy().tobytes() == want[k % 4][1], k
+    assert last.tobytes() == want[3][0].tobytes()
+    assert again.tobytes() == want[1][0].tobytes()
+
+
+@pytest.mark.parametrize("cls", [False, True])
 def test_streamed_frames_equal_synchronous_searches(cls):
     import torch
 
