@@ -915,13 +915,17 @@ class Bench:
                         eng.fetch_tuples(h_tup[k & 1].numpy().view(self.F.TUPLE))
 
         stream_steps()
+        eng.timing_history()
         _, ssec = timed(stream_steps, 1, self.world, self.dev)
+        shist = eng.timing_history()
         self.checks["stream_leg_equals_e2e"] = h_tup[(ss - 1) & 1].numpy().tobytes()[: len(self.own)] == self.own
         self.line["stream_value"] = {
             **self.per_step(ssec, ss),
             "step": "per frame: H2D on the context's copy stream into its second plane buffer, overlapped with the "
-                    "previous frame's search + search + tuples written by the resolve into pinned memory" +
-                    (" (per rank, no gather)" if self.world > 1 else "")}
+                    "previous frame's resolve + search + tuples written by the resolve into pinned memory" +
+                    (" (per rank, no gather)" if self.world > 1 else ""),
+            "phases_ms": {k: round(float(np.mean(shist["ms_" + k])), 3) if len(shist) else 0.0
+                          for k in ("prep", "search", "finish")}}
         eng.set_frame(self.d_frame if self.cuda else self.frame)
         eng.run()
 
