@@ -922,7 +922,7 @@ class Bench:
         self.line["stream_value"] = {
             **self.per_step(ssec, ss),
             "step": "per frame: H2D on the context's copy stream into its second plane buffer, overlapped with the "
-                    "previous frame's resolve + search + tuples written by the resolve into pinned memory" +
+                    "previous frame's kernels + search + tuples written by the resolve into pinned memory" +
                     (" (per rank, no gather)" if self.world > 1 else ""),
             "phases_ms": {k: round(float(np.mean(shist["ms_" + k])), 3) if len(shist) else 0.0
                           for k in ("prep", "search", "finish")}}
