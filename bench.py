@@ -107,6 +107,9 @@ def parse(argv=None):
                     help="N > 1: the process group's backend (nccl = RCCL; gloo only for tests)")
     ap.add_argument("--share-gpu", action="store_true",
                     help="test only: every rank on GPU 0 (a one-GPU box; with --backend gloo)")
+    ap.add_argument("--group", action="store_true",
+                    help="test only: initialise the process group at N = 1 too and take every N > 1 path (frame "
+                         "stripes, tuple exchange, node buffer, C5 all-gathers): an RCCL rehearsal on one GPU")
     ap.add_argument("--ab", action="store_true",
                     help="allow FRAC_LIB / A/B knobs in the environment (the line is then marked, not a headline)")
     return ap.parse_args(argv)
@@ -530,18 +533,19 @@ class ColorStep:
     the resolvers write the tuples into one buffer, plane after plane), one all-gather of the three planes'
     tuples (N > 1) and the D2H into pinned memory.  CPU engines take the host frame and hand back host tuples."""
 
-    def __init__(self, engines, rgb, plans, rank: int, dev):
+    def __init__(self, engines, rgb, plans, rank: int, dev, stripes=None):
         import torch
 
         self.engines, self.plans, self.rank, self.dev = engines, plans, rank, dev
         self.world = len(plans[0])
+        self.use_stripes = self.world > 1 if stripes is None else bool(stripes)
         self.cuda = dev.type == "cuda"
         H, W = rgb.shape[:2]
         self.H, self.W = H, W
         self.rgb_np = rgb if isinstance(rgb, np.ndarray) else None
         if self.cuda:
             self.rgb = rgb  # pinned host tensor [H, W, 3]
-            if self.world > 1:
+            if self.use_stripes:
                 from fractencode_amd.distributed import FrameStripes
 
                 self.stripes = FrameStripes(rgb.view(H, W * 3), self.world, rank, dev)
@@ -559,7 +563,7 @@ class ColorStep:
         import torch.distributed as dist
 
         if self.cuda:
-            if self.world > 1:
+            if self.use_stripes:
                 d_rgb = self.stripes().view(self.H, self.W, 3)
             else:
                 self.d_rgb.copy_(self.rgb, non_blocking=True)
@@ -637,7 +641,7 @@ def _setup(args, backend: str, cuda: bool):
         torch.cuda.set_device(dev)
     else:
         dev = torch.device("cpu")
-    if world > 1:
+    if world > 1 or getattr(args, "group", False):
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
@@ -700,6 +704,7 @@ class Bench:
             raise SystemExit(f"bench.py: the library was built from sources {self.build['build_id']}, these are "
                              f"{F.source_id()}: rebuild (__graft_entry__.build())")
         self.world, self.rank, self.dev, self.one_host = _setup(args, backend or args.backend, cuda)
+        self.ranked = self.world > 1 or bool(getattr(args, "group", False))  # the N > 1 paths (a group exists)
         S = self.S = args.size
         self.frame = value_noise(S, S, 1234)
         self.doms = F.create_uniform_grid(S, S, 16, 8)
@@ -741,10 +746,10 @@ class Bench:
     # ---- the headline: the end-to-end step ----
     def headline(self) -> None:
         args, world, rank, dev, eng = self.args, self.world, self.rank, self.dev, self.eng
-        use_node = world > 1 and self.one_host and args.tuples == "node"
+        use_node = self.ranked and self.one_host and args.tuples == "node"
         node, node_err = (_node_buffer(self.plan, rank, dev, world) if use_node else (None, ""))
         clock = PhaseClock(dev)
-        step = FrameStep(eng, self.h_frame, self.plan, rank, dev, node_tuples=node, clock=clock)
+        step = FrameStep(eng, self.h_frame, self.plan, rank, dev, stripes=self.ranked, node_tuples=node, clock=clock)
         for _ in range(args.warmup):
             step()
         _sync(dev)
@@ -768,7 +773,7 @@ class Bench:
             node.close()
         self.engine_name = {1: "valu", 2: "mfma"}.get(st["engine"], "valu")
         self.form = self.F.FORM_NAMES.get(st["search_form"], self.engine_name)
-        self.tuples_out = "node" if use_node and not node_err else ("gather" if world > 1 else "sink")
+        self.tuples_out = "node" if use_node and not node_err else ("gather" if self.ranked else "sink")
         S, nr_total, n_d = self.S, self.nr_total, len(self.doms)
         line = self.line
         line.update(headline_fields(nr_total, world, args.steps, args.warmup, elapsed))
@@ -782,7 +787,7 @@ class Bench:
                        "engine": self.engine_name, "ranges_per_gpu": len(self.mine), "parallelism": f"ranges/{world}",
                        "env": frac_env(), "ab_run": bool(self.knobs)},
             "step": ("frame H2D (pinned, 16 MiB) + pool build + search + fit + 32-byte tuples written by the resolve "
-                     "into pinned host memory" if world == 1 else
+                     "into pinned host memory" if not self.ranked else
                      "frame H2D of the rank's 1/N stripe of rows (pinned) + RCCL all-gather of the frame + pool build "
                      "+ search + fit of the rank's shard + " +
                      ("its 32-byte tuples written by the resolve into the node's shared pinned tuple buffer + a "
@@ -852,7 +857,7 @@ class Bench:
             onode, oerr = (_node_buffer(self.plan, rank, dev, world) if self.one_host else
                            (None, "ranks on several hosts"))
         if other == "gather" or onode is not None:
-            ostep = FrameStep(self.eng, self.h_frame, self.plan, rank, dev, node_tuples=onode)
+            ostep = FrameStep(self.eng, self.h_frame, self.plan, rank, dev, stripes=True, node_tuples=onode)
             _, osec = _run_leg(ostep, self.side_steps, 1, world, dev)
             self.checks[f"{other}_equals_headline"] = ostep.tuples_bytes() == self.gathered
             self.line[f"{other}_value"] = {**self.per_step(osec, self.side_steps), "tuples_out": other}
@@ -923,7 +928,7 @@ class Bench:
             **self.per_step(ssec, ss),
             "step": "per frame: H2D on the context's copy stream into its second plane buffer, overlapped with the "
                     "previous frame's kernels + search + tuples written by the resolve into pinned memory" +
-                    (" (per rank, no gather)" if self.world > 1 else ""),
+                    (" (per rank, no gather)" if self.ranked else ""),
             "phases_ms": {k: round(float(np.mean(shist["ms_" + k])), 3) if len(shist) else 0.0
                           for k in ("prep", "search", "finish")}}
         eng.set_frame(self.d_frame if self.cuda else self.frame)
@@ -950,7 +955,7 @@ class Bench:
             e.set_frame(np.zeros((h, w), np.uint8))
             e.set_domains(F.create_uniform_grid(w, h, 16, 8))
             e.set_ranges(r[a:b])
-        cstep = ColorStep(c5_eng, h_rgb if self.cuda else rgb, c5_plans, rank, self.dev)
+        cstep = ColorStep(c5_eng, h_rgb if self.cuda else rgb, c5_plans, rank, self.dev, stripes=self.ranked)
         _, csec = _run_leg(cstep, ss, 1, self.world, self.dev)
         n5 = sum(len(r) for r in c5_rngs)
         self.line["c5"] = {
@@ -1008,7 +1013,7 @@ class Bench:
         args, world, rank = self.args, self.world, self.rank
         self.headline()
         if self.side_steps > 0:
-            if world > 1:
+            if self.ranked:
                 self.other_tuples_leg()
             self.device_leg()
             self.stream_leg()
@@ -1027,7 +1032,7 @@ class Bench:
             if args.out:
                 with open(args.out, "w") as f:
                     json.dump(self.line, f)
-        if world > 1:
+        if dist.is_initialized():
             dist.barrier()
             dist.destroy_process_group()
         return self.line

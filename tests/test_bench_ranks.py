@@ -20,16 +20,16 @@ SIZE = 64  # 64 ranges, 49 domains; C5: 64 + 16 + 16 ranges
 STEPS = 2
 
 
-def _run(tmp_path, world, tuples="gather", fail_rank=None):
+def _run(tmp_path, world, tuples="gather", fail_rank=None, group=False):
     import bench
 
-    out = str(tmp_path / f"line_{world}_{tuples}.json")
+    out = str(tmp_path / f"line_{world}_{tuples}{'_group' if group else ''}.json")
     argv = ["--gpus", str(world), "--size", str(SIZE), "--steps", str(STEPS), "--warmup", "1", "--side-steps", "1",
-            "--cpu-budget", "0", "--tuples", tuples, "--out", out]
+            "--cpu-budget", "0", "--tuples", tuples, "--out", out] + (["--group"] if group else [])
     env = dict(os.environ, OMP_NUM_THREADS="1")
     if fail_rank is not None:
         env["FAIL_RANK"] = str(fail_rank)
-    if world == 1:  # a single rank without a process group, as bench.py runs at N = 1
+    if world == 1 and not group:  # a single rank without a process group, as bench.py runs at N = 1
         rc = subprocess.call([sys.executable, SCRIPT, *argv], env=env)
     else:
         rc = bench.launch_ranks(world, script=SCRIPT, argv=argv, env=env)
@@ -102,6 +102,23 @@ def test_bench_main_on_gloo_ranks(tmp_path, single, world, tuples):
     for k, v in line["phases_ms"].items():
         assert v == max(r[k] for r in by), k
     assert all(r["frame_allgather"] > 0 and r["run"] > 0 and r["tuples"] > 0 for r in by)
+
+
+@pytest.mark.parametrize("tuples", ["gather", "node"])
+def test_group_rehearsal_at_world_one(tmp_path, single, tuples):
+    """--group: one rank with a process group takes every N > 1 path (frame stripes + all-gather, the tuple
+    exchange and the other one as a side leg, the node buffer, C5's all-gathers) — the rehearsal of the RCCL
+    line on a one-GPU box; its records equal the plain single-rank run's."""
+    rc, out = _run(tmp_path, 1, tuples, group=True)
+    assert rc == 0
+    line = json.load(open(out))
+    rec = line["records"]
+    other = "node" if tuples == "gather" else "gather"
+    assert line["n_gpus"] == 1 and line["tuples_out"] == tuples
+    assert rec["tuples_sha16"] == single["records"]["tuples_sha16"]
+    assert rec["own_slice_in_gather"] and rec["device_leg_equals_e2e"] and rec[f"{other}_equals_headline"]
+    assert line["c5"]["records"] == single["c5"]["records"]
+    assert line["phases_ms"]["frame_allgather"] > 0
 
 
 def test_launch_ranks_returns_the_childrens_status(tmp_path):

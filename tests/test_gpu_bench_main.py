@@ -49,3 +49,25 @@ def test_bench_main_two_ranks_on_one_gpu(tmp_path, one_rank, tuples):
         assert v == max(r[k] for r in line["phases_ms_by_rank"]), k
     assert all(r["frame_allgather"] > 0 and r["search"] > 0 for r in line["phases_ms_by_rank"])
     assert one_rank["records"]["own_slice_in_gather"] and one_rank["records"]["device_leg_equals_e2e"]
+
+
+@pytest.mark.parametrize("tuples", ["node", "gather"])
+def test_bench_main_rccl_group_at_world_one(tmp_path, one_rank, tuples):
+    """bench.py under torch.distributed.run with one rank and --group: the nccl (RCCL) process group on the GPU
+    and every N > 1 path the driver's 8-GPU line runs — frame stripes + RCCL all-gather, the RCCL tuple
+    all-gather and the node buffer's RCCL token, the float64 all-reduce / all-gather of the clocks, C5's
+    all-gathers — with the records equal to the plain one-rank run's."""
+    import bench
+
+    out = str(tmp_path / f"group_{tuples}.json")
+    rc = bench.launch_ranks(1, script=os.path.join(ROOT, "bench.py"),
+                            argv=[*ARGS, "--gpus", "1", "--group", "--tuples", tuples, "--out", out])
+    assert rc == 0
+    line = json.load(open(out))
+    rec, want = line["records"], one_rank["records"]
+    other = "node" if tuples == "gather" else "gather"
+    assert rec["tuples_sha16"] == want["tuples_sha16"] and rec["n"] == want["n"]
+    assert rec["own_slice_in_gather"] and rec["device_leg_equals_e2e"] and rec[f"{other}_equals_headline"]
+    assert line["tuples_out"] == tuples and line[f"{other}_value"]["value"] > 0
+    assert line["c5"]["records"] == one_rank["c5"]["records"]
+    assert line["phases_ms"]["frame_allgather"] > 0 and line["search_form"] == "fourier"
