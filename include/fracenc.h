@@ -308,7 +308,9 @@ int frac_pack_frc1(frac_ctx* ctx, uint32_t contrast_bits, uint32_t brightness_bi
 
 /* ---- host helpers (no device needed) ------------------------------------ */
 /* createUniformGrid (image/partition2.hpp:109-135): returns the item count and
- * writes min(count, cap) items (categories -1). */
+ * writes min(count, cap) items (categories -1).  Returns 0 where the reference's loop has no
+ * meaningful grid: a zero size or offset (it never ends) or an item larger than the plane (its
+ * do-while emits one item outside the plane, which every search entry refuses). */
 size_t frac_uniform_grid(uint32_t width, uint32_t height, uint32_t item_size, uint32_t item_offset,
                          frac_grid_item* out, size_t cap);
 /* The same with createUniformGrid's Size32u item size and offset (partition2.hpp:110-113): items

@@ -163,3 +163,35 @@ def test_product_library_has_no_ablation_kernels():
     assert set(map(int, dft)) == {123905, 9217}, sorted(set(dft))
     assert set(map(int, mfma)) == {130, 386}, sorted(set(mfma))  # 386: the float-C epilogue, n <= 4
     assert not _kernel_instances(r"fracenc::(search_dft2)<"), "the two-block A/B form is tuning-only"
+
+
+def test_uniform_grid_closed_form_count_and_cap(oracle):
+    """frac_uniform_grid2 counts in closed form and fills row by row (round 6: the loop's count cost 0.2 ms per
+    quadtree call): count, items and a short `cap` (the first cap items, the full count returned) equal
+    createUniformGrid's loop (the oracle, and the reference's own build when present) over random geometries,
+    edge cases included (item = plane, offset past the edge, degenerate sizes)."""
+    import ctypes as C
+
+    rng = np.random.default_rng(5)
+    cases = [(64, 64, (64, 64), (1, 1)), (64, 64, (8, 8), (100, 100)), (7, 5, (8, 8), (1, 1)), (9, 9, (1, 1), (1, 1)),
+             (64, 64, (0, 8), (8, 8)), (64, 64, (8, 8), (0, 8))]
+    for _ in range(40):
+        W, H = (int(v) for v in rng.integers(1, 200, 2))
+        cases.append((W, H, tuple(int(v) for v in rng.integers(1, 40, 2)), tuple(int(v) for v in rng.integers(1, 40, 2))))
+    lib = F.lib()
+    for W, H, (sw, sh), (ox, oy) in cases:
+        n = lib.frac_uniform_grid2(W, H, sw, sh, ox, oy, None, 0)
+        if 0 in (sw, sh, ox, oy) or sw > W or sh > H:  # no grid (the loop never ends / its item leaves the plane)
+            assert n == 0, (W, H, sw, sh, ox, oy)
+            continue
+        want = oracle.lib().or_uniform_grid2(W, H, sw, sh, ox, oy, None, 0)
+        assert n == want, (W, H, sw, sh, ox, oy)
+        if not n:
+            continue
+        g = F.create_uniform_grid(W, H, (sw, sh), (ox, oy))
+        o = oracle.uniform_grid(W, H, (sw, sh), (ox, oy))
+        assert g.tobytes() == o.tobytes(), (W, H, sw, sh, ox, oy)
+        cap = max(1, n // 3)
+        short = np.zeros(cap + 1, dtype=F.GRID_ITEM)
+        assert lib.frac_uniform_grid2(W, H, sw, sh, ox, oy, short.ctypes.data_as(C.c_void_p), cap) == n
+        assert short[:cap].tobytes() == g[:cap].tobytes() and short[cap].tobytes() == bytes(F.GRID_ITEM.itemsize)
