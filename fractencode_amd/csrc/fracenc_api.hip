@@ -3929,16 +3929,20 @@ int frac_pack_frc1(frac_ctx* c, uint32_t cbits, uint32_t bbits, uint8_t* out, si
     if (c->src.w != W || c->src.h != H)
         return c->fail(FRAC_E_INVALID, "pack_frc1: source and target planes must have one size");
     // the stream's implicit geometry: createUniformGrid ranges (row-major) and domains
+    // (compared item by item against the closed-form lattice, without building it: at C3 the two grids
+    // hold 0.5 M items)
     auto same_grid = [&](const std::vector<frac_grid_item>& g, uint32_t size, uint32_t off) {
         const size_t cnt = frac_uniform_grid(W, H, size, off, nullptr, 0);
         if (cnt != g.size())
             return false;
-        std::vector<frac_grid_item> u(cnt);
-        if (cnt)
-            frac_uniform_grid(W, H, size, off, u.data(), cnt);
-        for (size_t i = 0; i < cnt; ++i)
-            if (u[i].x != g[i].x || u[i].y != g[i].y || u[i].w != g[i].w || u[i].h != g[i].h)
-                return false;
+        if (!cnt)
+            return true;
+        const size_t cols = (W - size) / off + 1;
+        const frac_grid_item* it = g.data();
+        for (size_t r = 0, k = 0; k < cnt; ++r)
+            for (size_t q = 0; q < cols; ++q, ++k, ++it)
+                if (it->x != q * off || it->y != r * off || it->w != size || it->h != size)
+                    return false;
         return true;
     };
     if (n == 0)
