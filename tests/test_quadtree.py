@@ -200,6 +200,39 @@ def test_gpu_quadtree_leaves_into_pinned_memory():
         assert (pinned[len(short):] == np.zeros(1, dtype=F.ENCODE_ITEM)).all()  # nothing past the capacity
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("leaves", [False, True])
+def test_gpu_quadtree_levels_into_pinned_memory_across_frames(leaves):
+    """Pinned output at C4 size, every level's emit writing across PCIe: frames in turn (different frames, so a
+    stale item shows) and a capacity that ends inside the 8-pixel level's leaves equal the pageable path's items.
+    (Round 6 measured staging the earlier levels in HBM with a side-stream copy during the next level: slower,
+    C4q 1.305 → 1.336 ms, profiles/r06/c4q_host/.)"""
+    import torch
+
+    from fractencode_amd.synth import value_noise
+
+    big = value_noise(4096, 4096, 1234)
+    frames = [big[:2048, :2048].copy(), big[2048:, 2048:].copy(), big[:2048, 2048:].copy()]
+    dt = F.QT_LEAF if leaves else F.ENCODE_ITEM
+    cap = (2048 // 4) ** 2
+    pinned = torch.empty(cap * dt.itemsize, dtype=torch.uint8).pin_memory().numpy().view(dt)
+    with F.Engine(0, 4, True) as e:
+        for k, fr in enumerate(frames * 2):
+            e.set_frame(fr)
+            want, sw = e.encode_quadtree(16, 4, 0.05, leaves=leaves)
+            pinned[:] = np.zeros(1, dtype=dt)
+            got, sg = e.encode_quadtree(16, 4, 0.05, out=pinned, leaves=leaves)
+            assert np.shares_memory(got, pinned) and got.tobytes() == want.tobytes(), k
+            assert sg["items"] == sw["items"] and sg["rejected_mappings"] == sw["rejected_mappings"], k
+            sizes = want["w"] if not leaves else 1 << (want["code"] >> 28)
+            n16 = int((sizes == 16).sum())
+            m = n16 + int((sizes == 8).sum()) // 2  # inside the staged 8-pixel level
+            pinned[:] = np.zeros(1, dtype=dt)
+            part, sp = e.encode_quadtree(16, 4, 0.05, out=pinned[:m], leaves=leaves, allow_short=True)
+            assert sp["items"] == len(want) and part.tobytes() == want[:m].tobytes(), k
+            assert not pinned[m:].tobytes().strip(b"\0"), k  # nothing past the capacity
+
+
 def _leaves_from_records(rec, W):
     """numpy restatement of frac_qt_leaf packing (include/fracenc.h): the test's independent packer."""
     n = rec["w"].astype(np.int64)
