@@ -13,6 +13,9 @@
 //   Quantizer<T>        Frac::Quantizer (encode/Quantizer.hpp:7-45) as the built reference
 //                       computes it (value() with the FMA the compiler contracts)
 //   createUniformGrid / preclassify / encodeQuadtree / decode   — the C ABI entry points
+//   Engine's ABI 8/9 methods: an external HIP stream (void*), the tuple sink and 32-byte tuples,
+//                       frame streaming (setFrameAsync / setFrameDeviceAsync), 32-byte quadtree
+//                       leaves, per-run device times
 //
 // Errors throw fracenc::Error carrying frac_last_error.
 #pragma once
@@ -103,6 +106,40 @@ public:
         w_ = w;
         h_ = h;
     }
+    // ABI 9: frame streaming.  setFrameAsync uploads on the context's copy stream into its second plane buffer
+    // while the runs already enqueued read the current one (pinned host memory makes it asynchronous; the plane
+    // must stay unchanged until a later sync / fetch); setFrameDeviceAsync copies a device plane on the
+    // context's stream without a host wait.
+    void setFrameAsync(const uint8_t* plane, uint32_t w, uint32_t h, uint32_t stride)
+    {
+        check(frac_set_frame_async(ctx_, plane, w, h, stride));
+        w_ = w;
+        h_ = h;
+    }
+    void setFrameDeviceAsync(const void* d_plane, uint32_t w, uint32_t h, uint32_t stride)
+    {
+        check(frac_set_frame_device_async(ctx_, d_plane, w, h, stride));
+        w_ = w;
+        h_ = h;
+    }
+    // an external hipStream_t (as void*; nullptr: the context's own), ordered after the previous stream's work
+    void setStream(void* hip_stream) { check(frac_set_stream(ctx_, hip_stream)); }
+    void* stream() const { return frac_get_stream(ctx_); }
+    // ABI 8: every later run writes its 32-byte tuples into dst (device memory or pinned host memory); nullptr
+    // clears it
+    void setTupleSink(void* dst) { check(frac_set_tuple_sink(ctx_, dst)); }
+    // the last run's tuples (north_star's (domain, transform, s, o, rms)), synchronously
+    void fetchTuples(frac_tuple* out) { check(frac_fetch_tuples(ctx_, out)); }
+    // per-run device times since the previous call (FRAC_FLAG_TIMING, Params::timing)
+    std::vector<frac_run_timing> timingHistory()
+    {
+        size_t n = 0;
+        check(frac_timing_history(ctx_, nullptr, 0, &n));
+        std::vector<frac_run_timing> out(n);
+        check(frac_timing_history(ctx_, out.data(), out.size(), &n));
+        out.resize(n);
+        return out;
+    }
     void setDomains(const std::vector<frac_grid_item>& d) { check(frac_set_domains(ctx_, d.data(), d.size())); }
     void setRanges(const frac_grid_item* r, size_t n) { check(frac_set_ranges(ctx_, r, n)); }
     void run() { check(frac_run(ctx_)); }
@@ -132,6 +169,18 @@ public:
         std::vector<frac_encode_item> out(cap);
         frac_stats tmp{};
         check(frac_encode_quadtree(ctx_, &qp, out.data(), cap, &n, st ? st : &tmp));
+        out.resize(n);
+        return out;
+    }
+    // the same partition as 32-byte frac_qt_leaf items (ABI 7): half the bytes of encodeQuadtree's records
+    std::vector<frac_qt_leaf> encodeQuadtreeLeaves(uint32_t max_size, uint32_t min_size, double split_distance,
+                                                   frac_stats* st = nullptr)
+    {
+        const frac_quadtree_params qp{max_size, min_size, split_distance};
+        size_t cap = (size_t)(w_ / min_size) * (h_ / min_size), n = 0;
+        std::vector<frac_qt_leaf> out(cap);
+        frac_stats tmp{};
+        check(frac_encode_quadtree_leaves(ctx_, &qp, out.data(), cap, &n, st ? st : &tmp));
         out.resize(n);
         return out;
     }

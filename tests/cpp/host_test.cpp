@@ -4,6 +4,7 @@
 // reference goldens.  Usage: host_test <repo root> <output file>
 #include "fracenc.hpp"
 
+#include <algorithm>
 #include <cstdio>
 #include <fstream>
 #include <iostream>
@@ -87,6 +88,50 @@ int main(int argc, char** argv)
         const int32_t it = r.first;
         put(out, &it, 1);
         put(out, &r.second, 1);
+        // 5. ABI 9 frame streaming on one engine: three frames, each uploaded by setFrameAsync while the
+        //    previous one's run is enqueued, the tuples of every frame fetched; beside them each frame's tuples
+        //    from a synchronous setFrame + run
+        std::vector<std::vector<uint8_t>> frames(3, y);
+        for (uint32_t r = 0; r < H; ++r)
+            for (uint32_t c = 0; c < W; ++c) {
+                frames[1][(size_t)r * W + c] = y[(size_t)(H - 1 - r) * W + c];
+                frames[2][(size_t)r * W + c] = y[(size_t)r * W + (W - 1 - c)];
+            }
+        std::vector<frac_tuple> sync_t(rngs.size() * frames.size()), async_t(sync_t.size());
+        {
+            fracenc::Engine s(0, p);
+            s.setDomains(doms);
+            for (size_t k = 0; k < frames.size(); ++k) {
+                s.setFrame(frames[k].data(), W, H, W);
+                s.setRanges(rngs.data(), rngs.size());
+                s.run();
+                s.fetchTuples(sync_t.data() + k * rngs.size());
+            }
+        }
+        fracenc::Params pt = p;
+        pt.timing = true;
+        fracenc::Engine a(0, pt);
+        a.setFrame(frames[0].data(), W, H, W);
+        a.setDomains(doms);
+        a.setRanges(rngs.data(), rngs.size());
+        for (size_t k = 0; k < frames.size(); ++k) {
+            a.setFrameAsync(frames[k].data(), W, H, W);
+            a.run();
+            a.fetchTuples(async_t.data() + k * rngs.size());
+        }
+        put(out, sync_t.data(), sync_t.size());
+        put(out, async_t.data(), async_t.size());
+        // 6. the per-run device times of those three runs (Params::timing)
+        const auto hist = a.timingHistory();
+        const uint64_t nh = hist.size();
+        put(out, &nh, 1);
+        // 7. the quadtree partition as 32-byte leaves (ABI 7)
+        fracenc::Params pq;
+        pq.use_classifier = true;
+        fracenc::Engine q(0, pq);
+        q.setFrame(y.data(), W, H, W);
+        const auto leaves = q.encodeQuadtreeLeaves(16, 4, 4.0);
+        put(out, leaves.data(), leaves.size());
         std::cout << "host_test: ok (" << core.engineCount() << " engines)\n";
         return 0;
     } catch (const std::exception& ex) {

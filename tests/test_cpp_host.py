@@ -1,7 +1,8 @@
 """The C++ host layer (include/fracenc.hpp): tests/cpp/host_test drives EncodingEngineCore
-(two engines claiming 1,000-range batches), the device classifier, Quantizer<double> and the
-decoder from C++ with no Python in the loop; its output is compared here with the reference
-goldens."""
+(two engines claiming 1,000-range batches), the device classifier, Quantizer<double>, the
+decoder, frame streaming (setFrameAsync) with 32-byte tuples, per-run timings and the quadtree's
+32-byte leaves from C++ with no Python in the loop; its output is compared here with the reference
+goldens and with the Python layer's results on the same library."""
 import json
 import os
 import subprocess
@@ -74,3 +75,24 @@ def test_cpp_host_layer_matches_reference(tmp_path):
     np.testing.assert_array_equal(np.frombuffer(c[6], np.uint8).reshape(512, 512), d["plane"])
     assert int(np.frombuffer(c[7], np.int32)[0]) == dmeta["iterations"]
     assert float(np.frombuffer(c[8], np.float64)[0]) == dmeta["rms"]
+    # 5. frame streaming: every streamed frame's tuples equal its synchronous search's, and frame 0's equal the
+    # Python layer's tuples for the golden frame
+    nr = len(t4)
+    sync_t = np.frombuffer(c[9], dtype=F.TUPLE)
+    async_t = np.frombuffer(c[10], dtype=F.TUPLE)
+    assert len(sync_t) == len(async_t) == 3 * nr
+    assert sync_t.tobytes() == async_t.tobytes()
+    y = np.fromfile(os.path.join(GOLD, "lenna_y.u8"), np.uint8).reshape(512, 512)
+    with F.Engine(0, 4) as e:
+        e.set_frame(y)
+        e.set_domains(F.create_uniform_grid(512, 512, 16, 8))
+        e.search(F.create_uniform_grid(512, 512, 8, 8))
+        assert e.fetch_tuples().tobytes() == sync_t[:nr].tobytes()
+    assert not np.array_equal(sync_t[:nr], sync_t[nr:2 * nr])  # the frames differ
+    # 6. one timing entry per streamed run
+    assert int(np.frombuffer(c[11], np.uint64)[0]) == 3
+    # 7. the quadtree leaves equal the Python layer's
+    with F.Engine(0, 4, True) as e:
+        e.set_frame(y)
+        want, _ = e.encode_quadtree(16, 4, 4.0, leaves=True)
+    assert np.frombuffer(c[12], dtype=F.QT_LEAF).tobytes() == want.tobytes()
