@@ -643,6 +643,12 @@ def _setup(args, backend: str, cuda: bool):
         dev = torch.device("cpu")
     if world > 1 or getattr(args, "group", False):
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        if "MASTER_ADDR" not in os.environ:  # --group without a launcher: a one-rank group on this host
+            s = socket.socket()
+            s.bind(("127.0.0.1", 0))
+            os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(s.getsockname()[1]), RANK="0",
+                              WORLD_SIZE="1")
+            s.close()
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:

@@ -29,7 +29,10 @@ def _run(tmp_path, world, tuples="gather", fail_rank=None, group=False):
     env = dict(os.environ, OMP_NUM_THREADS="1")
     if fail_rank is not None:
         env["FAIL_RANK"] = str(fail_rank)
-    if world == 1 and not group:  # a single rank without a process group, as bench.py runs at N = 1
+    if world == 1 and group:  # no launcher: bench.py sets up the one-rank group itself
+        env = {k: v for k, v in env.items() if k not in ("MASTER_ADDR", "MASTER_PORT", "RANK", "WORLD_SIZE")}
+        rc = subprocess.call([sys.executable, SCRIPT, *argv], env=env)
+    elif world == 1:  # a single rank without a process group, as bench.py runs at N = 1
         rc = subprocess.call([sys.executable, SCRIPT, *argv], env=env)
     else:
         rc = bench.launch_ranks(world, script=SCRIPT, argv=argv, env=env)
